@@ -1,0 +1,224 @@
+"""Deterministic synthetic inputs for the plik_lite fast-parameter path.
+
+The real plik_lite dataset (``plik_lite_v18_*.clik`` or a native ``.dataset``)
+is not shipped with the reference (``.MISSING_LARGE_BLOBS``), so the parity
+tests, the oracle harness and ``bench.py`` all build the same synthetic dataset
+from a seed, exactly as SURVEY.md section 8(d) specifies:
+
+* bins: widths 5x14, 9x156, 17x30, 33x15 starting at l=30 (TT 215 bins to
+  l=2508; TE/EE use the first 199 bins, to l=1996) -- the layout of
+  ``TPlikLiteLikelihood`` (reference ``source/CMB.f90:33-36``);
+* ``weights`` file = 1/width per l (the reader multiplies by 2pi/(l(l+1)),
+  ``source/CMB.f90:230-233``);
+* ``X`` = binned best-fit theory x (1 + 0.01 N(0,1));
+* ``cov`` = D (I + 0.05 A A^T / N_b) D with sigma_b = 2% |X_b| (floored at
+  10% of the spectrum's rms |X| so TE zero crossings stay well conditioned),
+  A ~ N(0,1);
+* per-walker theory ``D_l (1 + 0.01 s_w(l))`` with ``s_w`` five cosine modes;
+* ``calPlanck ~ N(1, 0.0025)`` (``batch2/planck_calibration.ini:2``).
+
+Random numbers come from a counter-based splitmix64 stream + Box-Muller so
+the same arrays are reproduced bit-for-bit on any host (numpy only, no
+numpy.random version dependence).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+_GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+
+PLMIN = 30
+PLMAX = 2508
+NBINCL = (215, 199, 199)          # TT, TE, EE  (source/CMB.f90:36)
+BIN_WIDTHS = ((5, 14), (9, 156), (17, 30), (33, 15))
+
+# field-pair index of Theory%Cls(i,j), i>=j, T=1 E=2 B=3 P=4 (CosmologyTypes.f90:24)
+FIELD_TT, FIELD_TE, FIELD_EE, FIELD_BT, FIELD_BE, FIELD_BB = 0, 1, 2, 3, 4, 5
+FIELD_PT, FIELD_PE, FIELD_PB, FIELD_PP = 6, 7, 8, 9
+N_FIELDS = 10
+
+
+def splitmix64(seed: int, n: int, offset: int = 0) -> np.ndarray:
+    """n outputs of the splitmix64 stream for ``seed`` starting at ``offset``."""
+    with np.errstate(over="ignore"):
+        i = np.arange(offset + 1, offset + n + 1, dtype=np.uint64)
+        z = (np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + i * _GOLDEN) & _M64
+        z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & _M64
+        z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & _M64
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def uniforms(seed: int, n: int, offset: int = 0) -> np.ndarray:
+    """Uniform doubles in [0, 1) with 53 random bits."""
+    return (splitmix64(seed, n, offset) >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
+
+
+def gaussians(seed: int, n: int) -> np.ndarray:
+    """n standard normals (Box-Muller, cosine branch; two uniforms each)."""
+    u = uniforms(seed, 2 * n)
+    u1 = 1.0 - u[0::2]          # (0, 1]
+    u2 = u[1::2]
+    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+
+
+def _golden_dir() -> str:
+    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+
+
+def base_theory(lmax: int = PLMAX) -> np.ndarray:
+    """Best-fit D_l (muK^2) for the 10 field pairs, shape [10, lmax+1], l=0..lmax.
+
+    Source: ``data/base_plikHM_TTTEEE_lowl_lowE.minimum.theory_cl`` of the
+    reference (columns TT TE EE BB PP, l=2..2508), stored as a fixture.
+    """
+    z = np.load(os.path.join(_golden_dir(), "base_plikHM_TTTEEE_lowl_lowE.theory_cl.npz"))
+    L = z["L"]
+    out = np.zeros((N_FIELDS, lmax + 1))
+    m = L <= lmax
+    for f, key in ((FIELD_TT, "TT"), (FIELD_TE, "TE"), (FIELD_EE, "EE"), (FIELD_BB, "BB"), (FIELD_PP, "PP")):
+        out[f, L[m]] = z[key][m]
+    return out
+
+
+def plik_bins() -> tuple[np.ndarray, np.ndarray]:
+    """blmin/blmax as 0-based offsets from PLMIN (the on-disk convention, CMB.f90:224-227)."""
+    lo, hi = [], []
+    l = 0
+    for w, n in BIN_WIDTHS:
+        for _ in range(n):
+            lo.append(l)
+            hi.append(l + w - 1)
+            l += w
+    assert l == PLMAX - PLMIN + 1 and len(lo) == NBINCL[0]
+    return np.array(lo, dtype=np.int64), np.array(hi, dtype=np.int64)
+
+
+@dataclass
+class PlikLiteData:
+    """Synthetic plik_lite dataset in the on-disk form read by CMB.f90:208-303."""
+    blmin: np.ndarray      # [215] offsets from PLMIN
+    blmax: np.ndarray      # [215]
+    weights_file: np.ndarray  # [2479] raw weights (before the 2pi/(l(l+1)) factor)
+    X: np.ndarray          # [613] bandpowers (C_l units), TT|TE|EE
+    cov: np.ndarray        # [613, 613]
+
+    def internal_weights(self) -> np.ndarray:
+        """Weights as used in LogLike: w_l * 2pi/(l(l+1)), index 0 <-> l=PLMIN."""
+        ls = PLMIN + np.arange(self.weights_file.size, dtype=np.float64)
+        return self.weights_file * (2.0 * np.pi) / ls / (ls + 1.0)
+
+    def write(self, directory: str, name: str = "plik_lite_synth", use_cl: str = "TT TE EE",
+              extra: dict | None = None) -> str:
+        """Write the dataset files + a CosmoMC ``.dataset`` ini; return its path."""
+        os.makedirs(directory, exist_ok=True)
+        np.savetxt(os.path.join(directory, f"{name}_bins_min.txt"), self.blmin, fmt="%d")
+        np.savetxt(os.path.join(directory, f"{name}_bins_max.txt"), self.blmax, fmt="%d")
+        np.savetxt(os.path.join(directory, f"{name}_weights.txt"), self.weights_file, fmt="%.17e")
+        nb = self.X.size
+        np.savetxt(os.path.join(directory, f"{name}_data.txt"),
+                   np.column_stack([np.arange(1, nb + 1), self.X]), fmt=["%d", "%.17e"])
+        np.savetxt(os.path.join(directory, f"{name}_cov.txt"), self.cov, fmt="%.17e")
+        with open(os.path.join(directory, "planck_calib.paramnames"), "w") as f:
+            f.write("calPlanck     y_{\\rm cal}     # total Planck calibration\n")
+        path = os.path.join(directory, f"{name}.dataset")
+        lines = [
+            f"name = {name}",
+            "calibration_param = planck_calib.paramnames",
+            f"use_cl = {use_cl}",
+            f"data = {name}_data.txt",
+            f"blmin = {name}_bins_min.txt",
+            f"blmax = {name}_bins_max.txt",
+            f"weights = {name}_weights.txt",
+            f"cov_file = {name}_cov.txt",
+        ]
+        for k, v in (extra or {}).items():
+            lines.append(f"{k} = {v}")
+        with open(path, "w") as f:
+            f.write("\n".join(lines) + "\n")
+        return path
+
+
+def bin_theory(data: PlikLiteData, dl: np.ndarray) -> np.ndarray:
+    """Binned C_b for TT|TE|EE from D_l [10, lmax+1] (CMB.f90:315-325), no calibration."""
+    w = data.internal_weights()
+    out = []
+    for f, nb in zip((FIELD_TT, FIELD_TE, FIELD_EE), NBINCL):
+        for b in range(nb):
+            lo, hi = PLMIN + data.blmin[b], PLMIN + data.blmax[b]
+            out.append(np.dot(dl[f, lo:hi + 1], w[lo - PLMIN:hi - PLMIN + 1]))
+    return np.array(out)
+
+
+def make_plik_lite(seed: int = 12345) -> PlikLiteData:
+    blmin, blmax = plik_bins()
+    nl = PLMAX - PLMIN + 1
+    wfile = np.empty(nl)
+    for lo, hi in zip(blmin, blmax):
+        wfile[lo:hi + 1] = 1.0 / (hi - lo + 1)
+    proto = PlikLiteData(blmin, blmax, wfile, np.zeros(sum(NBINCL)), np.eye(sum(NBINCL)))
+    base = base_theory()
+    xb = bin_theory(proto, base)
+    nb = xb.size
+    g = gaussians(seed, nb + nb * nb)
+    X = xb * (1.0 + 0.01 * g[:nb])
+    A = g[nb:].reshape(nb, nb)
+    # sigma_b = 2% of |X_b|, floored at 0.2% of the block rms so that TE bins
+    # crossing zero do not make the covariance singular (cond ~1e5, not ~1e13)
+    sig = np.empty(nb)
+    o = 0
+    for n in NBINCL:
+        blk = X[o:o + n]
+        sig[o:o + n] = 0.02 * np.sqrt(blk ** 2 + (0.1 * np.sqrt(np.mean(blk ** 2))) ** 2)
+        o += n
+    M = np.eye(nb) + 0.05 * (A @ A.T) / nb
+    cov = sig[:, None] * M * sig[None, :]
+    cov = 0.5 * (cov + cov.T)
+    return PlikLiteData(blmin, blmax, wfile, X, cov)
+
+
+def _walker_mode_amplitudes(seeds: np.ndarray) -> np.ndarray:
+    """Five N(0,1) amplitudes per walker; walker stream = its own seed (vectorised)."""
+    with np.errstate(over="ignore"):
+        i = np.arange(1, 11, dtype=np.uint64)[None, :]
+        z = (seeds.astype(np.uint64)[:, None] + i * _GOLDEN) & _M64
+        z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & _M64
+        z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & _M64
+        z = z ^ (z >> np.uint64(31))
+    u = (z >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
+    u1 = 1.0 - u[:, 0::2]
+    u2 = u[:, 1::2]
+    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+
+
+def walker_theory(n_walkers: int, seed: int = 0xC05A0C, lmax: int = PLMAX,
+                  first_walker: int = 0, n_fields: int = N_FIELDS,
+                  ld_field: int | None = None) -> np.ndarray:
+    """Per-walker D_l, shape [W, n_fields, ld_field] (l = 0..lmax, zero padded).
+
+    D_l^w = base_l * (1 + 0.01 s_w(l)),
+    s_w(l) = sum_{m=1..5} a_{w,m} cos(pi m (l-2)/(lmax-2)), a ~ N(0,1) from the
+    splitmix64 stream ``seed + walker``. Field order is the Theory%Cls(i,j)
+    lower-triangle order TT, TE, EE, BT, BE, BB, PT, PE, PB, PP.
+    """
+    ld = lmax + 1 if ld_field is None else ld_field
+    base = base_theory(lmax)[:n_fields]
+    ell = np.arange(lmax + 1, dtype=np.float64)
+    modes = np.cos(np.pi * np.arange(1, 6)[:, None] * (ell[None, :] - 2.0) / (lmax - 2.0))
+    out = np.zeros((n_walkers, n_fields, ld))
+    chunk = 256
+    for c0 in range(0, n_walkers, chunk):
+        c1 = min(n_walkers, c0 + chunk)
+        a = _walker_mode_amplitudes(np.arange(seed + first_walker + c0, seed + first_walker + c1))
+        s = 1.0 + 0.01 * (a @ modes)
+        out[c0:c1, :, :lmax + 1] = base[None, :, :] * s[:, None, :]
+    return out
+
+
+def walker_calibrations(n_walkers: int, seed: int = 0xCA1, first_walker: int = 0) -> np.ndarray:
+    g = gaussians(seed, first_walker + n_walkers)[first_walker:]
+    return 1.0 + 0.0025 * g

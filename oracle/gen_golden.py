@@ -1,0 +1,167 @@
+"""ORACLE TEST INFRASTRUCTURE -- generates tests/golden/*.json from the compiled
+reference (oracle/_ref, built by `make -C oracle ref` from /root/reference).
+
+Runs only in the development container (the reference never travels to the
+GPU box).  Each fixture records the seeds that regenerate its inputs through
+cosmomc_amd.synthetic, plus the reference outputs; the committed fixtures are
+small, the inputs are rebuilt on both sides.
+
+    python oracle/gen_golden.py            # all fixtures
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+from cosmomc_amd import synthetic as syn  # noqa: E402
+
+REF_DIR = os.path.join(HERE, "_ref")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def run_cmb_harness(ini_text: str, theory: np.ndarray, nuis: np.ndarray, workdir: str) -> np.ndarray:
+    """theory [W, nfield, lmax+1]; nuis [W, n_nuis] -> reference -lnL [W]."""
+    W, nfield, nl = theory.shape
+    ini = os.path.join(workdir, "likes.ini")
+    with open(ini, "w") as f:
+        f.write(ini_text)
+    th = os.path.join(workdir, "theory.bin")
+    nu = os.path.join(workdir, "nuis.bin")
+    out = os.path.join(workdir, "out.txt")
+    np.ascontiguousarray(theory, dtype="<f8").tofile(th)
+    np.ascontiguousarray(nuis, dtype="<f8").tofile(nu)
+    cmd = [os.path.join(REF_DIR, "plik_harness"), ini, th, nu, str(W), str(nl - 1), str(nfield),
+           str(nuis.shape[1]), out]
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
+    subprocess.run(cmd, check=True, cwd=workdir, env=env, stdout=subprocess.DEVNULL)
+    return np.loadtxt(out, ndmin=1)
+
+
+PLIK_CASES = [
+    # name, override lines (cmb_dataset[PLIK_LITE,key] = value), walkers
+    ("plik_lite_TTTEEE", {}, 8),
+    ("plik_lite_TT", {"use_cl": "TT"}, 8),
+    ("plik_lite_TE", {"use_cl": "TE"}, 4),
+    ("plik_lite_TTEE", {"use_cl": "TT EE"}, 4),
+    ("plik_lite_TTTEEE_Lrange", {"bins_for_L_range": "100 1500"}, 4),
+]
+
+
+def gen_plik(data_seed=12345, theory_seed=0xC05A0C, cal_seed=0xCA1):
+    data = syn.make_plik_lite(data_seed)
+    out = {"generator": "cosmomc_amd.synthetic", "data_seed": data_seed,
+           "theory_seed": theory_seed, "cal_seed": cal_seed, "cases": {}}
+    with tempfile.TemporaryDirectory() as td:
+        ds = data.write(td)
+        for name, over, W in PLIK_CASES:
+            lines = [f"cmb_dataset[PLIK_LITE] = {ds}"]
+            lines += [f"cmb_dataset[PLIK_LITE,{k}] = {v}" for k, v in over.items()]
+            theory = syn.walker_theory(W, seed=theory_seed, n_fields=3)
+            cal = syn.walker_calibrations(W, seed=cal_seed)
+            cal[0] = 1.0            # the survey's cal = 1 anchor
+            lnl = run_cmb_harness("\n".join(lines) + "\n", theory, cal[:, None], td)
+            out["cases"][name] = {"overrides": over, "walkers": W, "cal": cal.tolist(),
+                                  "minus_lnL": lnl.tolist()}
+            print(f"{name:28s} W={W}  -lnL[0..2] = {lnl[:3]}")
+    with open(os.path.join(GOLDEN, "plik_lite_ref.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+def run_rng(mode: str, cfg_text: str, workdir: str) -> list[str]:
+    cfg = os.path.join(workdir, "cfg.txt")
+    out = os.path.join(workdir, "rng_out.txt")
+    with open(cfg, "w") as f:
+        f.write(cfg_text)
+    subprocess.run([os.path.join(REF_DIR, "rng_harness"), mode, cfg, out], check=True, cwd=workdir,
+                   stdout=subprocess.DEVNULL)
+    with open(out) as f:
+        return f.read().split("\n")
+
+
+def _fmt(a):
+    return " ".join(f"{x:.17e}" for x in np.ravel(a))
+
+
+# chain configurations: (name, n, blocks, slow_block_max, oversample_fast, propose_scale, fast_only, steps)
+CHAIN_CASES = [
+    # config 1: 6-D Gaussian, test_likelihood, one (slow) block, no fast/slow split
+    ("gauss6_single_block", 6, [[1, 2, 3, 4, 5, 6]], 1, 1, 2.4, 0, 400),
+    # slow 2 + fast 3 + fast 1, oversample_fast 2, full GetProposal cycle
+    ("gauss6_blocked", 6, [[1, 2], [3, 4, 5], [6]], 1, 2, 2.4, 0, 400),
+    # fast-only steps (FastParameterSample path) with propose_scale 1.9 (batch3/common.ini)
+    ("gauss6_fast_only", 6, [[1, 2], [3, 4, 5], [6]], 1, 1, 1.9, 1, 400),
+    # 1-D block of calPlanck-like width (sign flip RotMatrix branch, n=1)
+    ("gauss3_n1_blocks", 3, [[1], [2], [3]], 1, 3, 2.4, 0, 300),
+]
+
+
+def chain_problem(n: int, seed: int):
+    """SPD covariance, centre, bounds, priors for a test Gaussian chain."""
+    g = syn.gaussians(seed, n * n + 3 * n)
+    A = g[:n * n].reshape(n, n)
+    sig = 0.5 + np.abs(g[n * n:n * n + n])
+    corr = np.eye(n) + 0.3 * (A @ A.T) / n
+    d = 1.0 / np.sqrt(np.diag(corr))
+    corr = corr * d[:, None] * d[None, :]
+    cov = corr * sig[:, None] * sig[None, :]
+    center = g[n * n + n:n * n + 2 * n]
+    pmin = center - 4.0 * sig
+    pmax = center + 4.0 * sig
+    pmean = np.zeros(n)
+    pstd = np.zeros(n)
+    pmean[-1] = center[-1] + 0.2 * sig[-1]
+    pstd[-1] = 2.0 * sig[-1]
+    P0 = center + 0.5 * sig * g[n * n + 2 * n:n * n + 3 * n]
+    return cov, center, pmin, pmax, pmean, pstd, P0
+
+
+def gen_rng():
+    out = {"kat": None, "streams": {}, "chains": {}}
+    with tempfile.TemporaryDirectory() as td:
+        out["kat"] = [float(x) for x in run_rng("kat", "", td) if x.strip()]
+        for ij, kl in ((1802, 9373), (1234, 5678), (31328, 30081)):
+            n, nidx, nrot = 60, 12, 5
+            lines = [x for x in run_rng("stream", f"{ij} {kl} {n} {nidx} {nrot}\n", td) if x.strip()]
+            vals = [float(x) for x in lines]
+            out["streams"][f"{ij}_{kl}"] = {
+                "ij": ij, "kl": kl, "ranmar": vals[:n], "gaussian1": vals[n:2 * n],
+                "randexp1": vals[2 * n:3 * n], "rand_indices": [int(v) for v in vals[3 * n:3 * n + nidx]],
+                "rotation": vals[3 * n + nidx:], "nidx": nidx, "nrot": nrot}
+        for ci, (name, n, blocks, sbm, ovs, scale, fast_only, steps) in enumerate(CHAIN_CASES):
+            cov, center, pmin, pmax, pmean, pstd, P0 = chain_problem(n, 777 + ci)
+            ij, kl = 4321 + ci, 9373
+            T = 1.0
+            cfg = [f"{ij} {kl} {n} {steps} {fast_only}",
+                   f"{len(blocks)} {sbm} {ovs} {scale!r} {T!r}",
+                   " ".join(str(len(b)) for b in blocks)]
+            cfg += [" ".join(str(x) for x in b) for b in blocks]
+            cfg += [_fmt(cov), _fmt(cov), _fmt(center), _fmt(pmin), _fmt(pmax), _fmt(pmean), _fmt(pstd), _fmt(P0)]
+            lines = [x for x in run_rng("chain", "\n".join(cfg) + "\n", td) if x.strip()]
+            like0 = float(lines[0])
+            rows = np.array([[float(v) for v in l.split()] for l in lines[1:]])
+            out["chains"][name] = {
+                "ij": ij, "kl": kl, "n": n, "blocks": blocks, "slow_block_max": sbm,
+                "oversample_fast": ovs, "propose_scale": scale, "fast_only": fast_only,
+                "temperature": T, "steps": steps, "problem_seed": 777 + ci,
+                "cov": cov.tolist(), "center": center.tolist(), "pmin": pmin.tolist(), "pmax": pmax.tolist(),
+                "prior_mean": pmean.tolist(), "prior_std": pstd.tolist(), "P0": P0.tolist(),
+                "like0": like0, "accept": rows[:, 0].astype(int).tolist(), "trial_like": rows[:, 1].tolist(),
+                "cur_like": rows[:, 2].tolist(), "P": rows[:, 3:].tolist()}
+            print(f"chain {name:22s} accept rate {rows[:, 0].mean():.3f}  final -lnL {rows[-1, 2]:.6f}")
+    with open(os.path.join(GOLDEN, "rng_sampler_ref.json"), "w") as f:
+        json.dump(out, f, indent=0)
+
+
+if __name__ == "__main__":
+    if not os.path.exists(os.path.join(REF_DIR, "plik_harness")):
+        sys.exit("build the reference first: make -C oracle ref")
+    gen_plik()
+    gen_rng()

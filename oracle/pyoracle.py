@@ -1,0 +1,143 @@
+"""ORACLE TEST INFRASTRUCTURE -- ctypes view of oracle/liboracle.so.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, as the checker / CPU baseline.  Nothing in cosmomc_amd/ does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+_dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_ip = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_lp = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+
+
+class Rng(C.Structure):
+    _fields_ = [("u", C.c_double * 97), ("c", C.c_double), ("cd", C.c_double), ("cm", C.c_double),
+                ("i97", C.c_int), ("j97", C.c_int), ("iset", C.c_int), ("gset", C.c_double)]
+
+
+class Target(C.Structure):
+    _fields_ = [("num_params", C.c_int), ("pmin", C.c_void_p), ("pmax", C.c_void_p),
+                ("prior_mean", C.c_void_p), ("prior_std", C.c_void_p), ("temperature", C.c_double),
+                ("test_like", C.c_int), ("n_used", C.c_int), ("params_used", C.c_void_p),
+                ("test_covinv", C.c_void_p), ("center", C.c_void_p), ("plik", C.c_void_p),
+                ("plik_nuis_index", C.c_int), ("plik_dl", C.c_void_p), ("plik_ld_field", C.c_long)]
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            subprocess.run(["make", "-C", HERE, "oracle"], check=True, stdout=subprocess.DEVNULL)
+        L = C.CDLL(path)
+        L.orc_rmarin.argtypes = [C.POINTER(Rng), C.c_int, C.c_int]
+        L.orc_ranmar.argtypes = [C.POINTER(Rng)]
+        L.orc_ranmar.restype = C.c_double
+        L.orc_gaussian1.argtypes = [C.POINTER(Rng)]
+        L.orc_gaussian1.restype = C.c_double
+        L.orc_randexp1.argtypes = [C.POINTER(Rng)]
+        L.orc_randexp1.restype = C.c_float
+        L.orc_rand_indices.argtypes = [C.POINTER(Rng), _ip, C.c_int, C.c_int]
+        L.orc_rand_rotation.argtypes = [C.POINTER(Rng), _dp, C.c_int]
+        L.orc_matrix_inverse.argtypes = [_dp, C.c_int]
+        L.orc_matrix_inverse.restype = C.c_int
+        L.orc_quadform.argtypes = [_dp, _dp, C.c_int]
+        L.orc_quadform.restype = C.c_double
+        L.orc_plik_create.argtypes = [C.c_int, C.c_int, _dp, _lp, _lp, C.c_int, _ip, C.c_int, C.c_int,
+                                      C.c_int, _dp, _dp, C.c_int]
+        L.orc_plik_create.restype = C.c_void_p
+        L.orc_plik_nused.argtypes = [C.c_void_p]
+        L.orc_plik_loglike.argtypes = [C.c_void_p, C.c_void_p, C.c_long, C.c_double]
+        L.orc_plik_loglike.restype = C.c_double
+        L.orc_plik_free.argtypes = [C.c_void_p]
+        L.orc_proposer_create.argtypes = [C.c_int, _ip, _ip, C.c_int, C.c_int, C.c_double, C.c_int, _ip]
+        L.orc_proposer_create.restype = C.c_void_p
+        L.orc_proposer_set_covariance.argtypes = [C.c_void_p, _dp]
+        for fn in ("orc_proposer_get_proposal", "orc_proposer_get_proposal_slow", "orc_proposer_get_proposal_fast"):
+            getattr(L, fn).argtypes = [C.c_void_p, C.POINTER(Rng), _dp]
+        L.orc_proposer_get_proposal_fast_delta.argtypes = [C.c_void_p, C.POINTER(Rng), _dp, C.c_int]
+        L.orc_proposer_free.argtypes = [C.c_void_p]
+        L.orc_target_loglike.argtypes = [C.POINTER(Target), _dp]
+        L.orc_target_loglike.restype = C.c_double
+        L.orc_metropolis_accept.argtypes = [C.POINTER(Rng), C.c_double, C.c_double]
+        L.orc_metropolis_accept.restype = C.c_int
+        L.orc_mh_step.argtypes = [C.c_void_p, C.POINTER(Rng), C.POINTER(Target), _dp, C.POINTER(C.c_double),
+                                  C.c_int, C.POINTER(C.c_double)]
+        L.orc_mh_step.restype = C.c_int
+        L.orc_gelman_rubin.argtypes = [_dp, _dp, C.c_int]
+        L.orc_gelman_rubin.restype = C.c_double
+        _LIB = L
+    return _LIB
+
+
+class Ranmar:
+    """RANMAR stream as RandUtils.f90 (one chain's generator)."""
+
+    def __init__(self, ij: int, kl: int = 9373):
+        self.s = Rng()
+        lib().orc_rmarin(C.byref(self.s), ij, kl)
+
+    def ranmar(self, n=None):
+        if n is None:
+            return lib().orc_ranmar(C.byref(self.s))
+        return np.array([lib().orc_ranmar(C.byref(self.s)) for _ in range(n)])
+
+    def gaussian1(self):
+        return lib().orc_gaussian1(C.byref(self.s))
+
+    def randexp1(self):
+        return lib().orc_randexp1(C.byref(self.s))
+
+    def rand_indices(self, nmax, n):
+        out = np.zeros(n, dtype=np.int32)
+        lib().orc_rand_indices(C.byref(self.s), out, nmax, n)
+        return out
+
+    def rand_rotation(self, n):
+        R = np.zeros(n * n)
+        lib().orc_rand_rotation(C.byref(self.s), R, n)
+        return R.reshape(n, n)
+
+
+class PlikLite:
+    """Oracle TPlikLiteLikelihood built from cosmomc_amd.synthetic.PlikLiteData."""
+    USE_BITS = {"TT": 1, "TE": 2, "EE": 4}
+
+    def __init__(self, data, use_cl="TT TE EE", bins_for_L_range=None, plmin=30):
+        mask = 0
+        for tok in use_cl.split():
+            mask |= self.USE_BITS[tok]
+        rmin, rmax = (-1, -1) if bins_for_L_range is None else bins_for_L_range
+        nbincl = np.array([215, 199, 199], dtype=np.int32)
+        self._keep = (np.ascontiguousarray(data.weights_file, dtype=np.float64),
+                      np.ascontiguousarray(data.blmin, dtype=np.int64),
+                      np.ascontiguousarray(data.blmax, dtype=np.int64),
+                      np.ascontiguousarray(data.X, dtype=np.float64),
+                      np.ascontiguousarray(data.cov, dtype=np.float64))
+        w, lo, hi, X, cov = self._keep
+        self.h = lib().orc_plik_create(plmin, w.size, w, lo, hi, lo.size, nbincl, mask, rmin, rmax, X, cov, X.size)
+        if not self.h:
+            raise RuntimeError("oracle plik_lite: covariance not positive definite")
+        self.nused = lib().orc_plik_nused(self.h)
+
+    def loglike(self, dl: np.ndarray, cal: float) -> float:
+        """dl: [n_fields>=3, ld] float64 for one walker."""
+        dl = np.ascontiguousarray(dl, dtype=np.float64)
+        return lib().orc_plik_loglike(self.h, dl.ctypes.data, dl.shape[-1], float(cal))
+
+    def loglike_batch(self, dl: np.ndarray, cal: np.ndarray) -> np.ndarray:
+        return np.array([self.loglike(dl[i], cal[i]) for i in range(dl.shape[0])])
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_plik_free(self.h)
+            self.h = None
