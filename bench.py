@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Headline benchmark: fast-parameter likelihood evals/s on plik_lite TTTEEE.
+
+One *step* = one fast-parameter Metropolis step of every walker on this GPU
+(reference TMetropolisSampler FastParameterSample, source/MCMC.f90:309-335):
+BlockedProposer GetProposalFast (propose.f90:283-289) -> native plik_lite
+-lnL on the walker's cached slow-parameter theory (CMB.f90:305-329, full
+binning + 613x613 quadratic form every step, as the reference) + calPlanck
+prior -> Metropolis accept.  Each step is W likelihood evaluations.
+
+Workload: BASELINE.json configs[2] (plik_lite_TTTEEE, 1024 walkers on one
+MI355X, cached slow block) without its lowl (clik commander: unavailable,
+parity-unpinned) and lensing terms.  Synthetic inputs of the Planck l_max
+shape (cosmomc_amd.synthetic).  Multi-GPU: walkers are sharded across ranks
+with no per-step collective ("weak" scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 1024]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "fast-param likelihood evals/sec/node (plik_lite_TTTEEE ℓmax=2508); R-1 vs wall-clock"
+N_B = 613            # plik_lite TTTEEE bins (CMB.f90:35)
+N_L = 2479 + 1967 + 1967   # l values binned per eval (TT 30..2508, TE/EE 30..1996)
+FLOPS_QUADFORM = 2 * N_B * N_B + 2 * N_B          # DSYMV + DDOT per eval
+FLOPS_EVAL = 2 * N_L + 2 * N_B * N_B + 4 * N_B    # 766,816
+BYTES_BIN = 8 * N_L + 8                            # D_l + cal per walker, read once
+PEAK_FP64_TFLOPS = 78.6    # MI355X dense FP64 matrix, spec (datasheet)
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E, MI355X_MICROARCH.md
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=500)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--walkers", type=int, default=1024, help="walkers per GPU")
+    p.add_argument("--cpu-seconds", type=float, default=1.5, help="per-process CPU baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def build_problem(W, rank, tmpdir):
+    import torch
+    from cosmomc_amd import synthetic as syn
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    data = syn.make_plik_lite(12345)
+    ds = data.write(tmpdir)
+    like = NativeCMBLikelihood("PLIK_LITE", ds)
+    # parameters: 6 slow cosmological parameters (fixed theory cached per walker)
+    # + calPlanck (fast, nuisance of plik_lite); blocks slow | fast
+    names = ["omegabh2", "omegach2", "theta", "tau", "logA", "ns"]
+    P0 = np.array([0.02237, 0.1200, 1.04092, 0.0544, 3.044, 0.9649, 1.0])
+    sig = np.array([0.00015, 0.0012, 0.00031, 0.0073, 0.014, 0.0042, 0.0025])
+    pmin = P0 - 50 * sig
+    pmax = P0 + 50 * sig
+    pmin[6], pmax[6] = 0.9, 1.1                       # param[calPlanck]=1 0.9 1.1 ...
+    pm = np.zeros(7)
+    ps = np.zeros(7)
+    pm[6], ps[6] = 1.0, 0.0025                        # prior[calPlanck]=1 0.0025
+    like.nuisance_indices = [7]
+    smp = BatchedMCMC(W, 7, list(range(1, 8)), [list(range(1, 7)), [7]], 1, pmin, pmax, pm, ps,
+                      propose_scale=2.4, seed_ij=1802 + rank, seed_kl=9373, first_walker=rank * W)
+    smp.set_covariance(np.diag(sig ** 2))
+    theory = torch.tensor(syn.walker_theory(W, first_walker=rank * W, n_fields=3), device="cuda")
+    smp.add_likelihood(like, theory)
+    smp.set_start(np.tile(P0, (W, 1)))
+    return smp, like, theory, names
+
+
+def cpu_baseline(seconds):
+    """The reference's own plik_lite LogLike (oracle/_ref/plik_bench, compiled
+    from /root/reference) on this host's cores, one single-threaded process per
+    core like CosmoMC's one-chain-per-MPI-rank; falls back to the C
+    restatement (oracle/liboracle.so, kind "port") when _ref is absent."""
+    from cosmomc_amd import synthetic as syn
+    try:
+        ncores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncores = os.cpu_count() or 1
+    P = max(1, min(16, ncores))
+    exe = os.path.join(ROOT, "oracle", "_ref", "plik_bench")
+    data = syn.make_plik_lite(12345)
+    Wc = 16
+    th = syn.walker_theory(Wc, n_fields=3)
+    cal = syn.walker_calibrations(Wc)
+    with tempfile.TemporaryDirectory() as td:
+        ds = data.write(td)
+        if os.path.exists(exe):
+            ini = os.path.join(td, "l.ini")
+            with open(ini, "w") as f:
+                f.write(f"cmb_dataset[PLIK_LITE] = {ds}\n")
+            th.tofile(os.path.join(td, "t.bin"))
+            cal.tofile(os.path.join(td, "n.bin"))
+            env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
+            cmd = [exe, ini, os.path.join(td, "t.bin"), os.path.join(td, "n.bin"), str(Wc), "2508", "3", "1",
+                   str(seconds)]
+            procs = [subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env) for _ in range(P)]
+            rates = []
+            for pr in procs:
+                out, _ = pr.communicate(timeout=120)
+                n, t, _s = out.split()
+                rates.append(float(n) / float(t))
+            return {"value": float(sum(rates)), "unit": "evals/s", "cores": P, "kind": "reference",
+                    "sample": f"reference TPlikLiteLikelihood_LogLike (amdflang -O2 + OpenBLAS 1 thread), "
+                              f"{P} concurrent single-thread processes x {seconds:g} s over {Wc} synthetic "
+                              f"TTTEEE walkers"}
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as po
+        orc = po.PlikLite(data)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            orc.loglike(th[n % Wc], cal[n % Wc])
+            n += 1
+        dt = time.perf_counter() - t0
+        return {"value": n / dt, "unit": "evals/s", "cores": 1, "kind": "port",
+                "sample": f"C restatement oracle/liboracle.so, 1 thread, {seconds:g} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from cosmomc_amd import _native as N
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    N.require_gpu()
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    W = args.walkers
+    with tempfile.TemporaryDirectory() as td:
+        smp, like, theory, _ = build_problem(W, rank, td)
+
+        def barrier():
+            if world > 1:
+                dist.barrier()
+
+        smp.step(args.warmup, fast_only=True)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        smp.step(args.steps, fast_only=True)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        evals = world * W * args.steps
+
+        # roofline pass: same steps with per-kernel HIP events on the launch stream
+        N.profile_reset()
+        N.profile_enable(True)
+        smp.step(args.steps, fast_only=True)
+        torch.cuda.synchronize()
+        N.profile_enable(False)
+        kern = {k: N.profile_read(k) for k in ("plik_bin_delta", "plik_quadform_pairs", "plik_finalize",
+                                                "propose_kernel", "gather_nuis", "accept_kernel")}
+        _, _, _, nacc = smp.state()
+        acc_rate = float(nacc.sum()) / (W * (args.warmup + 2 * args.steps))
+
+    dom = max(kern, key=lambda k: kern[k][0])
+    avg_ms = {k: (v[0] / v[1] if v[1] else None) for k, v in kern.items()}
+    if dom == "plik_quadform_pairs":
+        ach = W * FLOPS_QUADFORM / (avg_ms[dom] * 1e-3) / 1e12
+        roof = {"kernel": dom, "bound": "mfma", "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / PEAK_FP64_TFLOPS, "traffic": None}
+    else:
+        ach = W * BYTES_BIN / (avg_ms[dom] * 1e-3) / 1e9 if dom == "plik_bin_delta" else None
+        roof = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": (ach / PEAK_HBM_GBS) if ach else None, "traffic": None}
+    roof["avg_kernel_us"] = {k: (v * 1e3 if v else None) for k, v in avg_ms.items()}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": evals / dt, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "plik_lite_TTTEEE fast-parameter Metropolis step (BASELINE configs[2] "
+                                   "minus lowl/lensing): GetProposalFast + native plik_lite (613 bins, "
+                                   "l<=2508, full binning + quadratic form) + calPlanck prior + accept",
+                       "walkers_per_gpu": W, "global_walkers": W * world, "nbins": N_B, "lmax": 2508,
+                       "parallelism": f"walkers sharded over {world} rank(s), no per-step collective",
+                       "accept_rate": acc_rate},
+            "roofline": roof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,266 @@
+// C ABI of libcosmomc_amd.so (include/cosmomc_amd.h).  Every entry point
+// catches internal errors and turns them into codes + messages.
+#include <cstring>
+
+#include "sampler.h"
+
+namespace cmamd {
+void sampler_create(cmbs *s, const cmbs_config_t *cfg);
+void sampler_set_covariance(cmbs *s, const double *cov);
+void sampler_set_test_gaussian(cmbs *s, const double *cov, const double *center);
+void sampler_add_likelihood(cmbs *s, cmbl_t *like, int nuis_index0, const double *dl, long long ld_field,
+                            long long ld_walker);
+void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream);
+void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream);
+void sampler_enable_history(cmbs *s, int capacity);
+void sampler_history_stats(cmbs *s, int first, int last, double *means, double *covs, hipStream_t stream);
+void launch_clik_to_dl(const double *clp, long long ld, const int *lm, double *dl, long long ld_field,
+                       long long ld_walker, int lmax_out, int W, hipStream_t stream);
+}  // namespace cmamd
+
+using cmamd::Error;
+
+static void put_err(char *buf, size_t len, const char *msg) {
+    if (buf && len) {
+        std::strncpy(buf, msg, len - 1);
+        buf[len - 1] = 0;
+    }
+}
+
+template <class F> static int guarded(std::string *err, F &&f) {
+    try {
+        f();
+        return CMBL_OK;
+    } catch (const Error &e) {
+        if (err) *err = e.what();
+        return e.code;
+    } catch (const std::exception &e) {
+        if (err) *err = e.what();
+        return CMBL_ERR_FORMAT;
+    }
+}
+
+cmamd::Profiler &cmamd::profiler() {
+    static Profiler p;
+    return p;
+}
+
+extern "C" {
+
+void cmbl_profile_enable(int on) {
+    auto &p = cmamd::profiler();
+    if (!on) p.collect();
+    p.on = on != 0;
+}
+
+void cmbl_profile_reset(void) {
+    auto &p = cmamd::profiler();
+    p.collect();
+    p.done.clear();
+}
+
+int cmbl_profile_read(const char *kernel, double *total_ms, long long *count) {
+    auto &p = cmamd::profiler();
+    p.collect();
+    auto it = p.done.find(kernel ? kernel : "");
+    if (it == p.done.end()) {
+        if (total_ms) *total_ms = 0;
+        if (count) *count = 0;
+        return CMBL_ERR_ARG;
+    }
+    if (total_ms) *total_ms = it->second.first;
+    if (count) *count = it->second.second;
+    return CMBL_OK;
+}
+
+int cmbl_open(const char *tag, const char *dataset_path, const char *override_ini, cmbl_t **out, char *errbuf,
+              size_t errlen) {
+    std::string err;
+    if (!out || !dataset_path || !tag) {
+        put_err(errbuf, errlen, "cmbl_open: null argument");
+        return CMBL_ERR_ARG;
+    }
+    *out = nullptr;
+    int rc = guarded(&err, [&] {
+        cmamd::Ini ini;
+        ini.open(dataset_path);
+        ini.override_text(override_ini);
+        std::unique_ptr<cmbl_t> h(new cmbl_t);
+        std::string t(tag);
+        if (t == "PLIK_LITE") h->like = cmamd::make_plik_lite(ini);
+        else cmamd::fail(CMBL_ERR_UNSUPPORTED, "cmbl_open: dataset tag '%s' not supported yet", tag);
+        *out = h.release();
+    });
+    if (rc) put_err(errbuf, errlen, err.c_str());
+    return rc;
+}
+
+void cmbl_close(cmbl_t *h) { delete h; }
+
+const char *cmbl_last_error(const cmbl_t *h) { return h && h->like ? h->like->last_error.c_str() : ""; }
+
+int cmbl_info(const cmbl_t *h, int *n_nuis, int *cl_lmax, int *speed, const char **name,
+              const char **nuisance_names) {
+    if (!h || !h->like) return CMBL_ERR_ARG;
+    const auto &L = *h->like;
+    if (n_nuis) *n_nuis = L.n_nuis;
+    if (cl_lmax) std::memcpy(cl_lmax, L.cl_lmax, sizeof L.cl_lmax);
+    if (speed) *speed = L.speed;
+    if (name) *name = L.name.c_str();
+    if (nuisance_names) *nuisance_names = L.nuisance_names.c_str();
+    return CMBL_OK;
+}
+
+size_t cmbl_workspace_size(const cmbl_t *h, int W) { return h && h->like ? h->like->workspace_size(W) : 0; }
+
+int cmbl_loglike_batch(cmbl_t *h, int W, const double *dl, long long ld_field, long long ld_walker,
+                       const double *nuis, long long ld_nuis, double *out, void *workspace, void *stream) {
+    if (!h || !h->like) return CMBL_ERR_ARG;
+    return guarded(&h->like->last_error, [&] {
+        if (W < 0 || (W > 0 && (!dl || !out))) cmamd::fail(CMBL_ERR_ARG, "cmbl_loglike_batch: bad arguments");
+        h->like->loglike_batch(W, dl, ld_field, ld_walker, nuis, ld_nuis, out, workspace, (hipStream_t)stream);
+    });
+}
+
+int cmbl_loglike_batch_host(cmbl_t *h, int W, const double *dl, long long ld_field, long long ld_walker,
+                            const double *nuis, long long ld_nuis, double *out) {
+    if (!h || !h->like) return CMBL_ERR_ARG;
+    return guarded(&h->like->last_error, [&] {
+        if (W <= 0) return;
+        const size_t nd = (size_t)ld_walker * W, nn = (size_t)(ld_nuis > 0 ? ld_nuis : 1) * W;
+        cmamd::DevBuf d_dl(nd * 8), d_n(nn * 8), d_out((size_t)W * 8), ws(h->like->workspace_size(W));
+        d_dl.upload(dl, nd * 8);
+        if (nuis) d_n.upload(nuis, nn * 8);
+        h->like->loglike_batch(W, d_dl.as<double>(), ld_field, ld_walker, nuis ? d_n.as<double>() : nullptr,
+                               ld_nuis, d_out.as<double>(), ws.p, 0);
+        HIP_CHECK(hipMemcpy(out, d_out.p, (size_t)W * 8, hipMemcpyDeviceToHost));
+    });
+}
+
+int cmbl_clik_compute_batch(cmbl_t *h, int W, const int *clik_lmax, const double *cl_and_pars, long long ld,
+                            double *lnlike, void *workspace, void *stream) {
+    if (!h || !h->like) return CMBL_ERR_ARG;
+    return guarded(&h->like->last_error, [&] {
+        if (h->like->tag != "PLIK_LITE") cmamd::fail(CMBL_ERR_UNSUPPORTED, "clik entry only routes to PLIK_LITE");
+        if (W <= 0) return;
+        int lm[6];
+        long long ncl = 0;
+        for (int i = 0; i < 6; i++) {
+            lm[i] = clik_lmax[i];
+            ncl += lm[i] + 1;                // lmax = -1 -> absent (0 entries)
+        }
+        // D_l rows long enough for every spectrum the native likelihood reads
+        const int lmax_out = std::max(h->like->cl_lmax[0], std::max(h->like->cl_lmax[4], h->like->cl_lmax[5]));
+        const long long ldf = lmax_out + 1, ldw = 3 * ldf;
+        const size_t need = (size_t)ldw * W * 8 + (size_t)W * 8 + h->like->workspace_size(W);
+        (void)workspace;
+        cmamd::DevBuf tmp(need);
+        double *dl = tmp.as<double>();
+        double *mlnl = dl + (size_t)ldw * W;
+        void *lws = mlnl + W;
+        cmamd::launch_clik_to_dl(cl_and_pars, ld, lm, dl, ldf, ldw, lmax_out, W, (hipStream_t)stream);
+        // nuisance parameters follow the C_l blocks (cliklike.f90:157-163)
+        h->like->loglike_batch(W, dl, ldf, ldw, cl_and_pars + ncl, ld, mlnl, lws, (hipStream_t)stream);
+        // lnlike = -(-lnL): clik_compute returns +lnL (cliklike.f90:166)
+        std::vector<double> hv(W);
+        HIP_CHECK(hipMemcpyAsync(hv.data(), mlnl, (size_t)W * 8, hipMemcpyDeviceToHost, (hipStream_t)stream));
+        HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+        for (auto &v : hv) v = -v;
+        HIP_CHECK(hipMemcpy(lnlike, hv.data(), (size_t)W * 8, hipMemcpyHostToDevice));
+    });
+}
+
+// ------------------------------------------------------------ sampler
+
+void cmbs_walker_seed(int seed_ij, int seed_kl, int walker, int *ij, int *kl) {
+    // walker 0 keeps (seed_ij, seed_kl) -- the reference's rand_seed chain --
+    // later walkers step ij through its full range, then kl.
+    const long long t = (long long)seed_ij + walker;
+    *ij = (int)(t % 31329);
+    *kl = (int)(((long long)seed_kl + t / 31329) % 30082);
+}
+
+int cmbs_create(const cmbs_config_t *cfg, cmbs_t **out, char *errbuf, size_t errlen) {
+    std::string err;
+    if (!cfg || !out) return CMBL_ERR_ARG;
+    *out = nullptr;
+    std::unique_ptr<cmbs> s(new cmbs);
+    int rc = guarded(&err, [&] { cmamd::sampler_create(s.get(), cfg); });
+    if (rc) {
+        put_err(errbuf, errlen, err.c_str());
+        return rc;
+    }
+    *out = s.release();
+    return CMBL_OK;
+}
+
+void cmbs_destroy(cmbs_t *s) { delete s; }
+const char *cmbs_last_error(const cmbs_t *s) { return s ? s->last_error.c_str() : ""; }
+
+int cmbs_set_covariance(cmbs_t *s, const double *cov) {
+    if (!s || !cov) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_set_covariance(s, cov); });
+}
+
+int cmbs_set_test_gaussian(cmbs_t *s, const double *cov, const double *center) {
+    if (!s || !cov || !center) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_set_test_gaussian(s, cov, center); });
+}
+
+int cmbs_add_likelihood(cmbs_t *s, cmbl_t *like, int nuis_index0, const double *dl, long long ld_field,
+                        long long ld_walker) {
+    if (!s) return CMBL_ERR_ARG;
+    return guarded(&s->last_error,
+                   [&] { cmamd::sampler_add_likelihood(s, like, nuis_index0, dl, ld_field, ld_walker); });
+}
+
+int cmbs_set_start(cmbs_t *s, const double *P0, void *stream) {
+    if (!s || !P0) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_set_start(s, P0, (hipStream_t)stream); });
+}
+
+int cmbs_step(cmbs_t *s, int n_steps, int fast_only, void *stream) {
+    if (!s) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_step(s, n_steps, fast_only, (hipStream_t)stream); });
+}
+
+int cmbs_enable_history(cmbs_t *s, int capacity) {
+    if (!s || capacity <= 0) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_enable_history(s, capacity); });
+}
+
+int cmbs_history_stats(cmbs_t *s, int first, int last, double *means, double *covs, void *stream) {
+    if (!s) return CMBL_ERR_ARG;
+    return guarded(&s->last_error,
+                   [&] { cmamd::sampler_history_stats(s, first, last, means, covs, (hipStream_t)stream); });
+}
+
+int cmbs_history_count(const cmbs_t *s) { return s ? s->hist_count : 0; }
+
+int cmbs_state(cmbs_t *s, double **P, double **cur_like, double **mult, int **num_accept) {
+    if (!s) return CMBL_ERR_ARG;
+    if (P) *P = s->dc.P;
+    if (cur_like) *cur_like = s->dc.cur_like;
+    if (mult) *mult = s->dc.mult;
+    if (num_accept) *num_accept = s->dc.num_accept;
+    return CMBL_OK;
+}
+
+int cmbs_get_state_host(cmbs_t *s, double *P, double *cur_like, double *mult, int *num_accept) {
+    if (!s) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] {
+        HIP_CHECK(hipDeviceSynchronize());
+        const int W = s->W, np = s->np;
+        if (P) {
+            std::vector<double> t((size_t)np * W);
+            HIP_CHECK(hipMemcpy(t.data(), s->dc.P, t.size() * 8, hipMemcpyDeviceToHost));
+            for (int w = 0; w < W; w++)
+                for (int i = 0; i < np; i++) P[(size_t)w * np + i] = t[(size_t)i * W + w];
+        }
+        if (cur_like) HIP_CHECK(hipMemcpy(cur_like, s->dc.cur_like, (size_t)W * 8, hipMemcpyDeviceToHost));
+        if (mult) HIP_CHECK(hipMemcpy(mult, s->dc.mult, (size_t)W * 8, hipMemcpyDeviceToHost));
+        if (num_accept) HIP_CHECK(hipMemcpy(num_accept, s->dc.num_accept, (size_t)W * 4, hipMemcpyDeviceToHost));
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,171 @@
+// Shared internals of libcosmomc_amd.so (not part of the C ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/cosmomc_amd.h"
+
+namespace cmamd {
+
+// Error carrying a C-ABI code; caught at the ABI boundary (api.cpp).
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+[[noreturn]] inline void fail(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    throw Error(code, buf);
+}
+
+#define HIP_CHECK(expr)                                                                      \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            ::cmamd::fail(CMBL_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #expr,            \
+                         hipGetErrorString(e_));                                             \
+    } while (0)
+
+// RAII device buffer
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t n) { alloc(n); }
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void alloc(size_t n) {
+        release();
+        if (n) HIP_CHECK(hipMalloc(&p, n));
+        bytes = n;
+    }
+    void grow(size_t n) {
+        if (n > bytes) alloc(n);
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+    void upload(const void *src, size_t n) { HIP_CHECK(hipMemcpy(p, src, n, hipMemcpyHostToDevice)); }
+};
+
+// ---------------- per-kernel event timing (cmbl_profile_*) ----------------
+// Off by default.  When on, every library kernel launch is bracketed by a
+// pair of HIP events recorded on the launch stream, so the average device
+// duration of each kernel can be read back (bench.py roofline pass).
+struct Profiler {
+    bool on = false;
+    struct Rec {
+        hipEvent_t a, b;
+    };
+    std::map<std::string, std::vector<Rec>> pending;
+    std::map<std::string, std::pair<double, long long>> done;   // total ms, count
+    std::vector<hipEvent_t> pool;
+    hipEvent_t get() {
+        hipEvent_t e;
+        if (!pool.empty()) {
+            e = pool.back();
+            pool.pop_back();
+        } else {
+            (void)hipEventCreate(&e);
+        }
+        return e;
+    }
+    void collect() {
+        for (auto &kv : pending) {
+            auto &d = done[kv.first];
+            for (auto &r : kv.second) {
+                float ms = 0.f;
+                (void)hipEventSynchronize(r.b);
+                (void)hipEventElapsedTime(&ms, r.a, r.b);
+                d.first += ms;
+                d.second += 1;
+                pool.push_back(r.a);
+                pool.push_back(r.b);
+            }
+            kv.second.clear();
+        }
+    }
+};
+Profiler &profiler();
+
+template <class F> inline void timed_launch(const char *name, hipStream_t stream, F &&launch) {
+    Profiler &p = profiler();
+    if (!p.on) {
+        launch();
+        return;
+    }
+    Profiler::Rec r{p.get(), p.get()};
+    (void)hipEventRecord(r.a, stream);
+    launch();
+    (void)hipEventRecord(r.b, stream);
+    p.pending[name].push_back(r);
+    if (p.pending[name].size() > 4096) p.collect();
+}
+
+// ---------------- ini files (IniObjects.f90 subset) ----------------
+// key = value lines, '#' comments, INCLUDE(file)/DEFAULT(file), first
+// definition wins (TNameValueList ignoreDuplicates), overrides applied first
+// (TIniFile%Override), relative file names resolved against the ini's
+// directory (Ini_ReadRelativeFileName / ResolveLinkedFile, IniObjects.f90:403-424).
+class Ini {
+  public:
+    void open(const std::string &filename);
+    void override_text(const char *text);          // "key = value" lines
+    bool has(const std::string &key) const { return kv_.count(key) != 0; }
+    std::string str(const std::string &key, const std::string &def = "") const;
+    std::string str_required(const std::string &key) const;
+    std::string relative_filename(const std::string &key, bool required) const;
+    const std::string &filename() const { return filename_; }
+
+  private:
+    void add_line(const std::string &line, bool only_if_undefined);
+    void open_rec(const std::string &filename, bool only_if_undefined, int depth);
+    std::map<std::string, std::string> kv_;
+    std::string filename_;
+};
+
+std::string dirname_of(const std::string &path);
+bool file_exists(const std::string &path);
+// File%LoadTxt: whitespace-separated numeric matrix, '#' comment lines skipped
+std::vector<std::vector<double>> load_txt(const std::string &path);
+std::vector<std::string> split_ws(const std::string &s);
+
+// ---------------- likelihood object ----------------
+struct Like {
+    virtual ~Like() = default;
+    std::string name, tag, nuisance_names;
+    int n_nuis = 0;
+    int speed = -1;
+    int cl_lmax[16] = {0};
+    std::string last_error;
+    virtual size_t workspace_size(int W) const = 0;
+    virtual void loglike_batch(int W, const double *dl, long long ld_field, long long ld_walker,
+                               const double *nuis, long long ld_nuis, double *out, void *ws,
+                               hipStream_t stream) = 0;
+    // internal workspace for ws == nullptr
+    DevBuf own_ws;
+};
+
+std::unique_ptr<Like> make_plik_lite(const Ini &ini);
+
+}  // namespace cmamd
+
+struct cmbl {
+    std::unique_ptr<cmamd::Like> like;
+};

@@ -1,0 +1,180 @@
+/* cosmomc_amd -- MI355X-native fast-parameter likelihood + MCMC step for CosmoMC.
+ *
+ * C ABI of libcosmomc_amd.so.  Plain pointers and sizes only; every device
+ * pointer argument is a HIP device pointer (e.g. torch.Tensor.data_ptr() of a
+ * cuda tensor), every stream a hipStream_t (NULL = default stream).
+ * Errors are returned as negative codes plus a message (never an abort);
+ * the message of the last failing call on a handle is cmbl_last_error().
+ *
+ * Reference interfaces replaced (SouthPoleTelescope/CosmoMC):
+ *   cmbl_open            CMBLikelihood_Add tag dispatch + ReadDatasetFile/ReadIni
+ *                        (source/CMB.f90:54-123, source/likelihood.f90:36-66,
+ *                         source/CMB.f90:208-303 for PLIK_LITE)
+ *   cmbl_info            TDataLikelihood metadata (source/GeneralTypes.f90:105-126):
+ *                        nuisance params, cl_lmax(4,4), speed, name
+ *   cmbl_loglike_batch   like%LogLike(CMB, Theory, DataParams) for W walkers at once
+ *                        (source/CMB.f90:305-329; called from calclike.f90:380)
+ *   cmbl_clik_compute_batch  clik_lnlike packing (source/cliklike.f90:129-170) routed
+ *                        to the native kernel; returns +lnL like clik_compute
+ *   cmbs_*               BlockedProposer (source/propose.f90:53-298) + Metropolis
+ *                        (source/MCMC.f90:119-335) + GetLogLike bounds/priors/temperature
+ *                        (source/calclike.f90:82-151), batched over W independent chains
+ */
+#ifndef COSMOMC_AMD_H
+#define COSMOMC_AMD_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMBL_LOGZERO 1e30          /* settings.f90:114 logZero */
+
+enum {
+    CMBL_OK = 0,
+    CMBL_ERR_ARG = -1,             /* bad argument */
+    CMBL_ERR_IO = -2,              /* dataset / data file unreadable */
+    CMBL_ERR_FORMAT = -3,          /* dataset content invalid */
+    CMBL_ERR_NUMERIC = -4,         /* covariance not positive definite, ... */
+    CMBL_ERR_HIP = -5,             /* HIP runtime error */
+    CMBL_ERR_UNSUPPORTED = -6      /* dataset type / option not implemented */
+};
+
+/* Theory layout: field pair f of Theory%Cls(i,j), i>=j with T=1,E=2,B=3,P=4,
+ * f = i*(i-1)/2 + j - 1: TT=0 TE=1 EE=2 BT=3 BE=4 BB=5 PT=6 PE=7 PB=8 PP=9.
+ * D_l = l(l+1)C_l/2pi in muK^2 (source/CosmoTheory.f90:25), indexed from l=0:
+ *   dl[w*ld_walker + f*ld_field + l]. */
+#define CMBL_NFIELDS 10
+
+typedef struct cmbl cmbl_t;
+
+/* tag: "PLIK_LITE" (native plik_lite); other tags return CMBL_ERR_UNSUPPORTED.
+ * override_ini: "key = value" lines applied over the dataset file, as
+ * cmb_dataset[TAG,key] = value (source/CMB.f90:71-74); may be NULL. */
+int  cmbl_open(const char *tag, const char *dataset_path, const char *override_ini,
+               cmbl_t **out, char *errbuf, size_t errlen);
+void cmbl_close(cmbl_t *h);
+const char *cmbl_last_error(const cmbl_t *h);
+
+/* cl_lmax: 16 ints, cl_lmax[(i-1)*4 + (j-1)] = cl_lmax(i,j) (0 = unused).
+ * speed: likelihood speed (-1 = slow default of TCMBLikelihood).
+ * nuisance_names: space separated names from the calibration/nuisance
+ * .paramnames (pointer owned by the handle). */
+int  cmbl_info(const cmbl_t *h, int *n_nuis, int *cl_lmax, int *speed,
+               const char **name, const char **nuisance_names);
+
+/* Bytes of device workspace cmbl_loglike_batch needs for W walkers. */
+size_t cmbl_workspace_size(const cmbl_t *h, int W);
+
+/* -lnL for W walkers (device pointers, asynchronous on `stream`):
+ *   dl    [W] x [10 fields] x [l]  (strides ld_walker, ld_field, 1)
+ *   nuis  [W] x n_nuis (stride ld_nuis)   -- DataParams of each walker
+ *   out   [W]
+ * workspace: cmbl_workspace_size(h, W) bytes of device memory, or NULL to use
+ * the handle's own (then calls on one handle must not overlap). */
+int  cmbl_loglike_batch(cmbl_t *h, int W,
+                        const double *dl, long long ld_field, long long ld_walker,
+                        const double *nuis, long long ld_nuis,
+                        double *out, void *workspace, void *stream);
+
+/* Same with HOST arrays: stages through device memory over PCIe and
+ * synchronises.  For hosts that keep C_l in CPU memory. */
+int  cmbl_loglike_batch_host(cmbl_t *h, int W,
+                             const double *dl, long long ld_field, long long ld_walker,
+                             const double *nuis, long long ld_nuis, double *out);
+
+/* clik-compatible entry (source/cliklike.f90:138-166): each walker row of
+ * cl_and_pars (stride ld) holds C_l (not D_l) for l=0..lmax of TT, EE, BB,
+ * TE, TB, EB (lmax per spectrum from clik_lmax[6], -1 = absent) followed by
+ * the nuisance parameters.  Writes +lnL (= -(-lnL)) like clik_compute.
+ * Device pointers. */
+int  cmbl_clik_compute_batch(cmbl_t *h, int W, const int *clik_lmax,
+                             const double *cl_and_pars, long long ld,
+                             double *lnlike, void *workspace, void *stream);
+
+/* Per-kernel device timing (HIP events around every library launch; off by
+ * default).  cmbl_profile_read: accumulated milliseconds and launch count of
+ * the kernel named `kernel` (e.g. "plik_quadform_pairs"); synchronises. */
+void cmbl_profile_enable(int on);
+void cmbl_profile_reset(void);
+int  cmbl_profile_read(const char *kernel, double *total_ms, long long *count);
+
+/* ------------------------------------------------------------------ */
+/* Batched Metropolis sampler (W independent chains, one per walker).  */
+
+typedef struct cmbs cmbs_t;
+
+typedef struct {
+    int n_walkers;
+    int num_params;            /* length of P (all parameters, used or fixed) */
+    int n_used;                /* number of varying parameters */
+    const int *params_used;    /* n_used, 1-based indices into P (settings.f90:97) */
+    int n_blocks;              /* BaseParams%param_blocks (slow -> fast) */
+    const int *block_n;        /* n_blocks sizes */
+    const int *block_params;   /* concatenated, 1-based indices into params_used */
+    int slow_block_max;        /* blocks 1..slow_block_max are slow (propose.f90:151) */
+    int oversample_fast;
+    double propose_scale;      /* MCMC.f90:38 default 2.4 */
+    double temperature;        /* calclike.f90 Temperature */
+    const double *pmin, *pmax; /* num_params hard bounds */
+    const double *prior_mean, *prior_std; /* num_params Gaussian priors, std 0 = none */
+    int seed_ij, seed_kl;      /* RANMAR seeds of walker 0; walker w uses
+                                  cmbs_walker_seed() (documented in DESIGN.md) */
+    int first_walker;          /* global index of walker 0 (for sharding) */
+} cmbs_config_t;
+
+/* walker w's RANMAR seeds (ij in 0..31328, kl in 0..30081) */
+void cmbs_walker_seed(int seed_ij, int seed_kl, int walker, int *ij, int *kl);
+
+int  cmbs_create(const cmbs_config_t *cfg, cmbs_t **out, char *errbuf, size_t errlen);
+void cmbs_destroy(cmbs_t *s);
+const char *cmbs_last_error(const cmbs_t *s);
+
+/* proposal covariance of the used parameters, n_used x n_used row-major host
+ * array (BlockedProposer_SetCovariance, propose.f90:210-244) */
+int  cmbs_set_covariance(cmbs_t *s, const double *cov);
+
+/* test_likelihood term (calclike.f90:180-199): -lnL += (P-c)^T C^-1 (P-c)/2
+ * over params_used; cov is n_used x n_used (inverted here), center num_params. */
+int  cmbs_set_test_gaussian(cmbs_t *s, const double *cov, const double *center);
+
+/* Add a CMB likelihood evaluated on cached per-walker theory:
+ * DataParams = P[nuis_index0 - 1 .. + n_nuis) (1-based nuis_index0, the
+ * contiguous nuisance_indices of AddNuisanceParameters, GeneralTypes.f90:618-669).
+ * dl is a device array laid out as for cmbl_loglike_batch for this sampler's
+ * walkers; it must stay alive while the sampler is used. */
+int  cmbs_add_likelihood(cmbs_t *s, cmbl_t *like, int nuis_index0,
+                         const double *dl, long long ld_field, long long ld_walker);
+
+/* Initial points (host, W x num_params) -> evaluates the starting -lnL. */
+int  cmbs_set_start(cmbs_t *s, const double *P0, void *stream);
+
+/* n_steps Metropolis steps for every walker.  fast_only != 0:
+ * FastParameterSample (MCMC.f90:309-335, GetProposalFast) every step;
+ * otherwise TMetropolisSampler_GetNewSample (MCMC.f90:269-307, GetProposal).
+ * Asynchronous on stream. */
+int  cmbs_step(cmbs_t *s, int n_steps, int fast_only, void *stream);
+
+/* Optional history capture for convergence statistics: every step appends
+ * each walker's current used-parameter vector to a device ring of `capacity`
+ * steps (SampleCollector AddNewPoint, SampleCollector.f90:324-456). */
+int  cmbs_enable_history(cmbs_t *s, int capacity);
+/* Per-walker statistics over history rows [first, last] (inclusive, oldest
+ * row = 0): counts[W], means[W][n_used], covs[W][n_used][n_used], device ptrs
+ * (SampleCollector.f90:235-246 "second half" window is first = count/2). */
+int  cmbs_history_stats(cmbs_t *s, int first, int last, double *means, double *covs, void *stream);
+int  cmbs_history_count(const cmbs_t *s);
+
+/* Device pointers of the walker state (valid until destroy), walker-minor:
+ * P [num_params][W], cur_like [W], mult [W] (double), num_accept [W] (int). */
+int  cmbs_state(cmbs_t *s, double **P, double **cur_like, double **mult, int **num_accept);
+
+/* Synchronising copy of the walker state to HOST arrays (any may be NULL):
+ * P [W][num_params], cur_like [W], mult [W], num_accept [W]. */
+int  cmbs_get_state_host(cmbs_t *s, double *P, double *cur_like, double *mult, int *num_accept);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

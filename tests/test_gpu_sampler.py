@@ -1,0 +1,151 @@
+"""Batched Metropolis / BlockedProposer on the GPU vs the reference chains
+(golden fixtures from the compiled Fortran) and the C restatement.  GPU only.
+
+Walker 0 is seeded with the reference chain's (ij, kl), so its whole
+trajectory must follow the reference chain: identical accept/reject
+decisions, parameters to rounding (the GPU's log/sqrt may differ from libm by
+an ulp, hence rtol 1e-11 rather than bit equality).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+from cosmomc_amd import synthetic as syn
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+CHAINS = ["gauss6_single_block", "gauss6_blocked", "gauss6_fast_only", "gauss3_n1_blocks"]
+
+
+def _make_sampler(ch, W):
+    from cosmomc_amd.sampler import BatchedMCMC
+    n = ch["n"]
+    s = BatchedMCMC(W, n, list(range(1, n + 1)), ch["blocks"], ch["slow_block_max"], ch["pmin"], ch["pmax"],
+                    ch["prior_mean"], ch["prior_std"], oversample_fast=ch["oversample_fast"],
+                    propose_scale=ch["propose_scale"], temperature=ch["temperature"], seed_ij=ch["ij"],
+                    seed_kl=ch["kl"])
+    s.set_covariance(np.array(ch["cov"]))
+    s.set_test_gaussian(np.array(ch["cov"]), np.array(ch["center"]))
+    s.set_start(np.tile(np.array(ch["P0"]), (W, 1)))
+    return s
+
+
+def _oracle_chain(ch, ij, kl, steps):
+    from test_oracle import _target, make_oracle_proposer
+    t, keep = _target(ch)
+    h = make_oracle_proposer(ch)
+    r = po.Ranmar(ij, kl)
+    P = np.array(ch["P0"], dtype=np.float64)
+    cur = C.c_double(po.lib().orc_target_loglike(C.byref(t), P))
+    tl = C.c_double(0.0)
+    Ps, likes = [], []
+    for _ in range(steps):
+        po.lib().orc_mh_step(h, C.byref(r.s), C.byref(t), P, C.byref(cur), ch["fast_only"], C.byref(tl))
+        Ps.append(P.copy())
+        likes.append(cur.value)
+    po.lib().orc_proposer_free(h)
+    return np.array(Ps), np.array(likes)
+
+
+@pytest.mark.parametrize("name", CHAINS)
+def test_walker0_follows_reference_chain(rng_golden, name):
+    ch = rng_golden["chains"][name]
+    W = 8
+    s = _make_sampler(ch, W)
+    P, like, mult, nacc = s.state()
+    assert like[0] == pytest.approx(ch["like0"], rel=1e-13)
+    for k in range(ch["steps"]):
+        s.step(1, fast_only=bool(ch["fast_only"]))
+        P, like, mult, nacc = s.state()
+        np.testing.assert_allclose(P[0], ch["P"][k], rtol=1e-11, atol=1e-12, err_msg=f"step {k}")
+        assert like[0] == pytest.approx(ch["cur_like"][k], rel=1e-10, abs=1e-12)
+    assert int(nacc[0]) <= int(sum(ch["accept"]))
+
+
+@pytest.mark.parametrize("name", ["gauss6_blocked", "gauss3_n1_blocks"])
+def test_all_walkers_vs_oracle(rng_golden, name):
+    from cosmomc_amd.sampler import walker_seed
+    ch = rng_golden["chains"][name]
+    W, steps = 70, 150
+    s = _make_sampler(ch, W)
+    s.step(steps, fast_only=bool(ch["fast_only"]))
+    P, like, _, _ = s.state()
+    for w in (1, 17, 63, 64, 69):
+        ij, kl = walker_seed(ch["ij"], ch["kl"], w)
+        Ps, likes = _oracle_chain(ch, ij, kl, steps)
+        np.testing.assert_allclose(P[w], Ps[-1], rtol=1e-10, atol=1e-11)
+        assert like[w] == pytest.approx(likes[-1], rel=1e-9)
+
+
+def test_plik_fast_chain_vs_oracle(tmp_path):
+    """Fast-only Metropolis on calPlanck with native plik_lite TTTEEE on per-walker
+    cached theory + the calPlanck prior (batch2/planck_calibration.ini)."""
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC, walker_seed
+    data = syn.make_plik_lite(12345)
+    like = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    like.nuisance_indices = [2]
+    W, steps = 96, 60
+    th = syn.walker_theory(W, seed=3, n_fields=3)
+    dl = torch.tensor(th, device="cuda")
+    np_ = 3
+    P0 = np.array([0.0222, 1.0, 3.05])
+    pmin = np.array([0.0222, 0.9, 3.05])
+    pmax = np.array([0.0222, 1.1, 3.05])
+    pm = np.array([0.0, 1.0, 0.0])
+    ps = np.array([0.0, 0.0025, 0.0])
+    s = BatchedMCMC(W, np_, [2], [[1]], 0, pmin, pmax, pm, ps, propose_scale=2.4, seed_ij=55, seed_kl=66)
+    s.set_covariance(np.array([[0.002 ** 2]]))
+    s.add_likelihood(like, dl)
+    s.set_start(np.tile(P0, (W, 1)))
+    s.step(steps, fast_only=True)
+    P, lk, _, nacc = s.state()
+    assert np.all(nacc > 0)
+    orc = po.PlikLite(data)
+    for w in (0, 5, 64, 95):
+        ij, kl = walker_seed(55, 66, w)
+        bn = np.array([1], dtype=np.int32)
+        h = po.lib().orc_proposer_create(1, bn, np.array([1], dtype=np.int32), 0, 1, 2.4, 1,
+                                         np.array([2], dtype=np.int32))
+        po.lib().orc_proposer_set_covariance(h, np.array([0.002 ** 2]))
+        t = po.Target()
+        keep = [np.ascontiguousarray(a) for a in (pmin, pmax, pm, ps)]
+        dlw = np.ascontiguousarray(th[w])
+        t.num_params = np_
+        t.pmin, t.pmax, t.prior_mean, t.prior_std = [a.ctypes.data for a in keep]
+        t.temperature = 1.0
+        t.plik, t.plik_nuis_index, t.plik_dl, t.plik_ld_field = orc.h, 2, dlw.ctypes.data, dlw.shape[1]
+        r = po.Ranmar(ij, kl)
+        Q = P0.copy()
+        cur = C.c_double(po.lib().orc_target_loglike(C.byref(t), Q))
+        for _ in range(steps):
+            po.lib().orc_mh_step(h, C.byref(r.s), C.byref(t), Q, C.byref(cur), 1, None)
+        po.lib().orc_proposer_free(h)
+        np.testing.assert_allclose(P[w], Q, rtol=1e-11)
+        assert lk[w] == pytest.approx(cur.value, rel=1e-9)
+
+
+def test_history_stats():
+    """Per-walker second-half mean/cov on device == numpy on the same trajectory."""
+    from cosmomc_amd.sampler import BatchedMCMC
+    n, W = 2, 16
+    s = BatchedMCMC(W, n, [1, 2], [[1, 2]], 1, [-10, -10], [10, 10], seed_ij=7, seed_kl=8)
+    s.set_covariance(np.eye(2))
+    s.set_test_gaussian(np.array([[1.0, 0.3], [0.3, 2.0]]), np.zeros(2))
+    s.set_start(np.zeros((W, n)))
+    s.enable_history(64)
+    traj = []
+    for _ in range(40):
+        s.step(1)
+        traj.append(s.state()[0].copy())
+    traj = np.array(traj)                 # [40, W, n]
+    m, c = s.history_stats(20, 39)
+    x = traj[20:40]
+    mu = x.mean(axis=0)
+    d = x - mu
+    cov = np.einsum("twi,twj->wij", d, d) / x.shape[0]
+    np.testing.assert_allclose(m.cpu().numpy(), mu, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(c.cpu().numpy(), cov, rtol=1e-10, atol=1e-13)
