@@ -93,8 +93,10 @@ class NativeCMBLikelihood(DataLikelihood):
         W = dl.shape[0]
         if out is None:
             out = torch.empty(W, dtype=torch.float64, device=dl.device)
-        assert dl.dtype == torch.float64 and nuis.dtype == torch.float64 and dl.is_cuda
-        assert dl.stride(2) == 1 and nuis.stride(1) == 1
+        if dl.dtype != torch.float64 or nuis.dtype != torch.float64 or not (dl.is_cuda and nuis.is_cuda):
+            raise TypeError("dl and nuis must be float64 cuda tensors")
+        if dl.stride(2) != 1 or nuis.stride(1) != 1:
+            raise ValueError("dl rows (l) and nuisance rows must be contiguous")
         ws = workspace.data_ptr() if workspace is not None else None
         rc = N.lib().cmbl_loglike_batch(self._h, W, dl.data_ptr(), dl.stride(1), dl.stride(0), nuis.data_ptr(),
                                         nuis.stride(0), out.data_ptr(), ws, N.current_stream_ptr(dl.device))

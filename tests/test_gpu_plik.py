@@ -50,7 +50,7 @@ def test_plik_vs_reference_golden(plik_golden, dataset, case):
     like = _open(dataset, CASES[case])
     assert like.nuisance_names == ["calPlanck"]
     th = torch.tensor(syn.walker_theory(c["walkers"], seed=plik_golden["theory_seed"], n_fields=3), device="cuda")
-    cal = torch.tensor(c["cal"], device="cuda").reshape(-1, 1)
+    cal = torch.tensor(c["cal"], dtype=torch.float64, device="cuda").reshape(-1, 1)
     got = like.loglike_batch(th, cal).cpu().numpy()
     np.testing.assert_allclose(got, c["minus_lnL"], rtol=RTOL, atol=0)
 
