@@ -17,9 +17,12 @@
 //                       then the column dot with Delta_I and x2 off-diagonal.
 //                       Writes partial[pair][w].
 //   plik_finalize       -lnL[w] = sum_pair partial[pair][w] / 2, fixed order.
+#include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstring>
 #include <fstream>
+#include <functional>
 
 #include "common.h"
 
@@ -28,7 +31,6 @@ namespace cmamd {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 static constexpr int TILE = 64;          // C^-1 block edge and walker tile
-static constexpr int LDSW = TILE + 2;    // padded LDS row (66 doubles): conflict-free f64 MFMA fragments
 
 // ------------------------------------------------------------------ kernels
 
@@ -39,36 +41,65 @@ struct BinInfo {
     int pad;
 };
 
+struct Item {     // one workgroup's share of the symmetric quadratic form
+    int I;        // row block (64 rows of C^-1)
+    int J0, nJ;   // column blocks J0 .. J0+nJ-1, all >= I
+    int pad;
+};
+
+struct FieldRanges {   // per used field: l range staged in LDS (even-aligned)
+    int lo[3], hi[3], off[3];
+};
+
+// Binning + residual.  One workgroup per walker: the walker's TT/TE/EE D_l
+// rows are read once (16-byte loads when the layout allows), multiplied by the
+// plik weights and kept in LDS; each thread then sums whole bins in l order
+// (the reference's dot_product order) and writes Delta = X - cl / cal^2.
+// Block 0 also zeroes the split-K arrival counters of the quadratic-form
+// kernel that follows on the same stream.
 __global__ __launch_bounds__(256) void plik_bin_delta(
     const double *__restrict__ dl, long long ld_field, long long ld_walker,
     const double *__restrict__ nuis, long long ld_nuis,
-    const double *__restrict__ wts,          // by absolute l
+    const double *__restrict__ wts,          // by absolute l, zero outside the bins
     const BinInfo *__restrict__ bins, const double *__restrict__ X,
-    int nused, int Np, int3 flo, int3 fhi, int3 foff,
-    double *__restrict__ delta)
+    int nused, int Np, FieldRanges fr, int vec_ok,
+    double *__restrict__ delta, unsigned int *__restrict__ counters, int n_counters)
 {
-    extern __shared__ double prod[];       // D_l * w_l for the used l ranges of each field
+    extern __shared__ __attribute__((aligned(16))) double prod[];
     const int w = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (w == 0)
+        for (int i = tid; i < n_counters; i += blockDim.x) counters[i] = 0u;
     const double *D = dl + (long long)w * ld_walker;
-    const int lo[3] = {flo.x, flo.y, flo.z};
-    const int hi[3] = {fhi.x, fhi.y, fhi.z};
-    const int off[3] = {foff.x, foff.y, foff.z};
 #pragma unroll
     for (int f = 0; f < 3; f++) {
-        if (hi[f] < lo[f]) continue;
+        const int lo = fr.lo[f], hi = fr.hi[f];
+        if (hi < lo) continue;
         const double *Df = D + f * ld_field;
-        for (int l = lo[f] + (int)threadIdx.x; l <= hi[f]; l += blockDim.x)
-            prod[off[f] + l - lo[f]] = Df[l] * wts[l];
+        double *P = prod + fr.off[f] - lo;
+        if (vec_ok) {
+            // lo is even; pairs (l, l+1), l <= hi (hi odd after alignment)
+#pragma unroll 4
+            for (int l = lo + 2 * tid; l <= hi; l += 2 * blockDim.x) {
+                const double2 d = *reinterpret_cast<const double2 *>(Df + l);
+                const double2 q = *reinterpret_cast<const double2 *>(wts + l);
+                *reinterpret_cast<double2 *>(P + l) = make_double2(d.x * q.x, d.y * q.y);
+            }
+        } else {
+            const int hs = hi < ld_field ? hi : (int)ld_field - 1;   // never read past the row
+#pragma unroll 4
+            for (int l = lo + tid; l <= hs; l += blockDim.x) P[l] = Df[l] * wts[l];
+        }
     }
     __syncthreads();
     const double cal = nuis[(long long)w * ld_nuis];
     const double c2 = cal * cal;
     double *out = delta + (long long)w * Np;
-    for (int i = threadIdx.x; i < Np; i += blockDim.x) {
+    for (int i = tid; i < Np; i += blockDim.x) {
         double d = 0.0;
         if (i < nused) {
             const BinInfo b = bins[i];
-            const double *p = prod + off[b.field] - lo[b.field];
+            const double *p = prod + fr.off[b.field] - fr.lo[b.field];
             double acc = 0.0;
             for (int l = b.lmin; l <= b.lmax; l++) acc += p[l];
             d = X[i] - acc / c2;
@@ -77,74 +108,144 @@ __global__ __launch_bounds__(256) void plik_bin_delta(
     }
 }
 
-__global__ __launch_bounds__(256) void plik_quadform_pairs(
-    const double *__restrict__ invcov, int Np,
-    const double *__restrict__ delta, int W, int Wpad,
-    const int2 *__restrict__ pairs, double *__restrict__ partial)
+static constexpr int BK = 32;            // k depth staged per pipeline step
+static constexpr int LDK = BK + 2;       // padded LDS row: conflict-free f64 MFMA fragment reads
+
+// Quadratic form, symmetric split-K.  With Ct = C^-1 whose diagonal 64x64
+// blocks are halved,  Delta^T C^-1 Delta / 2 = sum_I Delta_I^T sum_{J>=I} Ct_IJ Delta_J,
+// so -lnL needs only the upper block triangle.  A workgroup owns one
+// (row block I, column-block range) item for 64 walkers: a register-staged,
+// double-buffered K loop over its column blocks (f64 MFMA 16x16x4 into four
+// 16x16 accumulators per wave), then the dot with Delta_I.  Partials are
+// handed off in-launch: the last workgroup of each walker tile (agent-scope
+// release / ticket / acquire, cdna_hip_programming.md section 5 split-K recipe) sums
+// them in fixed item order, so the result is deterministic.
+__global__ __launch_bounds__(256, 2) void plik_quadform_ksplit(
+    const double *__restrict__ Ct, int Np, const double *__restrict__ delta, int W,
+    const Item *__restrict__ items, int n_items,
+    double *__restrict__ partial, unsigned int *__restrict__ counters, double *__restrict__ out)
 {
-    __shared__ __attribute__((aligned(16))) double smem[2 * TILE * LDSW];
-    double *As = smem;                    // As[i][k] = C^-1[I*64+i][J*64+k]
-    double *Bs = smem + TILE * LDSW;      // Bs[n][k] = Delta[w0+n][J*64+k]
-    const int p = blockIdx.x;
-    const int I = pairs[p].x, J = pairs[p].y;
-    const int w0 = blockIdx.y * TILE;
+    __shared__ __attribute__((aligned(16))) double smem[2 * 2 * TILE * LDK];
+    const Item it = items[blockIdx.x];
+    const int tile = blockIdx.y, w0 = tile * TILE;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-    for (int e = tid; e < TILE * TILE / 2; e += 256) {
-        const int r = e >> 5, c2 = (e & 31) * 2;
-        double2 a = *reinterpret_cast<const double2 *>(invcov + (size_t)(I * TILE + r) * Np + J * TILE + c2);
-        *reinterpret_cast<double2 *>(As + r * LDSW + c2) = a;
-        const int w = w0 + r;
-        double2 b = make_double2(0.0, 0.0);
-        if (w < W) b = *reinterpret_cast<const double2 *>(delta + (size_t)w * Np + J * TILE + c2);
-        *reinterpret_cast<double2 *>(Bs + r * LDSW + c2) = b;
-    }
-    __syncthreads();
-
     const int li = lane & 15, lk = lane >> 4;
+    const int nsteps = it.nJ * (TILE / BK);
+    const int kbase0 = it.J0 * TILE;
+    const double *Arow = Ct + (size_t)(it.I * TILE) * Np;
+
+    // staging map: 64 rows x BK doubles per operand = 1024 double2, 4 per thread.
+    // Delta rows of padding walkers (W <= w < Wpad) lie inside the workspace;
+    // they are loaded unconditionally and replaced by zeros (no flat loads).
+    const int sr = tid >> 4, sc = (tid & 15) * 2;            // rows sr, sr+16, sr+32, sr+48
+    const double *ga = Arow + (size_t)sr * Np + kbase0 + sc;
+    const double *gb = delta + (size_t)(w0 + sr) * Np + kbase0 + sc;
+    const bool bv0 = w0 + sr < W, bv1 = w0 + sr + 16 < W, bv2 = w0 + sr + 32 < W, bv3 = w0 + sr + 48 < W;
+    const double2 z2 = make_double2(0.0, 0.0);
+    double2 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
+#define QF_GLOAD(s_)                                                                            \
+    {                                                                                            \
+        const int ko = (s_) * BK;                                                                \
+        ra0 = *reinterpret_cast<const double2 *>(ga + ko);                                       \
+        ra1 = *reinterpret_cast<const double2 *>(ga + (size_t)16 * Np + ko);                     \
+        ra2 = *reinterpret_cast<const double2 *>(ga + (size_t)32 * Np + ko);                     \
+        ra3 = *reinterpret_cast<const double2 *>(ga + (size_t)48 * Np + ko);                     \
+        rb0 = *reinterpret_cast<const double2 *>(gb + ko);                                \
+        if (!bv0) rb0 = z2;                                                                  \
+        rb1 = *reinterpret_cast<const double2 *>(gb + (size_t)16 * Np + ko);                                \
+        if (!bv1) rb1 = z2;                                                                  \
+        rb2 = *reinterpret_cast<const double2 *>(gb + (size_t)32 * Np + ko);                                \
+        if (!bv2) rb2 = z2;                                                                  \
+        rb3 = *reinterpret_cast<const double2 *>(gb + (size_t)48 * Np + ko);                                \
+        if (!bv3) rb3 = z2;                                                                  \
+    }
+#define QF_LSTORE(buf_)                                                                         \
+    {                                                                                            \
+        double *A_ = smem + (buf_) * 2 * TILE * LDK + sr * LDK + sc;                             \
+        double *B_ = A_ + TILE * LDK;                                                            \
+        *reinterpret_cast<double2 *>(A_) = ra0;                                                  \
+        *reinterpret_cast<double2 *>(A_ + 16 * LDK) = ra1;                                       \
+        *reinterpret_cast<double2 *>(A_ + 32 * LDK) = ra2;                                       \
+        *reinterpret_cast<double2 *>(A_ + 48 * LDK) = ra3;                                       \
+        *reinterpret_cast<double2 *>(B_) = rb0;                                                  \
+        *reinterpret_cast<double2 *>(B_ + 16 * LDK) = rb1;                                       \
+        *reinterpret_cast<double2 *>(B_ + 32 * LDK) = rb2;                                       \
+        *reinterpret_cast<double2 *>(B_ + 48 * LDK) = rb3;                                       \
+    }
+
     f64x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-    const double *brow = Bs + (16 * wave + li) * LDSW + lk;
-#pragma unroll 4
-    for (int kk = 0; kk < TILE / 4; kk++) {
-        const double b = brow[4 * kk];
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const double a = As[(16 * t + li) * LDSW + 4 * kk + lk];
-            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
-        }
-    }
+    QF_GLOAD(0);
+    QF_LSTORE(0);
     __syncthreads();
-    // Delta_I tile into the A buffer: As[n][i] = Delta[w0+n][I*64+i]
+    for (int s = 0; s < nsteps; s++) {
+        const int buf = s & 1;
+        if (s + 1 < nsteps) QF_GLOAD(s + 1);        // next tiles in flight under the MFMAs
+        const double *A = smem + buf * 2 * TILE * LDK;
+        const double *brow = A + TILE * LDK + (16 * wave + li) * LDK + lk;
+        const double *arow = A + li * LDK + lk;
+#pragma unroll
+        for (int kk = 0; kk < BK / 4; kk++) {
+            const double b = brow[4 * kk];
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(arow[16 * t * LDK + 4 * kk], b, acc[t], 0, 0, 0);
+        }
+        if (s + 1 < nsteps) QF_LSTORE(buf ^ 1);
+        __syncthreads();
+    }
+    // Delta_I tile: smem[n][i] (row stride TILE+2)
     for (int e = tid; e < TILE * TILE / 2; e += 256) {
         const int r = e >> 5, c2 = (e & 31) * 2;
         const int w = w0 + r;
-        double2 v = make_double2(0.0, 0.0);
-        if (w < W) v = *reinterpret_cast<const double2 *>(delta + (size_t)w * Np + I * TILE + c2);
-        *reinterpret_cast<double2 *>(As + r * LDSW + c2) = v;
+        double2 v = *reinterpret_cast<const double2 *>(delta + (size_t)w * Np + it.I * TILE + c2);
+        if (w >= W) v = make_double2(0.0, 0.0);
+        *reinterpret_cast<double2 *>(smem + r * (TILE + 2) + c2) = v;
     }
     __syncthreads();
     // f64 16x16x4 C/D layout: col = lane&15 (walker n), row = (lane>>4) + 4*r (i)
     const int n = 16 * wave + li;
-    double s = 0.0;
+    double sacc = 0.0;
 #pragma unroll
     for (int t = 0; t < 4; t++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) s += acc[t][r] * As[n * LDSW + 16 * t + lk + 4 * r];
-    s += __shfl_xor(s, 16);
-    s += __shfl_xor(s, 32);
-    if (lk == 0 && w0 + n < W) partial[(size_t)p * Wpad + w0 + n] = (I == J ? s : 2.0 * s);
-}
+        for (int r = 0; r < 4; r++) sacc += acc[t][r] * smem[n * (TILE + 2) + 16 * t + lk + 4 * r];
+    sacc += __shfl_xor(sacc, 16);
+    sacc += __shfl_xor(sacc, 32);
+    double *tile_part = partial + (size_t)tile * n_items * TILE;
+    if (lk == 0) tile_part[(size_t)blockIdx.x * TILE + n] = sacc;
 
-__global__ void plik_finalize(const double *__restrict__ partial, int npairs, int W, int Wpad,
-                              double *__restrict__ out)
-{
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= W) return;
-    double s = 0.0;
-    for (int p = 0; p < npairs; p++) s += partial[(size_t)p * Wpad + w];
-    out[w] = s / 2.0;
+    // ---- in-launch hand-off of the tile's partials to its last-arriving workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned int *flag = reinterpret_cast<unsigned int *>(smem);
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned int t = __hip_atomic_fetch_add(counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = (t == (unsigned int)n_items - 1u) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (flag[0] == 0u) return;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // four item groups per walker, combined in fixed order
+    const int g = tid >> 6;
+    double part = 0.0;
+    for (int k = g; k < n_items; k += 4) part += tile_part[(size_t)k * TILE + lane];
+    double *red = smem + 8;
+    __syncthreads();
+    red[g * TILE + lane] = part;
+    __syncthreads();
+    if (tid < TILE) {
+        const double v = ((red[lane] + red[TILE + lane]) + red[2 * TILE + lane]) + red[3 * TILE + lane];
+        if (w0 + lane < W) out[w0 + lane] = v;
+        if (lane == 0) counters[tile] = 0u;
+    }
 }
 
 // clik packing (cliklike.f90:138-163) -> D_l fields TT, TE, EE for the native kernel
@@ -251,9 +352,15 @@ struct PlikLite final : Like {
     static constexpr int plmin = 30;     // CMB.f90:33
     static constexpr int nbins_total = 613;
     const int nbincl[3] = {215, 199, 199};
-    int nused = 0, Np = 0, nblk = 0, npairs = 0, lmax_needed = 0;
-    int flo[3], fhi[3], foff[3], lds_doubles = 0;
-    DevBuf d_wts, d_bins, d_X, d_invcov, d_pairs;
+    int nused = 0, Np = 0, nblk = 0, lmax_needed = 0;
+    FieldRanges fr{};
+    int lds_doubles = 0;
+    DevBuf d_wts, d_bins, d_X, d_invcov;
+    // work-item lists for column-block chunk sizes KB = 1..MAXKB
+    static constexpr int MAXKB = 5;
+    DevBuf d_items[MAXKB + 1];
+    std::vector<Item> items[MAXKB + 1];
+    std::map<int, int> kb_for_tiles;
     DevBuf conv;   // clik -> D_l staging
 
     explicit PlikLite(const Ini &ini) {
@@ -353,30 +460,44 @@ struct PlikLite final : Like {
         // device layout
         Np = (nused + TILE - 1) / TILE * TILE;
         nblk = Np / TILE;
+        // Ct: C^-1 padded to Np with the diagonal 64x64 blocks halved (exact: x0.5)
         std::vector<double> icp((size_t)Np * Np, 0.0), Xp(Np, 0.0);
         for (int i = 0; i < nused; i++) {
             Xp[i] = X[i];
-            for (int j = 0; j < nused; j++) icp[(size_t)i * Np + j] = ic[(size_t)i * nused + j];
+            for (int j = 0; j < nused; j++) {
+                const double v = ic[(size_t)i * nused + j];
+                icp[(size_t)i * Np + j] = (i / TILE == j / TILE) ? 0.5 * v : v;
+            }
         }
-        std::vector<int2> pairs;
-        for (int I = 0; I < nblk; I++)
-            for (int J = I; J < nblk; J++) pairs.push_back(make_int2(I, J));
-        npairs = (int)pairs.size();
+        for (int kb = 1; kb <= MAXKB; kb++)
+            for (int I = 0; I < nblk; I++)
+                for (int J0 = I; J0 < nblk; J0 += kb) items[kb].push_back(Item{I, J0, std::min(kb, nblk - J0), 0});
+        // LDS ranges per field, widened to even start / odd end for 16-byte access
         lds_doubles = 0;
         for (int f = 0; f < 3; f++) {
-            flo[f] = 1 << 30;
-            fhi[f] = -1;
+            fr.lo[f] = 1 << 30;
+            fr.hi[f] = -1;
         }
         for (auto &b : binfo) {
-            flo[b.field] = std::min(flo[b.field], b.lmin);
-            fhi[b.field] = std::max(fhi[b.field], b.lmax);
+            fr.lo[b.field] = std::min(fr.lo[b.field], b.lmin);
+            fr.hi[b.field] = std::max(fr.hi[b.field], b.lmax);
         }
         for (int f = 0; f < 3; f++) {
-            foff[f] = lds_doubles;
-            if (fhi[f] >= flo[f]) lds_doubles += fhi[f] - flo[f] + 1;
-            else { flo[f] = 0; fhi[f] = -1; }
+            fr.off[f] = lds_doubles;
+            if (fr.hi[f] >= fr.lo[f]) {
+                fr.lo[f] &= ~1;
+                fr.hi[f] |= 1;
+                lds_doubles += fr.hi[f] - fr.lo[f] + 1;
+            } else {
+                fr.lo[f] = 0;
+                fr.hi[f] = -1;
+            }
         }
+
         binfo.resize(Np, BinInfo{0, 1, 0, 0});
+        int wmax = lmax_needed;
+        for (int f = 0; f < 3; f++) wmax = std::max(wmax, fr.hi[f]);
+        wts.resize((size_t)wmax + 2, 0.0);
         d_wts.alloc(wts.size() * 8);
         d_wts.upload(wts.data(), wts.size() * 8);
         d_bins.alloc(binfo.size() * sizeof(BinInfo));
@@ -385,8 +506,10 @@ struct PlikLite final : Like {
         d_X.upload(Xp.data(), Xp.size() * 8);
         d_invcov.alloc(icp.size() * 8);
         d_invcov.upload(icp.data(), icp.size() * 8);
-        d_pairs.alloc(pairs.size() * sizeof(int2));
-        d_pairs.upload(pairs.data(), pairs.size() * sizeof(int2));
+        for (int kb = 1; kb <= MAXKB; kb++) {
+            d_items[kb].alloc(items[kb].size() * sizeof(Item));
+            d_items[kb].upload(items[kb].data(), items[kb].size() * sizeof(Item));
+        }
         const size_t lds = (size_t)lds_doubles * 8;
         if (lds > 64 * 1024)
             HIP_CHECK(hipFuncSetAttribute((const void *)plik_bin_delta,
@@ -395,9 +518,37 @@ struct PlikLite final : Like {
 
     static int wpad(int W) { return (W + TILE - 1) / TILE * TILE; }
 
+    // Column-block chunk per work item: the largest chunk whose longest-first
+    // greedy schedule over 2 workgroups/CU x 256 CUs is (near) the fastest,
+    // counting a fixed per-workgroup overhead of half a block.
+    int choose_kb(int tiles) {
+        auto itk = kb_for_tiles.find(tiles);
+        if (itk != kb_for_tiles.end()) return itk->second;
+        const int slots = 512;
+        int best_kb = 1;
+        double best = 1e300;
+        for (int kb = 1; kb <= MAXKB; kb++) {
+            std::vector<double> load(slots, 0.0);
+            std::vector<double> jobs;
+            for (auto &x : items[kb])
+                for (int t = 0; t < tiles; t++) jobs.push_back(x.nJ + 0.5);
+            std::sort(jobs.begin(), jobs.end(), std::greater<double>());
+            for (double j : jobs) *std::min_element(load.begin(), load.end()) += j;
+            const double makespan = *std::max_element(load.begin(), load.end()) + 0.02 * items[kb].size();
+            if (makespan < best * 0.98) {
+                best = makespan;
+                best_kb = kb;
+            }
+        }
+        kb_for_tiles[tiles] = best_kb;
+        return best_kb;
+    }
+
     size_t workspace_size(int W) const override {
-        const size_t Wp = (size_t)wpad(W);
-        return (Wp * Np + (size_t)npairs * Wp) * sizeof(double);
+        const size_t Wp = (size_t)wpad(W), tiles = Wp / TILE;
+        size_t nmax = 0;
+        for (int kb = 1; kb <= MAXKB; kb++) nmax = std::max(nmax, items[kb].size());
+        return (Wp * Np + tiles * nmax * TILE) * sizeof(double) + ((tiles * 4 + 255) & ~size_t(255));
     }
 
     void loglike_batch(int W, const double *dl, long long ld_field, long long ld_walker,
@@ -407,28 +558,32 @@ struct PlikLite final : Like {
         if (n_nuis < 1 || !nuis) fail(CMBL_ERR_ARG, "plik_lite needs the calibration nuisance parameter");
         if (ld_field < lmax_needed + 1) fail(CMBL_ERR_ARG, "ld_field %lld < lmax+1 = %d", ld_field, lmax_needed + 1);
         if (ld_walker < 3 * ld_field) fail(CMBL_ERR_ARG, "ld_walker must cover the TT, TE, EE fields");
-        const int Wp = wpad(W);
+        const int Wp = wpad(W), tiles = Wp / TILE;
         if (!ws) {
             own_ws.grow(workspace_size(W));
             ws = own_ws.p;
         }
+        const int kb = choose_kb(tiles);
+        const int n_items = (int)items[kb].size();
+        size_t nmax = 0;
+        for (int k = 1; k <= MAXKB; k++) nmax = std::max(nmax, items[k].size());
         double *delta = static_cast<double *>(ws);
         double *partial = delta + (size_t)Wp * Np;
+        unsigned int *counters = reinterpret_cast<unsigned int *>(partial + (size_t)tiles * nmax * TILE);
+        // 16-byte D_l loads need 16-byte aligned rows and the widened ranges inside each row
+        int vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && (ld_field % 2 == 0) && (ld_walker % 2 == 0);
+        for (int f = 0; f < 3; f++)
+            if (fr.hi[f] >= fr.lo[f] && fr.hi[f] >= ld_field) vec_ok = 0;
         timed_launch("plik_bin_delta", stream, [&] {
             hipLaunchKernelGGL(plik_bin_delta, dim3(W), dim3(256), (size_t)lds_doubles * 8, stream, dl, ld_field,
                                ld_walker, nuis, ld_nuis, d_wts.as<double>(), d_bins.as<BinInfo>(), d_X.as<double>(),
-                               nused, Np, make_int3(flo[0], flo[1], flo[2]), make_int3(fhi[0], fhi[1], fhi[2]),
-                               make_int3(foff[0], foff[1], foff[2]), delta);
+                               nused, Np, fr, vec_ok, delta, counters, tiles);
         });
         HIP_CHECK(hipGetLastError());
-        timed_launch("plik_quadform_pairs", stream, [&] {
-            hipLaunchKernelGGL(plik_quadform_pairs, dim3(npairs, Wp / TILE), dim3(256), 0, stream,
-                               d_invcov.as<double>(), Np, delta, W, Wp, d_pairs.as<int2>(), partial);
-        });
-        HIP_CHECK(hipGetLastError());
-        timed_launch("plik_finalize", stream, [&] {
-            hipLaunchKernelGGL(plik_finalize, dim3((W + 255) / 256), dim3(256), 0, stream, partial, npairs, W, Wp,
-                               out);
+        timed_launch("plik_quadform_ksplit", stream, [&] {
+            hipLaunchKernelGGL(plik_quadform_ksplit, dim3(n_items, tiles), dim3(256), 0, stream,
+                               d_invcov.as<double>(), Np, delta, W, d_items[kb].as<Item>(), n_items, partial,
+                               counters, out);
         });
         HIP_CHECK(hipGetLastError());
     }

@@ -35,7 +35,12 @@ struct DevCfg {
     int *num_accept;                // [W]
     int n_like;
     const double *like_terms;       // [n_like][W] -lnL of each likelihood at trial
+    int like_nuis0[8], like_nn[8];  // nuisance slice of each likelihood (0-based start, count)
+    double *like_nuis[8];           // [W][like_nn] DataParams buffers written by mh_kernel
+    int max_blk;                    // largest proposal block
 };
+
+static constexpr int MAXLIKE = 8;
 
 struct LikeSlot {
     cmbl_t *like;
@@ -53,7 +58,8 @@ struct cmbs {
     int slow_block_max = 0;
     std::string last_error;
     // device buffers
-    cmamd::DevBuf tables, state, covinv, center, like_terms, nuis_buf, ws, hist;
+    cmamd::DevBuf tables, state, covinv, center, like_terms, ws, hist;
+    cmamd::DevBuf nuis_bufs[cmamd::MAXLIKE];
     std::vector<cmamd::LikeSlot> likes;
     // host copies of the proposer structure
     std::vector<int> indices, proposer_for_index, blk_start, blk_nchanged, used_params_changed_all;

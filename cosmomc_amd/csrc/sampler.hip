@@ -142,30 +142,40 @@ __global__ void rng_init_kernel(DevCfg c, const int *ij, const int *kl)
 
 // ------------------------------------------------------------ proposer (propose.f90)
 
-__device__ int cyc_next(const DevCfg &c, Rng &r, int w, int which, int n, int base)
+// Per-walker arrays that need dynamic indexing live in LDS, one column per lane.
+template <class T> struct Col {
+    T *p;
+    int s;   // stride between consecutive elements (the block size)
+    __device__ T &operator[](int i) const { return p[i * s]; }
+};
+
+__device__ int cyc_next(const DevCfg &c, Rng &r, int w, int which, int n, int base, Col<int> tmp)
 {   // CyclicIndexRandomizer%Next, propose.f90:75-86 (RandIndices RandUtils.f90:93-108)
     int *loopix = c.cyc_loopix + (size_t)which * c.W + w;
-    int lp = *loopix % n + 1;
+    const int lp = *loopix % n + 1;
     *loopix = lp;
     int *idx = c.cyc + (size_t)base * c.W + w;    // idx[k*W]
     if (lp == 1) {
-        int tmp[MAXP];
-        for (int i = 0; i < n; i++) tmp[i] = i + 1;
-        for (int i = 1; i <= n; i++) {
-            const int ix = (int)(ranmar(r) * (n + 1 - i)) + 1;
-            idx[(size_t)(i - 1) * c.W] = tmp[ix - 1];
-            tmp[ix - 1] = tmp[n + 1 - i - 1];
+        if (n == 1) {
+            (void)ranmar(r);                        // ix = int(ranmar()*1)+1 = 1
+            idx[0] = 1;
+        } else {
+            for (int i = 0; i < n; i++) tmp[i] = i + 1;
+            for (int i = 1; i <= n; i++) {
+                const int ix = (int)(ranmar(r) * (n + 1 - i)) + 1;
+                idx[(size_t)(i - 1) * c.W] = tmp[ix - 1];
+                tmp[ix - 1] = tmp[n + 1 - i - 1];
+            }
         }
     }
     return idx[(size_t)(lp - 1) * c.W];
 }
 
-__device__ void rot_matrix(const DevCfg &c, Rng &r, double *R, int n)
+__device__ void rot_matrix(const DevCfg &c, Rng &r, double *R, int n, Col<double> vec)
 {   // RotMatrix propose.f90:88-102 -> RandRotationD RandUtils.f90:133-153
     // R element (j,i) (row j) at R[(j*n+i)*W]
     const size_t W = c.W;
     if (n > 1) {
-        double vec[MAXBLK];
         for (int j = 0; j < n; j++) {
             double norm;
             for (;;) {
@@ -188,7 +198,12 @@ __device__ void rot_matrix(const DevCfg &c, Rng &r, double *R, int n)
     }
 }
 
-__device__ void block_proposal(const DevCfg &c, Rng &r, int w, int bi /*1-based*/, double *trial)
+struct Scratch {
+    Col<double> trial, vec;
+    Col<int> itmp;
+};
+
+__device__ void block_proposal(const DevCfg &c, Rng &r, int w, int bi /*1-based*/, const Scratch &sc)
 {   // GetBlockProposal :247-254 -> ProposeVec :105-120 -> Propose_r :122-139 -> UpdateParams :142-149
     const int b = bi - 1;
     const int n = c.blk_n[b];
@@ -197,7 +212,7 @@ __device__ void block_proposal(const DevCfg &c, Rng &r, int w, int bi /*1-based*
     int *loopix = c.blk_loopix + (size_t)b * W + w;
     int lp = *loopix;
     if (lp % n == 0) {
-        rot_matrix(c, r, R, n);
+        rot_matrix(c, r, R, n, sc.vec);
         lp = 0;
     }
     lp++;
@@ -215,61 +230,59 @@ __device__ void block_proposal(const DevCfg &c, Rng &r, int w, int bi /*1-based*
         rf = sqrt(rf / m);
     }
     const double scale = rf * c.propose_scale;
-    double vec[MAXBLK];
-    for (int k = 0; k < n; k++) vec[k] = R[((size_t)k * n + (lp - 1)) * W] * scale;
+    // vec(k) = R(k, loopix) * (r * wid);  P(changed) += mapping_matrix . vec
     const int nc = c.blk_nchanged[b];
     const double *M = c.mapping + c.blk_map_off[b];
     const int *chg = c.changed + c.blk_changed_off[b];
     for (int j = 0; j < nc; j++) {
         double s = 0.0;
-        for (int k = 0; k < n; k++) s += M[j * n + k] * vec[k];
-        trial[chg[j]] += s;
+        for (int k = 0; k < n; k++) s += M[j * n + k] * (R[((size_t)k * n + (lp - 1)) * W] * scale);
+        sc.trial[chg[j]] += s;
     }
 }
 
-__device__ void proposal_fast(const DevCfg &c, Rng &r, int w, double *trial)
+__device__ void proposal_fast(const DevCfg &c, Rng &r, int w, const Scratch &sc)
 {   // :283-289
-    const int k = cyc_next(c, r, w, 2, c.fast_n, c.all_n + c.slow_n);
-    block_proposal(c, r, w, c.proposer_for_index[c.slow_n + k - 1], trial);
+    const int k = cyc_next(c, r, w, 2, c.fast_n, c.all_n + c.slow_n, sc.itmp);
+    block_proposal(c, r, w, c.proposer_for_index[c.slow_n + k - 1], sc);
 }
 
-__device__ void proposal_slow(const DevCfg &c, Rng &r, int w, double *trial)
+__device__ void proposal_slow(const DevCfg &c, Rng &r, int w, const Scratch &sc)
 {   // :275-281
-    const int k = cyc_next(c, r, w, 1, c.slow_n, c.all_n);
-    block_proposal(c, r, w, c.proposer_for_index[k - 1], trial);
+    const int k = cyc_next(c, r, w, 1, c.slow_n, c.all_n, sc.itmp);
+    block_proposal(c, r, w, c.proposer_for_index[k - 1], sc);
 }
 
-__device__ void proposal(const DevCfg &c, Rng &r, int w, double *trial)
+__device__ void proposal(const DevCfg &c, Rng &r, int w, const Scratch &sc)
 {   // GetProposal :257-273
     int fix = c.fast_ix[w];
     if (fix != 0) {
-        proposal_fast(c, r, w, trial);
+        proposal_fast(c, r, w, sc);
         fix--;
-    } else if (cyc_next(c, r, w, 0, c.all_n, 0) > c.slow_n) {
-        proposal_fast(c, r, w, trial);
+    } else if (cyc_next(c, r, w, 0, c.all_n, 0, sc.itmp) > c.slow_n) {
+        proposal_fast(c, r, w, sc);
         fix = c.oversample_fast - 1;
     } else {
-        proposal_slow(c, r, w, trial);
+        proposal_slow(c, r, w, sc);
     }
     c.fast_ix[w] = fix;
 }
 
 // ------------------------------------------------------------ likelihood assembly
 
-__device__ double target_like(const DevCfg &c, int w, const double *Q)
+template <class Q> __device__ double target_like(const DevCfg &c, int w, const Q &q)
 {   // GetLogLike calclike.f90:136-151 with AddLikeTemp :82-94
     for (int i = 0; i < c.np; i++)
-        if (Q[i] > c.pmax[i] || Q[i] < c.pmin[i]) return LOGZERO;   // GetLogLikeBounds :97-109
+        if (q[i] > c.pmax[i] || q[i] < c.pmin[i]) return LOGZERO;   // GetLogLikeBounds :97-109
     double main = 0.0;
     if (c.test_like) {                                               // TestLikelihoodFunction :180-199
-        double X[MAXP];
         const int n = c.n_used;
-        for (int i = 0; i < n; i++) X[i] = Q[c.params_used[i]] - c.center[c.params_used[i]];
         double d = 0.0;
         for (int i = 0; i < n; i++) {
             double s = 0.0;
-            for (int j = 0; j < n; j++) s += c.test_covinv[i * n + j] * X[j];
-            d += X[i] * s;
+            for (int j = 0; j < n; j++)
+                s += c.test_covinv[i * n + j] * (q[c.params_used[j]] - c.center[c.params_used[j]]);
+            d += (q[c.params_used[i]] - c.center[c.params_used[i]]) * s;
         }
         main = d / 2.0;
     }
@@ -283,7 +296,7 @@ __device__ double target_like(const DevCfg &c, int w, const double *Q)
         double pri = 0.0;
         for (int i = 0; i < c.np; i++)
             if (c.prior_std[i] != 0.0) {
-                const double z = (Q[i] - c.prior_mean[i]) / c.prior_std[i];
+                const double z = (q[i] - c.prior_mean[i]) / c.prior_std[i];
                 pri += z * z;
             }
         like = like + (pri / 2.0) / c.temperature;
@@ -291,59 +304,91 @@ __device__ double target_like(const DevCfg &c, int w, const double *Q)
     return like;
 }
 
-__global__ void propose_kernel(DevCfg c, int fast_only)
+// One launch per Metropolis step boundary: accept/reject the pending trial
+// (MetropolisAccept MCMC.f90:119-131 + MoveDone :166-190), then propose the
+// next trial (GetProposal / GetProposalFast) and scatter its nuisance
+// parameters for the likelihood kernels.  One 64-lane wavefront per 64
+// walkers; the walker's RANMAR state (97 doubles) is staged in LDS with one
+// coalesced pass in and out, so the sequential RNG calls never wait on HBM.
+template <bool ACCEPT, bool PROPOSE>
+__global__ __launch_bounds__(64) void mh_kernel(DevCfg c, int fast_only, double *hist_row)
 {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= c.W) return;
-    double trial[MAXP];
-    for (int i = 0; i < c.np; i++) trial[i] = c.P[(size_t)i * c.W + w];     // Trial = CurParams
-    Rng r = load_rng(c, w);
-    if (fast_only) proposal_fast(c, r, w, trial);
-    else proposal(c, r, w, trial);
-    store_rng(c, w, r);
-    for (int i = 0; i < c.np; i++) c.trial[(size_t)i * c.W + w] = trial[i];
-}
-
-__global__ void accept_kernel(DevCfg c, double *hist_row /* [n_used][W] or null */)
-{   // TMetropolisSampler_GetNewSample tail (MCMC.f90:279-296) + MoveDone (:166-190)
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= c.W) return;
-    double trial[MAXP];
-    for (int i = 0; i < c.np; i++) trial[i] = c.trial[(size_t)i * c.W + w];
-    const double like = target_like(c, w, trial);
-    const double cur = c.cur_like[w];
-    bool acc = false;
-    if (like != LOGZERO) {                                          // MetropolisAccept :119-131
-        acc = cur > like;
-        if (!acc) {
-            Rng r = load_rng(c, w);
-            acc = (double)randexp1(r) > like - cur;
-            store_rng(c, w, r);
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int lane = threadIdx.x;
+    const int w = blockIdx.x * 64 + lane;
+    const bool act = w < c.W;
+    const int wc = act ? w : c.W - 1;
+    double *ul = lds;                           // [97][64]
+    double *tl = lds + 97 * 64;                 // [np][64]
+    double *vl = tl + c.np * 64;                // [max_blk][64]
+    int *il = reinterpret_cast<int *>(vl + c.max_blk * 64);   // [all_n][64]
+    for (int i = 0; i < 97; i++) ul[i * 64 + lane] = c.rng_u[(size_t)i * c.W + wc];
+    for (int i = 0; i < c.np; i++) tl[i * 64 + lane] = c.trial[(size_t)i * c.W + wc];
+    if (!act) return;
+    Rng r;
+    r.u = ul + lane;
+    r.W = 64;
+    r.c = c.rng_c[w];
+    r.i97 = c.rng_i97[w];
+    r.j97 = c.rng_j97[w];
+    r.iset = c.rng_iset[w];
+    r.gset = c.rng_gset[w];
+    Scratch sc{Col<double>{tl + lane, 64}, Col<double>{vl + lane, 64}, Col<int>{il + lane, 64}};
+    if (ACCEPT) {
+        const double like = target_like(c, w, sc.trial);
+        const double cur = c.cur_like[w];
+        bool acc = false;
+        if (like != LOGZERO) {
+            acc = cur > like;
+            if (!acc) acc = (double)randexp1(r) > like - cur;
         }
+        if (acc) {
+            if (c.mult[w] > 0) c.num_accept[w] += 1;
+            c.mult[w] = 1.0;
+            for (int i = 0; i < c.np; i++) c.P[(size_t)i * c.W + w] = sc.trial[i];
+            c.cur_like[w] = like;
+        } else {
+            c.mult[w] += 1.0;
+            for (int i = 0; i < c.np; i++) sc.trial[i] = c.P[(size_t)i * c.W + w];
+        }
+        if (hist_row)
+            for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = sc.trial[c.params_used[i]];
+    } else if (PROPOSE) {
+        for (int i = 0; i < c.np; i++) sc.trial[i] = c.P[(size_t)i * c.W + w];   // Trial = CurParams
     }
-    if (acc) {
-        if (c.mult[w] > 0) c.num_accept[w] += 1;
-        c.mult[w] = 1.0;
-        for (int i = 0; i < c.np; i++) c.P[(size_t)i * c.W + w] = trial[i];
-        c.cur_like[w] = like;
-    } else {
-        c.mult[w] += 1.0;
+    if (PROPOSE) {
+        if (fast_only) proposal_fast(c, r, w, sc);
+        else proposal(c, r, w, sc);
+        for (int i = 0; i < c.np; i++) c.trial[(size_t)i * c.W + w] = sc.trial[i];
+        for (int l = 0; l < c.n_like; l++)
+            for (int k = 0; k < c.like_nn[l]; k++)
+                c.like_nuis[l][(size_t)w * c.like_nn[l] + k] = sc.trial[c.like_nuis0[l] + k];
     }
-    if (hist_row)
-        for (int i = 0; i < c.n_used; i++)
-            hist_row[(size_t)i * c.W + w] = c.P[(size_t)c.params_used[i] * c.W + w];
+    c.rng_c[w] = r.c;
+    c.rng_i97[w] = r.i97;
+    c.rng_j97[w] = r.j97;
+    c.rng_iset[w] = r.iset;
+    c.rng_gset[w] = r.gset;
+    for (int i = 0; i < 97; i++) c.rng_u[(size_t)i * c.W + w] = ul[i * 64 + lane];
 }
 
 __global__ void start_kernel(DevCfg c)
 {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= c.W) return;
-    double q[MAXP];
-    for (int i = 0; i < c.np; i++) q[i] = c.trial[(size_t)i * c.W + w];
+    Col<double> q{c.trial + w, c.W};
     c.cur_like[w] = target_like(c, w, q);
     for (int i = 0; i < c.np; i++) c.P[(size_t)i * c.W + w] = q[i];
     c.mult[w] = 0.0;
     c.num_accept[w] = 0;
+}
+
+// scatter the nuisance slice of every walker's trial point: out[w][k] = trial[nuis0 + k][w]
+__global__ void gather_nuis(const double *trial, int W, int nuis0, int n_nuis, double *out)
+{
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    for (int k = 0; k < n_nuis; k++) out[(size_t)w * n_nuis + k] = trial[(size_t)(nuis0 + k) * W + w];
 }
 
 __global__ void hist_stats_kernel(const double *hist, int cap, int W, int n, int first, int last,
@@ -374,13 +419,9 @@ __global__ void hist_stats_kernel(const double *hist, int cap, int W, int n, int
     for (int i = 0; i < n * n; i++) C[i] /= cnt;
 }
 
-// gather the contiguous nuisance slice of every walker's trial point:
-// nuis[w][k] = trial[nuis0 + k][w]
-__global__ void gather_nuis(const double *trial, int W, int nuis0, int n_nuis, double *out)
-{
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= W) return;
-    for (int k = 0; k < n_nuis; k++) out[(size_t)w * n_nuis + k] = trial[(size_t)(nuis0 + k) * W + w];
+
+static size_t mh_lds_bytes(const cmbs *s) {
+    return (size_t)(97 + s->np + s->dc.max_blk) * 64 * 8 + (size_t)s->all_n * 64 * 4;
 }
 
 static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -519,6 +560,14 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     d.params_used = (const int *)(base + offs[12]);
     d.has_priors = has_pri;
     d.R_total = s->R_total;
+    d.max_blk = 1;
+    for (int bn : s->blk_n) d.max_blk = std::max(d.max_blk, bn);
+    {
+        const int lds = (int)mh_lds_bytes(s);
+        HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    }
 
     // ---- per-walker state
     offs.clear();
@@ -652,32 +701,48 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, int nuis_index0, const double
     if (!like) fail(CMBL_ERR_ARG, "null likelihood");
     const int nn = like->like->n_nuis;
     if (nuis_index0 < 1 || nuis_index0 - 1 + nn > s->np) fail(CMBL_ERR_ARG, "nuisance indices out of range");
+    if ((int)s->likes.size() >= MAXLIKE) fail(CMBL_ERR_ARG, "at most %d likelihoods per sampler", MAXLIKE);
+    const int li = (int)s->likes.size();
     s->likes.push_back({like, nuis_index0 - 1, dl, ld_field, ld_walker});
     s->like_terms.alloc(s->likes.size() * (size_t)s->W * 8);
     s->dc.n_like = (int)s->likes.size();
     s->dc.like_terms = s->like_terms.as<double>();
-    int maxn = 1;
+    s->nuis_bufs[li].alloc((size_t)std::max(nn, 1) * s->W * 8);
+    s->dc.like_nuis[li] = s->nuis_bufs[li].as<double>();
+    s->dc.like_nuis0[li] = nuis_index0 - 1;
+    s->dc.like_nn[li] = nn;
     size_t maxws = 0;
-    for (auto &l : s->likes) {
-        maxn = std::max(maxn, l.like->like->n_nuis);
-        maxws = std::max(maxws, l.like->like->workspace_size(s->W));
-    }
-    s->nuis_buf.alloc((size_t)maxn * s->W * 8);
+    for (auto &l : s->likes) maxws = std::max(maxws, l.like->like->workspace_size(s->W));
     s->ws.alloc(maxws);
 }
 
-static void eval_likes(cmbs *s, hipStream_t stream) {
+static void eval_likes(cmbs *s, hipStream_t stream, bool gather) {
     for (size_t i = 0; i < s->likes.size(); i++) {
         auto &l = s->likes[i];
         const int nn = l.like->like->n_nuis;
-        timed_launch("gather_nuis", stream, [&] {
+        double *nb = s->dc.like_nuis[i];
+        if (gather) {   // mh_kernel scatters the nuisance slices itself on every step
             hipLaunchKernelGGL(gather_nuis, dim3((s->W + 255) / 256), dim3(256), 0, stream, s->dc.trial, s->W,
-                               l.nuis0, nn, s->nuis_buf.as<double>());
-        });
-        HIP_CHECK(hipGetLastError());
-        l.like->like->loglike_batch(s->W, l.dl, l.ld_field, l.ld_walker, s->nuis_buf.as<double>(), nn,
+                               l.nuis0, nn, nb);
+            HIP_CHECK(hipGetLastError());
+        }
+        l.like->like->loglike_batch(s->W, l.dl, l.ld_field, l.ld_walker, nb, nn,
                                     s->like_terms.as<double>() + i * (size_t)s->W, s->ws.p, stream);
     }
+}
+
+static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, double *row, hipStream_t stream) {
+    const dim3 g((s->W + 63) / 64), b(64);
+    const size_t lds = mh_lds_bytes(s);
+    timed_launch("mh_kernel", stream, [&] {
+        if (accept && propose)
+            hipLaunchKernelGGL((mh_kernel<true, true>), g, b, lds, stream, s->dc, fast_only, row);
+        else if (accept)
+            hipLaunchKernelGGL((mh_kernel<true, false>), g, b, lds, stream, s->dc, fast_only, row);
+        else
+            hipLaunchKernelGGL((mh_kernel<false, true>), g, b, lds, stream, s->dc, fast_only, row);
+    });
+    HIP_CHECK(hipGetLastError());
 }
 
 void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream) {
@@ -686,7 +751,7 @@ void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream) {
     for (int w = 0; w < s->W; w++)
         for (int i = 0; i < s->np; i++) t[(size_t)i * s->W + w] = P0[(size_t)w * s->np + i];
     HIP_CHECK(hipMemcpyAsync(s->dc.trial, t.data(), t.size() * 8, hipMemcpyHostToDevice, stream));
-    eval_likes(s, stream);
+    eval_likes(s, stream, true);
     hipLaunchKernelGGL(start_kernel, dim3((s->W + 255) / 256), dim3(256), 0, stream, s->dc);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(stream));
@@ -696,18 +761,21 @@ void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream) {
 void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (!s->started) fail(CMBL_ERR_ARG, "cmbs_set_start must be called before cmbs_step");
     if (fast_only && s->fast_n == 0) fail(CMBL_ERR_ARG, "no fast parameters");
-    const dim3 g((s->W + 255) / 256), b(256);
-    for (int k = 0; k < n_steps; k++) {
-        timed_launch("propose_kernel", stream,
-                     [&] { hipLaunchKernelGGL(propose_kernel, g, b, 0, stream, s->dc, fast_only); });
-        HIP_CHECK(hipGetLastError());
-        eval_likes(s, stream);
-        double *row = nullptr;
-        if (s->hist_cap > 0) row = s->hist.as<double>() + (size_t)(s->hist_count % s->hist_cap) * s->n_used * s->W;
-        timed_launch("accept_kernel", stream, [&] { hipLaunchKernelGGL(accept_kernel, g, b, 0, stream, s->dc, row); });
-        HIP_CHECK(hipGetLastError());
-        if (s->hist_cap > 0) s->hist_count++;
+    if (n_steps <= 0) return;
+    auto next_row = [&]() -> double * {
+        if (s->hist_cap == 0) return nullptr;
+        double *row = s->hist.as<double>() + (size_t)(s->hist_count % s->hist_cap) * s->n_used * s->W;
+        s->hist_count++;
+        return row;
+    };
+    // propose(1) | likes | accept(1)+propose(2) | likes | ... | likes | accept(n)
+    launch_mh(s, false, true, fast_only, nullptr, stream);
+    eval_likes(s, stream, false);
+    for (int k = 1; k < n_steps; k++) {
+        launch_mh(s, true, true, fast_only, next_row(), stream);
+        eval_likes(s, stream, false);
     }
+    launch_mh(s, true, false, fast_only, next_row(), stream);
 }
 
 void sampler_enable_history(cmbs *s, int capacity) {
