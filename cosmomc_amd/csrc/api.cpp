@@ -14,6 +14,7 @@ void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream);
 void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream);
 void sampler_enable_history(cmbs *s, int capacity);
 void sampler_history_stats(cmbs *s, int first, int last, double *means, double *covs, hipStream_t stream);
+void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, int *num_accept);
 void launch_clik_to_dl(const double *clp, long long ld, const int *lm, double *dl, long long ld_field,
                        long long ld_walker, int lmax_out, int W, hipStream_t stream);
 }  // namespace cmamd
@@ -239,28 +240,18 @@ int cmbs_history_count(const cmbs_t *s) { return s ? s->hist_count : 0; }
 
 int cmbs_state(cmbs_t *s, double **P, double **cur_like, double **mult, int **num_accept) {
     if (!s) return CMBL_ERR_ARG;
-    if (P) *P = s->dc.P;
-    if (cur_like) *cur_like = s->dc.cur_like;
-    if (mult) *mult = s->dc.mult;
-    if (num_accept) *num_accept = s->dc.num_accept;
+    const auto &R = s->dc.rows;
+    const size_t W = s->W;
+    if (P) *P = s->dc.sd + R.P * W;
+    if (cur_like) *cur_like = s->dc.sd + R.L * W;
+    if (mult) *mult = s->dc.sd + R.M * W;
+    if (num_accept) *num_accept = s->dc.si + R.NACC * W;
     return CMBL_OK;
 }
 
 int cmbs_get_state_host(cmbs_t *s, double *P, double *cur_like, double *mult, int *num_accept) {
     if (!s) return CMBL_ERR_ARG;
-    return guarded(&s->last_error, [&] {
-        HIP_CHECK(hipDeviceSynchronize());
-        const int W = s->W, np = s->np;
-        if (P) {
-            std::vector<double> t((size_t)np * W);
-            HIP_CHECK(hipMemcpy(t.data(), s->dc.P, t.size() * 8, hipMemcpyDeviceToHost));
-            for (int w = 0; w < W; w++)
-                for (int i = 0; i < np; i++) P[(size_t)w * np + i] = t[(size_t)i * W + w];
-        }
-        if (cur_like) HIP_CHECK(hipMemcpy(cur_like, s->dc.cur_like, (size_t)W * 8, hipMemcpyDeviceToHost));
-        if (mult) HIP_CHECK(hipMemcpy(mult, s->dc.mult, (size_t)W * 8, hipMemcpyDeviceToHost));
-        if (num_accept) HIP_CHECK(hipMemcpy(num_accept, s->dc.num_accept, (size_t)W * 4, hipMemcpyDeviceToHost));
-    });
+    return guarded(&s->last_error, [&] { cmamd::sampler_get_state_host(s, P, cur_like, mult, num_accept); });
 }
 
 }  // extern "C"

@@ -5,42 +5,52 @@
 
 namespace cmamd {
 
-struct DevCfg {
-    int W, np, n_used, nblocks, slow_n, fast_n, all_n, oversample_fast;
-    double propose_scale, temperature;
-    // shared proposer tables
-    const int *blk_n, *blk_nchanged, *blk_changed_off, *blk_map_off, *blk_R_off;
-    const int *changed;             // 0-based parameter indices
-    const double *mapping;          // per block nchanged x n, row-major
-    const int *proposer_for_index;  // all_n, 1-based block
-    const double *pmin, *pmax, *prior_mean, *prior_std;
-    int has_priors;
-    // test gaussian
-    int test_like;
-    const int *params_used;         // n_used, 0-based
-    const double *test_covinv;      // n_used^2
-    const double *center;           // np
-    // per-walker state (SoA)
-    double *rng_u;                  // [97][W]
-    double *rng_c, *rng_gset;       // [W]
-    int *rng_i97, *rng_j97, *rng_iset;
-    int R_total;                    // sum n_b^2
-    double *R;                      // [R_total][W]
-    int *blk_loopix;                // [nblocks][W]
-    int *cyc;                       // [all_n + slow_n + fast_n][W] index permutations
-    int *cyc_loopix;                // [3][W]: all, slow, fast
-    int *fast_ix;                   // [W]
-    double *P, *trial;              // [np][W]
-    double *cur_like, *mult;        // [W]
-    int *num_accept;                // [W]
-    int n_like;
-    const double *like_terms;       // [n_like][W] -lnL of each likelihood at trial
-    int like_nuis0[8], like_nn[8];  // nuisance slice of each likelihood (0-based start, count)
-    double *like_nuis[8];           // [W][like_nn] DataParams buffers written by mh_kernel
-    int max_blk;                    // largest proposal block
+static constexpr int MAXLIKE = 8;
+
+// Per-walker state is two row-major SoA arrays in HBM, sd[ND][W] (doubles)
+// and si[NI][W] (ints): row r of walker w at sd[r*W + w].  mh_kernel copies
+// a 64-walker column block of every row into LDS with independent coalesced
+// loads, runs the sequential chain logic out of LDS, and writes it back.
+struct Rows {
+    // double rows
+    int U = 0;          // 97 rows: RANMAR u(1:97)
+    int C = 97;         // RANMAR c
+    int G = 98;         // Gaussian1 saved deviate gset
+    int R = 99;         // R_total rows: per-block random rotations (row j col i of block b at R + off_b + j*n+i)
+    int P, T, L, M;     // np rows current point, np rows trial, cur_like, mult
+    int ND;
+    // int rows
+    int I97 = 0, J97 = 1, ISET = 2, FASTIX = 3, NACC = 4;
+    int CYCLP = 5;      // 3 rows: All, Slow, Fast CyclicIndexRandomizer%loopix
+    int BLKLP = 8;      // nblocks rows: RandDirectionProposer%loopix
+    int CYC;            // all_n + slow_n + fast_n rows: the three index permutations
+    int NI;
 };
 
-static constexpr int MAXLIKE = 8;
+// Shared read-only tables (copied to LDS by every mh_kernel block).
+struct TabLayout {
+    // int table offsets (ints)
+    int blk_n, blk_nchanged, blk_changed_off, blk_map_off, blk_R_off, changed, pfi, params_used, n_int;
+    // double table offsets (doubles)
+    int mapping, pmin, pmax, pmean, pstd, covinv, center, n_dbl;
+};
+
+struct DevCfg {
+    int W, np, n_used, nblocks, slow_n, fast_n, all_n, oversample_fast, max_blk, R_total;
+    double propose_scale, temperature;
+    int has_priors, test_like;
+    Rows rows;
+    TabLayout tl;
+    const int *tab_i;       // [tl.n_int]
+    const double *tab_d;    // [tl.n_dbl]
+    double *sd;             // [ND][W]
+    int *si;                // [NI][W]
+    int stage_R;            // R rows staged in LDS (else read in place, stride W)
+    int n_like;
+    const double *like_terms;       // [n_like][W] -lnL of each likelihood at the trial point
+    int like_nuis0[MAXLIKE], like_nn[MAXLIKE];
+    double *like_nuis[MAXLIKE];     // [W][like_nn] DataParams buffers written by mh_kernel
+};
 
 struct LikeSlot {
     cmbl_t *like;
@@ -54,18 +64,18 @@ struct LikeSlot {
 struct cmbs {
     cmamd::DevCfg dc{};
     int W = 0, np = 0, n_used = 0;
-    std::vector<int> params_used, blk_n, blk_params;
-    int slow_block_max = 0;
+    std::vector<int> params_used;
     std::string last_error;
-    // device buffers
-    cmamd::DevBuf tables, state, covinv, center, like_terms, ws, hist;
+    cmamd::DevBuf tab_i, tab_d, sd, si, like_terms, ws, hist;
     cmamd::DevBuf nuis_bufs[cmamd::MAXLIKE];
+    std::vector<int> h_tab_i;
+    std::vector<double> h_tab_d;
     std::vector<cmamd::LikeSlot> likes;
     // host copies of the proposer structure
-    std::vector<int> indices, proposer_for_index, blk_start, blk_nchanged, used_params_changed_all;
+    std::vector<int> indices, proposer_for_index, blk_start, blk_n, blk_nchanged, used_params_changed_all;
     std::vector<int> blk_changed_off, blk_map_off, blk_R_off, changed;
     int all_n = 0, slow_n = 0, fast_n = 0, nblocks = 0, R_total = 0, map_total = 0;
+    size_t mh_lds = 0;
     int hist_cap = 0, hist_count = 0;
     bool started = false;
 };
-

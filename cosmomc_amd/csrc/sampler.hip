@@ -1,5 +1,5 @@
 // Batched Metropolis sampler: W independent CosmoMC chains, one per walker
-// (one GPU thread per walker for the sequential per-chain logic), with the
+// (one GPU lane per walker for the sequential per-chain logic), with the
 // likelihoods evaluated as batched kernels over all walkers in between.
 //
 // Per-walker semantics follow the reference exactly, including the random
@@ -11,8 +11,12 @@
 //   GetLogLike = bounds + like/T + priors/T                        calclike.f90:82-151
 //   MetropolisAccept, MoveDone multiplicity                        MCMC.f90:119-190
 //
-// Walker state lives in HBM as structure-of-arrays ([field][walker]) so the
-// per-thread state accesses of a wavefront fall on consecutive addresses.
+// The chain logic is a long chain of dependent state reads (RNG index ->
+// RNG table -> block cycle -> rotation -> mapping ...).  Served from HBM each
+// would cost a memory round trip; instead mh_kernel stages the whole
+// per-walker state (sampler.h Rows) and the shared tables into LDS with
+// independent coalesced loads, runs the chain out of LDS and writes back.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -21,26 +25,31 @@
 namespace cmamd {
 
 static constexpr double LOGZERO = CMBL_LOGZERO;
-static constexpr int MAXP = 64;        // max parameters per chain handled in registers/stack
+static constexpr int MAXP = 64;        // max parameters per chain
 static constexpr int MAXBLK = 32;      // max block size
+static constexpr int NB = 64;          // walkers per mh_kernel block (one wavefront)
+
+// strided per-walker column view (LDS: stride NB; HBM: stride W)
+template <class T> struct Col {
+    T *p;
+    int s;
+    __device__ T &operator[](int i) const { return p[(size_t)i * s]; }
+};
 
 // ------------------------------------------------------------ RNG (RandUtils.f90)
 
 struct Rng {
-    double *u;      // column w of [97][W]
-    int W;
+    Col<double> u;  // u(1:97)
     double c;
     int i97, j97, iset;
     double gset;
 };
 
-__device__ inline double U(const Rng &r, int i) { return r.u[(size_t)(i - 1) * r.W]; }
-
 __device__ double ranmar(Rng &r)
 {   // RandUtils.f90:350-374
-    double uni = U(r, r.i97) - U(r, r.j97);
+    double uni = r.u[r.i97 - 1] - r.u[r.j97 - 1];
     if (uni < 0.0) uni += 1.0;
-    r.u[(size_t)(r.i97 - 1) * r.W] = uni;
+    r.u[r.i97 - 1] = uni;
     if (--r.i97 == 0) r.i97 = 97;
     if (--r.j97 == 0) r.j97 = 97;
     const double cd = 7654321.0 / 16777216.0, cm = 16777213.0 / 16777216.0;
@@ -70,7 +79,7 @@ __device__ double gaussian1(Rng &r)
 }
 
 __device__ float randexp1(Rng &r)
-{   // RandUtils.f90:189-233, REAL(4) arithmetic (no contraction: see -ffp-contract=off)
+{   // RandUtils.f90:189-233, REAL(4) arithmetic (built with -ffp-contract=off)
     const float alog2 = 0.6931471805599453f, a = 5.7133631526454228f, b = 3.4142135623730950f;
     const float c = -1.6734053240284925f, p = 0.9802581434685472f, aa = 5.6005707569738080f;
     const float bb = 3.3468106480569850f, hh = 0.0026106723602095f, dd = 0.0857864376269050f;
@@ -93,32 +102,11 @@ __device__ float randexp1(Rng &r)
     }
 }
 
-__device__ Rng load_rng(const DevCfg &c, int w)
-{
-    Rng r;
-    r.u = c.rng_u + w;
-    r.W = c.W;
-    r.c = c.rng_c[w];
-    r.i97 = c.rng_i97[w];
-    r.j97 = c.rng_j97[w];
-    r.iset = c.rng_iset[w];
-    r.gset = c.rng_gset[w];
-    return r;
-}
-
-__device__ void store_rng(const DevCfg &c, int w, const Rng &r)
-{
-    c.rng_c[w] = r.c;
-    c.rng_i97[w] = r.i97;
-    c.rng_j97[w] = r.j97;
-    c.rng_iset[w] = r.iset;
-    c.rng_gset[w] = r.gset;
-}
-
 __global__ void rng_init_kernel(DevCfg c, const int *ij, const int *kl)
 {   // RMARIN, RandUtils.f90:286-348
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= c.W) return;
+    const size_t W = c.W;
     int i = (ij[w] / 177) % 177 + 2, j = ij[w] % 177 + 2, k = (kl[w] / 169) % 178 + 1, l = kl[w] % 169;
     for (int ii = 0; ii < 97; ii++) {
         double s = 0.0, t = 0.5;
@@ -131,149 +119,151 @@ __global__ void rng_init_kernel(DevCfg c, const int *ij, const int *kl)
             if ((l * m) % 64 >= 32) s += t;
             t *= 0.5;
         }
-        c.rng_u[(size_t)ii * c.W + w] = s;
+        c.sd[(c.rows.U + ii) * W + w] = s;
     }
-    c.rng_c[w] = 362436.0 / 16777216.0;
-    c.rng_i97[w] = 97;
-    c.rng_j97[w] = 33;
-    c.rng_iset[w] = 0;
-    c.rng_gset[w] = 0.0;
+    c.sd[c.rows.C * W + w] = 362436.0 / 16777216.0;
+    c.sd[c.rows.G * W + w] = 0.0;
+    c.si[c.rows.I97 * W + w] = 97;
+    c.si[c.rows.J97 * W + w] = 33;
+    c.si[c.rows.ISET * W + w] = 0;
 }
 
-// ------------------------------------------------------------ proposer (propose.f90)
+// ------------------------------------------------------------ per-walker view
 
-// Per-walker arrays that need dynamic indexing live in LDS, one column per lane.
-template <class T> struct Col {
-    T *p;
-    int s;   // stride between consecutive elements (the block size)
-    __device__ T &operator[](int i) const { return p[i * s]; }
+struct Tabs {   // shared tables (LDS copies)
+    const int *blk_n, *blk_nchanged, *blk_changed_off, *blk_map_off, *blk_R_off, *changed, *pfi, *params_used;
+    const double *mapping, *pmin, *pmax, *pmean, *pstd, *covinv, *center;
 };
 
-__device__ int cyc_next(const DevCfg &c, Rng &r, int w, int which, int n, int base, Col<int> tmp)
+__device__ Tabs make_tabs(const DevCfg &c, const int *ti, const double *td)
+{
+    const TabLayout &l = c.tl;
+    return Tabs{ti + l.blk_n, ti + l.blk_nchanged, ti + l.blk_changed_off, ti + l.blk_map_off, ti + l.blk_R_off,
+                ti + l.changed, ti + l.pfi, ti + l.params_used, td + l.mapping, td + l.pmin, td + l.pmax,
+                td + l.pmean, td + l.pstd, td + l.covinv, td + l.center};
+}
+
+struct Walker {
+    Rng r;
+    Col<double> R, P, trial, vec;
+    Col<int> cyc, cyclp, blklp, itmp;
+    int fast_ix;
+};
+
+__device__ int cyc_next(Walker &k, int which, int n, int base)
 {   // CyclicIndexRandomizer%Next, propose.f90:75-86 (RandIndices RandUtils.f90:93-108)
-    int *loopix = c.cyc_loopix + (size_t)which * c.W + w;
-    const int lp = *loopix % n + 1;
-    *loopix = lp;
-    int *idx = c.cyc + (size_t)base * c.W + w;    // idx[k*W]
+    const int lp = k.cyclp[which] % n + 1;
+    k.cyclp[which] = lp;
     if (lp == 1) {
         if (n == 1) {
-            (void)ranmar(r);                        // ix = int(ranmar()*1)+1 = 1
-            idx[0] = 1;
+            (void)ranmar(k.r);                      // ix = int(ranmar()*1)+1 = 1
+            k.cyc[base] = 1;
         } else {
-            for (int i = 0; i < n; i++) tmp[i] = i + 1;
+            for (int i = 0; i < n; i++) k.itmp[i] = i + 1;
             for (int i = 1; i <= n; i++) {
-                const int ix = (int)(ranmar(r) * (n + 1 - i)) + 1;
-                idx[(size_t)(i - 1) * c.W] = tmp[ix - 1];
-                tmp[ix - 1] = tmp[n + 1 - i - 1];
+                const int ix = (int)(ranmar(k.r) * (n + 1 - i)) + 1;
+                k.cyc[base + i - 1] = k.itmp[ix - 1];
+                k.itmp[ix - 1] = k.itmp[n + 1 - i - 1];
             }
         }
     }
-    return idx[(size_t)(lp - 1) * c.W];
+    return k.cyc[base + lp - 1];
 }
 
-__device__ void rot_matrix(const DevCfg &c, Rng &r, double *R, int n, Col<double> vec)
+__device__ void rot_matrix(Walker &k, int off, int n)
 {   // RotMatrix propose.f90:88-102 -> RandRotationD RandUtils.f90:133-153
-    // R element (j,i) (row j) at R[(j*n+i)*W]
-    const size_t W = c.W;
+    // element (j,i) (row j) of this block's R at R[off + j*n + i]
     if (n > 1) {
         for (int j = 0; j < n; j++) {
             double norm;
             for (;;) {
-                for (int i = 0; i < n; i++) vec[i] = gaussian1(r);
+                for (int i = 0; i < n; i++) k.vec[i] = gaussian1(k.r);
                 for (int i = 0; i < j; i++) {
                     double s = 0.0;
-                    for (int k = 0; k < n; k++) s += vec[k] * R[(i * n + k) * W];
-                    for (int k = 0; k < n; k++) vec[k] = vec[k] - s * R[(i * n + k) * W];
+                    for (int q = 0; q < n; q++) s += k.vec[q] * k.R[off + i * n + q];
+                    for (int q = 0; q < n; q++) k.vec[q] = k.vec[q] - s * k.R[off + i * n + q];
                 }
                 norm = 0.0;
-                for (int k = 0; k < n; k++) norm += vec[k] * vec[k];
+                for (int q = 0; q < n; q++) norm += k.vec[q] * k.vec[q];
                 if (norm > 1e-3) break;
             }
             const double sn = sqrt(norm);
-            for (int k = 0; k < n; k++) R[(j * n + k) * W] = vec[k] / sn;
+            for (int q = 0; q < n; q++) k.R[off + j * n + q] = k.vec[q] / sn;
         }
     } else {
-        for (int i = 0; i < n * n; i++) R[i * W] = 0.0;
-        for (int i = 0; i < n; i++) R[(i * n + i) * W] = (ranmar(r) - 0.5) >= 0.0 ? 1.0 : -1.0;
+        for (int i = 0; i < n * n; i++) k.R[off + i] = 0.0;
+        for (int i = 0; i < n; i++) k.R[off + i * n + i] = (ranmar(k.r) - 0.5) >= 0.0 ? 1.0 : -1.0;
     }
 }
 
-struct Scratch {
-    Col<double> trial, vec;
-    Col<int> itmp;
-};
-
-__device__ void block_proposal(const DevCfg &c, Rng &r, int w, int bi /*1-based*/, const Scratch &sc)
+__device__ void block_proposal(const DevCfg &c, const Tabs &t, Walker &k, int bi /*1-based*/)
 {   // GetBlockProposal :247-254 -> ProposeVec :105-120 -> Propose_r :122-139 -> UpdateParams :142-149
     const int b = bi - 1;
-    const int n = c.blk_n[b];
-    const size_t W = c.W;
-    double *R = c.R + (size_t)c.blk_R_off[b] * W + w;
-    int *loopix = c.blk_loopix + (size_t)b * W + w;
-    int lp = *loopix;
+    const int n = t.blk_n[b];
+    const int off = t.blk_R_off[b];
+    int lp = k.blklp[b];
     if (lp % n == 0) {
-        rot_matrix(c, r, R, n, sc.vec);
+        rot_matrix(k, off, n);
         lp = 0;
     }
     lp++;
-    *loopix = lp;
+    k.blklp[b] = lp;
     double rf;
-    if (ranmar(r) < 0.33) {
-        rf = (double)randexp1(r);
+    if (ranmar(k.r) < 0.33) {
+        rf = (double)randexp1(k.r);
     } else {
         const int m = n < 2 ? n : 2;
         rf = 0.0;
         for (int i = 0; i < m; i++) {
-            const double g = gaussian1(r);
+            const double g = gaussian1(k.r);
             rf += g * g;
         }
         rf = sqrt(rf / m);
     }
     const double scale = rf * c.propose_scale;
-    // vec(k) = R(k, loopix) * (r * wid);  P(changed) += mapping_matrix . vec
-    const int nc = c.blk_nchanged[b];
-    const double *M = c.mapping + c.blk_map_off[b];
-    const int *chg = c.changed + c.blk_changed_off[b];
+    // vec(q) = R(q, loopix) * (r * wid);  P(changed) += mapping_matrix . vec
+    const int nc = t.blk_nchanged[b];
+    const double *M = t.mapping + t.blk_map_off[b];
+    const int *chg = t.changed + t.blk_changed_off[b];
     for (int j = 0; j < nc; j++) {
         double s = 0.0;
-        for (int k = 0; k < n; k++) s += M[j * n + k] * (R[((size_t)k * n + (lp - 1)) * W] * scale);
-        sc.trial[chg[j]] += s;
+        for (int q = 0; q < n; q++) s += M[j * n + q] * (k.R[off + q * n + (lp - 1)] * scale);
+        k.trial[chg[j]] += s;
     }
 }
 
-__device__ void proposal_fast(const DevCfg &c, Rng &r, int w, const Scratch &sc)
+__device__ void proposal_fast(const DevCfg &c, const Tabs &t, Walker &k)
 {   // :283-289
-    const int k = cyc_next(c, r, w, 2, c.fast_n, c.all_n + c.slow_n, sc.itmp);
-    block_proposal(c, r, w, c.proposer_for_index[c.slow_n + k - 1], sc);
+    const int q = cyc_next(k, 2, c.fast_n, c.all_n + c.slow_n);
+    block_proposal(c, t, k, t.pfi[c.slow_n + q - 1]);
 }
 
-__device__ void proposal_slow(const DevCfg &c, Rng &r, int w, const Scratch &sc)
+__device__ void proposal_slow(const DevCfg &c, const Tabs &t, Walker &k)
 {   // :275-281
-    const int k = cyc_next(c, r, w, 1, c.slow_n, c.all_n, sc.itmp);
-    block_proposal(c, r, w, c.proposer_for_index[k - 1], sc);
+    const int q = cyc_next(k, 1, c.slow_n, c.all_n);
+    block_proposal(c, t, k, t.pfi[q - 1]);
 }
 
-__device__ void proposal(const DevCfg &c, Rng &r, int w, const Scratch &sc)
+__device__ void proposal(const DevCfg &c, const Tabs &t, Walker &k)
 {   // GetProposal :257-273
-    int fix = c.fast_ix[w];
-    if (fix != 0) {
-        proposal_fast(c, r, w, sc);
-        fix--;
-    } else if (cyc_next(c, r, w, 0, c.all_n, 0, sc.itmp) > c.slow_n) {
-        proposal_fast(c, r, w, sc);
-        fix = c.oversample_fast - 1;
+    if (k.fast_ix != 0) {
+        proposal_fast(c, t, k);
+        k.fast_ix--;
+    } else if (cyc_next(k, 0, c.all_n, 0) > c.slow_n) {
+        proposal_fast(c, t, k);
+        k.fast_ix = c.oversample_fast - 1;
     } else {
-        proposal_slow(c, r, w, sc);
+        proposal_slow(c, t, k);
     }
-    c.fast_ix[w] = fix;
 }
 
-// ------------------------------------------------------------ likelihood assembly
-
-template <class Q> __device__ double target_like(const DevCfg &c, int w, const Q &q)
-{   // GetLogLike calclike.f90:136-151 with AddLikeTemp :82-94
+// GetLogLike calclike.f90:136-151 with AddLikeTemp :82-94; likes[l] are the
+// data-likelihood terms at q (LogLikeWithTheorySet :374-387)
+template <class Q, class L>
+__device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const L &likes)
+{
     for (int i = 0; i < c.np; i++)
-        if (q[i] > c.pmax[i] || q[i] < c.pmin[i]) return LOGZERO;   // GetLogLikeBounds :97-109
+        if (q[i] > t.pmax[i] || q[i] < t.pmin[i]) return LOGZERO;   // GetLogLikeBounds :97-109
     double main = 0.0;
     if (c.test_like) {                                               // TestLikelihoodFunction :180-199
         const int n = c.n_used;
@@ -281,13 +271,13 @@ template <class Q> __device__ double target_like(const DevCfg &c, int w, const Q
         for (int i = 0; i < n; i++) {
             double s = 0.0;
             for (int j = 0; j < n; j++)
-                s += c.test_covinv[i * n + j] * (q[c.params_used[j]] - c.center[c.params_used[j]]);
-            d += (q[c.params_used[i]] - c.center[c.params_used[i]]) * s;
+                s += t.covinv[i * n + j] * (q[t.params_used[j]] - t.center[t.params_used[j]]);
+            d += (q[t.params_used[i]] - t.center[t.params_used[i]]) * s;
         }
         main = d / 2.0;
     }
-    for (int l = 0; l < c.n_like; l++) {                             // LogLikeWithTheorySet :374-387
-        const double v = c.like_terms[(size_t)l * c.W + w];
+    for (int l = 0; l < c.n_like; l++) {
+        const double v = likes[l];
         if (v == LOGZERO) return LOGZERO;
         main += v;
     }
@@ -295,8 +285,8 @@ template <class Q> __device__ double target_like(const DevCfg &c, int w, const Q
     if (c.has_priors) {                                              // GetLogPriors :111-134
         double pri = 0.0;
         for (int i = 0; i < c.np; i++)
-            if (c.prior_std[i] != 0.0) {
-                const double z = (q[i] - c.prior_mean[i]) / c.prior_std[i];
+            if (t.pstd[i] != 0.0) {
+                const double z = (q[i] - t.pmean[i]) / t.pstd[i];
                 pri += z * z;
             }
         like = like + (pri / 2.0) / c.temperature;
@@ -304,86 +294,148 @@ template <class Q> __device__ double target_like(const DevCfg &c, int w, const Q
     return like;
 }
 
+// Copy rows [r0, r1) of a [rows][W] HBM array into an LDS [rows][NB] column
+// block, 8 independent loads in flight per lane before their LDS writes.
+template <class T>
+__device__ void stage_in(T *dst, int dst_r0, const T *src, int r0, int r1, size_t W, int wc, int lane)
+{
+    int r = r0;
+    for (; r + 8 <= r1; r += 8) {
+        T v[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) v[q] = src[(size_t)(r + q) * W + wc];
+#pragma unroll
+        for (int q = 0; q < 8; q++) dst[(size_t)(dst_r0 + r - r0 + q) * NB + lane] = v[q];
+    }
+    for (; r < r1; r++) dst[(size_t)(dst_r0 + r - r0) * NB + lane] = src[(size_t)r * W + wc];
+}
+
+template <class T>
+__device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size_t W, int w, int lane)
+{
+    for (int r = r0; r < r1; r++) dst[(size_t)r * W + w] = src[(size_t)(src_r0 + r - r0) * NB + lane];
+}
+
 // One launch per Metropolis step boundary: accept/reject the pending trial
 // (MetropolisAccept MCMC.f90:119-131 + MoveDone :166-190), then propose the
 // next trial (GetProposal / GetProposalFast) and scatter its nuisance
-// parameters for the likelihood kernels.  One 64-lane wavefront per 64
-// walkers; the walker's RANMAR state (97 doubles) is staged in LDS with one
-// coalesced pass in and out, so the sequential RNG calls never wait on HBM.
+// parameters for the likelihood kernels.  One wavefront per 64 walkers.
 template <bool ACCEPT, bool PROPOSE>
-__global__ __launch_bounds__(64) void mh_kernel(DevCfg c, int fast_only, double *hist_row)
+__global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double *hist_row)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
+    const Rows &R = c.rows;
     const int lane = threadIdx.x;
-    const int w = blockIdx.x * 64 + lane;
+    const int w = blockIdx.x * NB + lane;
     const bool act = w < c.W;
     const int wc = act ? w : c.W - 1;
-    double *ul = lds;                           // [97][64]
-    double *tl = lds + 97 * 64;                 // [np][64]
-    double *vl = tl + c.np * 64;                // [max_blk][64]
-    int *il = reinterpret_cast<int *>(vl + c.max_blk * 64);   // [all_n][64]
-    for (int i = 0; i < 97; i++) ul[i * 64 + lane] = c.rng_u[(size_t)i * c.W + wc];
-    for (int i = 0; i < c.np; i++) tl[i * 64 + lane] = c.trial[(size_t)i * c.W + wc];
+    const size_t W = c.W;
+    // LDS carve: state doubles | like terms | vec scratch | tables(d) | state ints | itmp | tables(i)
+    const int nd_st = c.stage_R ? R.ND : R.ND - c.R_total;      // staged double rows
+    double *sd = lds;                                            // [nd_st][NB]
+    double *lk = sd + (size_t)nd_st * NB;                        // [n_like][NB]
+    double *vc = lk + (size_t)c.n_like * NB;                     // [max_blk][NB]
+    double *td = vc + (size_t)c.max_blk * NB;                    // [n_dbl]
+    int *si = reinterpret_cast<int *>(td + c.tl.n_dbl);          // [NI][NB]
+    int *it = si + (size_t)R.NI * NB;                            // [all_n][NB]
+    int *ti = it + (size_t)c.all_n * NB;                         // [n_int]
+    const bool skipR = !c.stage_R;
+    // staged double row index of global row r (rotation rows dropped when not staged)
+#define SROW(r) ((skipR && (r) >= R.R) ? (r) - c.R_total : (r))
+
+    for (int i = lane; i < c.tl.n_dbl; i += NB) td[i] = c.tab_d[i];
+    for (int i = lane; i < c.tl.n_int; i += NB) ti[i] = c.tab_i[i];
+    const int rEnd = R.R + c.R_total;
+    if (skipR) {
+        stage_in(sd, 0, c.sd, 0, R.R, W, wc, lane);
+        stage_in(sd, R.R, c.sd, rEnd, R.ND, W, wc, lane);
+    } else {
+        stage_in(sd, 0, c.sd, 0, R.ND, W, wc, lane);
+    }
+    stage_in(si, 0, c.si, 0, R.NI, W, wc, lane);
+    stage_in(lk, 0, c.like_terms, 0, c.n_like, W, wc, lane);
+    __syncthreads();                 // tables are shared across lanes
     if (!act) return;
-    Rng r;
-    r.u = ul + lane;
-    r.W = 64;
-    r.c = c.rng_c[w];
-    r.i97 = c.rng_i97[w];
-    r.j97 = c.rng_j97[w];
-    r.iset = c.rng_iset[w];
-    r.gset = c.rng_gset[w];
-    Scratch sc{Col<double>{tl + lane, 64}, Col<double>{vl + lane, 64}, Col<int>{il + lane, 64}};
+
+    const Tabs t = make_tabs(c, ti, td);
+    Walker k;
+    k.r.u = Col<double>{sd + (size_t)R.U * NB + lane, NB};
+    k.r.c = sd[(size_t)R.C * NB + lane];
+    k.r.gset = sd[(size_t)R.G * NB + lane];
+    k.r.i97 = si[(size_t)R.I97 * NB + lane];
+    k.r.j97 = si[(size_t)R.J97 * NB + lane];
+    k.r.iset = si[(size_t)R.ISET * NB + lane];
+    k.R = c.stage_R ? Col<double>{sd + (size_t)R.R * NB + lane, NB} : Col<double>{c.sd + (size_t)R.R * W + w, c.W};
+    k.P = Col<double>{sd + (size_t)SROW(R.P) * NB + lane, NB};
+    k.trial = Col<double>{sd + (size_t)SROW(R.T) * NB + lane, NB};
+    k.vec = Col<double>{vc + lane, NB};
+    k.cyc = Col<int>{si + (size_t)R.CYC * NB + lane, NB};
+    k.cyclp = Col<int>{si + (size_t)R.CYCLP * NB + lane, NB};
+    k.blklp = Col<int>{si + (size_t)R.BLKLP * NB + lane, NB};
+    k.itmp = Col<int>{it + lane, NB};
+    k.fast_ix = si[(size_t)R.FASTIX * NB + lane];
+    double &cur = sd[(size_t)SROW(R.L) * NB + lane];
+    double &mult = sd[(size_t)SROW(R.M) * NB + lane];
+    int &nacc = si[(size_t)R.NACC * NB + lane];
+
     if (ACCEPT) {
-        const double like = target_like(c, w, sc.trial);
-        const double cur = c.cur_like[w];
+        const double like = target_like(c, t, k.trial, Col<double>{lk + lane, NB});
         bool acc = false;
         if (like != LOGZERO) {
             acc = cur > like;
-            if (!acc) acc = (double)randexp1(r) > like - cur;
+            if (!acc) acc = (double)randexp1(k.r) > like - cur;
         }
         if (acc) {
-            if (c.mult[w] > 0) c.num_accept[w] += 1;
-            c.mult[w] = 1.0;
-            for (int i = 0; i < c.np; i++) c.P[(size_t)i * c.W + w] = sc.trial[i];
-            c.cur_like[w] = like;
+            if (mult > 0) nacc += 1;
+            mult = 1.0;
+            for (int i = 0; i < c.np; i++) k.P[i] = k.trial[i];
+            cur = like;
         } else {
-            c.mult[w] += 1.0;
-            for (int i = 0; i < c.np; i++) sc.trial[i] = c.P[(size_t)i * c.W + w];
+            mult += 1.0;
         }
         if (hist_row)
-            for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = sc.trial[c.params_used[i]];
-    } else if (PROPOSE) {
-        for (int i = 0; i < c.np; i++) sc.trial[i] = c.P[(size_t)i * c.W + w];   // Trial = CurParams
+            for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * W + w] = k.P[t.params_used[i]];
     }
     if (PROPOSE) {
-        if (fast_only) proposal_fast(c, r, w, sc);
-        else proposal(c, r, w, sc);
-        for (int i = 0; i < c.np; i++) c.trial[(size_t)i * c.W + w] = sc.trial[i];
+        for (int i = 0; i < c.np; i++) k.trial[i] = k.P[i];          // Trial = CurParams
+        if (fast_only) proposal_fast(c, t, k);
+        else proposal(c, t, k);
         for (int l = 0; l < c.n_like; l++)
-            for (int k = 0; k < c.like_nn[l]; k++)
-                c.like_nuis[l][(size_t)w * c.like_nn[l] + k] = sc.trial[c.like_nuis0[l] + k];
+            for (int q = 0; q < c.like_nn[l]; q++)
+                c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = k.trial[c.like_nuis0[l] + q];
     }
-    c.rng_c[w] = r.c;
-    c.rng_i97[w] = r.i97;
-    c.rng_j97[w] = r.j97;
-    c.rng_iset[w] = r.iset;
-    c.rng_gset[w] = r.gset;
-    for (int i = 0; i < 97; i++) c.rng_u[(size_t)i * c.W + w] = ul[i * 64 + lane];
+    sd[(size_t)R.C * NB + lane] = k.r.c;
+    sd[(size_t)R.G * NB + lane] = k.r.gset;
+    si[(size_t)R.I97 * NB + lane] = k.r.i97;
+    si[(size_t)R.J97 * NB + lane] = k.r.j97;
+    si[(size_t)R.ISET * NB + lane] = k.r.iset;
+    si[(size_t)R.FASTIX * NB + lane] = k.fast_ix;
+    if (skipR) {
+        stage_out(c.sd, sd, 0, 0, R.R, W, w, lane);
+        stage_out(c.sd, sd, R.R, rEnd, R.ND, W, w, lane);
+    } else {
+        stage_out(c.sd, sd, 0, 0, R.ND, W, w, lane);
+    }
+    stage_out(c.si, si, 0, 0, R.NI, W, w, lane);
+#undef SROW
 }
 
+// Starting point: -lnL of P = trial (likelihood terms already evaluated)
 __global__ void start_kernel(DevCfg c)
 {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= c.W) return;
-    Col<double> q{c.trial + w, c.W};
-    c.cur_like[w] = target_like(c, w, q);
-    for (int i = 0; i < c.np; i++) c.P[(size_t)i * c.W + w] = q[i];
-    c.mult[w] = 0.0;
-    c.num_accept[w] = 0;
+    const size_t W = c.W;
+    const Tabs t = make_tabs(c, c.tab_i, c.tab_d);
+    Col<double> q{c.sd + (size_t)c.rows.T * W + w, c.W};
+    Col<const double> lk{c.like_terms + w, c.W};
+    c.sd[(size_t)c.rows.L * W + w] = target_like(c, t, q, lk);
+    for (int i = 0; i < c.np; i++) c.sd[(size_t)(c.rows.P + i) * W + w] = q[i];
+    c.sd[(size_t)c.rows.M * W + w] = 0.0;
+    c.si[(size_t)c.rows.NACC * W + w] = 0;
 }
 
-// scatter the nuisance slice of every walker's trial point: out[w][k] = trial[nuis0 + k][w]
+// nuisance slice of every walker's trial point: out[w][k] = trial[nuis0 + k][w]
 __global__ void gather_nuis(const double *trial, int W, int nuis0, int n_nuis, double *out)
 {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
@@ -397,34 +449,52 @@ __global__ void hist_stats_kernel(const double *hist, int cap, int W, int n, int
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
     const int cnt = last - first + 1;
-    double m[MAXP];
+    double *m = means + (size_t)w * n;
     for (int i = 0; i < n; i++) m[i] = 0.0;
-    for (int t = first; t <= last; t++) {
-        const double *row = hist + (size_t)(t % cap) * n * W;
+    for (int tt = first; tt <= last; tt++) {
+        const double *row = hist + (size_t)(tt % cap) * n * W;
         for (int i = 0; i < n; i++) m[i] += row[(size_t)i * W + w];
     }
-    for (int i = 0; i < n; i++) {
-        m[i] /= cnt;
-        means[(size_t)w * n + i] = m[i];
-    }
+    for (int i = 0; i < n; i++) m[i] /= cnt;
     double *C = covs + (size_t)w * n * n;
     for (int i = 0; i < n * n; i++) C[i] = 0.0;
-    for (int t = first; t <= last; t++) {
-        const double *row = hist + (size_t)(t % cap) * n * W;
-        double d[MAXP];
-        for (int i = 0; i < n; i++) d[i] = row[(size_t)i * W + w] - m[i];
-        for (int j = 0; j < n; j++)
-            for (int i = 0; i < n; i++) C[i * n + j] += d[i] * d[j];
+    for (int tt = first; tt <= last; tt++) {
+        const double *row = hist + (size_t)(tt % cap) * n * W;
+        for (int j = 0; j < n; j++) {
+            const double dj = row[(size_t)j * W + w] - m[j];
+            for (int i = 0; i < n; i++) C[i * n + j] += (row[(size_t)i * W + w] - m[i]) * dj;
+        }
     }
     for (int i = 0; i < n * n; i++) C[i] /= cnt;
 }
 
+// ------------------------------------------------------------ host side
 
-static size_t mh_lds_bytes(const cmbs *s) {
-    return (size_t)(97 + s->np + s->dc.max_blk) * 64 * 8 + (size_t)s->all_n * 64 * 4;
+static size_t mh_lds_bytes(const cmbs *s, int stage_R) {
+    const DevCfg &d = s->dc;
+    const int nd_st = stage_R ? d.rows.ND : d.rows.ND - d.R_total;
+    return (size_t)(nd_st + MAXLIKE + d.max_blk) * NB * 8 + (size_t)d.tl.n_dbl * 8 +
+           (size_t)(d.rows.NI + d.all_n) * NB * 4 + (size_t)d.tl.n_int * 4 + 64;
 }
 
-static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+static void set_mh_lds(cmbs *s) {
+    s->mh_lds = mh_lds_bytes(s, s->dc.stage_R);
+    if (s->mh_lds > 160 * 1024) fail(CMBL_ERR_ARG, "sampler state too large for LDS (%zu bytes)", s->mh_lds);
+    const int lds = (int)s->mh_lds;
+    HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+}
+
+static void upload_tables(cmbs *s) {
+    HIP_CHECK(hipDeviceSynchronize());     // the old tables may be read by queued kernels
+    s->tab_i.alloc(s->h_tab_i.size() * 4 + 4);
+    s->tab_i.upload(s->h_tab_i.data(), s->h_tab_i.size() * 4);
+    s->tab_d.alloc(s->h_tab_d.size() * 8 + 8);
+    s->tab_d.upload(s->h_tab_d.data(), s->h_tab_d.size() * 8);
+    s->dc.tab_i = s->tab_i.as<int>();
+    s->dc.tab_d = s->tab_d.as<double>();
+}
 
 void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     if (cfg->n_walkers <= 0 || cfg->num_params <= 0 || cfg->num_params > MAXP)
@@ -451,6 +521,7 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     for (int b = 0; b < cfg->n_blocks; b++) boff[b + 1] = boff[b] + cfg->block_n[b];
     s->fast_n = s->all_n - s->slow_n;
     s->nblocks = (int)used_blocks.size();
+    if (s->nblocks == 0) fail(CMBL_ERR_ARG, "no parameter blocks");
     s->indices.assign(s->all_n, 0);
     s->proposer_for_index.assign(s->all_n, 0);
     int ix = 1;
@@ -482,58 +553,9 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
         s->map_total += nc * s->blk_n[i];
         s->R_total += s->blk_n[i] * s->blk_n[i];
     }
-    if (s->fast_n > MAXP || s->all_n > MAXP) fail(CMBL_ERR_ARG, "too many parameters");
+    if (s->all_n > MAXP) fail(CMBL_ERR_ARG, "too many parameters");
 
-    // ---- device tables
     const int np = s->np, W = s->W, nb = s->nblocks;
-    std::vector<size_t> offs;
-    size_t tot = 0;
-    auto add = [&](size_t bytes) {
-        offs.push_back(tot);
-        tot += align_up(bytes);
-    };
-    add(nb * 4);                      // 0 blk_n
-    add(nb * 4);                      // 1 blk_nchanged
-    add(nb * 4);                      // 2 blk_changed_off
-    add(nb * 4);                      // 3 blk_map_off
-    add(nb * 4);                      // 4 blk_R_off
-    add(s->changed.size() * 4);       // 5 changed
-    add((size_t)s->map_total * 8);    // 6 mapping
-    add(s->all_n * 4);                // 7 proposer_for_index
-    add(np * 8);                      // 8 pmin
-    add(np * 8);                      // 9 pmax
-    add(np * 8);                      // 10 prior_mean
-    add(np * 8);                      // 11 prior_std
-    add(s->n_used * 4);               // 12 params_used (0-based)
-    s->tables.alloc(tot);
-    char *base = s->tables.as<char>();
-    auto up = [&](int k, const void *src, size_t bytes) {
-        if (bytes) HIP_CHECK(hipMemcpy(base + offs[k], src, bytes, hipMemcpyHostToDevice));
-    };
-    up(0, s->blk_n.data(), nb * 4);
-    up(1, s->blk_nchanged.data(), nb * 4);
-    up(2, s->blk_changed_off.data(), nb * 4);
-    up(3, s->blk_map_off.data(), nb * 4);
-    up(4, s->blk_R_off.data(), nb * 4);
-    up(5, s->changed.data(), s->changed.size() * 4);
-    up(7, s->proposer_for_index.data(), s->all_n * 4);
-    up(8, cfg->pmin, np * 8);
-    up(9, cfg->pmax, np * 8);
-    std::vector<double> pm(np, 0.0), ps(np, 0.0);
-    bool has_pri = false;
-    if (cfg->prior_mean && cfg->prior_std) {
-        for (int i = 0; i < np; i++) {
-            pm[i] = cfg->prior_mean[i];
-            ps[i] = cfg->prior_std[i];
-            has_pri |= ps[i] != 0.0;
-        }
-    }
-    up(10, pm.data(), np * 8);
-    up(11, ps.data(), np * 8);
-    std::vector<int> pu0(s->n_used);
-    for (int i = 0; i < s->n_used; i++) pu0[i] = s->params_used[i] - 1;
-    up(12, pu0.data(), s->n_used * 4);
-
     DevCfg &d = s->dc;
     d.W = W;
     d.np = np;
@@ -545,69 +567,74 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     d.oversample_fast = cfg->oversample_fast < 1 ? 1 : cfg->oversample_fast;
     d.propose_scale = cfg->propose_scale;
     d.temperature = cfg->temperature > 0 ? cfg->temperature : 1.0;
-    d.blk_n = (const int *)(base + offs[0]);
-    d.blk_nchanged = (const int *)(base + offs[1]);
-    d.blk_changed_off = (const int *)(base + offs[2]);
-    d.blk_map_off = (const int *)(base + offs[3]);
-    d.blk_R_off = (const int *)(base + offs[4]);
-    d.changed = (const int *)(base + offs[5]);
-    d.mapping = (const double *)(base + offs[6]);
-    d.proposer_for_index = (const int *)(base + offs[7]);
-    d.pmin = (const double *)(base + offs[8]);
-    d.pmax = (const double *)(base + offs[9]);
-    d.prior_mean = (const double *)(base + offs[10]);
-    d.prior_std = (const double *)(base + offs[11]);
-    d.params_used = (const int *)(base + offs[12]);
-    d.has_priors = has_pri;
     d.R_total = s->R_total;
     d.max_blk = 1;
     for (int bn : s->blk_n) d.max_blk = std::max(d.max_blk, bn);
-    {
-        const int lds = (int)mh_lds_bytes(s);
-        HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    }
 
-    // ---- per-walker state
-    offs.clear();
-    tot = 0;
-    const int ncyc = s->all_n + s->slow_n + s->fast_n;
-    add((size_t)97 * W * 8);          // 0 rng_u
-    add((size_t)W * 8);               // 1 rng_c
-    add((size_t)W * 8);               // 2 rng_gset
-    add((size_t)W * 4);               // 3 i97
-    add((size_t)W * 4);               // 4 j97
-    add((size_t)W * 4);               // 5 iset
-    add((size_t)s->R_total * W * 8);  // 6 R
-    add((size_t)nb * W * 4);          // 7 blk_loopix
-    add((size_t)ncyc * W * 4);        // 8 cyc
-    add((size_t)3 * W * 4);           // 9 cyc_loopix
-    add((size_t)W * 4);               // 10 fast_ix
-    add((size_t)np * W * 8);          // 11 P
-    add((size_t)np * W * 8);          // 12 trial
-    add((size_t)W * 8);               // 13 cur_like
-    add((size_t)W * 8);               // 14 mult
-    add((size_t)W * 4);               // 15 num_accept
-    s->state.alloc(tot);
-    HIP_CHECK(hipMemset(s->state.p, 0, tot));
-    base = s->state.as<char>();
-    d.rng_u = (double *)(base + offs[0]);
-    d.rng_c = (double *)(base + offs[1]);
-    d.rng_gset = (double *)(base + offs[2]);
-    d.rng_i97 = (int *)(base + offs[3]);
-    d.rng_j97 = (int *)(base + offs[4]);
-    d.rng_iset = (int *)(base + offs[5]);
-    d.R = (double *)(base + offs[6]);
-    d.blk_loopix = (int *)(base + offs[7]);
-    d.cyc = (int *)(base + offs[8]);
-    d.cyc_loopix = (int *)(base + offs[9]);
-    d.fast_ix = (int *)(base + offs[10]);
-    d.P = (double *)(base + offs[11]);
-    d.trial = (double *)(base + offs[12]);
-    d.cur_like = (double *)(base + offs[13]);
-    d.mult = (double *)(base + offs[14]);
-    d.num_accept = (int *)(base + offs[15]);
+    // ---- shared tables
+    TabLayout &tl = d.tl;
+    auto &vi = s->h_tab_i;
+    auto &vd = s->h_tab_d;
+    auto put_i = [&](int &off, const std::vector<int> &v) {
+        off = (int)vi.size();
+        vi.insert(vi.end(), v.begin(), v.end());
+    };
+    auto put_d = [&](int &off, const double *v, int n) {
+        off = (int)vd.size();
+        vd.insert(vd.end(), v, v + n);
+    };
+    put_i(tl.blk_n, s->blk_n);
+    put_i(tl.blk_nchanged, s->blk_nchanged);
+    put_i(tl.blk_changed_off, s->blk_changed_off);
+    put_i(tl.blk_map_off, s->blk_map_off);
+    put_i(tl.blk_R_off, s->blk_R_off);
+    put_i(tl.changed, s->changed);
+    put_i(tl.pfi, s->proposer_for_index);
+    std::vector<int> pu0(s->n_used);
+    for (int i = 0; i < s->n_used; i++) pu0[i] = s->params_used[i] - 1;
+    put_i(tl.params_used, pu0);
+    tl.n_int = (int)vi.size();
+    std::vector<double> zeros(std::max(s->map_total, np), 0.0);
+    put_d(tl.mapping, zeros.data(), s->map_total);
+    put_d(tl.pmin, cfg->pmin, np);
+    put_d(tl.pmax, cfg->pmax, np);
+    std::vector<double> pm(np, 0.0), ps(np, 0.0);
+    bool has_pri = false;
+    if (cfg->prior_mean && cfg->prior_std) {
+        for (int i = 0; i < np; i++) {
+            pm[i] = cfg->prior_mean[i];
+            ps[i] = cfg->prior_std[i];
+            has_pri |= ps[i] != 0.0;
+        }
+    }
+    put_d(tl.pmean, pm.data(), np);
+    put_d(tl.pstd, ps.data(), np);
+    tl.covinv = tl.center = (int)vd.size();   // set by cmbs_set_test_gaussian
+    tl.n_dbl = (int)vd.size();
+    d.has_priors = has_pri;
+    d.test_like = 0;
+    upload_tables(s);
+
+    // ---- per-walker state rows
+    Rows &R = d.rows;
+    R.P = R.R + s->R_total;
+    R.T = R.P + np;
+    R.L = R.T + np;
+    R.M = R.L + 1;
+    R.ND = R.M + 1;
+    R.CYC = R.BLKLP + nb;
+    R.NI = R.CYC + s->all_n + s->slow_n + s->fast_n;
+    s->sd.alloc((size_t)R.ND * W * 8);
+    s->si.alloc((size_t)R.NI * W * 4);
+    HIP_CHECK(hipMemset(s->sd.p, 0, (size_t)R.ND * W * 8));
+    HIP_CHECK(hipMemset(s->si.p, 0, (size_t)R.NI * W * 4));
+    d.sd = s->sd.as<double>();
+    d.si = s->si.as<int>();
+
+    // LDS budget: stage the rotation matrices too when everything fits
+    d.stage_R = 1;
+    if (mh_lds_bytes(s, 1) > 144 * 1024) d.stage_R = 0;
+    set_mh_lds(s);
 
     // seeds
     std::vector<int> ij(W), kl(W);
@@ -652,17 +679,16 @@ void sampler_set_covariance(cmbs *s, const double *cov) {
     for (int i = 0; i < na; i++)
         for (int j = 0; j < na; j++) L[i * na + j] = corr[(s->indices[i] - 1) * n + (s->indices[j] - 1)];
     cholesky_lower(L, na);
-    std::vector<double> map(s->map_total);
     int uoff = 0;
     for (int i = 0; i < s->nblocks; i++) {
         const int bn = s->blk_n[i], st = s->blk_start[i], nc = s->blk_nchanged[i];
         for (int j = 0; j < nc; j++)
             for (int k = 0; k < bn; k++)
-                map[s->blk_map_off[i] + j * bn + k] =
+                s->h_tab_d[s->dc.tl.mapping + s->blk_map_off[i] + j * bn + k] =
                     sig[s->used_params_changed_all[uoff + j] - 1] * L[(st - 1 + j) * na + (st - 1 + k)];
         uoff += nc;
     }
-    HIP_CHECK(hipMemcpy(const_cast<double *>(s->dc.mapping), map.data(), map.size() * 8, hipMemcpyHostToDevice));
+    upload_tables(s);
 }
 
 void sampler_set_test_gaussian(cmbs *s, const double *cov, const double *center) {
@@ -687,13 +713,16 @@ void sampler_set_test_gaussian(cmbs *s, const double *cov, const double *center)
             for (int k = i; k < n; k++) x += A[k * n + i] * A[k * n + j];
             T[i * n + j] = T[j * n + i] = x;
         }
-    s->covinv.alloc(T.size() * 8);
-    s->covinv.upload(T.data(), T.size() * 8);
-    s->center.alloc(s->np * 8);
-    s->center.upload(center, s->np * 8);
+    auto &vd = s->h_tab_d;
+    TabLayout &tl = s->dc.tl;
+    vd.resize(tl.covinv);                   // replace any previous test_likelihood
+    vd.insert(vd.end(), T.begin(), T.end());
+    tl.center = (int)vd.size();
+    vd.insert(vd.end(), center, center + s->np);
+    tl.n_dbl = (int)vd.size();
+    set_mh_lds(s);
     s->dc.test_like = 1;
-    s->dc.test_covinv = s->covinv.as<double>();
-    s->dc.center = s->center.as<double>();
+    upload_tables(s);
 }
 
 void sampler_add_likelihood(cmbs *s, cmbl_t *like, int nuis_index0, const double *dl, long long ld_field,
@@ -704,7 +733,10 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, int nuis_index0, const double
     if ((int)s->likes.size() >= MAXLIKE) fail(CMBL_ERR_ARG, "at most %d likelihoods per sampler", MAXLIKE);
     const int li = (int)s->likes.size();
     s->likes.push_back({like, nuis_index0 - 1, dl, ld_field, ld_walker});
-    s->like_terms.alloc(s->likes.size() * (size_t)s->W * 8);
+    DevBuf nt(s->likes.size() * (size_t)s->W * 8);
+    if (li > 0) HIP_CHECK(hipMemcpy(nt.p, s->like_terms.p, (size_t)li * s->W * 8, hipMemcpyDeviceToDevice));
+    std::swap(nt.p, s->like_terms.p);
+    std::swap(nt.bytes, s->like_terms.bytes);
     s->dc.n_like = (int)s->likes.size();
     s->dc.like_terms = s->like_terms.as<double>();
     s->nuis_bufs[li].alloc((size_t)std::max(nn, 1) * s->W * 8);
@@ -722,8 +754,8 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather) {
         const int nn = l.like->like->n_nuis;
         double *nb = s->dc.like_nuis[i];
         if (gather) {   // mh_kernel scatters the nuisance slices itself on every step
-            hipLaunchKernelGGL(gather_nuis, dim3((s->W + 255) / 256), dim3(256), 0, stream, s->dc.trial, s->W,
-                               l.nuis0, nn, nb);
+            hipLaunchKernelGGL(gather_nuis, dim3((s->W + 255) / 256), dim3(256), 0, stream,
+                               s->dc.sd + (size_t)s->dc.rows.T * s->W, s->W, l.nuis0, nn, nb);
             HIP_CHECK(hipGetLastError());
         }
         l.like->like->loglike_batch(s->W, l.dl, l.ld_field, l.ld_walker, nb, nn,
@@ -732,8 +764,8 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather) {
 }
 
 static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, double *row, hipStream_t stream) {
-    const dim3 g((s->W + 63) / 64), b(64);
-    const size_t lds = mh_lds_bytes(s);
+    const dim3 g((s->W + NB - 1) / NB), b(NB);
+    const size_t lds = s->mh_lds;
     timed_launch("mh_kernel", stream, [&] {
         if (accept && propose)
             hipLaunchKernelGGL((mh_kernel<true, true>), g, b, lds, stream, s->dc, fast_only, row);
@@ -746,11 +778,12 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, double 
 }
 
 void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream) {
-    // host [W][np] -> device trial [np][W]
+    // host [W][np] -> device trial rows [np][W]
     std::vector<double> t((size_t)s->np * s->W);
     for (int w = 0; w < s->W; w++)
         for (int i = 0; i < s->np; i++) t[(size_t)i * s->W + w] = P0[(size_t)w * s->np + i];
-    HIP_CHECK(hipMemcpyAsync(s->dc.trial, t.data(), t.size() * 8, hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipMemcpyAsync(s->dc.sd + (size_t)s->dc.rows.T * s->W, t.data(), t.size() * 8,
+                             hipMemcpyHostToDevice, stream));
     eval_likes(s, stream, true);
     hipLaunchKernelGGL(start_kernel, dim3((s->W + 255) / 256), dim3(256), 0, stream, s->dc);
     HIP_CHECK(hipGetLastError());
@@ -792,6 +825,22 @@ void sampler_history_stats(cmbs *s, int first, int last, double *means, double *
     hipLaunchKernelGGL(hist_stats_kernel, dim3((s->W + 127) / 128), dim3(128), 0, stream, s->hist.as<double>(),
                        s->hist_cap, s->W, s->n_used, first, last, means, covs);
     HIP_CHECK(hipGetLastError());
+}
+
+void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, int *num_accept) {
+    HIP_CHECK(hipDeviceSynchronize());
+    const int W = s->W, np = s->np;
+    const Rows &R = s->dc.rows;
+    if (P) {
+        std::vector<double> t((size_t)np * W);
+        HIP_CHECK(hipMemcpy(t.data(), s->dc.sd + (size_t)R.P * W, t.size() * 8, hipMemcpyDeviceToHost));
+        for (int w = 0; w < W; w++)
+            for (int i = 0; i < np; i++) P[(size_t)w * np + i] = t[(size_t)i * W + w];
+    }
+    if (cur_like) HIP_CHECK(hipMemcpy(cur_like, s->dc.sd + (size_t)R.L * W, (size_t)W * 8, hipMemcpyDeviceToHost));
+    if (mult) HIP_CHECK(hipMemcpy(mult, s->dc.sd + (size_t)R.M * W, (size_t)W * 8, hipMemcpyDeviceToHost));
+    if (num_accept)
+        HIP_CHECK(hipMemcpy(num_accept, s->dc.si + (size_t)R.NACC * W, (size_t)W * 4, hipMemcpyDeviceToHost));
 }
 
 }  // namespace cmamd
