@@ -241,7 +241,7 @@ int cmbs_history_count(const cmbs_t *s) { return s ? s->hist_count : 0; }
 int cmbs_state(cmbs_t *s, double **P, double **cur_like, double **mult, int **num_accept) {
     if (!s) return CMBL_ERR_ARG;
     const auto &R = s->dc.rows;
-    const size_t W = s->W;
+    const size_t W = s->dc.ld;
     if (P) *P = s->dc.sd + R.P * W;
     if (cur_like) *cur_like = s->dc.sd + R.L * W;
     if (mult) *mult = s->dc.sd + R.M * W;

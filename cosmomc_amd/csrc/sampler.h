@@ -16,15 +16,17 @@ struct Rows {
     int U = 0;          // 97 rows: RANMAR u(1:97)
     int C = 97;         // RANMAR c
     int G = 98;         // Gaussian1 saved deviate gset
-    int R = 99;         // R_total rows: per-block random rotations (row j col i of block b at R + off_b + j*n+i)
+    int R = 100;        // R_rows rows (R_total rounded up to even): per-block random rotations
+                        //   (row j col i of block b at R + off_b + j*n+i); row 99 is padding
+    int RR;             // R_rows
     int P, T, L, M;     // np rows current point, np rows trial, cur_like, mult
-    int ND;
+    int ND;             // even: rows are moved in pairs (16-byte LDS-DMA pieces)
     // int rows
     int I97 = 0, J97 = 1, ISET = 2, FASTIX = 3, NACC = 4;
     int CYCLP = 5;      // 3 rows: All, Slow, Fast CyclicIndexRandomizer%loopix
     int BLKLP = 8;      // nblocks rows: RandDirectionProposer%loopix
     int CYC;            // all_n + slow_n + fast_n rows: the three index permutations
-    int NI;
+    int NI;             // multiple of 4: rows are moved four at a time
 };
 
 // Shared read-only tables (copied to LDS by every mh_kernel block).
@@ -37,17 +39,18 @@ struct TabLayout {
 
 struct DevCfg {
     int W, np, n_used, nblocks, slow_n, fast_n, all_n, oversample_fast, max_blk, R_total;
+    int ld;                 // row stride of sd / si / like_terms: W rounded up to 64
     double propose_scale, temperature;
     int has_priors, test_like;
     Rows rows;
     TabLayout tl;
-    const int *tab_i;       // [tl.n_int]
-    const double *tab_d;    // [tl.n_dbl]
-    double *sd;             // [ND][W]
-    int *si;                // [NI][W]
+    const int *tab_i;       // [tl.n_int] (allocation padded to a multiple of 64 words)
+    const double *tab_d;    // [tl.n_dbl] (allocation padded to a multiple of 32 doubles)
+    double *sd;             // [ND][ld]
+    int *si;                // [NI][ld]
     int stage_R;            // R rows staged in LDS (else read in place, stride W)
     int n_like;
-    const double *like_terms;       // [n_like][W] -lnL of each likelihood at the trial point
+    const double *like_terms;       // [n_like (even)][ld] -lnL of each likelihood at the trial point
     int like_nuis0[MAXLIKE], like_nn[MAXLIKE];
     double *like_nuis[MAXLIKE];     // [W][like_nn] DataParams buffers written by mh_kernel
 };

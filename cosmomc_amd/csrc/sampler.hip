@@ -106,7 +106,7 @@ __global__ void rng_init_kernel(DevCfg c, const int *ij, const int *kl)
 {   // RMARIN, RandUtils.f90:286-348
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= c.W) return;
-    const size_t W = c.W;
+    const size_t W = c.ld;
     int i = (ij[w] / 177) % 177 + 2, j = ij[w] % 177 + 2, k = (kl[w] / 169) % 178 + 1, l = kl[w] % 169;
     for (int ii = 0; ii < 97; ii++) {
         double s = 0.0, t = 0.5;
@@ -294,26 +294,45 @@ __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const 
     return like;
 }
 
-// Copy rows [r0, r1) of a [rows][W] HBM array into an LDS [rows][NB] column
-// block, 8 independent loads in flight per lane before their LDS writes.
-template <class T>
-__device__ void stage_in(T *dst, int dst_r0, const T *src, int r0, int r1, size_t W, int wc, int lane)
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+// LDS-DMA (global_load_lds_dwordx4): rows [r0, r0+n) (n even) of a [rows][ld]
+// double array, columns wb..wb+63, into LDS rows [d0, d0+n) of [row][NB].
+// One wave instruction moves two 512-byte rows; nothing passes through VGPRs,
+// so every piece of the walker state is in flight at once.
+__device__ inline void dma_rows_f64(double *dst, int d0, const double *src, int r0, int n, size_t ld, int wb,
+                                    int lane)
 {
-    int r = r0;
-    for (; r + 8 <= r1; r += 8) {
-        T v[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) v[q] = src[(size_t)(r + q) * W + wc];
-#pragma unroll
-        for (int q = 0; q < 8; q++) dst[(size_t)(dst_r0 + r - r0 + q) * NB + lane] = v[q];
+    for (int r = 0; r < n; r += 2) {
+        const double *g = src + (size_t)(r0 + r + (lane >> 5)) * ld + wb + 2 * (lane & 31);
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)g, (lds_void_t *)(dst + (size_t)(d0 + r) * NB), 16, 0, 0);
     }
-    for (; r < r1; r++) dst[(size_t)(dst_r0 + r - r0) * NB + lane] = src[(size_t)r * W + wc];
+}
+
+// same for int rows (n multiple of 4): one instruction moves four 256-byte rows
+__device__ inline void dma_rows_i32(int *dst, const int *src, int n, size_t ld, int wb, int lane)
+{
+    for (int r = 0; r < n; r += 4) {
+        const int *g = src + (size_t)(r + (lane >> 4)) * ld + wb + 4 * (lane & 15);
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)g, (lds_void_t *)(dst + (size_t)r * NB), 16, 0, 0);
+    }
+}
+
+// flat copy of n 4-byte words (source allocation padded to a multiple of 64 words)
+__device__ inline void dma_words(void *dst, const void *src, int n, int lane)
+{
+    for (int i = 0; i < n; i += 64) {
+        const unsigned *g = reinterpret_cast<const unsigned *>(src) + i + lane;
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)g, (lds_void_t *)(reinterpret_cast<unsigned *>(dst) + i), 4,
+                                         0, 0);
+    }
 }
 
 template <class T>
-__device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size_t W, int w, int lane)
+__device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size_t ld, int w, int lane)
 {
-    for (int r = r0; r < r1; r++) dst[(size_t)r * W + w] = src[(size_t)(src_r0 + r - r0) * NB + lane];
+    for (int r = r0; r < r1; r++) dst[(size_t)r * ld + w] = src[(size_t)(src_r0 + r - r0) * NB + lane];
 }
 
 // One launch per Metropolis step boundary: accept/reject the pending trial
@@ -326,35 +345,37 @@ __global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double 
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Rows &R = c.rows;
     const int lane = threadIdx.x;
-    const int w = blockIdx.x * NB + lane;
+    const int wb = blockIdx.x * NB;
+    const int w = wb + lane;
     const bool act = w < c.W;
-    const int wc = act ? w : c.W - 1;
-    const size_t W = c.W;
+    const size_t W = c.ld;
+    const int nlk = (c.n_like + 1) & ~1;
     // LDS carve: state doubles | like terms | vec scratch | tables(d) | state ints | itmp | tables(i)
-    const int nd_st = c.stage_R ? R.ND : R.ND - c.R_total;      // staged double rows
+    const int nd_st = c.stage_R ? R.ND : R.ND - R.RR;           // staged double rows
     double *sd = lds;                                            // [nd_st][NB]
-    double *lk = sd + (size_t)nd_st * NB;                        // [n_like][NB]
-    double *vc = lk + (size_t)c.n_like * NB;                     // [max_blk][NB]
-    double *td = vc + (size_t)c.max_blk * NB;                    // [n_dbl]
-    int *si = reinterpret_cast<int *>(td + c.tl.n_dbl);          // [NI][NB]
+    double *lk = sd + (size_t)nd_st * NB;                        // [nlk][NB]
+    double *vc = lk + (size_t)nlk * NB;                          // [max_blk][NB]
+    double *td = vc + (size_t)c.max_blk * NB;                    // [n_dbl rounded to 32]
+    int *si = reinterpret_cast<int *>(td + ((c.tl.n_dbl + 31) & ~31));   // [NI][NB]
     int *it = si + (size_t)R.NI * NB;                            // [all_n][NB]
-    int *ti = it + (size_t)c.all_n * NB;                         // [n_int]
+    int *ti = it + (size_t)c.all_n * NB;                         // [n_int rounded to 64]
     const bool skipR = !c.stage_R;
     // staged double row index of global row r (rotation rows dropped when not staged)
-#define SROW(r) ((skipR && (r) >= R.R) ? (r) - c.R_total : (r))
+#define SROW(r) ((skipR && (r) >= R.R) ? (r) - R.RR : (r))
 
-    for (int i = lane; i < c.tl.n_dbl; i += NB) td[i] = c.tab_d[i];
-    for (int i = lane; i < c.tl.n_int; i += NB) ti[i] = c.tab_i[i];
-    const int rEnd = R.R + c.R_total;
+    const int rEnd = R.R + R.RR;
     if (skipR) {
-        stage_in(sd, 0, c.sd, 0, R.R, W, wc, lane);
-        stage_in(sd, R.R, c.sd, rEnd, R.ND, W, wc, lane);
+        dma_rows_f64(sd, 0, c.sd, 0, R.R, W, wb, lane);
+        dma_rows_f64(sd, R.R, c.sd, rEnd, R.ND - rEnd, W, wb, lane);
     } else {
-        stage_in(sd, 0, c.sd, 0, R.ND, W, wc, lane);
+        dma_rows_f64(sd, 0, c.sd, 0, R.ND, W, wb, lane);
     }
-    stage_in(si, 0, c.si, 0, R.NI, W, wc, lane);
-    stage_in(lk, 0, c.like_terms, 0, c.n_like, W, wc, lane);
-    __syncthreads();                 // tables are shared across lanes
+    dma_rows_f64(lk, 0, c.like_terms, 0, nlk, W, wb, lane);
+    dma_rows_i32(si, c.si, R.NI, W, wb, lane);
+    dma_words(td, c.tab_d, 2 * c.tl.n_dbl, lane);
+    dma_words(ti, c.tab_i, c.tl.n_int, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (!act) return;
 
     const Tabs t = make_tabs(c, ti, td);
@@ -365,7 +386,7 @@ __global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double 
     k.r.i97 = si[(size_t)R.I97 * NB + lane];
     k.r.j97 = si[(size_t)R.J97 * NB + lane];
     k.r.iset = si[(size_t)R.ISET * NB + lane];
-    k.R = c.stage_R ? Col<double>{sd + (size_t)R.R * NB + lane, NB} : Col<double>{c.sd + (size_t)R.R * W + w, c.W};
+    k.R = c.stage_R ? Col<double>{sd + (size_t)R.R * NB + lane, NB} : Col<double>{c.sd + (size_t)R.R * W + w, c.ld};
     k.P = Col<double>{sd + (size_t)SROW(R.P) * NB + lane, NB};
     k.trial = Col<double>{sd + (size_t)SROW(R.T) * NB + lane, NB};
     k.vec = Col<double>{vc + lane, NB};
@@ -425,10 +446,10 @@ __global__ void start_kernel(DevCfg c)
 {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= c.W) return;
-    const size_t W = c.W;
+    const size_t W = c.ld;
     const Tabs t = make_tabs(c, c.tab_i, c.tab_d);
-    Col<double> q{c.sd + (size_t)c.rows.T * W + w, c.W};
-    Col<const double> lk{c.like_terms + w, c.W};
+    Col<double> q{c.sd + (size_t)c.rows.T * W + w, c.ld};
+    Col<const double> lk{c.like_terms + w, c.ld};
     c.sd[(size_t)c.rows.L * W + w] = target_like(c, t, q, lk);
     for (int i = 0; i < c.np; i++) c.sd[(size_t)(c.rows.P + i) * W + w] = q[i];
     c.sd[(size_t)c.rows.M * W + w] = 0.0;
@@ -436,11 +457,11 @@ __global__ void start_kernel(DevCfg c)
 }
 
 // nuisance slice of every walker's trial point: out[w][k] = trial[nuis0 + k][w]
-__global__ void gather_nuis(const double *trial, int W, int nuis0, int n_nuis, double *out)
+__global__ void gather_nuis(const double *trial, int W, int ld, int nuis0, int n_nuis, double *out)
 {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
-    for (int k = 0; k < n_nuis; k++) out[(size_t)w * n_nuis + k] = trial[(size_t)(nuis0 + k) * W + w];
+    for (int k = 0; k < n_nuis; k++) out[(size_t)w * n_nuis + k] = trial[(size_t)(nuis0 + k) * ld + w];
 }
 
 __global__ void hist_stats_kernel(const double *hist, int cap, int W, int n, int first, int last,
@@ -472,9 +493,9 @@ __global__ void hist_stats_kernel(const double *hist, int cap, int W, int n, int
 
 static size_t mh_lds_bytes(const cmbs *s, int stage_R) {
     const DevCfg &d = s->dc;
-    const int nd_st = stage_R ? d.rows.ND : d.rows.ND - d.R_total;
-    return (size_t)(nd_st + MAXLIKE + d.max_blk) * NB * 8 + (size_t)d.tl.n_dbl * 8 +
-           (size_t)(d.rows.NI + d.all_n) * NB * 4 + (size_t)d.tl.n_int * 4 + 64;
+    const int nd_st = stage_R ? d.rows.ND : d.rows.ND - d.rows.RR;
+    return (size_t)(nd_st + MAXLIKE + d.max_blk) * NB * 8 + (size_t)((d.tl.n_dbl + 31) & ~31) * 8 +
+           (size_t)(d.rows.NI + d.all_n) * NB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 + 64;
 }
 
 static void set_mh_lds(cmbs *s) {
@@ -488,9 +509,10 @@ static void set_mh_lds(cmbs *s) {
 
 static void upload_tables(cmbs *s) {
     HIP_CHECK(hipDeviceSynchronize());     // the old tables may be read by queued kernels
-    s->tab_i.alloc(s->h_tab_i.size() * 4 + 4);
+    // padded to whole 256-byte LDS-DMA pieces
+    s->tab_i.alloc(((s->h_tab_i.size() + 63) / 64 + 1) * 256);
     s->tab_i.upload(s->h_tab_i.data(), s->h_tab_i.size() * 4);
-    s->tab_d.alloc(s->h_tab_d.size() * 8 + 8);
+    s->tab_d.alloc(((s->h_tab_d.size() + 31) / 32 + 1) * 256);
     s->tab_d.upload(s->h_tab_d.data(), s->h_tab_d.size() * 8);
     s->dc.tab_i = s->tab_i.as<int>();
     s->dc.tab_d = s->tab_d.as<double>();
@@ -617,17 +639,19 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
 
     // ---- per-walker state rows
     Rows &R = d.rows;
-    R.P = R.R + s->R_total;
+    R.RR = (s->R_total + 1) & ~1;
+    R.P = R.R + R.RR;
     R.T = R.P + np;
     R.L = R.T + np;
     R.M = R.L + 1;
-    R.ND = R.M + 1;
+    R.ND = (R.M + 2) & ~1;
     R.CYC = R.BLKLP + nb;
-    R.NI = R.CYC + s->all_n + s->slow_n + s->fast_n;
-    s->sd.alloc((size_t)R.ND * W * 8);
-    s->si.alloc((size_t)R.NI * W * 4);
-    HIP_CHECK(hipMemset(s->sd.p, 0, (size_t)R.ND * W * 8));
-    HIP_CHECK(hipMemset(s->si.p, 0, (size_t)R.NI * W * 4));
+    R.NI = (R.CYC + s->all_n + s->slow_n + s->fast_n + 3) & ~3;
+    d.ld = (W + NB - 1) / NB * NB;
+    s->sd.alloc((size_t)R.ND * d.ld * 8);
+    s->si.alloc((size_t)R.NI * d.ld * 4);
+    HIP_CHECK(hipMemset(s->sd.p, 0, (size_t)R.ND * d.ld * 8));
+    HIP_CHECK(hipMemset(s->si.p, 0, (size_t)R.NI * d.ld * 4));
     d.sd = s->sd.as<double>();
     d.si = s->si.as<int>();
 
@@ -733,8 +757,10 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, int nuis_index0, const double
     if ((int)s->likes.size() >= MAXLIKE) fail(CMBL_ERR_ARG, "at most %d likelihoods per sampler", MAXLIKE);
     const int li = (int)s->likes.size();
     s->likes.push_back({like, nuis_index0 - 1, dl, ld_field, ld_walker});
-    DevBuf nt(s->likes.size() * (size_t)s->W * 8);
-    if (li > 0) HIP_CHECK(hipMemcpy(nt.p, s->like_terms.p, (size_t)li * s->W * 8, hipMemcpyDeviceToDevice));
+    const size_t nlk = (s->likes.size() + 1) & ~size_t(1);
+    DevBuf nt(nlk * (size_t)s->dc.ld * 8);
+    HIP_CHECK(hipMemset(nt.p, 0, nt.bytes));
+    if (li > 0) HIP_CHECK(hipMemcpy(nt.p, s->like_terms.p, (size_t)li * s->dc.ld * 8, hipMemcpyDeviceToDevice));
     std::swap(nt.p, s->like_terms.p);
     std::swap(nt.bytes, s->like_terms.bytes);
     s->dc.n_like = (int)s->likes.size();
@@ -755,11 +781,11 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather) {
         double *nb = s->dc.like_nuis[i];
         if (gather) {   // mh_kernel scatters the nuisance slices itself on every step
             hipLaunchKernelGGL(gather_nuis, dim3((s->W + 255) / 256), dim3(256), 0, stream,
-                               s->dc.sd + (size_t)s->dc.rows.T * s->W, s->W, l.nuis0, nn, nb);
+                               s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld, s->W, s->dc.ld, l.nuis0, nn, nb);
             HIP_CHECK(hipGetLastError());
         }
         l.like->like->loglike_batch(s->W, l.dl, l.ld_field, l.ld_walker, nb, nn,
-                                    s->like_terms.as<double>() + i * (size_t)s->W, s->ws.p, stream);
+                                    s->like_terms.as<double>() + i * (size_t)s->dc.ld, s->ws.p, stream);
     }
 }
 
@@ -782,8 +808,8 @@ void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream) {
     std::vector<double> t((size_t)s->np * s->W);
     for (int w = 0; w < s->W; w++)
         for (int i = 0; i < s->np; i++) t[(size_t)i * s->W + w] = P0[(size_t)w * s->np + i];
-    HIP_CHECK(hipMemcpyAsync(s->dc.sd + (size_t)s->dc.rows.T * s->W, t.data(), t.size() * 8,
-                             hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipMemcpy2DAsync(s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld, (size_t)s->dc.ld * 8, t.data(),
+                               (size_t)s->W * 8, (size_t)s->W * 8, s->np, hipMemcpyHostToDevice, stream));
     eval_likes(s, stream, true);
     hipLaunchKernelGGL(start_kernel, dim3((s->W + 255) / 256), dim3(256), 0, stream, s->dc);
     HIP_CHECK(hipGetLastError());
@@ -830,17 +856,18 @@ void sampler_history_stats(cmbs *s, int first, int last, double *means, double *
 void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, int *num_accept) {
     HIP_CHECK(hipDeviceSynchronize());
     const int W = s->W, np = s->np;
+    const size_t ld = s->dc.ld;
     const Rows &R = s->dc.rows;
     if (P) {
-        std::vector<double> t((size_t)np * W);
-        HIP_CHECK(hipMemcpy(t.data(), s->dc.sd + (size_t)R.P * W, t.size() * 8, hipMemcpyDeviceToHost));
+        std::vector<double> t((size_t)np * ld);
+        HIP_CHECK(hipMemcpy(t.data(), s->dc.sd + (size_t)R.P * ld, t.size() * 8, hipMemcpyDeviceToHost));
         for (int w = 0; w < W; w++)
-            for (int i = 0; i < np; i++) P[(size_t)w * np + i] = t[(size_t)i * W + w];
+            for (int i = 0; i < np; i++) P[(size_t)w * np + i] = t[(size_t)i * ld + w];
     }
-    if (cur_like) HIP_CHECK(hipMemcpy(cur_like, s->dc.sd + (size_t)R.L * W, (size_t)W * 8, hipMemcpyDeviceToHost));
-    if (mult) HIP_CHECK(hipMemcpy(mult, s->dc.sd + (size_t)R.M * W, (size_t)W * 8, hipMemcpyDeviceToHost));
+    if (cur_like) HIP_CHECK(hipMemcpy(cur_like, s->dc.sd + (size_t)R.L * ld, (size_t)W * 8, hipMemcpyDeviceToHost));
+    if (mult) HIP_CHECK(hipMemcpy(mult, s->dc.sd + (size_t)R.M * ld, (size_t)W * 8, hipMemcpyDeviceToHost));
     if (num_accept)
-        HIP_CHECK(hipMemcpy(num_accept, s->dc.si + (size_t)R.NACC * W, (size_t)W * 4, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(num_accept, s->dc.si + (size_t)R.NACC * ld, (size_t)W * 4, hipMemcpyDeviceToHost));
 }
 
 }  // namespace cmamd
