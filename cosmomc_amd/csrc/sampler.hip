@@ -415,7 +415,7 @@ __global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double 
             mult += 1.0;
         }
         if (hist_row)
-            for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * W + w] = k.P[t.params_used[i]];
+            for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = k.P[t.params_used[i]];
     }
     if (PROPOSE) {
         for (int i = 0; i < c.np; i++) k.trial[i] = k.P[i];          // Trial = CurParams
