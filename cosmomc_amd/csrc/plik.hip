@@ -71,21 +71,42 @@ __global__ __launch_bounds__(256) void plik_bin_delta(
     if (w == 0)
         for (int i = tid; i < n_counters; i += blockDim.x) counters[i] = 0u;
     const double *D = dl + (long long)w * ld_walker;
+    if (vec_ok) {
+        // all 16-byte pieces of the three fields, flattened; every thread's
+        // loads are issued before any product is stored (latency, not
+        // bandwidth, bounds one walker's 51 KB)
+        const int n0 = fr.hi[0] >= fr.lo[0] ? (fr.hi[0] - fr.lo[0] + 1) >> 1 : 0;
+        const int n1 = fr.hi[1] >= fr.lo[1] ? (fr.hi[1] - fr.lo[1] + 1) >> 1 : 0;
+        const int n2 = fr.hi[2] >= fr.lo[2] ? (fr.hi[2] - fr.lo[2] + 1) >> 1 : 0;
+        const int np2 = n0 + n1 + n2;
+        constexpr int PER = 16;                      // pieces per thread per round (<= 4096 per walker)
+        for (int base = 0; base < np2; base += PER * 256) {
+            double2 dv[PER], wv[PER];
+            int loff[PER];
 #pragma unroll
-    for (int f = 0; f < 3; f++) {
-        const int lo = fr.lo[f], hi = fr.hi[f];
-        if (hi < lo) continue;
-        const double *Df = D + f * ld_field;
-        double *P = prod + fr.off[f] - lo;
-        if (vec_ok) {
-            // lo is even; pairs (l, l+1), l <= hi (hi odd after alignment)
-#pragma unroll 4
-            for (int l = lo + 2 * tid; l <= hi; l += 2 * blockDim.x) {
-                const double2 d = *reinterpret_cast<const double2 *>(Df + l);
-                const double2 q = *reinterpret_cast<const double2 *>(wts + l);
-                *reinterpret_cast<double2 *>(P + l) = make_double2(d.x * q.x, d.y * q.y);
+            for (int j = 0; j < PER; j++) {
+                const int p = base + j * 256 + tid;
+                int f = 0, q = p;
+                if (q >= n0) { q -= n0; f = 1; if (q >= n1) { q -= n1; f = 2; } }
+                const bool ok = p < np2;
+                const int l = fr.lo[f] + 2 * q;
+                loff[j] = ok ? fr.off[f] + 2 * q : -1;
+                const double *src = ok ? D + f * ld_field + l : D;
+                dv[j] = *reinterpret_cast<const double2 *>(src);
+                wv[j] = *reinterpret_cast<const double2 *>(wts + (ok ? l : 0));
             }
-        } else {
+#pragma unroll
+            for (int j = 0; j < PER; j++)
+                if (loff[j] >= 0)
+                    *reinterpret_cast<double2 *>(prod + loff[j]) = make_double2(dv[j].x * wv[j].x, dv[j].y * wv[j].y);
+        }
+    } else {
+#pragma unroll
+        for (int f = 0; f < 3; f++) {
+            const int lo = fr.lo[f], hi = fr.hi[f];
+            if (hi < lo) continue;
+            const double *Df = D + f * ld_field;
+            double *P = prod + fr.off[f] - lo;
             const int hs = hi < ld_field ? hi : (int)ld_field - 1;   // never read past the row
 #pragma unroll 4
             for (int l = lo + tid; l <= hs; l += blockDim.x) P[l] = Df[l] * wts[l];
@@ -108,93 +129,108 @@ __global__ __launch_bounds__(256) void plik_bin_delta(
     }
 }
 
-static constexpr int BK = 32;            // k depth staged per pipeline step
-static constexpr int LDK = BK + 2;       // padded LDS row: conflict-free f64 MFMA fragment reads
+static constexpr int BK = 32;            // k depth staged per pipeline step (16 chunks of 16 B per row)
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+// LDS image of a 64-row x BK-double operand tile: rows of 256 B, unpadded;
+// the 16-byte chunk c of row r lives at physical chunk c ^ swz(r).  The
+// swizzle makes both the LDS-DMA fill (linear 1 KB pieces) and the MFMA
+// fragment reads (ds_read_b128, 8 consecutive k per lane) bank-conflict free.
+__device__ __forceinline__ int swz(int r) { return ((r >> 2) & 3) | ((r & 3) << 2); }
+
+// Fill one 64 x BK tile: rows row0..row0+63 of a row-major matrix (stride ld
+// doubles), columns k0..k0+BK-1.  4 waves x 4 instructions of 1 KB; lane l
+// of instruction j writes LDS bytes [l*16, l*16+16) of piece j = physical
+// chunk (l & 15) of row 4j + (l >> 4), so it loads the logical chunk
+// (l & 15) ^ swz(row) from global memory.
+__device__ __forceinline__ void dma_tile(double *lds_tile, const double *g, size_t ld, int k0, int wave, int lane)
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int piece = wave * 4 + q;                 // 0..15, 4 rows each
+        const int r = piece * 4 + (lane >> 4);
+        const int lc = (lane & 15) ^ swz(r);
+        const double *src = g + (size_t)r * ld + k0 + lc * 2;
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)src, (lds_void_t *)(lds_tile + piece * 4 * BK), 16, 0, 0);
+    }
+}
 
 // Quadratic form, symmetric split-K.  With Ct = C^-1 whose diagonal 64x64
 // blocks are halved,  Delta^T C^-1 Delta / 2 = sum_I Delta_I^T sum_{J>=I} Ct_IJ Delta_J,
 // so -lnL needs only the upper block triangle.  A workgroup owns one
-// (row block I, column-block range) item for 64 walkers: a register-staged,
-// double-buffered K loop over its column blocks (f64 MFMA 16x16x4 into four
-// 16x16 accumulators per wave), then the dot with Delta_I.  Partials are
-// handed off in-launch: the last workgroup of each walker tile (agent-scope
-// release / ticket / acquire, cdna_hip_programming.md section 5 split-K recipe) sums
-// them in fixed item order, so the result is deterministic.
+// (row block I, column-block range) item for 64 walkers: a double-buffered
+// K loop (LDS-DMA fills one BK step ahead) of f64 MFMA 16x16x4 into four
+// 16x16 accumulators per wave, then the dot with Delta_I.  Within a BK step
+// lane group g = lane>>4 takes k = 8g .. 8g+7 (any k order is valid as long
+// as A and B agree), so each lane reads its fragments as ds_read_b128.
+// Partials are handed off in-launch: the last workgroup of each walker tile
+// (agent-scope release / ticket / acquire, cdna_hip_programming.md section 5
+// split-K recipe) sums them in fixed item order: deterministic results.
 __global__ __launch_bounds__(256, 2) void plik_quadform_ksplit(
     const double *__restrict__ Ct, int Np, const double *__restrict__ delta, int W,
-    const Item *__restrict__ items, int n_items,
+    const Item *__restrict__ items, int n_items, int xcd_map,
     double *__restrict__ partial, unsigned int *__restrict__ counters, double *__restrict__ out)
 {
-    __shared__ __attribute__((aligned(16))) double smem[2 * 2 * TILE * LDK];
-    const Item it = items[blockIdx.x];
-    const int tile = blockIdx.y, w0 = tile * TILE;
+    __shared__ __attribute__((aligned(16))) double smem[2 * 2 * TILE * BK];   // [buf][A|B][64][BK], 64 KB
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
+    // XCD-aware placement: blocks b and b+8 share an XCD; give each XCD whole
+    // walker tiles so a tile's Delta stays in one L2 (speed only)
+    int item_ix = blockIdx.x, tile = blockIdx.y;
+    if (xcd_map) {
+        const int b = blockIdx.x + blockIdx.y * gridDim.x;
+        const int x = b & 7, j = b >> 3;
+        tile = x + 8 * (j / n_items);
+        item_ix = j % n_items;
+    }
+    const Item it = items[item_ix];
+    const int w0 = tile * TILE;
     const int nsteps = it.nJ * (TILE / BK);
     const int kbase0 = it.J0 * TILE;
-    const double *Arow = Ct + (size_t)(it.I * TILE) * Np;
-
-    // staging map: 64 rows x BK doubles per operand = 1024 double2, 4 per thread.
-    // Delta rows of padding walkers (W <= w < Wpad) lie inside the workspace;
-    // they are loaded unconditionally and replaced by zeros (no flat loads).
-    const int sr = tid >> 4, sc = (tid & 15) * 2;            // rows sr, sr+16, sr+32, sr+48
-    const double *ga = Arow + (size_t)sr * Np + kbase0 + sc;
-    const double *gb = delta + (size_t)(w0 + sr) * Np + kbase0 + sc;
-    const bool bv0 = w0 + sr < W, bv1 = w0 + sr + 16 < W, bv2 = w0 + sr + 32 < W, bv3 = w0 + sr + 48 < W;
-    const double2 z2 = make_double2(0.0, 0.0);
-    double2 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
-#define QF_GLOAD(s_)                                                                            \
-    {                                                                                            \
-        const int ko = (s_) * BK;                                                                \
-        ra0 = *reinterpret_cast<const double2 *>(ga + ko);                                       \
-        ra1 = *reinterpret_cast<const double2 *>(ga + (size_t)16 * Np + ko);                     \
-        ra2 = *reinterpret_cast<const double2 *>(ga + (size_t)32 * Np + ko);                     \
-        ra3 = *reinterpret_cast<const double2 *>(ga + (size_t)48 * Np + ko);                     \
-        rb0 = *reinterpret_cast<const double2 *>(gb + ko);                                \
-        if (!bv0) rb0 = z2;                                                                  \
-        rb1 = *reinterpret_cast<const double2 *>(gb + (size_t)16 * Np + ko);                                \
-        if (!bv1) rb1 = z2;                                                                  \
-        rb2 = *reinterpret_cast<const double2 *>(gb + (size_t)32 * Np + ko);                                \
-        if (!bv2) rb2 = z2;                                                                  \
-        rb3 = *reinterpret_cast<const double2 *>(gb + (size_t)48 * Np + ko);                                \
-        if (!bv3) rb3 = z2;                                                                  \
-    }
-#define QF_LSTORE(buf_)                                                                         \
-    {                                                                                            \
-        double *A_ = smem + (buf_) * 2 * TILE * LDK + sr * LDK + sc;                             \
-        double *B_ = A_ + TILE * LDK;                                                            \
-        *reinterpret_cast<double2 *>(A_) = ra0;                                                  \
-        *reinterpret_cast<double2 *>(A_ + 16 * LDK) = ra1;                                       \
-        *reinterpret_cast<double2 *>(A_ + 32 * LDK) = ra2;                                       \
-        *reinterpret_cast<double2 *>(A_ + 48 * LDK) = ra3;                                       \
-        *reinterpret_cast<double2 *>(B_) = rb0;                                                  \
-        *reinterpret_cast<double2 *>(B_ + 16 * LDK) = rb1;                                       \
-        *reinterpret_cast<double2 *>(B_ + 32 * LDK) = rb2;                                       \
-        *reinterpret_cast<double2 *>(B_ + 48 * LDK) = rb3;                                       \
-    }
+    const double *Arow = Ct + (size_t)(it.I * TILE) * Np;      // rows of the I panel
+    const double *Brow = delta + (size_t)w0 * Np;               // walker rows of the tile
 
     f64x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-    QF_GLOAD(0);
-    QF_LSTORE(0);
-    __syncthreads();
+    dma_tile(smem, Arow, Np, kbase0, wave, lane);
+    dma_tile(smem + TILE * BK, Brow, Np, kbase0, wave, lane);
     for (int s = 0; s < nsteps; s++) {
         const int buf = s & 1;
-        if (s + 1 < nsteps) QF_GLOAD(s + 1);        // next tiles in flight under the MFMAs
-        const double *A = smem + buf * 2 * TILE * LDK;
-        const double *brow = A + TILE * LDK + (16 * wave + li) * LDK + lk;
-        const double *arow = A + li * LDK + lk;
-#pragma unroll
-        for (int kk = 0; kk < BK / 4; kk++) {
-            const double b = brow[4 * kk];
-#pragma unroll
-            for (int t = 0; t < 4; t++)
-                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(arow[16 * t * LDK + 4 * kk], b, acc[t], 0, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();                              // tile s landed for every wave; buf^1 free
+        if (s + 1 < nsteps) {
+            double *nb = smem + (buf ^ 1) * 2 * TILE * BK;
+            dma_tile(nb, Arow, Np, kbase0 + (s + 1) * BK, wave, lane);
+            dma_tile(nb + TILE * BK, Brow, Np, kbase0 + (s + 1) * BK, wave, lane);
         }
-        if (s + 1 < nsteps) QF_LSTORE(buf ^ 1);
-        __syncthreads();
+        const double *A = smem + buf * 2 * TILE * BK;
+        const double *B = A + TILE * BK;
+        double2 a[4][4], b[4];
+        {
+            const int r = 16 * wave + li;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                b[q] = *reinterpret_cast<const double2 *>(B + r * BK + (((lk * 4 + q) ^ swz(r)) * 2));
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int r = 16 * t + li;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                a[t][q] = *reinterpret_cast<const double2 *>(A + r * BK + (((lk * 4 + q) ^ swz(r)) * 2));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][q].x, b[q].x, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][q].y, b[q].y, acc[t], 0, 0, 0);
+            }
     }
+    __syncthreads();                                  // all waves done with the operand buffers
     // Delta_I tile: smem[n][i] (row stride TILE+2)
     for (int e = tid; e < TILE * TILE / 2; e += 256) {
         const int r = e >> 5, c2 = (e & 31) * 2;
@@ -214,12 +250,12 @@ __global__ __launch_bounds__(256, 2) void plik_quadform_ksplit(
     sacc += __shfl_xor(sacc, 16);
     sacc += __shfl_xor(sacc, 32);
     double *tile_part = partial + (size_t)tile * n_items * TILE;
-    if (lk == 0) tile_part[(size_t)blockIdx.x * TILE + n] = sacc;
+    if (lk == 0) tile_part[(size_t)item_ix * TILE + n] = sacc;
 
     // ---- in-launch hand-off of the tile's partials to its last-arriving workgroup
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    unsigned int *flag = reinterpret_cast<unsigned int *>(smem);
+    unsigned int *flag = reinterpret_cast<unsigned int *>(smem + 64 * (TILE + 2));
     if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -237,8 +273,7 @@ __global__ __launch_bounds__(256, 2) void plik_quadform_ksplit(
     const int g = tid >> 6;
     double part = 0.0;
     for (int k = g; k < n_items; k += 4) part += tile_part[(size_t)k * TILE + lane];
-    double *red = smem + 8;
-    __syncthreads();
+    double *red = smem + 64 * (TILE + 2) + 8;
     red[g * TILE + lane] = part;
     __syncthreads();
     if (tid < TILE) {
@@ -582,8 +617,8 @@ struct PlikLite final : Like {
         HIP_CHECK(hipGetLastError());
         timed_launch("plik_quadform_ksplit", stream, [&] {
             hipLaunchKernelGGL(plik_quadform_ksplit, dim3(n_items, tiles), dim3(256), 0, stream,
-                               d_invcov.as<double>(), Np, delta, W, d_items[kb].as<Item>(), n_items, partial,
-                               counters, out);
+                               d_invcov.as<double>(), Np, delta, W, d_items[kb].as<Item>(), n_items,
+                               (int)(tiles % 8 == 0), partial, counters, out);
         });
         HIP_CHECK(hipGetLastError());
     }
