@@ -47,12 +47,14 @@ def parse():
     p.add_argument("--steps", type=int, default=500)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--walkers", type=int, default=1024, help="walkers per GPU")
+    p.add_argument("--groups", type=int, default=int(os.environ.get("CMBS_GROUPS", "1")),
+                   help="walker groups stepped on concurrent streams (cmbs_set_groups)")
     p.add_argument("--cpu-seconds", type=float, default=1.5, help="per-process CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
 
 
-def build_problem(W, rank, tmpdir):
+def build_problem(W, rank, tmpdir, groups=1):
     import torch
     from cosmomc_amd import synthetic as syn
     from cosmomc_amd.likelihood import NativeCMBLikelihood
@@ -75,6 +77,7 @@ def build_problem(W, rank, tmpdir):
     smp = BatchedMCMC(W, 7, list(range(1, 8)), [list(range(1, 7)), [7]], 1, pmin, pmax, pm, ps,
                       propose_scale=2.4, seed_ij=1802 + rank, seed_kl=9373, first_walker=rank * W)
     smp.set_covariance(np.diag(sig ** 2))
+    smp.set_groups(groups)
     theory = torch.tensor(syn.walker_theory(W, first_walker=rank * W, n_fields=3, ld_field=2512), device="cuda")
     smp.add_likelihood(like, theory)
     smp.set_start(np.tile(P0, (W, 1)))
@@ -145,7 +148,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     W = args.walkers
     with tempfile.TemporaryDirectory() as td:
-        smp, like, theory, _ = build_problem(W, rank, td)
+        smp, like, theory, _ = build_problem(W, rank, td, args.groups)
 
         def barrier():
             if world > 1:
@@ -198,7 +201,7 @@ def main():
             "config": {"workload": "plik_lite_TTTEEE fast-parameter Metropolis step (BASELINE configs[2] "
                                    "minus lowl/lensing): GetProposalFast + native plik_lite (613 bins, "
                                    "l<=2508, full binning + quadratic form) + calPlanck prior + accept",
-                       "walkers_per_gpu": W, "global_walkers": W * world, "nbins": N_B, "lmax": 2508,
+                       "walkers_per_gpu": W, "stream_groups": args.groups, "global_walkers": W * world, "nbins": N_B, "lmax": 2508,
                        "parallelism": f"walkers sharded over {world} rank(s), no per-step collective",
                        "accept_rate": acc_rate},
             "roofline": roof,

@@ -79,6 +79,7 @@ def lib():
         L.cmbs_add_likelihood.argtypes = [vp, vp, i, vp, ll, ll]
         L.cmbs_set_start.argtypes = [vp, vp, vp]
         L.cmbs_step.argtypes = [vp, i, i, vp]
+        L.cmbs_set_groups.argtypes = [vp, i]
         L.cmbs_enable_history.argtypes = [vp, i]
         L.cmbs_history_stats.argtypes = [vp, i, i, vp, vp, vp]
         L.cmbs_history_count.argtypes = [vp]

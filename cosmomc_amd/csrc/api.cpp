@@ -225,6 +225,11 @@ int cmbs_step(cmbs_t *s, int n_steps, int fast_only, void *stream) {
     return guarded(&s->last_error, [&] { cmamd::sampler_step(s, n_steps, fast_only, (hipStream_t)stream); });
 }
 
+int cmbs_set_groups(cmbs_t *s, int n_groups) {
+    if (!s) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_set_groups(s, n_groups); });
+}
+
 int cmbs_enable_history(cmbs_t *s, int capacity) {
     if (!s || capacity <= 0) return CMBL_ERR_ARG;
     return guarded(&s->last_error, [&] { cmamd::sampler_enable_history(s, capacity); });

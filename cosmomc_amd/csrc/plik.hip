@@ -71,42 +71,21 @@ __global__ __launch_bounds__(256) void plik_bin_delta(
     if (w == 0)
         for (int i = tid; i < n_counters; i += blockDim.x) counters[i] = 0u;
     const double *D = dl + (long long)w * ld_walker;
-    if (vec_ok) {
-        // all 16-byte pieces of the three fields, flattened; every thread's
-        // loads are issued before any product is stored (latency, not
-        // bandwidth, bounds one walker's 51 KB)
-        const int n0 = fr.hi[0] >= fr.lo[0] ? (fr.hi[0] - fr.lo[0] + 1) >> 1 : 0;
-        const int n1 = fr.hi[1] >= fr.lo[1] ? (fr.hi[1] - fr.lo[1] + 1) >> 1 : 0;
-        const int n2 = fr.hi[2] >= fr.lo[2] ? (fr.hi[2] - fr.lo[2] + 1) >> 1 : 0;
-        const int np2 = n0 + n1 + n2;
-        constexpr int PER = 16;                      // pieces per thread per round (<= 4096 per walker)
-        for (int base = 0; base < np2; base += PER * 256) {
-            double2 dv[PER], wv[PER];
-            int loff[PER];
 #pragma unroll
-            for (int j = 0; j < PER; j++) {
-                const int p = base + j * 256 + tid;
-                int f = 0, q = p;
-                if (q >= n0) { q -= n0; f = 1; if (q >= n1) { q -= n1; f = 2; } }
-                const bool ok = p < np2;
-                const int l = fr.lo[f] + 2 * q;
-                loff[j] = ok ? fr.off[f] + 2 * q : -1;
-                const double *src = ok ? D + f * ld_field + l : D;
-                dv[j] = *reinterpret_cast<const double2 *>(src);
-                wv[j] = *reinterpret_cast<const double2 *>(wts + (ok ? l : 0));
+    for (int f = 0; f < 3; f++) {
+        const int lo = fr.lo[f], hi = fr.hi[f];
+        if (hi < lo) continue;
+        const double *Df = D + f * ld_field;
+        double *P = prod + fr.off[f] - lo;
+        if (vec_ok) {
+            // lo is even; pairs (l, l+1), l <= hi (hi odd after alignment)
+#pragma unroll 4
+            for (int l = lo + 2 * tid; l <= hi; l += 2 * blockDim.x) {
+                const double2 d = *reinterpret_cast<const double2 *>(Df + l);
+                const double2 q = *reinterpret_cast<const double2 *>(wts + l);
+                *reinterpret_cast<double2 *>(P + l) = make_double2(d.x * q.x, d.y * q.y);
             }
-#pragma unroll
-            for (int j = 0; j < PER; j++)
-                if (loff[j] >= 0)
-                    *reinterpret_cast<double2 *>(prod + loff[j]) = make_double2(dv[j].x * wv[j].x, dv[j].y * wv[j].y);
-        }
-    } else {
-#pragma unroll
-        for (int f = 0; f < 3; f++) {
-            const int lo = fr.lo[f], hi = fr.hi[f];
-            if (hi < lo) continue;
-            const double *Df = D + f * ld_field;
-            double *P = prod + fr.off[f] - lo;
+        } else {
             const int hs = hi < ld_field ? hi : (int)ld_field - 1;   // never read past the row
 #pragma unroll 4
             for (int l = lo + tid; l <= hs; l += blockDim.x) P[l] = Df[l] * wts[l];

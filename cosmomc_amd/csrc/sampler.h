@@ -6,6 +6,7 @@
 namespace cmamd {
 
 static constexpr int MAXLIKE = 8;
+static constexpr int MAXGROUPS = 8;
 
 // Per-walker state is two row-major SoA arrays in HBM, sd[ND][W] (doubles)
 // and si[NI][W] (ints): row r of walker w at sd[r*W + w].  mh_kernel copies
@@ -81,4 +82,22 @@ struct cmbs {
     size_t mh_lds = 0;
     int hist_cap = 0, hist_count = 0;
     bool started = false;
+    // walker groups: contiguous 64-walker-aligned slices [grp0[g], grp0[g+1]) each
+    // stepped on its own stream so one group's Metropolis kernel and the other
+    // groups' likelihood kernels share the chip (cmbs_set_groups)
+    int n_groups = 1;
+    std::vector<int> grp0{0};
+    hipStream_t streams[cmamd::MAXGROUPS] = {};
+    hipEvent_t events[cmamd::MAXGROUPS + 1] = {};
+    cmamd::DevBuf ws_g[cmamd::MAXGROUPS];
+    ~cmbs() {
+        for (auto &st : streams)
+            if (st) (void)hipStreamDestroy(st);
+        for (auto &e : events)
+            if (e) (void)hipEventDestroy(e);
+    }
 };
+
+namespace cmamd {
+void sampler_set_groups(cmbs *s, int n_groups);
+}

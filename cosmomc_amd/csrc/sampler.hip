@@ -340,12 +340,12 @@ __device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size
 // next trial (GetProposal / GetProposalFast) and scatter its nuisance
 // parameters for the likelihood kernels.  One wavefront per 64 walkers.
 template <bool ACCEPT, bool PROPOSE>
-__global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double *hist_row)
+__global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double *hist_row, int blk0)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Rows &R = c.rows;
     const int lane = threadIdx.x;
-    const int wb = blockIdx.x * NB;
+    const int wb = (blk0 + blockIdx.x) * NB;
     const int w = wb + lane;
     const bool act = w < c.W;
     const size_t W = c.ld;
@@ -772,9 +772,12 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, int nuis_index0, const double
     size_t maxws = 0;
     for (auto &l : s->likes) maxws = std::max(maxws, l.like->like->workspace_size(s->W));
     s->ws.alloc(maxws);
+    if (s->n_groups > 1) sampler_set_groups(s, s->n_groups);   // resize the group workspaces
 }
 
-static void eval_likes(cmbs *s, hipStream_t stream, bool gather) {
+// likelihood terms of walkers [g0, g1) at their trial points
+static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1, void *ws) {
+    const int Wg = g1 - g0;
     for (size_t i = 0; i < s->likes.size(); i++) {
         auto &l = s->likes[i];
         const int nn = l.like->like->n_nuis;
@@ -784,21 +787,24 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather) {
                                s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld, s->W, s->dc.ld, l.nuis0, nn, nb);
             HIP_CHECK(hipGetLastError());
         }
-        l.like->like->loglike_batch(s->W, l.dl, l.ld_field, l.ld_walker, nb, nn,
-                                    s->like_terms.as<double>() + i * (size_t)s->dc.ld, s->ws.p, stream);
+        l.like->like->loglike_batch(Wg, l.dl + (size_t)g0 * l.ld_walker, l.ld_field, l.ld_walker,
+                                    nb + (size_t)g0 * nn, nn, s->like_terms.as<double>() + i * (size_t)s->dc.ld + g0,
+                                    ws, stream);
     }
 }
 
-static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, double *row, hipStream_t stream) {
-    const dim3 g((s->W + NB - 1) / NB), b(NB);
+static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, double *row, hipStream_t stream, int g0,
+                      int g1) {
+    const dim3 g((g1 - g0 + NB - 1) / NB), b(NB);
+    const int blk0 = g0 / NB;
     const size_t lds = s->mh_lds;
     timed_launch("mh_kernel", stream, [&] {
         if (accept && propose)
-            hipLaunchKernelGGL((mh_kernel<true, true>), g, b, lds, stream, s->dc, fast_only, row);
+            hipLaunchKernelGGL((mh_kernel<true, true>), g, b, lds, stream, s->dc, fast_only, row, blk0);
         else if (accept)
-            hipLaunchKernelGGL((mh_kernel<true, false>), g, b, lds, stream, s->dc, fast_only, row);
+            hipLaunchKernelGGL((mh_kernel<true, false>), g, b, lds, stream, s->dc, fast_only, row, blk0);
         else
-            hipLaunchKernelGGL((mh_kernel<false, true>), g, b, lds, stream, s->dc, fast_only, row);
+            hipLaunchKernelGGL((mh_kernel<false, true>), g, b, lds, stream, s->dc, fast_only, row, blk0);
     });
     HIP_CHECK(hipGetLastError());
 }
@@ -810,7 +816,7 @@ void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream) {
         for (int i = 0; i < s->np; i++) t[(size_t)i * s->W + w] = P0[(size_t)w * s->np + i];
     HIP_CHECK(hipMemcpy2DAsync(s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld, (size_t)s->dc.ld * 8, t.data(),
                                (size_t)s->W * 8, (size_t)s->W * 8, s->np, hipMemcpyHostToDevice, stream));
-    eval_likes(s, stream, true);
+    eval_likes(s, stream, true, 0, s->W, s->ws.p);
     hipLaunchKernelGGL(start_kernel, dim3((s->W + 255) / 256), dim3(256), 0, stream, s->dc);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(stream));
@@ -828,13 +834,50 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
         return row;
     };
     // propose(1) | likes | accept(1)+propose(2) | likes | ... | likes | accept(n)
-    launch_mh(s, false, true, fast_only, nullptr, stream);
-    eval_likes(s, stream, false);
-    for (int k = 1; k < n_steps; k++) {
-        launch_mh(s, true, true, fast_only, next_row(), stream);
-        eval_likes(s, stream, false);
+    const int G = s->n_groups;
+    if (G == 1) {
+        launch_mh(s, false, true, fast_only, nullptr, stream, 0, s->W);
+        eval_likes(s, stream, false, 0, s->W, s->ws.p);
+        for (int k = 1; k < n_steps; k++) {
+            launch_mh(s, true, true, fast_only, next_row(), stream, 0, s->W);
+            eval_likes(s, stream, false, 0, s->W, s->ws.p);
+        }
+        launch_mh(s, true, false, fast_only, next_row(), stream, 0, s->W);
+        return;
     }
-    launch_mh(s, true, false, fast_only, next_row(), stream);
+    // groups are independent chains: fork from the caller's stream, issue the
+    // step chain of every group breadth-first so the queues interleave, join
+    HIP_CHECK(hipEventRecord(s->events[MAXGROUPS], stream));
+    for (int g = 0; g < G; g++) HIP_CHECK(hipStreamWaitEvent(s->streams[g], s->events[MAXGROUPS], 0));
+    for (int k = 0; k <= n_steps; k++) {
+        double *row = k > 0 ? next_row() : nullptr;
+        for (int g = 0; g < G; g++) {
+            const int g0 = s->grp0[g], g1 = s->grp0[g + 1];
+            launch_mh(s, k > 0, k < n_steps, fast_only, row, s->streams[g], g0, g1);
+            if (k < n_steps) eval_likes(s, s->streams[g], false, g0, g1, s->ws_g[g].p);
+        }
+    }
+    for (int g = 0; g < G; g++) {
+        HIP_CHECK(hipEventRecord(s->events[g], s->streams[g]));
+        HIP_CHECK(hipStreamWaitEvent(stream, s->events[g], 0));
+    }
+}
+
+void sampler_set_groups(cmbs *s, int n_groups) {
+    const int nblk = (s->W + NB - 1) / NB;
+    if (n_groups < 1 || n_groups > MAXGROUPS) fail(CMBL_ERR_ARG, "n_groups must be in 1..%d", MAXGROUPS);
+    if (n_groups > nblk) n_groups = nblk;
+    s->grp0.assign(n_groups + 1, 0);
+    for (int g = 0; g <= n_groups; g++) s->grp0[g] = std::min(s->W, (int)((long long)nblk * g / n_groups) * NB);
+    for (int g = 0; g < n_groups; g++) {
+        if (!s->streams[g]) HIP_CHECK(hipStreamCreateWithFlags(&s->streams[g], hipStreamNonBlocking));
+        size_t ws = 0;
+        for (auto &l : s->likes) ws = std::max(ws, l.like->like->workspace_size(s->grp0[g + 1] - s->grp0[g]));
+        s->ws_g[g].alloc(ws);
+    }
+    for (auto &e : s->events)
+        if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    s->n_groups = n_groups;
 }
 
 void sampler_enable_history(cmbs *s, int capacity) {

@@ -87,6 +87,11 @@ class BatchedMCMC:
         p = np.ascontiguousarray(P0, dtype=np.float64).reshape(self.W, self.np)
         self._check(N.lib().cmbs_set_start(self._h, p.ctypes.data, stream))
 
+    def set_groups(self, n_groups: int):
+        """Step the walkers as ``n_groups`` slices on concurrent internal
+        streams (cmbs_set_groups; execution tuning, results unchanged)."""
+        self._check(N.lib().cmbs_set_groups(self._h, int(n_groups)))
+
     def step(self, n_steps: int = 1, fast_only: bool = False, stream=None):
         if stream is None:
             stream = N.current_stream_ptr()

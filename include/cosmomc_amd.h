@@ -156,6 +156,12 @@ int  cmbs_set_start(cmbs_t *s, const double *P0, void *stream);
  * Asynchronous on stream. */
 int  cmbs_step(cmbs_t *s, int n_steps, int fast_only, void *stream);
 
+/* Execution tuning (no reference counterpart; results are unchanged): split the
+ * walkers into n_groups 64-aligned slices, each stepped on an internal stream
+ * forked from / joined to the caller's, so the Metropolis kernel of one slice
+ * overlaps the likelihood kernels of the others.  Default 1. */
+int  cmbs_set_groups(cmbs_t *s, int n_groups);
+
 /* Optional history capture for convergence statistics: every step appends
  * each walker's current used-parameter vector to a device ring of `capacity`
  * steps (SampleCollector AddNewPoint, SampleCollector.f90:324-456). */

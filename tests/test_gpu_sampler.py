@@ -149,3 +149,40 @@ def test_history_stats():
     cov = np.einsum("twi,twj->wij", d, d) / x.shape[0]
     np.testing.assert_allclose(m.cpu().numpy(), mu, rtol=1e-12, atol=1e-14)
     np.testing.assert_allclose(c.cpu().numpy(), cov, rtol=1e-10, atol=1e-13)
+
+
+@pytest.mark.parametrize("groups", [2, 3, 8])
+def test_walker_groups_same_chains(tmp_path, groups):
+    """cmbs_set_groups only changes how the step is scheduled: every walker's
+    chain is the one the single-stream path produces (the quadratic-form
+    split may differ with the group size, so -lnL agrees to rounding and the
+    accept decisions exactly)."""
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    data = syn.make_plik_lite(12345)
+    like = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    like.nuisance_indices = [2]
+    W, steps = 200, 25
+    dl = torch.tensor(syn.walker_theory(W, seed=4, n_fields=3), device="cuda")
+    P0 = np.array([0.0222, 1.0])
+    pmin, pmax = np.array([0.0222, 0.9]), np.array([0.0222, 1.1])
+    pm, ps = np.array([0.0, 1.0]), np.array([0.0, 0.0025])
+    runs = []
+    for g in (1, groups):
+        s = BatchedMCMC(W, 2, [2], [[1]], 0, pmin, pmax, pm, ps, propose_scale=2.4, seed_ij=3, seed_kl=4)
+        s.set_covariance(np.array([[0.002 ** 2]]))
+        s.set_groups(g)
+        s.add_likelihood(like, dl)
+        s.set_start(np.tile(P0, (W, 1)))
+        s.enable_history(steps)
+        s.step(steps, fast_only=True)
+        P, lk, mult, nacc = s.state()
+        m, _ = s.history_stats(0, steps - 1)
+        runs.append((P.copy(), lk.copy(), mult.copy(), nacc.copy(), m.cpu().numpy()))
+        s.close()
+    a, b = runs
+    np.testing.assert_array_equal(a[3], b[3])
+    np.testing.assert_array_equal(a[2], b[2])
+    np.testing.assert_allclose(b[0], a[0], rtol=1e-12)
+    np.testing.assert_allclose(b[1], a[1], rtol=1e-10)
+    np.testing.assert_allclose(b[4], a[4], rtol=1e-12)
