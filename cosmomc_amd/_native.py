@@ -13,7 +13,8 @@ import subprocess
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "lib", "libcosmomc_amd.so")
+# COSMOMC_AMD_LIB selects an instrumented build of the same sources (tools/)
+LIB_PATH = os.environ.get("COSMOMC_AMD_LIB") or os.path.join(PKG, "lib", "libcosmomc_amd.so")
 HEADER = os.path.join(ROOT, "include", "cosmomc_amd.h")
 
 CMBL_LOGZERO = 1e30

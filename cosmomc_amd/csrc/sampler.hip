@@ -294,6 +294,19 @@ __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const 
     return like;
 }
 
+// Phase timestamps (s_memtime) of the first 64 mh_kernel blocks, only in the
+// instrumented build (make EXTRA=-DCMAMD_STAMPS; tools/mh_stamps.py).
+#ifdef CMAMD_STAMPS
+__device__ unsigned long long g_stamps[64][8];
+#define STAMP(i)                                                                                \
+    do {                                                                                        \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                            \
+        if (ACCEPT && PROPOSE && lane == 0 && blockIdx.x < 64) g_stamps[blockIdx.x][i] = t_;                         \
+    } while (0)
+#else
+#define STAMP(i) ((void)0)
+#endif
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void gbl_void_t;
 
@@ -363,6 +376,7 @@ __global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double 
     // staged double row index of global row r (rotation rows dropped when not staged)
 #define SROW(r) ((skipR && (r) >= R.R) ? (r) - R.RR : (r))
 
+    STAMP(0);
     const int rEnd = R.R + R.RR;
     if (skipR) {
         dma_rows_f64(sd, 0, c.sd, 0, R.R, W, wb, lane);
@@ -374,8 +388,10 @@ __global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double 
     dma_rows_i32(si, c.si, R.NI, W, wb, lane);
     dma_words(td, c.tab_d, 2 * c.tl.n_dbl, lane);
     dma_words(ti, c.tab_i, c.tl.n_int, lane);
+    STAMP(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    STAMP(2);
     if (!act) return;
 
     const Tabs t = make_tabs(c, ti, td);
@@ -417,6 +433,7 @@ __global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double 
         if (hist_row)
             for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = k.P[t.params_used[i]];
     }
+    STAMP(3);
     if (PROPOSE) {
         for (int i = 0; i < c.np; i++) k.trial[i] = k.P[i];          // Trial = CurParams
         if (fast_only) proposal_fast(c, t, k);
@@ -425,6 +442,7 @@ __global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double 
             for (int q = 0; q < c.like_nn[l]; q++)
                 c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = k.trial[c.like_nuis0[l] + q];
     }
+    STAMP(4);
     sd[(size_t)R.C * NB + lane] = k.r.c;
     sd[(size_t)R.G * NB + lane] = k.r.gset;
     si[(size_t)R.I97 * NB + lane] = k.r.i97;
@@ -438,6 +456,11 @@ __global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double 
         stage_out(c.sd, sd, 0, 0, R.ND, W, w, lane);
     }
     stage_out(c.si, si, 0, 0, R.NI, W, w, lane);
+    STAMP(5);
+#ifdef CMAMD_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(6);
+#endif
 #undef SROW
 }
 
@@ -914,3 +937,9 @@ void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, 
 }
 
 }  // namespace cmamd
+
+#ifdef CMAMD_STAMPS
+extern "C" int cmamd_debug_stamps(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_stamps), sizeof(cmamd::g_stamps)) == hipSuccess ? 0 : -5;
+}
+#endif

@@ -2,8 +2,8 @@
 # bench.py over a walker-count sweep (no CPU baseline, no profiler)
 set -u
 mkdir -p gpurun_out
-# usage: gpu_sweep.sh W... ; GROUPS="1 2 4" sweeps stream groups too
-for G in ${GROUPS:-1}; do
+# usage: gpu_sweep.sh W... ; STREAM_GROUPS="1 2 4" sweeps stream groups too
+for G in ${STREAM_GROUPS:-1}; do
 for W in "$@"; do
   f=gpurun_out/sweep_W${W}_G$G
   timeout -k 10 180 python bench.py --no-cpu-baseline --walkers $W --groups $G > $f.json 2> $f.err
