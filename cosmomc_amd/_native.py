@@ -81,6 +81,7 @@ def lib():
         L.cmbs_set_start.argtypes = [vp, vp, vp]
         L.cmbs_step.argtypes = [vp, i, i, vp]
         L.cmbs_set_groups.argtypes = [vp, i]
+        L.cmbs_chain_moments.argtypes = [vp, i, i, vp, vp, vp]
         L.cmbs_enable_history.argtypes = [vp, i]
         L.cmbs_history_stats.argtypes = [vp, i, i, vp, vp, vp]
         L.cmbs_history_count.argtypes = [vp]

@@ -225,6 +225,12 @@ int cmbs_step(cmbs_t *s, int n_steps, int fast_only, void *stream) {
     return guarded(&s->last_error, [&] { cmamd::sampler_step(s, n_steps, fast_only, (hipStream_t)stream); });
 }
 
+int cmbs_chain_moments(cmbs_t *s, int first, int last, const double *gmean, double *out, void *stream) {
+    if (!s || !out) return CMBL_ERR_ARG;
+    return guarded(&s->last_error,
+                   [&] { cmamd::sampler_chain_moments(s, first, last, gmean, out, (hipStream_t)stream); });
+}
+
 int cmbs_set_groups(cmbs_t *s, int n_groups) {
     if (!s) return CMBL_ERR_ARG;
     return guarded(&s->last_error, [&] { cmamd::sampler_set_groups(s, n_groups); });

@@ -70,7 +70,7 @@ struct cmbs {
     int W = 0, np = 0, n_used = 0;
     std::vector<int> params_used;
     std::string last_error;
-    cmamd::DevBuf tab_i, tab_d, sd, si, like_terms, ws, hist;
+    cmamd::DevBuf tab_i, tab_d, sd, si, like_terms, ws, hist, mom;
     cmamd::DevBuf nuis_bufs[cmamd::MAXLIKE];
     std::vector<int> h_tab_i;
     std::vector<double> h_tab_d;
@@ -100,4 +100,5 @@ struct cmbs {
 
 namespace cmamd {
 void sampler_set_groups(cmbs *s, int n_groups);
+void sampler_chain_moments(cmbs *s, int first, int last, const double *gmean, double *out, hipStream_t stream);
 }

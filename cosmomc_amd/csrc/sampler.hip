@@ -512,6 +512,52 @@ __global__ void hist_stats_kernel(const double *hist, int cap, int W, int n, int
     for (int i = 0; i < n * n; i++) C[i] /= cnt;
 }
 
+// Per-GPU partial sums of the chain moments for the convergence exchange
+// (TMpiChainCollector_UpdateCovAndCheckConverge, SampleCollector.f90:233-286):
+// every walker is one chain with count = last-first+1 samples.
+//   gmean == nullptr : out = [S0 = sum count, sum count*m (n), sum count*cov (n*n),
+//                             sum cov (n*n), number of chains]
+//   gmean != nullptr : out = sum count*(m-gmean)(m-gmean)^T (n*n)
+// One block; each thread owns a fixed strided set of walkers and the partials
+// are combined in a fixed tree order, so the sums are deterministic.
+__global__ __launch_bounds__(256) void chain_moments_kernel(const double *means, const double *covs, int W, int n,
+                                                           double count, const double *gmean, double *out)
+{
+    __shared__ double red[256];
+    const int nout = gmean ? n * n : 2 + n + 2 * n * n;
+    for (int o = 0; o < nout; o++) {
+        double acc = 0.0;
+        for (int w = threadIdx.x; w < W; w += 256) {
+            const double *m = means + (size_t)w * n;
+            const double *C = covs + (size_t)w * n * n;
+            double v;
+            if (gmean) {
+                const int i = o / n, j = o % n;
+                v = count * (m[i] - gmean[i]) * (m[j] - gmean[j]);
+            } else if (o == 0) {
+                v = count;
+            } else if (o <= n) {
+                v = count * m[o - 1];
+            } else if (o <= n + n * n) {
+                v = count * C[o - 1 - n];
+            } else if (o <= n + 2 * n * n) {
+                v = C[o - 1 - n - n * n];
+            } else {
+                v = 1.0;
+            }
+            acc += v;
+        }
+        red[threadIdx.x] = acc;
+        __syncthreads();
+        for (int h = 128; h > 0; h >>= 1) {
+            if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[o] = red[0];
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------ host side
 
 static size_t mh_lds_bytes(const cmbs *s, int stage_R) {
@@ -916,6 +962,16 @@ void sampler_history_stats(cmbs *s, int first, int last, double *means, double *
              s->hist_count, s->hist_cap);
     hipLaunchKernelGGL(hist_stats_kernel, dim3((s->W + 127) / 128), dim3(128), 0, stream, s->hist.as<double>(),
                        s->hist_cap, s->W, s->n_used, first, last, means, covs);
+    HIP_CHECK(hipGetLastError());
+}
+
+void sampler_chain_moments(cmbs *s, int first, int last, const double *gmean, double *out, hipStream_t stream) {
+    const int n = s->n_used;
+    s->mom.grow((size_t)s->W * (n + n * n) * 8);
+    double *means = s->mom.as<double>(), *covs = means + (size_t)s->W * n;
+    sampler_history_stats(s, first, last, means, covs, stream);
+    hipLaunchKernelGGL(chain_moments_kernel, dim3(1), dim3(256), 0, stream, means, covs, s->W, n,
+                       (double)(last - first + 1), gmean, out);
     HIP_CHECK(hipGetLastError());
 }
 

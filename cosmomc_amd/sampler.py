@@ -113,6 +113,20 @@ class BatchedMCMC:
                                                N.current_stream_ptr()))
         return means, covs
 
+    def chain_moments(self, first: int, last: int, gmean=None):
+        """This GPU's partial sums for the convergence exchange (cmbs_chain_moments)."""
+        import torch
+        n = len(self.params_used)
+        out = torch.empty(2 + n + 2 * n * n if gmean is None else n * n, dtype=torch.float64, device="cuda")
+        g = None
+        if gmean is not None:
+            g = torch.as_tensor(gmean, dtype=torch.float64, device="cuda").contiguous()
+        self._check(N.lib().cmbs_chain_moments(self._h, first, last, None if g is None else g.data_ptr(),
+                                               out.data_ptr(), N.current_stream_ptr()))
+        return out
+
+    device = "cuda"
+
     def state(self):
         P = np.empty((self.W, self.np))
         like = np.empty(self.W)

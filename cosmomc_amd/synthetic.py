@@ -222,3 +222,15 @@ def walker_theory(n_walkers: int, seed: int = 0xC05A0C, lmax: int = PLMAX,
 def walker_calibrations(n_walkers: int, seed: int = 0xCA1, first_walker: int = 0) -> np.ndarray:
     g = gaussians(seed, first_walker + n_walkers)[first_walker:]
     return 1.0 + 0.0025 * g
+
+
+def chain_ensemble(n_chains: int, n_samples: int, n: int, seed: int, spread: float) -> np.ndarray:
+    """Samples [n_chains, n_samples, n] of correlated Gaussian 'chains' whose
+    centres scatter by ``spread`` (in units of the marginal width): a
+    convergence-statistics test input with R-1 of order spread^2."""
+    g = gaussians(seed, n * n + n_chains * n + n_chains * n_samples * n)
+    A = g[:n * n].reshape(n, n)
+    L = np.linalg.cholesky(np.eye(n) + 0.5 * (A @ A.T) / n)
+    off = spread * g[n * n:n * n + n_chains * n].reshape(n_chains, n)
+    z = g[n * n + n_chains * n:].reshape(n_chains, n_samples, n)
+    return (off[:, None, :] + z) @ L.T

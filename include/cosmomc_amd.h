@@ -171,6 +171,16 @@ int  cmbs_enable_history(cmbs_t *s, int capacity);
  * (SampleCollector.f90:235-246 "second half" window is first = count/2). */
 int  cmbs_history_stats(cmbs_t *s, int first, int last, double *means, double *covs, void *stream);
 int  cmbs_history_count(const cmbs_t *s);
+/* This GPU's partial sums for the convergence / proposal-learning exchange
+ * (TMpiChainCollector_UpdateCovAndCheckConverge, SampleCollector.f90:212-322):
+ * each walker is one chain whose samples are history rows [first, last].
+ * Device out:
+ *   gmean == NULL: [sum count, sum count*mean (n), sum count*cov (n*n),
+ *                   sum cov (n*n), number of chains]      (2 + n + 2n^2)
+ *   gmean != NULL: sum count*(mean-gmean)(mean-gmean)^T    (n^2)
+ * where n = n_used.  Summed over GPUs these give the reference's pooled
+ * mean, MPICovMat, mean-of-covariances and covariance-of-means. */
+int  cmbs_chain_moments(cmbs_t *s, int first, int last, const double *gmean, double *out, void *stream);
 
 /* Device pointers of the walker state (valid until destroy), walker-minor:
  * P [num_params][W], cur_like [W], mult [W] (double), num_accept [W] (int). */

@@ -160,8 +160,42 @@ def gen_rng():
         json.dump(out, f, indent=0)
 
 
+# convergence cases: (name, chains, samples per chain, n_used, centre spread, seed)
+GR_CASES = [("gr_n3_m8", 8, 400, 3, 0.3, 501), ("gr_n6_m16", 16, 301, 6, 0.05, 502),
+            ("gr_n2_m4", 4, 1000, 2, 1.0, 503), ("gr_n7_m32", 32, 120, 7, 0.01, 504)]
+
+
+def gen_gr():
+    """GelmanRubinEvalues of the compiled reference on the pooled statistics of
+    synthetic chain ensembles (cosmomc_amd.synthetic.chain_ensemble)."""
+    sys.path.insert(0, HERE)
+    import pyoracle as po
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for name, M, T, n, spread, seed in GR_CASES:
+            x = syn.chain_ensemble(M, T, n, seed, spread)
+            st = po.pool_chain_statistics(list(x))
+            # Fortran reads column-major: transpose so cov(i,j) is row i col j
+            lines = [x_ for x_ in run_rng("gr", f"{n}\n{_fmt(st['cov'].T)}\n{_fmt(st['meanscov'].T)}\n", td)
+                     if x_.strip()]
+            ok = int(lines[0])
+            ev = [float(v) for v in lines[1:]]
+            out[name] = {"chains": M, "samples": T, "n": n, "spread": spread, "seed": seed, "ok": ok,
+                         "evals": ev, "R": max(ev), "mean": st["mean"].tolist(),
+                         "propose_cov": st["propose_cov"].tolist(), "cov": st["cov"].tolist(),
+                         "meanscov": st["meanscov"].tolist()}
+            print(f"{name}: R-1 = {max(ev):.6e}")
+    with open(os.path.join(GOLDEN, "gr_ref.json"), "w") as f:
+        json.dump(out, f, indent=0)
+
+
 if __name__ == "__main__":
     if not os.path.exists(os.path.join(REF_DIR, "plik_harness")):
         sys.exit("build the reference first: make -C oracle ref")
-    gen_plik()
-    gen_rng()
+    only = sys.argv[1:]
+    if not only or "plik" in only:
+        gen_plik()
+    if not only or "rng" in only:
+        gen_rng()
+    if not only or "gr" in only:
+        gen_gr()

@@ -141,3 +141,47 @@ class PlikLite:
         if getattr(self, "h", None):
             lib().orc_plik_free(self.h)
             self.h = None
+
+
+def pool_chain_statistics(samples):
+    """TMpiChainCollector_UpdateCovAndCheckConverge pooling (SampleCollector.f90:233-286)
+    restated with explicit loops: samples [M chains][Count][n]; each chain uses
+    Items Count/2 .. Count (1-based, inclusive).  Returns the count-weighted
+    pooled mean, MPICovMat (count-weighted mean of the chain covariances, the
+    learnt proposal), cov (plain mean of covariances) and meanscov (weighted
+    covariance of the chain means times M/(M-1))."""
+    M = len(samples)
+    n = samples[0].shape[1]
+    counts, means, covs = [], [], []
+    for x in samples:
+        cnt = x.shape[0]
+        lo = cnt // 2                       # 1-based Count/2 -> 0-based lo-1
+        rows = x[lo - 1:cnt]
+        c0 = cnt - cnt // 2 + 1
+        m = np.zeros(n)
+        for r in rows:
+            m += r
+        m /= c0
+        C = np.zeros((n, n))
+        for r in rows:
+            d = r - m
+            C += np.outer(d, d)
+        counts.append(float(c0)); means.append(m); covs.append(C / c0)
+    w = np.array(counts)
+    norm = w.sum()
+    mean = sum(w[c] * means[c] for c in range(M)) / norm
+    mpicov = np.zeros((n, n)); cov = np.zeros((n, n)); meanscov = np.zeros((n, n))
+    for i in range(n):
+        for j in range(i, n):
+            mpicov[i, j] = sum(w[c] * covs[c][i, j] for c in range(M)) / norm
+            cov[i, j] = sum(covs[c][i, j] for c in range(M)) / M
+            meanscov[i, j] = sum(w[c] * (means[c][i] - mean[i]) * (means[c][j] - mean[j]) for c in range(M)) / norm
+            mpicov[j, i], cov[j, i], meanscov[j, i] = mpicov[i, j], cov[i, j], meanscov[i, j]
+    meanscov = meanscov * M / (M - 1)
+    return {"counts": w, "mean": mean, "propose_cov": mpicov, "cov": cov, "meanscov": meanscov}
+
+
+def gelman_rubin(cov, meanscov):
+    """max eigenvalue of GelmanRubinEvalues (samples.f90:41-67); 1e6 if not invertible."""
+    n = cov.shape[0]
+    return lib().orc_gelman_rubin(np.ascontiguousarray(cov), np.ascontiguousarray(meanscov), n)

@@ -6,6 +6,8 @@
 !
 !   mode "kat"    : RANMAR known-answer test (RandUtils.f90:262-283)
 !   mode "stream" : ranmar / Gaussian1 / randexp1 / RandIndices / RandRotationD
+!   mode "gr"     : GelmanRubinEvalues (samples.f90:41-67) on a given
+!                   (mean-of-covariances, covariance-of-means) pair
 !   mode "chain"  : BlockedProposer + Metropolis chain on the test_likelihood
 !                   Gaussian (calclike.f90:180-199) with hard bounds
 !                   (calclike.f90:97-109) and Gaussian priors (:111-134).
@@ -14,13 +16,14 @@
 !                   (their modules drag in every likelihood); the RNG,
 !                   proposer, Cholesky and inverse are the reference's own code.
 !
-! usage: rng_harness kat|stream|chain <config.txt> <out.txt>
+! usage: rng_harness kat|stream|chain|gr <config.txt> <out.txt>
 program rng_harness
     use settings
     use RandUtils
     use GeneralTypes
     use MatrixUtils
     use propose
+    use Samples, only: GelmanRubinEvalues
     implicit none
     character(LEN=1024) :: mode, cfg, outf
     integer :: u_in, u_out, i, j, k, n, nsteps, nblocks, slow_block_max, oversample, ij, kl, nrot
@@ -33,6 +36,7 @@ program rng_harness
     Type(BlockedProposer) :: Prop
     logical :: accpt
     real :: e
+    real(mcp), allocatable :: mcov(:,:), evals(:)
 
     call get_command_argument(1, mode)
     call get_command_argument(2, cfg)
@@ -49,6 +53,16 @@ program rng_harness
         do i = 1, 6
             write(u_out, '(F12.1)') 4096.d0*4096.d0*ranmar()
         end do
+    case ('gr')
+        open(newunit=u_in, file=trim(cfg), status='old')
+        read(u_in, *) n
+        allocate(cov(n, n), mcov(n, n), evals(n))
+        read(u_in, *) cov
+        read(u_in, *) mcov
+        close(u_in)
+        accpt = GelmanRubinEvalues(cov, mcov, evals, n)
+        write(u_out, '(I2)') merge(1, 0, accpt)
+        if (accpt) write(u_out, '(ES25.17)') evals
     case ('stream')
         open(newunit=u_in, file=trim(cfg), status='old')
         read(u_in, *) ij, kl, n, nidx, nrot

@@ -27,3 +27,8 @@ def plik_golden():
 @pytest.fixture(scope="session")
 def rng_golden():
     return load_golden("rng_sampler_ref.json")
+
+
+@pytest.fixture(scope="session")
+def gr_golden():
+    return load_golden("gr_ref.json")

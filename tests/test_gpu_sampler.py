@@ -186,3 +186,34 @@ def test_walker_groups_same_chains(tmp_path, groups):
     np.testing.assert_allclose(b[0], a[0], rtol=1e-12)
     np.testing.assert_allclose(b[1], a[1], rtol=1e-10)
     np.testing.assert_allclose(b[4], a[4], rtol=1e-12)
+
+
+def test_convergence_exchange_on_device():
+    """cmbs_chain_moments + ConvergenceExchange (world 1) == the reference
+    pooling restated in the oracle over the same per-walker trajectories."""
+    from cosmomc_amd.converge import CollectorSettings, ConvergenceExchange, reference_window
+    from cosmomc_amd.sampler import BatchedMCMC
+    n, W, T = 3, 70, 60
+    s = BatchedMCMC(W, n, [1, 2, 3], [[1, 2], [3]], 1, [-10] * 3, [10] * 3, seed_ij=17, seed_kl=18)
+    cov = np.array([[1.0, 0.3, 0.1], [0.3, 2.0, 0.2], [0.1, 0.2, 0.5]])
+    s.set_covariance(cov)
+    s.set_test_gaussian(cov, np.zeros(n))
+    s.set_start(np.tile([0.5, -0.5, 0.2], (W, 1)))
+    s.enable_history(T)
+    traj = []
+    for _ in range(T):
+        s.step(1)
+        traj.append(s.state()[0].copy())
+    traj = np.array(traj).transpose(1, 0, 2)          # [W, T, n]
+    ref = po.pool_chain_statistics(list(traj))
+    first, last = reference_window(T)
+    ex = ConvergenceExchange(n, CollectorSettings(MPI_Min_Sample_Update=20))
+    r = ex.update_cov_and_check_converge(s, first, last)
+    np.testing.assert_allclose(r.mean, ref["mean"], rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(r.propose_cov, ref["propose_cov"], rtol=1e-10, atol=1e-14)
+    np.testing.assert_allclose(r.cov, ref["cov"], rtol=1e-10, atol=1e-14)
+    np.testing.assert_allclose(r.meanscov, ref["meanscov"], rtol=1e-8, atol=1e-14)
+    assert r.R == pytest.approx(po.gelman_rubin(ref["cov"], ref["meanscov"]), rel=1e-8)
+    s.set_covariance(r.propose_cov)                   # learnt proposal (SetCovariance, :317)
+    s.step(5)
+    assert np.all(np.isfinite(s.state()[1]))
