@@ -133,6 +133,24 @@ def cpu_baseline(seconds):
                 "sample": f"C restatement oracle/liboracle.so, 1 thread, {seconds:g} s"}
 
 
+def pmc_traffic(kernel, W):
+    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC pass
+    (tools/gpu_pmc.sh -> tools/pmc_summary.py, FETCH_SIZE x2 + WRITE_SIZE per the
+    MI355X guide) when it was taken at this walker count; else null."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("walkers") != W:
+        return None, None
+    t = d["per_launch"].get(kernel)
+    if not t:
+        return None, None
+    return t["fetch_bytes"] + t["write_bytes"], "profiles/pmc_traffic.json"
+
+
 def main():
     args = parse()
     import torch
@@ -192,6 +210,7 @@ def main():
         roof = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": (ach / PEAK_HBM_GBS) if ach else None, "traffic": None}
     roof["avg_kernel_us"] = {k: (v * 1e3 if v else None) for k, v in avg_ms.items()}
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(dom, W)
 
     if rank == 0:
         out = {

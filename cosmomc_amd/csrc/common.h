@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdarg>
 #include <cstdio>
@@ -104,16 +105,18 @@ struct Profiler {
 };
 Profiler &profiler();
 
+// launch(start, stop) must pass the two events to hipExtLaunchKernelGGL, which
+// stamps them from the kernel's own dispatch (the same interval rocprofv3
+// reports), not from separate queue packets around it; null when profiling is off.
 template <class F> inline void timed_launch(const char *name, hipStream_t stream, F &&launch) {
     Profiler &p = profiler();
     if (!p.on) {
-        launch();
+        launch(hipEvent_t(nullptr), hipEvent_t(nullptr));
         return;
     }
+    (void)stream;
     Profiler::Rec r{p.get(), p.get()};
-    (void)hipEventRecord(r.a, stream);
-    launch();
-    (void)hipEventRecord(r.b, stream);
+    launch(r.a, r.b);
     p.pending[name].push_back(r);
     if (p.pending[name].size() > 4096) p.collect();
 }

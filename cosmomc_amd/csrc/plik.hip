@@ -588,14 +588,14 @@ struct PlikLite final : Like {
         int vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && (ld_field % 2 == 0) && (ld_walker % 2 == 0);
         for (int f = 0; f < 3; f++)
             if (fr.hi[f] >= fr.lo[f] && fr.hi[f] >= ld_field) vec_ok = 0;
-        timed_launch("plik_bin_delta", stream, [&] {
-            hipLaunchKernelGGL(plik_bin_delta, dim3(W), dim3(256), (size_t)lds_doubles * 8, stream, dl, ld_field,
+        timed_launch("plik_bin_delta", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            hipExtLaunchKernelGGL(plik_bin_delta, dim3(W), dim3(256), (size_t)lds_doubles * 8, stream, e0, e1, 0, dl, ld_field,
                                ld_walker, nuis, ld_nuis, d_wts.as<double>(), d_bins.as<BinInfo>(), d_X.as<double>(),
                                nused, Np, fr, vec_ok, delta, counters, tiles);
         });
         HIP_CHECK(hipGetLastError());
-        timed_launch("plik_quadform_ksplit", stream, [&] {
-            hipLaunchKernelGGL(plik_quadform_ksplit, dim3(n_items, tiles), dim3(256), 0, stream,
+        timed_launch("plik_quadform_ksplit", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            hipExtLaunchKernelGGL(plik_quadform_ksplit, dim3(n_items, tiles), dim3(256), 0, stream, e0, e1, 0,
                                d_invcov.as<double>(), Np, delta, W, d_items[kb].as<Item>(), n_items,
                                (int)(tiles % 8 == 0), partial, counters, out);
         });

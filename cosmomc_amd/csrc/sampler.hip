@@ -867,13 +867,13 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, double 
     const dim3 g((g1 - g0 + NB - 1) / NB), b(NB);
     const int blk0 = g0 / NB;
     const size_t lds = s->mh_lds;
-    timed_launch("mh_kernel", stream, [&] {
+    timed_launch("mh_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
         if (accept && propose)
-            hipLaunchKernelGGL((mh_kernel<true, true>), g, b, lds, stream, s->dc, fast_only, row, blk0);
+            hipExtLaunchKernelGGL(mh_kernel<true, true>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row, blk0);
         else if (accept)
-            hipLaunchKernelGGL((mh_kernel<true, false>), g, b, lds, stream, s->dc, fast_only, row, blk0);
+            hipExtLaunchKernelGGL(mh_kernel<true, false>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row, blk0);
         else
-            hipLaunchKernelGGL((mh_kernel<false, true>), g, b, lds, stream, s->dc, fast_only, row, blk0);
+            hipExtLaunchKernelGGL(mh_kernel<false, true>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row, blk0);
     });
     HIP_CHECK(hipGetLastError());
 }
