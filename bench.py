@@ -145,7 +145,8 @@ def pmc_traffic(kernel, W):
         return None, None
     if d.get("walkers") != W:
         return None, None
-    t = d["per_launch"].get(kernel)
+    symbol = {"plik_quadform_ksplit": "quadform_ksplit"}.get(kernel, kernel)   # profiler label -> kernel
+    t = d["per_launch"].get(symbol)
     if not t:
         return None, None
     return t["fetch_bytes"] + t["write_bytes"], "profiles/pmc_traffic.json"

@@ -1,0 +1,55 @@
+// Batched symmetric quadratic form  q_w = x_w^T M x_w / 2  for a fixed SPD
+// (inverse-covariance) matrix M and W walker vectors x_w, on the f64 MFMA.
+// Shared by every likelihood whose -lnL ends in Matrix_QuadForm
+// (source/Matrix_utils_new.f90:2033-2047): plik_lite (CMB.f90:327) and
+// CMBlikes (CMBlikes.f90:1220).
+//
+// Layout: the producer kernel writes x into the workspace as rows
+// x[w][Np] (Np = n rounded up to 64, zero-padded) and zeroes the
+// arrival counters (counters(ws)) before launch() runs on the same stream.
+#pragma once
+
+#include <map>
+#include <vector>
+
+#include "common.h"
+
+namespace cmamd {
+
+static constexpr int QF_TILE = 64;   // M block edge and walker tile
+
+struct QFItem {   // one workgroup's share: row block I x column blocks J0 .. J0+nJ-1 (all >= I)
+    int I, J0, nJ, pad;
+};
+
+class QuadForm {
+  public:
+    // M: n x n row-major symmetric
+    void init(const std::vector<double> &M, int n);
+    int n = 0, Np = 0;
+    static int wpad(int W) { return (W + QF_TILE - 1) / QF_TILE * QF_TILE; }
+    size_t workspace_size(int W) const;
+    double *x_rows(void *ws) const { return static_cast<double *>(ws); }
+    unsigned int *counters(void *ws, int W) const;
+    int n_counters(int W) const { return wpad(W) / QF_TILE; }
+    // out[w] = x_w^T M x_w / 2 + (addend ? addend[w] : 0)
+    void launch(int W, void *ws, const double *addend, double *out, hipStream_t stream, const char *prof_name);
+
+  private:
+    static constexpr int MAXKB = 5;
+    int nblk = 0;
+    DevBuf d_ct;
+    DevBuf d_items[MAXKB + 1];
+    std::vector<QFItem> items[MAXKB + 1];
+    std::map<int, int> kb_for_tiles;
+    size_t nmax_items() const;
+    int choose_kb(int tiles);
+};
+
+// host symmetric-matrix helpers (row-major)
+void spd_inverse(std::vector<double> &A, int n);                       // Matrix_Inverse
+void sym_eigen(std::vector<double> A, int n, std::vector<double> &evals,
+               std::vector<double> &evecs);                            // Matrix_Diagonalize
+void sym_power(std::vector<double> &A, int n, double pw);             // Matrix_Root
+
+}  // namespace cmamd

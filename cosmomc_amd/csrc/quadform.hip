@@ -1,0 +1,352 @@
+// Batched symmetric quadratic form on the f64 MFMA (see quadform.h).
+#include <algorithm>
+#include <cmath>
+#include <functional>
+
+#include "quadform.h"
+
+namespace cmamd {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+static constexpr int BK = 32;            // k depth staged per pipeline step (16 chunks of 16 B per row)
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+// LDS image of a 64-row x BK-double operand tile: rows of 256 B, unpadded;
+// the 16-byte chunk c of row r lives at physical chunk c ^ swz(r).  The
+// swizzle makes both the LDS-DMA fill (linear 1 KB pieces) and the MFMA
+// fragment reads (ds_read_b128, 8 consecutive k per lane) bank-conflict free.
+__device__ __forceinline__ int swz(int r) { return ((r >> 2) & 3) | ((r & 3) << 2); }
+
+// Fill one 64 x BK tile: rows row0..row0+63 of a row-major matrix (stride ld
+// doubles), columns k0..k0+BK-1.  4 waves x 4 instructions of 1 KB; lane l
+// of instruction j writes LDS bytes [l*16, l*16+16) of piece j = physical
+// chunk (l & 15) of row 4j + (l >> 4), so it loads the logical chunk
+// (l & 15) ^ swz(row) from global memory.
+__device__ __forceinline__ void dma_tile(double *lds_tile, const double *g, size_t ld, int k0, int wave, int lane)
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int piece = wave * 4 + q;                 // 0..15, 4 rows each
+        const int r = piece * 4 + (lane >> 4);
+        const int lc = (lane & 15) ^ swz(r);
+        const double *src = g + (size_t)r * ld + k0 + lc * 2;
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)src, (lds_void_t *)(lds_tile + piece * 4 * BK), 16, 0, 0);
+    }
+}
+
+// Quadratic form, symmetric split-K.  With Ct = C^-1 whose diagonal 64x64
+// blocks are halved,  Delta^T C^-1 Delta / 2 = sum_I Delta_I^T sum_{J>=I} Ct_IJ Delta_J,
+// so -lnL needs only the upper block triangle.  A workgroup owns one
+// (row block I, column-block range) item for 64 walkers: a double-buffered
+// K loop (LDS-DMA fills one BK step ahead) of f64 MFMA 16x16x4 into four
+// 16x16 accumulators per wave, then the dot with Delta_I.  Within a BK step
+// lane group g = lane>>4 takes k = 8g .. 8g+7 (any k order is valid as long
+// as A and B agree), so each lane reads its fragments as ds_read_b128.
+// Partials are handed off in-launch: the last workgroup of each walker tile
+// (agent-scope release / ticket / acquire, cdna_hip_programming.md section 5
+// split-K recipe) sums them in fixed item order: deterministic results.
+__global__ __launch_bounds__(256, 2) void quadform_ksplit(
+    const double *__restrict__ Ct, int Np, const double *__restrict__ delta, int W,
+    const QFItem *__restrict__ items, int n_items, int xcd_map,
+    double *__restrict__ partial, unsigned int *__restrict__ counters, const double *__restrict__ addend,
+    double *__restrict__ out)
+{
+    __shared__ __attribute__((aligned(16))) double smem[2 * 2 * QF_TILE * BK];   // [buf][A|B][64][BK], 64 KB
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    // XCD-aware placement: blocks b and b+8 share an XCD; give each XCD whole
+    // walker tiles so a tile's Delta stays in one L2 (speed only)
+    int item_ix = blockIdx.x, tile = blockIdx.y;
+    if (xcd_map) {
+        const int b = blockIdx.x + blockIdx.y * gridDim.x;
+        const int x = b & 7, j = b >> 3;
+        tile = x + 8 * (j / n_items);
+        item_ix = j % n_items;
+    }
+    const QFItem it = items[item_ix];
+    const int w0 = tile * QF_TILE;
+    const int nsteps = it.nJ * (QF_TILE / BK);
+    const int kbase0 = it.J0 * QF_TILE;
+    const double *Arow = Ct + (size_t)(it.I * QF_TILE) * Np;      // rows of the I panel
+    const double *Brow = delta + (size_t)w0 * Np;               // walker rows of the tile
+
+    f64x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+    dma_tile(smem, Arow, Np, kbase0, wave, lane);
+    dma_tile(smem + QF_TILE * BK, Brow, Np, kbase0, wave, lane);
+    for (int s = 0; s < nsteps; s++) {
+        const int buf = s & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();                              // tile s landed for every wave; buf^1 free
+        if (s + 1 < nsteps) {
+            double *nb = smem + (buf ^ 1) * 2 * QF_TILE * BK;
+            dma_tile(nb, Arow, Np, kbase0 + (s + 1) * BK, wave, lane);
+            dma_tile(nb + QF_TILE * BK, Brow, Np, kbase0 + (s + 1) * BK, wave, lane);
+        }
+        const double *A = smem + buf * 2 * QF_TILE * BK;
+        const double *B = A + QF_TILE * BK;
+        double2 a[4][4], b[4];
+        {
+            const int r = 16 * wave + li;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                b[q] = *reinterpret_cast<const double2 *>(B + r * BK + (((lk * 4 + q) ^ swz(r)) * 2));
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int r = 16 * t + li;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                a[t][q] = *reinterpret_cast<const double2 *>(A + r * BK + (((lk * 4 + q) ^ swz(r)) * 2));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][q].x, b[q].x, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][q].y, b[q].y, acc[t], 0, 0, 0);
+            }
+    }
+    __syncthreads();                                  // all waves done with the operand buffers
+    // Delta_I tile: smem[n][i] (row stride QF_TILE+2)
+    for (int e = tid; e < QF_TILE * QF_TILE / 2; e += 256) {
+        const int r = e >> 5, c2 = (e & 31) * 2;
+        const int w = w0 + r;
+        double2 v = *reinterpret_cast<const double2 *>(delta + (size_t)w * Np + it.I * QF_TILE + c2);
+        if (w >= W) v = make_double2(0.0, 0.0);
+        *reinterpret_cast<double2 *>(smem + r * (QF_TILE + 2) + c2) = v;
+    }
+    __syncthreads();
+    // f64 16x16x4 C/D layout: col = lane&15 (walker n), row = (lane>>4) + 4*r (i)
+    const int n = 16 * wave + li;
+    double sacc = 0.0;
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) sacc += acc[t][r] * smem[n * (QF_TILE + 2) + 16 * t + lk + 4 * r];
+    sacc += __shfl_xor(sacc, 16);
+    sacc += __shfl_xor(sacc, 32);
+    double *tile_part = partial + (size_t)tile * n_items * QF_TILE;
+    if (lk == 0) tile_part[(size_t)item_ix * QF_TILE + n] = sacc;
+
+    // ---- in-launch hand-off of the tile's partials to its last-arriving workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned int *flag = reinterpret_cast<unsigned int *>(smem + 64 * (QF_TILE + 2));
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned int t = __hip_atomic_fetch_add(counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = (t == (unsigned int)n_items - 1u) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (flag[0] == 0u) return;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // four item groups per walker, combined in fixed order
+    const int g = tid >> 6;
+    double part = 0.0;
+    for (int k = g; k < n_items; k += 4) part += tile_part[(size_t)k * QF_TILE + lane];
+    double *red = smem + 64 * (QF_TILE + 2) + 8;
+    red[g * QF_TILE + lane] = part;
+    __syncthreads();
+    if (tid < QF_TILE) {
+        const double v = ((red[lane] + red[QF_TILE + lane]) + red[2 * QF_TILE + lane]) + red[3 * QF_TILE + lane];
+        if (w0 + lane < W) out[w0 + lane] = addend ? v + addend[w0 + lane] : v;
+        if (lane == 0) counters[tile] = 0u;
+    }
+}
+
+
+// ------------------------------------------------------------------ host side
+
+void QuadForm::init(const std::vector<double> &M, int n_) {
+    n = n_;
+    Np = (n + QF_TILE - 1) / QF_TILE * QF_TILE;
+    nblk = Np / QF_TILE;
+    // Ct: M padded to Np with the diagonal 64x64 blocks halved (exact: x0.5), so
+    // x^T M x / 2 = sum_I x_I^T sum_{J>=I} Ct_IJ x_J needs only the upper block triangle
+    std::vector<double> ct((size_t)Np * Np, 0.0);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            const double v = M[(size_t)i * n + j];
+            ct[(size_t)i * Np + j] = (i / QF_TILE == j / QF_TILE) ? 0.5 * v : v;
+        }
+    d_ct.alloc(ct.size() * 8);
+    d_ct.upload(ct.data(), ct.size() * 8);
+    for (int kb = 1; kb <= MAXKB; kb++) {
+        items[kb].clear();
+        for (int I = 0; I < nblk; I++)
+            for (int J0 = I; J0 < nblk; J0 += kb) items[kb].push_back(QFItem{I, J0, std::min(kb, nblk - J0), 0});
+        d_items[kb].alloc(items[kb].size() * sizeof(QFItem));
+        d_items[kb].upload(items[kb].data(), items[kb].size() * sizeof(QFItem));
+    }
+    kb_for_tiles.clear();
+}
+
+size_t QuadForm::nmax_items() const {
+    size_t nmax = 0;
+    for (int kb = 1; kb <= MAXKB; kb++) nmax = std::max(nmax, items[kb].size());
+    return nmax;
+}
+
+size_t QuadForm::workspace_size(int W) const {
+    const size_t Wp = (size_t)wpad(W), tiles = Wp / QF_TILE;
+    return (Wp * Np + tiles * nmax_items() * QF_TILE) * sizeof(double) + ((tiles * 4 + 255) & ~size_t(255));
+}
+
+unsigned int *QuadForm::counters(void *ws, int W) const {
+    const size_t Wp = (size_t)wpad(W), tiles = Wp / QF_TILE;
+    return reinterpret_cast<unsigned int *>(static_cast<double *>(ws) + Wp * Np + tiles * nmax_items() * QF_TILE);
+}
+
+// Column-block chunk per work item: the largest chunk whose longest-first
+// greedy schedule over 2 workgroups/CU x 256 CUs is (near) the fastest,
+// counting a fixed per-workgroup overhead of half a block.
+int QuadForm::choose_kb(int tiles) {
+    auto itk = kb_for_tiles.find(tiles);
+    if (itk != kb_for_tiles.end()) return itk->second;
+    const int slots = 512;
+    int best_kb = 1;
+    double best = 1e300;
+    for (int kb = 1; kb <= MAXKB; kb++) {
+        std::vector<double> load(slots, 0.0);
+        std::vector<double> jobs;
+        for (auto &x : items[kb])
+            for (int t = 0; t < tiles; t++) jobs.push_back(x.nJ + 0.5);
+        std::sort(jobs.begin(), jobs.end(), std::greater<double>());
+        for (double j : jobs) *std::min_element(load.begin(), load.end()) += j;
+        const double makespan = *std::max_element(load.begin(), load.end()) + 0.02 * items[kb].size();
+        if (makespan < best * 0.98) {
+            best = makespan;
+            best_kb = kb;
+        }
+    }
+    kb_for_tiles[tiles] = best_kb;
+    return best_kb;
+}
+
+void QuadForm::launch(int W, void *ws, const double *addend, double *out, hipStream_t stream, const char *prof_name) {
+    const int tiles = wpad(W) / QF_TILE;
+    const int kb = choose_kb(tiles);
+    const int n_items = (int)items[kb].size();
+    double *x = x_rows(ws);
+    double *partial = x + (size_t)wpad(W) * Np;
+    unsigned int *cnt = counters(ws, W);
+    timed_launch(prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
+        hipExtLaunchKernelGGL(quadform_ksplit, dim3(n_items, tiles), dim3(256), 0, stream, e0, e1, 0,
+                              d_ct.as<double>(), Np, (const double *)x, W, d_items[kb].as<QFItem>(), n_items,
+                              (int)(tiles % 8 == 0), partial, cnt, addend, out);
+    });
+    HIP_CHECK(hipGetLastError());
+}
+
+// Cholesky inverse of an SPD matrix (Matrix_Inverse: dpotrf 'L' + dpotri,
+// source/Matrix_utils_new.f90:1478-1569), row-major, in place.
+void spd_inverse(std::vector<double> &A, int n) {
+    for (int i = 0; i < n; i++)
+        if (std::fabs(A[(size_t)i * n + i]) < 1e-30) fail(CMBL_ERR_NUMERIC, "Matrix_Inverse: very small diagonal");
+    for (int j = 0; j < n; j++) {
+        double d = A[(size_t)j * n + j];
+        for (int k = 0; k < j; k++) d -= A[(size_t)j * n + k] * A[(size_t)j * n + k];
+        if (!(d > 0.0)) fail(CMBL_ERR_NUMERIC, "Matrix_Inverse: covariance not positive definite (%d)", j + 1);
+        d = std::sqrt(d);
+        A[(size_t)j * n + j] = d;
+        for (int i = j + 1; i < n; i++) {
+            double s = A[(size_t)i * n + j];
+            for (int k = 0; k < j; k++) s -= A[(size_t)i * n + k] * A[(size_t)j * n + k];
+            A[(size_t)i * n + j] = s / d;
+        }
+    }
+    for (int j = 0; j < n; j++) {           // L^-1, lower
+        A[(size_t)j * n + j] = 1.0 / A[(size_t)j * n + j];
+        for (int i = j + 1; i < n; i++) {
+            double s = 0.0;
+            for (int k = j; k < i; k++) s += A[(size_t)i * n + k] * A[(size_t)k * n + j];
+            A[(size_t)i * n + j] = -s / A[(size_t)i * n + i];
+        }
+    }
+    std::vector<double> T((size_t)n * n);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j <= i; j++) {
+            double s = 0.0;
+            for (int k = i; k < n; k++) s += A[(size_t)k * n + i] * A[(size_t)k * n + j];
+            T[(size_t)i * n + j] = s;
+            T[(size_t)j * n + i] = s;
+        }
+    A.swap(T);
+}
+
+
+// Symmetric eigen-decomposition by cyclic Jacobi (host; data-set set-up only):
+// evals ascending, evecs row-major with eigenvector k in column k, as
+// Matrix_Diagonalize (DSYEV 'V', source/Matrix_utils_new.f90:361-383).
+void sym_eigen(std::vector<double> A, int n, std::vector<double> &evals, std::vector<double> &evecs) {
+    std::vector<double> V((size_t)n * n, 0.0);
+    for (int i = 0; i < n; i++) V[(size_t)i * n + i] = 1.0;
+    for (int sweep = 0; sweep < 100; sweep++) {
+        double off = 0.0, tot = 0.0;
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) {
+                const double a = A[(size_t)i * n + j] * A[(size_t)i * n + j];
+                tot += a;
+                if (i != j) off += a;
+            }
+        if (off <= 1e-32 * tot || off == 0.0) break;
+        for (int p = 0; p < n - 1; p++)
+            for (int q = p + 1; q < n; q++) {
+                const double apq = A[(size_t)p * n + q];
+                if (apq == 0.0) continue;
+                const double app = A[(size_t)p * n + p], aqq = A[(size_t)q * n + q];
+                const double theta = (aqq - app) / (2.0 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+                const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < n; k++) {    // A <- A J
+                    const double akp = A[(size_t)k * n + p], akq = A[(size_t)k * n + q];
+                    A[(size_t)k * n + p] = c * akp - s * akq;
+                    A[(size_t)k * n + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < n; k++) {    // A <- J^T A
+                    const double apk = A[(size_t)p * n + k], aqk = A[(size_t)q * n + k];
+                    A[(size_t)p * n + k] = c * apk - s * aqk;
+                    A[(size_t)q * n + k] = s * apk + c * aqk;
+                }
+                A[(size_t)p * n + q] = A[(size_t)q * n + p] = 0.0;
+                for (int k = 0; k < n; k++) {    // V <- V J
+                    const double vkp = V[(size_t)k * n + p], vkq = V[(size_t)k * n + q];
+                    V[(size_t)k * n + p] = c * vkp - s * vkq;
+                    V[(size_t)k * n + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    std::vector<int> ord(n);
+    for (int i = 0; i < n; i++) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](int a, int b) { return A[(size_t)a * n + a] < A[(size_t)b * n + b]; });
+    evals.resize(n);
+    evecs.assign((size_t)n * n, 0.0);
+    for (int k = 0; k < n; k++) {
+        evals[k] = A[(size_t)ord[k] * n + ord[k]];
+        for (int i = 0; i < n; i++) evecs[(size_t)i * n + k] = V[(size_t)i * n + ord[k]];
+    }
+}
+
+// M <- U D^pw U^T  (Matrix_Root, source/Matrix_utils_new.f90:421-440)
+void sym_power(std::vector<double> &A, int n, double pw) {
+    std::vector<double> d, U;
+    sym_eigen(A, n, d, U);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            double s = 0.0;
+            for (int k = 0; k < n; k++) s += U[(size_t)i * n + k] * std::pow(d[k], pw) * U[(size_t)j * n + k];
+            A[(size_t)i * n + j] = s;
+        }
+}
+
+}  // namespace cmamd
