@@ -88,8 +88,11 @@ int cmbl_open(const char *tag, const char *dataset_path, const char *override_in
         ini.override_text(override_ini);
         std::unique_ptr<cmbl_t> h(new cmbl_t);
         std::string t(tag);
+        // tag -> likelihood class as CMBLikelihood_Add (source/CMB.f90:80-97)
         if (t == "PLIK_LITE") h->like = cmamd::make_plik_lite(ini);
-        else cmamd::fail(CMBL_ERR_UNSUPPORTED, "cmbl_open: dataset tag '%s' not supported yet", tag);
+        else if (t == "WMAP" || t == "SPTPOL_TEEE" || t == "SPTPOL_BB" || t == "SMICA")
+            cmamd::fail(CMBL_ERR_UNSUPPORTED, "cmbl_open: dataset tag '%s' not supported yet", tag);
+        else h->like = cmamd::make_cmblikes(ini, t);      // TCMBLikes, or TBK_planck for BKPLANCK
         *out = h.release();
     });
     if (rc) put_err(errbuf, errlen, err.c_str());

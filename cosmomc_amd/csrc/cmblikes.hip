@@ -1,0 +1,1177 @@
+// CMBlikes bandpower likelihoods (reference TCMBLikes, source/CMBlikes.f90)
+// and the BICEP/Keck/Planck foreground model (TBK_planck,
+// source/CMB_BK_Planck.f90), batched over W walkers on MI355X.
+//
+// Per walker (CMBLikes_LogLike, CMBlikes.f90:1165-1227):
+//   map spectra  MapCl_ij(l) = Theory_{f_i f_j}(l) [+ aberration] [+ foregrounds] [/ cal^2]
+//                                             (GetTheoryMapCls / AdaptTheoryForMaps :1022-1126)
+//   binning      Cls(out, b) = sum_win dot(W(:,win,b), MapCl_in(win))  [+ linear correction]
+//                                             (TBinWindows_bin :1230-1256, GetBinnedMapCls :981-995)
+//   per bin      C = Cls (+ noise);  HL:  X_b = Transform(C, Chat_b, Cfid_b^1/2)   (:861-914)
+//                                    gaussian: X_b = C - Chat_b
+//   -lnL         = (bigX^T C^-1 bigX + (ln cal / sigma)^2) / 2         (:1220-1225)
+//
+// Kernels:
+//   cmbl_bin_kernel   one 256-thread workgroup per walker: foreground SEDs,
+//                     per map pair the spectrum in LDS, every window column as
+//                     a wave dot product, then the binned Cls per (bin, cl);
+//                     gaussian writes bigX rows, HL writes the C matrices.
+//   cmbl_hl_kernel    one wave per (walker, bin): two symmetric
+//                     eigendecompositions (parallel-order cyclic Jacobi in
+//                     LDS) and the HL transform, writes the bigX entries.
+//   quadform_ksplit   bigX^T C^-1 bigX / 2 on the f64 MFMA (quadform.hip).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <fstream>
+#include <set>
+#include <sstream>
+
+#include "quadform.h"
+
+namespace cmamd {
+
+static constexpr int CL_MAXMAPS = 16;          // HL matrices up to 16 x 16 in one wave
+static constexpr int CL_MAXREQ = 32;            // required maps
+static constexpr int BK_NPARAM = 16;            // BKPlanck.paramnames
+
+struct CLPair {      // one required map pair (i >= j)
+    int field;       // theory field index 0..9 (TT TE EE BT BE BB PT PE PB PP)
+    int cmb;         // both theory indices <= B: aberration and calibration apply
+    int fg;          // foregrounds: 0 none, 1 EE, 2 BB
+    int mi, mj;      // required-map indices (0-based)
+    int lo, hi;      // l range needed by this pair's columns
+    int col0, ncol;  // its columns: col_of_pair[col0 .. col0+ncol)
+};
+
+struct CLCol {       // one window column (bin, window entry)
+    int lo, hi;      // nonzero l range of the window
+    long long off;   // offset of W(lo) in the packed window array
+};
+
+struct BKMap {       // per required map: bandpass samples and constants (Read_Bandpass :72-105)
+    int off, n;      // samples in bp_nu / bp_R / bp_dnu
+    int bc;          // band-centre error slot: 0 none, 1 '95', 2 '150', 3 '220'
+    double th_dust, th_sync, nu_bar;
+};
+
+struct CLDev {
+    int lmin, lmax;                 // pcl_lmin, pcl_lmax
+    int npair, ncol, nb, ncl, ncl_used, nX, Np;
+    int approx;                     // 1 HL, 2 gaussian
+    int has_corr;
+    int cal_index;                  // 0-based in DataParams, -1 none
+    double log_cal_prior;           // > 0: add (ln cal / prior)^2 to chi^2
+    double aberration;
+    int lpair;                      // max pair l-range length (LDS buffer)
+    const CLPair *pairs;
+    const CLCol *cols;
+    const int *col_of_pair;         // columns grouped by pair
+    const double *wts;              // packed windows
+    const double *col_fixed;        // [ncol] constant dot with fixed spectra (fix_cl), used when fixed_mask
+    const unsigned char *col_is_fixed;
+    const int *sum_off;             // [nb*ncl+1] main windows of (bin, cl) in window order: sum_cols[...]
+    const int *sum_cols;
+    const int *corr_off;            // [nb*ncl+1] linear-correction windows
+    const int *corr_cols;
+    const double *fidcorr;          // [nb][ncl]
+    const double *noise;            // [nb][ncl] (HL)
+    const double *chat;             // [nb][ncl] lower-triangle elements of Chat (gaussian)
+    const int *cl_use;              // [ncl_used]
+    // BK foregrounds
+    int bk, nreq;
+    const BKMap *bkmaps;
+    const double *bp_nu, *bp_R, *bp_dnu;
+    double fpivot_dust, fpivot_sync, decorr_dust[2], decorr_sync[2];
+    int lform_dust, lform_sync;     // 0 flat, 1 lin, 2 quad
+};
+
+static constexpr double BK_TCMB = 2.72548;
+static constexpr double BK_H = 6.62606957e-34;
+static constexpr double BK_KB = 1.3806488e-23;
+__host__ __device__ inline double ghz_kelvin() { return BK_H / BK_KB * 1e9; }
+
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Decorrelation (CMB_BK_Planck.f90:187-227)
+__device__ inline double bk_decorr(double Delta, double nu0, double nu1, const double *piv, int l, int lform) {
+    const double lpivot = 80.0;
+    const double a = log(nu0 / nu1), b = log(piv[0] / piv[1]);
+    const double scl_nu = (a * a) / (b * b);
+    double scl_ell = 1.0;
+    if (lform == 1) scl_ell = l / lpivot;
+    else if (lform == 2) {
+        const double t = l / lpivot;
+        scl_ell = t * t;
+    }
+    if (Delta > 1.0) return 2.0 - exp(log(2.0 - Delta) * scl_nu * scl_ell);
+    return exp(log(Delta) * scl_nu * scl_ell);
+}
+
+__global__ __launch_bounds__(256) void cmbl_bin_kernel(CLDev c, const double *__restrict__ dl, long long ld_field,
+                                                      long long ld_walker, const double *__restrict__ nuis,
+                                                      long long ld_nuis, double *__restrict__ xrows,
+                                                      double *__restrict__ cmat, double *__restrict__ addend,
+                                                      unsigned int *__restrict__ counters, int n_counters)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int w = blockIdx.x;
+    if (w == 0)
+        for (int i = tid; i < n_counters; i += blockDim.x) counters[i] = 0u;
+    const int L = c.lmax - c.lmin + 1;
+    // LDS carve: buf[2][lpair] | colval[ncol] | cls[nb*ncl] | fg[3][L] | fd[nreq] fs[nreq]
+    double *buf = lds;
+    double *colval = buf + 2 * c.lpair;
+    double *cls = colval + c.ncol;
+    double *fgp = cls + c.nb * c.ncl;
+    double *fdust = fgp + (c.bk ? 3 * L : 0);
+    double *fsync = fdust + c.nreq;
+    const double *D = dl + (long long)w * ld_walker;
+    const double *P = nuis + (long long)w * ld_nuis;
+    const double cal = c.cal_index >= 0 ? P[c.cal_index] : 1.0;
+    const double calsq = cal * cal;
+
+    // ---- BK foreground SEDs and l profiles (TBK_planck_AddForegrounds :229-285)
+    double EEtoBB_dust = 0, EEtoBB_sync = 0, Delta_dust = 1, Delta_sync = 1;
+    bool need_dd = false, need_ds = false;
+    if (c.bk) {
+        const double Adust = P[0], Async = P[1], alphadust = P[2], betadust = P[3], Tdust = P[4];
+        const double alphasync = P[5], betasync = P[6], dustsync_corr = P[7];
+        EEtoBB_dust = P[8];
+        EEtoBB_sync = P[9];
+        Delta_dust = P[10];
+        Delta_sync = P[11];
+        need_dd = fabs(Delta_dust - 1) > 1e-5;
+        need_ds = fabs(Delta_sync - 1) > 1e-5;
+        const double G = ghz_kelvin();
+        for (int i = wave; i < c.nreq; i += 4) {           // one wave per map
+            const BKMap m = c.bkmaps[i];
+            double gb = 0.0, pl = 0.0;
+            for (int k = lane; k < m.n; k += 64) {
+                const double nu = c.bp_nu[m.off + k], R = c.bp_R[m.off + k], dn = c.bp_dnu[m.off + k];
+                gb += dn * R * pow(nu, 3 + betadust) / (exp(G * nu / Tdust) - 1);
+                pl += dn * R * pow(nu, 2 + betasync);
+            }
+            gb = wave_sum(gb);
+            pl = wave_sum(pl);
+            if (lane == 0) {
+                double bc = 1.0;
+                if (m.bc == 1) bc = P[12] + P[13] + 1.;
+                else if (m.bc == 2) bc = P[12] + P[14] + 1.;
+                else if (m.bc == 3) bc = P[12] + P[15] + 1.;
+                const double nu0d = c.fpivot_dust, nu0s = c.fpivot_sync;
+                const double gb0 = pow(nu0d, 3 + betadust) / (exp(G * nu0d / Tdust) - 1);
+                const double pl0 = pow(nu0s, 2 + betasync);
+                double th_err = 1.0, gb_err = 1.0, pl_err = 1.0;
+                if (bc != 1.) {                              // DustScaling :130-141, SyncScaling :169-178
+                    const double e1 = exp(G * m.nu_bar / BK_TCMB) - 1, e2 = exp(G * m.nu_bar * bc / BK_TCMB) - 1;
+                    th_err = (bc * bc * bc * bc) * exp(G * m.nu_bar * (bc - 1) / BK_TCMB) * (e1 * e1) / (e2 * e2);
+                    gb_err = pow(bc, 3 + betadust) * (exp(G * m.nu_bar / Tdust) - 1) /
+                             (exp(G * m.nu_bar * bc / Tdust) - 1);
+                    pl_err = pow(bc, 2 + betasync);
+                }
+                fdust[i] = (gb / gb0) / m.th_dust * (gb_err / th_err);
+                fsync[i] = (pl / pl0) / m.th_sync * (pl_err / th_err);
+                fsync[c.nreq + i] = bc;                      // band-centre error per map
+            }
+        }
+        const double lpivot = 80.0;
+        for (int l = c.lmin + tid; l <= c.lmax; l += blockDim.x) {
+            const int j = l - c.lmin;
+            fgp[j] = Adust * pow(l / lpivot, alphadust);
+            fgp[L + j] = Async * pow(l / lpivot, alphasync);
+            fgp[2 * L + j] = dustsync_corr * sqrt(Adust * Async) * pow(l / lpivot, (alphadust + alphasync) / 2);
+        }
+        __syncthreads();
+    }
+    const double *bcerr = fsync + c.nreq;
+
+    // ---- map spectra and window dot products, pair by pair; the spectrum
+    // buffers alternate per processed pair so one barrier per pair suffices
+    int nproc = 0;
+    for (int p = 0; p < c.npair; p++) {
+        const CLPair pr = c.pairs[p];
+        if (pr.ncol == 0) continue;
+        double *B = buf + (nproc++ & 1) * c.lpair - pr.lo;
+        const double *Df = D + (long long)pr.field * ld_field;
+        double dust = 0, sync = 0, dustsync = 0, dd_flat = 1, ds_flat = 1;
+        bool dd_l = false, ds_l = false;
+        double nu_i = 0, nu_j = 0;
+        if (pr.fg) {
+            const int i = pr.mi, j = pr.mj;
+            dust = fdust[i] * fdust[j];
+            sync = fsync[i] * fsync[j];
+            dustsync = fdust[i] * fsync[j] + fsync[i] * fdust[j];
+            if (pr.fg == 1) {
+                dust = dust * EEtoBB_dust;
+                sync = sync * EEtoBB_sync;
+                dustsync = dustsync * sqrt(EEtoBB_dust * EEtoBB_sync);
+            }
+            nu_i = c.bkmaps[i].nu_bar * bcerr[i];
+            nu_j = c.bkmaps[j].nu_bar * bcerr[j];
+            if (need_dd && i != j) {
+                if (c.lform_dust == 0) dd_flat = bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, 0, 0);
+                else dd_l = true;
+            }
+            if (need_ds && i != j) {
+                if (c.lform_sync == 0) ds_flat = bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, 0, 0);
+                else ds_l = true;
+            }
+        }
+        for (int l = pr.lo + tid; l <= pr.hi; l += blockDim.x) {
+            double v = Df[l];
+            if (c.aberration != 0.0 && pr.cmb) {              // AddAberration :1062-1101
+                int la = l - 1, lb = l + 1;
+                if (l == c.lmin) { la = l; lb = l + 2; }
+                else if (l == c.lmax) { la = l - 2; lb = l; }
+                const double ea = la, eb = lb, el = l;
+                const double ca = Df[la] / (ea * (ea + 1)), cb = Df[lb] / (eb * (eb + 1));
+                const double deriv = 0.5 * (cb - ca);
+                v = v + c.aberration * (el * el * (el + 1) * deriv);
+            }
+            if (pr.fg) {                                      // :329-334
+                const int j = l - c.lmin;
+                const double Dd = dd_l ? bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, l, c.lform_dust) : dd_flat;
+                const double Ds = ds_l ? bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, l, c.lform_sync) : ds_flat;
+                v = v + dust * fgp[j] * Dd + sync * fgp[L + j] * Ds + dustsync * fgp[2 * L + j];
+            }
+            if (c.cal_index >= 0 && pr.cmb) v = v / calsq;    // AdaptTheoryForMaps :1113-1124
+            B[l] = v;
+        }
+        __syncthreads();
+        for (int k = wave; k < pr.ncol; k += 4) {
+            const int ci = c.col_of_pair[pr.col0 + k];
+            const CLCol col = c.cols[ci];
+            const double *Wc = c.wts + col.off - col.lo;
+            double acc = 0.0;
+            for (int l = col.lo + lane; l <= col.hi; l += 64) acc += Wc[l] * B[l];
+            acc = wave_sum(acc);
+            if (lane == 0) colval[ci] = acc;
+        }
+        // the next pair writes the other buffer; the barrier at its top orders reuse
+    }
+    for (int ci = tid; ci < c.ncol; ci += blockDim.x)
+        if (c.col_is_fixed[ci]) colval[ci] = c.col_fixed[ci];
+    __syncthreads();
+
+    // ---- binned spectra per (bin, cl): window order, then the linear correction
+    for (int e = tid; e < c.nb * c.ncl; e += blockDim.x) {
+        double s = 0.0;
+        for (int q = c.sum_off[e]; q < c.sum_off[e + 1]; q++) s = s + colval[c.sum_cols[q]];
+        if (c.has_corr) {
+            double cs = 0.0;
+            for (int q = c.corr_off[e]; q < c.corr_off[e + 1]; q++) cs = cs + colval[c.corr_cols[q]];
+            s = s + (cs - c.fidcorr[e]);
+        }
+        cls[e] = s;
+    }
+    __syncthreads();
+    double *x = xrows + (long long)w * c.Np;
+    for (int k = c.nX + tid; k < c.Np; k += blockDim.x) x[k] = 0.0;
+    if (c.approx == 2) {
+        for (int e = tid; e < c.nX; e += blockDim.x) {
+            const int b = e / c.ncl_used, u = c.cl_use[e % c.ncl_used];
+            x[e] = cls[b * c.ncl + u] - c.chat[b * c.ncl + u];
+        }
+    } else {
+        double *cm = cmat + (long long)w * c.nb * c.ncl;
+        for (int e = tid; e < c.nb * c.ncl; e += blockDim.x) cm[e] = cls[e] + c.noise[e];
+    }
+    if (addend && tid == 0) {
+        double a = 0.0;
+        if (c.log_cal_prior > 0 && c.cal_index >= 0) {
+            const double t = log(cal) / c.log_cal_prior;
+            a = t * t / 2;
+        }
+        addend[w] = a;
+    }
+}
+
+// ---------------------------------------------------------------- HL (one wave)
+// Symmetric eigen-decomposition of the m x m (m even, <= 16) LDS matrix A by
+// cyclic Jacobi in round-robin order: every round rotates m/2 disjoint (p, q)
+// pairs at once; lanes own matrix elements.  V accumulates the rotations
+// (eigenvector k in column k).  A and V are double-buffered (A, A2), (V, V2);
+// the result is left in A / V.
+__device__ void wave_jacobi(double *A, double *A2, double *V, double *V2, double *cs, int *partner, int m, int lane)
+{
+    const int mm = m * m;
+    for (int e = lane; e < mm; e += 64) V[e] = (e / m == e % m) ? 1.0 : 0.0;
+    __syncthreads();
+    for (int sweep = 0; sweep < 40; sweep++) {
+        // convergence: all off-diagonal elements negligible against their diagonals
+        bool big = false;
+        for (int e = lane; e < mm; e += 64) {
+            const int i = e / m, j = e % m;
+            if (i < j) {
+                const double a = A[e];
+                if (a != 0.0 && fabs(a) > 1e-18 * sqrt(fabs(A[i * m + i] * A[j * m + j]))) big = true;
+            }
+        }
+        if (!__any(big)) break;
+        for (int r = 0; r < m - 1; r++) {
+            // pairs of this round (circle method): k = 0: (r, m-1); k > 0: ((r+k)%(m-1), (r-k)%(m-1))
+            if (lane < m / 2) {
+                int p, q;
+                if (lane == 0) { p = r; q = m - 1; }
+                else { p = (r + lane) % (m - 1); q = (r - lane + (m - 1)) % (m - 1); }
+                if (p > q) { const int t = p; p = q; q = t; }
+                const double apq = A[p * m + q], app = A[p * m + p], aqq = A[q * m + q];
+                double cc = 1.0, ss = 0.0;
+                if (apq != 0.0 && fabs(apq) > 1e-300) {
+                    const double theta = (aqq - app) / (2.0 * apq);
+                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                    cc = 1.0 / sqrt(t * t + 1.0);
+                    ss = t * cc;
+                }
+                partner[p] = q; partner[q] = p;
+                cs[2 * p] = cc; cs[2 * p + 1] = -ss;   // J[p][p] = c, J[q][p] = -s
+                cs[2 * q] = cc; cs[2 * q + 1] = ss;    // J[q][q] = c, J[p][q] = s
+            }
+            __syncthreads();
+            // A' = J^T A J ; element (i, j) mixes rows {i, i'} and columns {j, j'}
+            for (int e = lane; e < mm; e += 64) {
+                const int i = e / m, j = e % m, ip = partner[i], jp = partner[j];
+                const double ci = cs[2 * i], si = cs[2 * i + 1], cj = cs[2 * j], sj = cs[2 * j + 1];
+                // column i of J: J[i][i] = ci, J[ip][i] = si
+                const double v = ci * (A[i * m + j] * cj + A[i * m + jp] * sj) + si * (A[ip * m + j] * cj + A[ip * m + jp] * sj);
+                A2[e] = v;
+                V2[e] = V[i * m + j] * cj + V[i * m + jp] * sj;
+            }
+            __syncthreads();
+            for (int e = lane; e < mm; e += 64) {
+                A[e] = A2[e];
+                V[e] = V2[e];
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// C <- A B (n x n, row stride m), all in LDS
+__device__ inline void wave_matmul(double *C, const double *A, const double *B, int n, int m, int lane, bool transA,
+                                   bool transB)
+{
+    for (int e = lane; e < n * n; e += 64) {
+        const int i = e / n, j = e % n;
+        double s = 0.0;
+        for (int k = 0; k < n; k++) {
+            const double a = transA ? A[k * m + i] : A[i * m + k];
+            const double b = transB ? B[j * m + k] : B[k * m + j];
+            s += a * b;
+        }
+        C[i * m + j] = s;
+    }
+}
+
+struct HLDev {
+    int n, m, nb, ncl, ncl_used, nX, Np;
+    const double *chat;     // [nb][n][n]
+    const double *cfhalf;   // [nb][n][n]
+    const int *cl_use;
+};
+
+__global__ __launch_bounds__(64) void cmbl_hl_kernel(HLDev h, const double *__restrict__ cmat, double *__restrict__ xrows,
+                                                    int W)
+{
+    __shared__ double S[9 * CL_MAXMAPS * CL_MAXMAPS + 3 * CL_MAXMAPS];
+    __shared__ int partner[CL_MAXMAPS];
+    const int lane = threadIdx.x;
+    const int w = blockIdx.x / h.nb, b = blockIdx.x % h.nb;
+    if (w >= W) return;
+    const int n = h.n, m = h.m, MM = CL_MAXMAPS * CL_MAXMAPS;
+    double *A = S, *A2 = S + MM, *U = S + 2 * MM, *V2 = S + 3 * MM, *T = S + 4 * MM, *R = S + 5 * MM;
+    double *Vb = S + 6 * MM, *Ch = S + 7 * MM, *Cf = S + 8 * MM;
+    double *cs = S + 9 * MM, *dg = cs + 2 * CL_MAXMAPS;
+    const double *cm = cmat + ((long long)w * h.nb + b) * h.ncl;
+    // C from its lower-triangle elements (ElementsToMatrix :950-965), padded to m with zeros
+    for (int e = lane; e < m * m; e += 64) {
+        const int i = e / m, j = e % m;
+        double v = 0.0;
+        if (i < n && j < n) {
+            const int a = i > j ? i : j, bb = i > j ? j : i;
+            v = cm[a * (a + 1) / 2 + bb];
+        }
+        A[e] = v;
+        Ch[e] = (i < n && j < n) ? h.chat[((long long)b * n + i) * n + j] : 0.0;
+        Cf[e] = (i < n && j < n) ? h.cfhalf[((long long)b * n + i) * n + j] : 0.0;
+    }
+    __syncthreads();
+    // (1) C = U diag U^T
+    wave_jacobi(A, A2, U, V2, cs, partner, m, lane);
+    if (lane < m) dg[lane] = A[lane * m + lane];
+    __syncthreads();
+    // (2) Rot = U^T Chat U, scaled by 1/sqrt(diag) on rows and columns (:878-889)
+    wave_matmul(T, Ch, U, n, m, lane, false, false);
+    __syncthreads();
+    wave_matmul(R, U, T, n, m, lane, true, false);
+    __syncthreads();
+    for (int e = lane; e < n * n; e += 64) {
+        const int i = e / n, j = e % n;
+        const int lo = i < j ? i : j, hi = i < j ? j : i;
+        double v = R[i * m + j];
+        v = v / sqrt(dg[lo]);
+        v = v / sqrt(dg[hi]);
+        R[i * m + j] = v;
+    }
+    __syncthreads();
+    // (3) Rot = U Rot U^T (:891)
+    wave_matmul(T, R, U, n, m, lane, false, true);
+    __syncthreads();
+    wave_matmul(A, U, T, n, m, lane, false, false);
+    __syncthreads();
+    for (int e = lane; e < m * m; e += 64) {
+        const int i = e / m, j = e % m;
+        if (i >= n || j >= n) A[e] = 0.0;
+    }
+    __syncthreads();
+    // (4) Rot = V diag V^T; g(x) = sign(sqrt(2 max(0, x - ln x - 1)), x - 1)  (:892-894)
+    wave_jacobi(A, A2, Vb, V2, cs, partner, m, lane);
+    if (lane < n) {
+        const double x = A[lane * m + lane];
+        const double g = sqrt(2 * fmax(0.0, x - log(x) - 1));
+        dg[lane] = (x - 1 >= 0) ? g : -g;
+    }
+    __syncthreads();
+    // (5) U = Cfhalf V ; C = U diag(g) U^T (:907-912)
+    wave_matmul(T, Cf, Vb, n, m, lane, false, false);
+    __syncthreads();
+    for (int e = lane; e < n * n; e += 64) {
+        const int i = e / n, j = e % n;
+        R[i * m + j] = T[i * m + j] * dg[j];
+    }
+    __syncthreads();
+    wave_matmul(A, R, T, n, m, lane, false, true);
+    __syncthreads();
+    // vecp = lower-triangle elements (MatrixToElements :917-931); bigX entries of this bin
+    double *x = xrows + (long long)w * h.Np + (long long)b * h.ncl_used;
+    for (int u = lane; u < h.ncl_used; u += 64) {
+        const int k = h.cl_use[u];
+        int i = 0;
+        while ((i + 1) * (i + 2) / 2 <= k) i++;
+        const int j = k - i * (i + 1) / 2;
+        x[u] = A[i * m + j];
+    }
+}
+
+// ------------------------------------------------------------------ host side
+
+static std::vector<std::string> split_list(const std::string &s) { return split_ws(s); }
+
+static int type_index(char ch) {   // TypeIndex: T E B P -> 1..4 (:134-144)
+    const char *f = "TEBP";
+    const char *p = std::strchr(f, ch);
+    if (!p || !ch) fail(CMBL_ERR_FORMAT, "Invalid C_l part %c, must be one of: TEBP", ch);
+    return (int)(p - f) + 1;
+}
+
+static std::string format_u(const std::string &fmt, int i) {   // FormatString(filename, i) for %u
+    std::string s = fmt;
+    size_t p = s.find("%u");
+    if (p != std::string::npos) s.replace(p, 2, std::to_string(i));
+    return s;
+}
+
+// File%LastTopComment (FileUtils.f90:1150-1168)
+static std::string last_top_comment(const std::string &path) {
+    std::ifstream f(path);
+    if (!f) fail(CMBL_ERR_IO, "cannot read %s", path.c_str());
+    std::string line, res;
+    while (std::getline(f, line)) {
+        size_t a = line.find_first_not_of(" \t\r");
+        if (a == std::string::npos) continue;
+        if (line[0] == '#') {
+            std::string t = line.substr(1);
+            size_t b = t.find_first_not_of(" \t");
+            res = b == std::string::npos ? "" : t.substr(b);
+            while (!res.empty() && (res.back() == ' ' || res.back() == '\r' || res.back() == '\t')) res.pop_back();
+        } else {
+            break;
+        }
+    }
+    return res;
+}
+
+static double parse_double(const std::string &s) {
+    std::string t = s;
+    for (auto &ch : t)
+        if (ch == 'd' || ch == 'D') ch = 'e';
+    return std::stod(t);
+}
+
+static bool ini_logical(const Ini &ini, const std::string &key, bool def) {
+    std::string v = ini.str(key);
+    if (v.empty()) return def;
+    const char ch = (char)std::toupper(v[0] == '.' && v.size() > 1 ? v[1] : v[0]);
+    if (ch == 'T' || ch == '1' || ch == 'Y') return true;
+    if (ch == 'F' || ch == '0' || ch == 'N') return false;
+    fail(CMBL_ERR_FORMAT, "%s: bad logical %s = %s", ini.filename().c_str(), key.c_str(), v.c_str());
+    return def;
+}
+
+static int ini_int(const Ini &ini, const std::string &key, bool required, int def) {
+    std::string v = required ? ini.str_required(key) : ini.str(key);
+    if (v.empty()) return def;
+    return std::stoi(v);
+}
+
+static double ini_double(const Ini &ini, const std::string &key, double def) {
+    std::string v = ini.str(key);
+    return v.empty() ? def : parse_double(v);
+}
+
+struct Windows {                   // TBinWindows (:27-34) for bins bin_min..bin_max
+    std::vector<int> in_i, in_j;   // required-map indices (1-based, i >= j; 0 = not required)
+    std::vector<int> out;          // used cl index (1-based, 0 = not used)
+    std::vector<double> W;         // [bin][win][L]
+    std::vector<std::vector<double>> fix;   // per window: fixed spectrum over L (empty = theory)
+    bool present = false;
+};
+
+struct CMBLikes final : Like {
+    // ReadIni state
+    bool has_map_names = false, bk = false;
+    std::vector<std::string> map_names, used_map_order;
+    std::vector<int> map_fields, use_map, require_map, map_used_index, map_required_index, required_order;
+    int approx = 0, nmaps = 0, nreq = 0, ncl = 0, ncl_used = 0;
+    int lmin = 0, lmax = 0, nbins = 0, bin_min = 1, bin_max = 0, nb = 0;
+    double aberration = 0.0, log_cal_prior = -1.0;
+    int cal_index = -1;
+    Windows bw, cw;
+    std::vector<double> clhat, clnoise, clfid, fidcorr;   // [bin][ncl]
+    std::vector<int> cl_use;                               // 0-based
+    QuadForm qf;
+    int nX = 0;
+    // device tables
+    CLDev dev{};
+    HLDev hl{};
+    DevBuf d_pairs, d_cols, d_colpair, d_wts, d_colfixed, d_isfixed, d_sumoff, d_sumcols, d_corroff, d_corrcols,
+        d_fidcorr, d_noise, d_chat, d_cluse, d_bkmaps, d_bpnu, d_bpR, d_bpdnu, d_hlchat, d_hlcf;
+    size_t lds_bytes = 0;
+    int max_field = 0;
+
+    std::string cl_name(const std::vector<std::string> &names, int i, int j) const {   // Cl_i_j_name (:328-343)
+        return has_map_names ? names[i - 1] + "x" + names[j - 1] : names[i - 1] + names[j - 1];
+    }
+    int map_index(const std::string &s) const {
+        for (size_t k = 0; k < map_names.size(); k++)
+            if (map_names[k] == s) return (int)k + 1;
+        return -1;
+    }
+    void pair_to_map_indices(const std::string &S, int &i1, int &i2) const {   // :195-213
+        if (S.size() == 2) {
+            if (has_map_names) fail(CMBL_ERR_FORMAT, "CMBlikes: CL names must use MAP1xMAP2 names");
+            i1 = map_index(S.substr(0, 1));
+            i2 = map_index(S.substr(1, 1));
+        } else {
+            size_t ix = S.find('x');
+            if (ix == std::string::npos) fail(CMBL_ERR_FORMAT, "CMBLikes: invalid spectrum name %s", S.c_str());
+            i1 = map_index(S.substr(0, ix));
+            i2 = map_index(S.substr(ix + 1));
+        }
+        if (i1 == -1 || i2 == -1) fail(CMBL_ERR_FORMAT, "CMBLikes: unrecognised map name %s", S.c_str());
+    }
+    // UseString_to_Cl_i_j (:262-281) with PairStringToUsedMapIndices (:215-231)
+    void use_string_to_cl_i_j(const std::string &S, const std::vector<int> &used_index, std::vector<int> &ii,
+                              std::vector<int> &jj) const {
+        ii.clear();
+        jj.clear();
+        for (auto &t : split_list(S)) {
+            int i1, i2;
+            pair_to_map_indices(t, i1, i2);
+            i1 = used_index[i1 - 1];
+            i2 = used_index[i2 - 1];
+            if (i2 > i1) std::swap(i1, i2);
+            ii.push_back(i1);
+            jj.push_back(i2);
+        }
+    }
+    std::vector<int> use_string_to_cols(const std::string &S) const {   // :234-260
+        std::vector<int> ii, jj, cols;
+        use_string_to_cl_i_j(S, map_used_index, ii, jj);
+        for (size_t k = 0; k < ii.size(); k++) {
+            int ix = 0, c = 0;
+            for (int a = 1; a <= nmaps; a++)
+                for (int b = 1; b <= a; b++) {
+                    ix++;
+                    if (a == ii[k] && b == jj[k]) c = ix;
+                }
+            if (ii[k] == 0 || jj[k] == 0) c = 0;
+            cols.push_back(c);
+        }
+        return cols;
+    }
+    int cols_from_order(const std::string &order, std::vector<int> &cols) const {   // GetColsFromOrder :345-369
+        auto li = split_list(order);
+        auto index_of = [&](const std::string &s) {
+            for (size_t k = 0; k < li.size(); k++)
+                if (li[k] == s) return (int)k + 1;
+            return -1;
+        };
+        cols.assign(ncl, 0);
+        int ix = 0;
+        for (int i = 1; i <= nmaps; i++)
+            for (int j = 1; j <= i; j++) {
+                ix++;
+                int i1 = index_of(cl_name(used_map_order, i, j));
+                if (i1 == -1 && i != j) i1 = index_of(cl_name(used_map_order, j, i));
+                if (i1 != -1) {
+                    if (cols[ix - 1] > 0) fail(CMBL_ERR_FORMAT, "GetColsFromOrder: duplicate CL type");
+                    cols[ix - 1] = i1;
+                }
+            }
+        return (int)li.size();
+    }
+    // ReadClArr (:146-193): Cl [bin_min..bin_max][ncl]
+    bool read_cl_arr(const Ini &ini, const std::string &base, std::vector<double> &cl, bool optional) const {
+        std::string fn = ini.relative_filename(base + "_file", !optional);
+        if (fn.empty()) return false;
+        std::string order = ini.str(base + "_order"), incols;
+        if (order.empty()) {
+            incols = last_top_comment(fn);
+            if (incols.empty()) fail(CMBL_ERR_FORMAT, "No column order given for %s", fn.c_str());
+        } else {
+            incols = "L " + order;
+        }
+        std::vector<int> cols;
+        const int norder = cols_from_order(incols, cols) - 1;
+        cl.assign((size_t)nb * ncl, 0.0);
+        auto rows = load_txt(fn);
+        int ll = -1;
+        for (auto &r : rows) {
+            if ((int)r.size() < 1 + norder) fail(CMBL_ERR_FORMAT, "CMBLikes_ReadClArr: error reading line %s", fn.c_str());
+            const int l = (int)r[0];
+            ll = l;
+            if (l >= bin_min && l <= bin_max)
+                for (int ix = 0; ix < ncl; ix++)
+                    if (cols[ix] != 0) cl[(size_t)(l - bin_min) * ncl + ix] = r[cols[ix] - 1];
+        }
+        if (ll < bin_max) fail(CMBL_ERR_FORMAT, "CMBLikes_ReadClArr: C_l file does not go up to maximum used: %d (%s)",
+                               bin_max, fn.c_str());
+        return true;
+    }
+    void read_bin_windows(const Ini &ini, const std::string &type, Windows &bwin) {   // ReadBinWindows :371-464
+        const int L = lmax - lmin + 1;
+        std::string fname = ini.str_required(type + "_files");
+        std::string order1 = ini.str_required(type + "_in_order");
+        std::string order2 = ini.str(type + "_out_order", order1);
+        if (order2.empty()) order2 = order1;
+        use_string_to_cl_i_j(order1, map_required_index, bwin.in_i, bwin.in_j);
+        bwin.out = use_string_to_cols(order2);
+        const int norder = (int)bwin.in_i.size();
+        if (norder != (int)bwin.out.size())
+            fail(CMBL_ERR_FORMAT, "%s_in_order and %s_out_order must have same number of CL", type.c_str(), type.c_str());
+        bwin.W.assign((size_t)nb * norder * L, 0.0);
+        for (int b = bin_min; b <= bin_max; b++) {
+            std::string S = ini.resolve_path(format_u(fname, b));
+            auto rows = load_txt(S);
+            for (auto &r : rows) {
+                if ((int)r.size() < 1 + norder) fail(CMBL_ERR_FORMAT, "ReadBinWindows: error reading line %s", S.c_str());
+                const int l = (int)r[0];
+                if (l >= lmin && l <= lmax)
+                    for (int k = 0; k < norder; k++) bwin.W[((size_t)(b - bin_min) * norder + k) * L + (l - lmin)] = r[1 + k];
+            }
+        }
+        bwin.fix.assign(norder, {});
+        std::string fixf = ini.relative_filename(type + "_fix_cl_file", false);
+        if (!fixf.empty()) {
+            std::string o1 = ini.str(type + "_fix_cl_file_order");
+            if (o1.empty()) {
+                o1 = last_top_comment(fixf);
+                if (o1.empty()) fail(CMBL_ERR_FORMAT, "No column order given for %s", fixf.c_str());
+                while (!o1.empty() && (o1[0] == ' ' || o1[0] == 'L')) o1 = o1.substr(1);
+            }
+            std::vector<int> fi, fj, ui, uj;
+            use_string_to_cl_i_j(o1, map_required_index, fi, fj);
+            use_string_to_cl_i_j(ini.str_required(type + "_fix_cl"), map_required_index, ui, uj);
+            auto rows = load_txt(fixf);
+            for (size_t u = 0; u < ui.size(); u++) {
+                if (ui[u] == 0 || uj[u] == 0) continue;
+                int idx = -1;
+                for (size_t k = 0; k < fi.size(); k++)
+                    if (fi[k] == ui[u] && fj[k] == uj[u]) { idx = (int)k; break; }
+                if (idx < 0) fail(CMBL_ERR_FORMAT, "ReadBinWindows: fix_cl uses CL not in the fix_cl_file");
+                std::vector<double> spec(L, 0.0);
+                for (auto &r : rows) {
+                    const int l = (int)r[0];
+                    if (l >= lmin && l <= lmax && (int)r.size() > idx + 1) spec[l - lmin] = r[idx + 1];
+                }
+                for (int k = 0; k < norder; k++)
+                    if (bwin.in_i[k] == ui[u] && bwin.in_j[k] == uj[u]) bwin.fix[k] = spec;
+            }
+        }
+        bwin.present = true;
+    }
+
+    CMBLikes(const Ini &ini, const std::string &tag_) {
+        tag = tag_;
+        bk = (tag == "BKPLANCK");
+        name = ini.str("name");
+        if (name.empty()) {
+            std::string fn = ini.filename();
+            size_t s = fn.find_last_of('/');
+            fn = fn.substr(s == std::string::npos ? 0 : s + 1);
+            size_t d = fn.find_last_of('.');
+            name = d == std::string::npos ? fn : fn.substr(0, d);
+        }
+        // ---- CMBLikes_ReadIni (:466-749)
+        std::string fmt = ini.str("dataset_format");
+        if (fmt == "CMBLike") fail(CMBL_ERR_FORMAT, "CMBLikes dataset_format now CMBLike2");
+        if (!fmt.empty() && fmt != "CMBLike2") fail(CMBL_ERR_FORMAT, "CMBLikes wrong dataset_format");
+        std::string S = ini.str("map_names");
+        has_map_names = !S.empty();
+        if (has_map_names) {
+            map_names = split_list(S);
+            auto mf = split_list(ini.str_required("map_fields"));
+            if (mf.size() != map_names.size()) fail(CMBL_ERR_FORMAT, "CMBLikes: number of map_fields does not match map_names");
+            for (auto &f : mf) map_fields.push_back(type_index(f[0]));
+        } else {
+            map_names = {"T", "E", "B", "P"};
+            map_fields = {1, 2, 3, 4};
+        }
+        bool use_field[5] = {false, false, false, false, false};
+        S = ini.str("fields_use");
+        if (!S.empty()) {
+            for (auto &f : split_list(S)) use_field[type_index(f[0])] = true;
+        } else {
+            if (!has_map_names) fail(CMBL_ERR_FORMAT, "CMBlikes: must have fields_use or map_names");
+            for (int i = 1; i <= 4; i++) use_field[i] = true;
+        }
+        const int nm = (int)map_names.size();
+        use_map.assign(nm, 0);
+        S = ini.str("maps_use");
+        if (!S.empty()) {
+            for (auto &m : split_list(S)) {
+                const int j = map_index(m);
+                if (j == -1) fail(CMBL_ERR_FORMAT, "CMBlikes: maps_use item not found - %s", m.c_str());
+                use_map[j - 1] = 1;
+            }
+        } else {
+            for (int i = 0; i < nm; i++) use_map[i] = use_field[map_fields[i]];
+        }
+        require_map = use_map;
+        if (has_map_names) {
+            S = ini.str("maps_required");
+            if (ini.has("fields_required")) fail(CMBL_ERR_FORMAT, "CMBLikes: use maps_required not fields_required");
+        } else {
+            S = ini.str("fields_required");
+        }
+        for (auto &m : split_list(S)) {
+            const int j = map_index(m);
+            if (j == -1) fail(CMBL_ERR_FORMAT, "CMBlikes: required item not found - %s", m.c_str());
+            require_map[j - 1] = 1;
+        }
+        bool req_field[5] = {false, false, false, false, false};
+        for (int i = 0; i < nm; i++)
+            if (require_map[i]) req_field[map_fields[i]] = true;
+        std::string la = ini.str_required("like_approx");
+        if (la == "HL") approx = 1;
+        else if (la == "gaussian") approx = 2;
+        else if (la == "exact") fail(CMBL_ERR_UNSUPPORTED, "CMBlikes: like_approx = exact is not supported");
+        else fail(CMBL_ERR_FORMAT, "CMBlikes: unknown like_approx %s", la.c_str());
+        for (int i = 0; i < nm; i++) {
+            nmaps += use_map[i];
+            nreq += require_map[i];
+        }
+        if (nmaps < 1) fail(CMBL_ERR_FORMAT, "CMBlikes: no maps used");
+        if (approx == 1 && nmaps > CL_MAXMAPS) fail(CMBL_ERR_UNSUPPORTED, "CMBlikes HL: at most %d maps", CL_MAXMAPS);
+        if (nreq > CL_MAXREQ) fail(CMBL_ERR_UNSUPPORTED, "CMBlikes: at most %d required maps", CL_MAXREQ);
+        map_required_index.assign(nm, 0);
+        map_used_index.assign(nm, 0);
+        int ix = 0;
+        for (int i = 0; i < nm; i++)
+            if (require_map[i]) {
+                map_required_index[i] = ++ix;
+                required_order.push_back(i + 1);
+            }
+        ix = 0;
+        for (int i = 0; i < nm; i++)
+            if (use_map[i]) {
+                map_used_index[i] = ++ix;
+                used_map_order.push_back(map_names[i]);
+            }
+        ncl = nmaps * (nmaps + 1) / 2;
+        lmin = ini_int(ini, "cl_lmin", true, 0);
+        lmax = ini_int(ini, "cl_lmax", true, 0);
+        if (!ini_logical(ini, "binned", false))
+            fail(CMBL_ERR_UNSUPPORTED, "CMBlikes: unbinned likelihoods are not supported (untested in the reference)");
+        nbins = ini_int(ini, "nbins", false, 0);
+        aberration = ini_double(ini, "aberration_coeff", 0.0);
+        bin_min = ini_int(ini, "use_min", false, 1);
+        bin_max = ini_int(ini, "use_max", false, nbins);
+        if (bin_min < 1 || bin_min > nbins || bin_max < bin_min || bin_max > nbins)
+            fail(CMBL_ERR_FORMAT, "CMBlikes: use_min/use_max outside 1..nbins");
+        nb = bin_max - bin_min + 1;
+        read_bin_windows(ini, "bin_window", bw);
+        read_cl_arr(ini, "cl_hat", clhat, false);
+        if (approx == 1) read_cl_arr(ini, "cl_fiducial", clfid, false);
+        const bool includes_noise = ini_logical(ini, "cl_hat_includes_noise", false);
+        bool have_noise = false;
+        if (approx != 2 || includes_noise) {
+            read_cl_arr(ini, "cl_noise", clnoise, false);
+            have_noise = true;
+            if (!includes_noise) {
+                for (size_t k = 0; k < clhat.size(); k++) clhat[k] = clhat[k] + clnoise[k];
+            } else if (approx == 2) {
+                for (size_t k = 0; k < clhat.size(); k++) clhat[k] = clhat[k] - clnoise[k];
+                have_noise = false;
+            }
+        }
+        for (int i = 1; i <= 4; i++)
+            if (req_field[i]) cl_lmax[(i - 1) * 4 + (i - 1)] = lmax;
+        if (req_field[1] && req_field[2]) cl_lmax[(2 - 1) * 4 + (1 - 1)] = lmax;
+        if (ini.has("point_source_cl") || ini.has("beam_modes_file"))
+            fail(CMBL_ERR_FORMAT, "dataset uses keywords no longer supported");
+        bool fid_incl_noise = false;
+        if (approx != 2) fid_incl_noise = ini_logical(ini, "cl_fiducial_includes_noise", false);
+        // per-bin matrices (:711-724)
+        std::vector<double> chatM((size_t)nb * nmaps * nmaps), cfh((size_t)nb * nmaps * nmaps);
+        auto to_matrix = [&](const double *X, double *M) {
+            int q = 0;
+            for (int i = 0; i < nmaps; i++)
+                for (int j = 0; j <= i; j++, q++) M[i * nmaps + j] = M[j * nmaps + i] = X[q];
+        };
+        for (int b = 0; b < nb; b++) {
+            to_matrix(&clhat[(size_t)b * ncl], &chatM[(size_t)b * nmaps * nmaps]);
+            if (approx == 1) {
+                std::vector<double> f(clfid.begin() + (size_t)b * ncl, clfid.begin() + (size_t)(b + 1) * ncl);
+                if (!fid_incl_noise)
+                    for (int k = 0; k < ncl; k++) f[k] = f[k] + clnoise[(size_t)b * ncl + k];
+                std::vector<double> M((size_t)nmaps * nmaps);
+                to_matrix(f.data(), M.data());
+                sym_power(M, nmaps, 0.5);
+                std::copy(M.begin(), M.end(), cfh.begin() + (size_t)b * nmaps * nmaps);
+            }
+        }
+        read_covmat(ini);
+        std::vector<double> fc;
+        if (read_cl_arr(ini, "linear_correction_fiducial", fc, true)) {
+            fidcorr = fc;
+            read_bin_windows(ini, "linear_correction_bin_window", cw);
+        }
+        std::string cp = ini.relative_filename("calibration_param", false);
+        if (bk && !cp.empty()) fail(CMBL_ERR_UNSUPPORTED, "BKPLANCK with calibration_param is not supported");
+        if (!cp.empty()) {
+            nuisance_names = load_paramnames(cp, &n_nuis);
+            cal_index = n_nuis - 1;
+            log_cal_prior = ini_double(ini, "log_calibration_prior", -1.0);
+        }
+        // ---- TBK_planck_ReadIni (CMB_BK_Planck.f90:36-70)
+        std::vector<BKMap> bkm;
+        std::vector<double> bnu, bR, bdnu;
+        if (bk) {
+            nuisance_names = load_paramnames(ini.relative_filename("nuisance_params", true), &n_nuis);
+            if (n_nuis < BK_NPARAM) fail(CMBL_ERR_FORMAT, "BKPLANCK: nuisance_params needs %d parameters", BK_NPARAM);
+            dev.fpivot_dust = ini_double(ini, "fpivot_dust", 353.0);
+            dev.fpivot_sync = ini_double(ini, "fpivot_sync", 23.0);
+            dev.decorr_dust[0] = ini_double(ini, "fpivot_dust_decorr(1)", 217.0);
+            dev.decorr_dust[1] = ini_double(ini, "fpivot_dust_decorr(2)", 353.0);
+            dev.decorr_sync[0] = ini_double(ini, "fpivot_sync_decorr(1)", 23.0);
+            dev.decorr_sync[1] = ini_double(ini, "fpivot_sync_decorr(2)", 33.0);
+            auto lform = [&](const std::string &k) {
+                std::string v = ini.str(k, "flat");
+                return v == "lin" ? 1 : v == "quad" ? 2 : 0;
+            };
+            dev.lform_dust = lform("lform_dust_decorr");
+            dev.lform_sync = lform("lform_sync_decorr");
+            if (nreq != nmaps) fail(CMBL_ERR_UNSUPPORTED, "BKPLANCK: maps_required beyond maps_use not supported");
+            const double G = ghz_kelvin();
+            for (int i = 0; i < nreq; i++) {
+                const std::string &mn = used_map_order[i];
+                auto R = load_txt(ini.relative_filename("bandpass[" + mn + "]", true));
+                const int n = (int)R.size();
+                if (n < 2) fail(CMBL_ERR_FORMAT, "bandpass for %s too short", mn.c_str());
+                BKMap m{};
+                m.off = (int)bnu.size();
+                m.n = n;
+                std::vector<double> dnu(n);
+                dnu[0] = R[1][0] - R[0][0];
+                for (int k = 1; k < n - 1; k++) dnu[k] = (R[k + 1][0] - R[k - 1][0]) / 2;
+                dnu[n - 1] = R[n - 1][0] - R[n - 2][0];
+                double th_int = 0, s1 = 0, s2 = 0;
+                for (int k = 0; k < n; k++) {
+                    const double nu = R[k][0], r = R[k][1];
+                    const double e = std::exp(G * nu / BK_TCMB);
+                    th_int += dnu[k] * r * (nu * nu * nu * nu) * e / ((e - 1) * (e - 1));
+                    s1 += dnu[k] * nu * r;
+                    s2 += dnu[k] * r;
+                    bnu.push_back(nu);
+                    bR.push_back(r);
+                    bdnu.push_back(dnu[k]);
+                }
+                auto th0 = [&](double nu0) {
+                    const double e = std::exp(G * nu0 / BK_TCMB);
+                    return (nu0 * nu0 * nu0 * nu0) * e / ((e - 1) * (e - 1));
+                };
+                m.th_dust = th_int / th0(dev.fpivot_dust);
+                m.th_sync = th_int / th0(dev.fpivot_sync);
+                m.nu_bar = s1 / s2;
+                m.bc = mn.find("95") != std::string::npos ? 1 : mn.find("150") != std::string::npos ? 2
+                       : mn.find("220") != std::string::npos ? 3 : 0;
+                bkm.push_back(m);
+            }
+        }
+        build_device(have_noise, chatM, cfh, bkm, bnu, bR, bdnu);
+    }
+
+    std::vector<double> invcov;
+    void read_covmat(const Ini &ini) {   // ReadCovmat (:752-859), binned
+        std::string covmat_cl = ini.str_required("covmat_cl");
+        std::string fn = ini.relative_filename("covmat_fiducial", true);
+        const double scale = ini_double(ini, "covmat_scale", 1.0);
+        auto cl_in = use_string_to_cols(covmat_cl);
+        const int num_in = (int)cl_in.size();
+        std::vector<int> cov_cl_used;
+        for (int i = 0; i < num_in; i++)
+            if (cl_in[i] != 0) {
+                cl_use.push_back(cl_in[i] - 1);
+                cov_cl_used.push_back(i);
+            }
+        ncl_used = (int)cl_use.size();
+        if (ncl_used == 0) fail(CMBL_ERR_FORMAT, "CMBlikes: covmat_cl selects no used spectra");
+        const int nin = num_in * nbins;
+        std::vector<double> cov;
+        for (auto &r : load_txt(fn)) cov.insert(cov.end(), r.begin(), r.end());
+        if ((long long)cov.size() < (long long)nin * nin)
+            fail(CMBL_ERR_FORMAT, "%s: covariance needs %d x %d entries", fn.c_str(), nin, nin);
+        nX = nb * ncl_used;
+        invcov.assign((size_t)nX * nX, 0.0);
+        for (int bx = bin_min; bx <= bin_max; bx++)
+            for (int by = bin_min; by <= bin_max; by++)
+                for (int a = 0; a < ncl_used; a++)
+                    for (int b = 0; b < ncl_used; b++)
+                        invcov[(size_t)((bx - bin_min) * ncl_used + a) * nX + (by - bin_min) * ncl_used + b] =
+                            scale * cov[(size_t)((bx - 1) * num_in + cov_cl_used[a]) * nin + (by - 1) * num_in +
+                                        cov_cl_used[b]];
+        spd_inverse(invcov, nX);
+    }
+
+    void build_device(bool have_noise, const std::vector<double> &chatM, const std::vector<double> &cfh,
+                      const std::vector<BKMap> &bkm, const std::vector<double> &bnu, const std::vector<double> &bR,
+                      const std::vector<double> &bdnu) {
+        const int L = lmax - lmin + 1;
+        // required map pairs (InitMapCls :997-1019, MapPair_to_Theory_i_j :284-299)
+        std::vector<CLPair> pairs;
+        auto pair_index = [&](int i, int j) { return (i - 1) * i / 2 + (j - 1); };   // i >= j, 1-based
+        for (int i = 1; i <= nreq; i++)
+            for (int j = 1; j <= i; j++) {
+                int f1 = map_fields[required_order[i - 1] - 1], f2 = map_fields[required_order[j - 1] - 1];
+                if (f2 > f1) std::swap(f1, f2);
+                CLPair p{};
+                p.field = f1 * (f1 - 1) / 2 + (f2 - 1);
+                p.cmb = (f1 <= 3 && f2 <= 3);
+                p.fg = bk ? ((f1 == 2 && f2 == 2) ? 1 : (f1 == 3 && f2 == 3) ? 2 : 0) : 0;
+                p.mi = i - 1;
+                p.mj = j - 1;
+                p.lo = 1 << 30;
+                p.hi = -1;
+                pairs.push_back(p);
+            }
+        // window columns: main (bins x windows) then correction
+        std::vector<CLCol> cols;
+        std::vector<double> wpack, colfixed;
+        std::vector<unsigned char> isfixed;
+        std::vector<int> colpair;
+        std::vector<std::vector<int>> sum_lists((size_t)nb * ncl), corr_lists((size_t)nb * ncl);
+        auto add_windows = [&](const Windows &wn, std::vector<std::vector<int>> &lists) {
+            const int norder = (int)wn.in_i.size();
+            for (int b = 0; b < nb; b++)
+                for (int k = 0; k < norder; k++) {
+                    if (wn.out[k] <= 0) continue;
+                    const double *Wk = &wn.W[((size_t)b * norder + k) * L];
+                    int lo = L, hi = -1;
+                    for (int l = 0; l < L; l++)
+                        if (Wk[l] != 0.0) { lo = std::min(lo, l); hi = l; }
+                    CLCol c{};
+                    int pid = -1;
+                    double fixed = 0.0;
+                    bool fx = !wn.fix[k].empty();
+                    if (fx) {
+                        for (int l = 0; l < L; l++) fixed += Wk[l] * wn.fix[k][l];
+                    } else {
+                        if (wn.in_i[k] == 0 || wn.in_j[k] == 0)
+                            fail(CMBL_ERR_FORMAT, "CMBlikes: bin window uses a spectrum of a map that is not required");
+                        pid = pair_index(wn.in_i[k], wn.in_j[k]);
+                    }
+                    if (hi < lo) { lo = 0; hi = -1; }
+                    c.lo = lo + lmin;
+                    c.hi = hi + lmin;
+                    c.off = (long long)wpack.size();
+                    for (int l = lo; l <= hi; l++) wpack.push_back(Wk[l]);
+                    const int ci = (int)cols.size();
+                    cols.push_back(c);
+                    colfixed.push_back(fixed);
+                    isfixed.push_back(fx ? 1 : 0);
+                    colpair.push_back(pid);
+                    if (pid >= 0 && hi >= lo) {
+                        pairs[pid].lo = std::min(pairs[pid].lo, c.lo);
+                        pairs[pid].hi = std::max(pairs[pid].hi, c.hi);
+                    }
+                    lists[(size_t)b * ncl + (wn.out[k] - 1)].push_back(ci);
+                }
+        };
+        add_windows(bw, sum_lists);
+        if (cw.present) add_windows(cw, corr_lists);
+        // group columns by pair
+        std::vector<int> col_of_pair;
+        int lpair = 2;
+        for (size_t p = 0; p < pairs.size(); p++) {
+            pairs[p].col0 = (int)col_of_pair.size();
+            for (size_t ci = 0; ci < cols.size(); ci++)
+                if (colpair[ci] == (int)p && cols[ci].hi >= cols[ci].lo) col_of_pair.push_back((int)ci);
+            pairs[p].ncol = (int)col_of_pair.size() - pairs[p].col0;
+            if (pairs[p].ncol == 0) { pairs[p].lo = 0; pairs[p].hi = -1; }
+            else lpair = std::max(lpair, pairs[p].hi - pairs[p].lo + 1);
+        }
+        for (auto &p : pairs)
+            if (p.ncol > 0) max_field = std::max(max_field, p.field);
+        // columns with an empty window contribute 0 (mark fixed with value 0)
+        for (size_t ci = 0; ci < cols.size(); ci++)
+            if (cols[ci].hi < cols[ci].lo) isfixed[ci] = 1;
+        auto flatten = [&](const std::vector<std::vector<int>> &lists, std::vector<int> &off, std::vector<int> &all) {
+            off.assign(lists.size() + 1, 0);
+            for (size_t e = 0; e < lists.size(); e++) {
+                off[e] = (int)all.size();
+                all.insert(all.end(), lists[e].begin(), lists[e].end());
+            }
+            off[lists.size()] = (int)all.size();
+        };
+        std::vector<int> sum_off, sum_cols, corr_off, corr_cols;
+        flatten(sum_lists, sum_off, sum_cols);
+        flatten(corr_lists, corr_off, corr_cols);
+        if (sum_cols.empty()) sum_cols.push_back(0);
+        if (corr_cols.empty()) corr_cols.push_back(0);
+        if (wpack.empty()) wpack.push_back(0.0);
+        std::vector<double> fc((size_t)nb * ncl, 0.0), noise((size_t)nb * ncl, 0.0);
+        if (cw.present) fc = fidcorr;
+        if (have_noise) noise = clnoise;
+
+        auto up = [](DevBuf &d, const void *p, size_t bytes) {
+            d.alloc(std::max<size_t>(bytes, 16));
+            if (bytes) d.upload(p, bytes);
+        };
+        up(d_pairs, pairs.data(), pairs.size() * sizeof(CLPair));
+        up(d_cols, cols.data(), cols.size() * sizeof(CLCol));
+        up(d_colpair, col_of_pair.data(), col_of_pair.size() * 4);
+        up(d_wts, wpack.data(), wpack.size() * 8);
+        up(d_colfixed, colfixed.data(), colfixed.size() * 8);
+        up(d_isfixed, isfixed.data(), isfixed.size());
+        up(d_sumoff, sum_off.data(), sum_off.size() * 4);
+        up(d_sumcols, sum_cols.data(), sum_cols.size() * 4);
+        up(d_corroff, corr_off.data(), corr_off.size() * 4);
+        up(d_corrcols, corr_cols.data(), corr_cols.size() * 4);
+        up(d_fidcorr, fc.data(), fc.size() * 8);
+        up(d_noise, noise.data(), noise.size() * 8);
+        up(d_chat, clhat.data(), clhat.size() * 8);
+        up(d_cluse, cl_use.data(), cl_use.size() * 4);
+        up(d_hlchat, chatM.data(), chatM.size() * 8);
+        up(d_hlcf, cfh.data(), cfh.size() * 8);
+        if (bk) {
+            up(d_bkmaps, bkm.data(), bkm.size() * sizeof(BKMap));
+            up(d_bpnu, bnu.data(), bnu.size() * 8);
+            up(d_bpR, bR.data(), bR.size() * 8);
+            up(d_bpdnu, bdnu.data(), bdnu.size() * 8);
+        }
+        qf.init(invcov, nX);
+        dev.lmin = lmin;
+        dev.lmax = lmax;
+        dev.npair = (int)pairs.size();
+        dev.ncol = (int)cols.size();
+        dev.nb = nb;
+        dev.ncl = ncl;
+        dev.ncl_used = ncl_used;
+        dev.nX = nX;
+        dev.Np = qf.Np;
+        dev.approx = approx;
+        dev.has_corr = cw.present ? 1 : 0;
+        dev.cal_index = cal_index;
+        dev.log_cal_prior = log_cal_prior;
+        dev.aberration = aberration;
+        dev.lpair = (lpair + 1) & ~1;
+        dev.pairs = d_pairs.as<CLPair>();
+        dev.cols = d_cols.as<CLCol>();
+        dev.col_of_pair = d_colpair.as<int>();
+        dev.wts = d_wts.as<double>();
+        dev.col_fixed = d_colfixed.as<double>();
+        dev.col_is_fixed = d_isfixed.as<unsigned char>();
+        dev.sum_off = d_sumoff.as<int>();
+        dev.sum_cols = d_sumcols.as<int>();
+        dev.corr_off = d_corroff.as<int>();
+        dev.corr_cols = d_corrcols.as<int>();
+        dev.fidcorr = d_fidcorr.as<double>();
+        dev.noise = d_noise.as<double>();
+        dev.chat = d_chat.as<double>();
+        dev.cl_use = d_cluse.as<int>();
+        dev.bk = bk ? 1 : 0;
+        dev.nreq = nreq;
+        dev.bkmaps = bk ? d_bkmaps.as<BKMap>() : nullptr;
+        dev.bp_nu = bk ? d_bpnu.as<double>() : nullptr;
+        dev.bp_R = bk ? d_bpR.as<double>() : nullptr;
+        dev.bp_dnu = bk ? d_bpdnu.as<double>() : nullptr;
+        lds_bytes = (size_t)(2 * dev.lpair + dev.ncol + nb * ncl + (bk ? 3 * L : 0) + 3 * nreq + 2) * 8;
+        if (lds_bytes > 160 * 1024) fail(CMBL_ERR_UNSUPPORTED, "CMBlikes: dataset needs %zu bytes of LDS", lds_bytes);
+        if (lds_bytes > 64 * 1024)
+            HIP_CHECK(hipFuncSetAttribute((const void *)cmbl_bin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)lds_bytes));
+        hl.n = nmaps;
+        hl.m = (nmaps + 1) & ~1;
+        if (hl.m < 2) hl.m = 2;
+        hl.nb = nb;
+        hl.ncl = ncl;
+        hl.ncl_used = ncl_used;
+        hl.nX = nX;
+        hl.Np = qf.Np;
+        hl.chat = d_hlchat.as<double>();
+        hl.cfhalf = d_hlcf.as<double>();
+        hl.cl_use = d_cluse.as<int>();
+    }
+
+    size_t cmat_bytes(int W) const { return approx == 1 ? (size_t)W * nb * ncl * 8 : 0; }
+    size_t workspace_size(int W) const override {
+        return qf.workspace_size(W) + ((cmat_bytes(W) + (size_t)W * 8 + 255) & ~size_t(255)) + 256;
+    }
+
+    void loglike_batch(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis,
+                       long long ld_nuis, double *out, void *ws, hipStream_t stream) override {
+        if (W <= 0) return;
+        if (n_nuis > 0 && !nuis) fail(CMBL_ERR_ARG, "%s needs its %d nuisance parameters", name.c_str(), n_nuis);
+        if (ld_field < lmax + 1) fail(CMBL_ERR_ARG, "ld_field %lld < cl_lmax+1 = %d", ld_field, lmax + 1);
+        if (W > 1 && ld_walker < (long long)(max_field + 1) * ld_field)
+            fail(CMBL_ERR_ARG, "ld_walker must cover theory fields 0..%d", max_field);
+        if (!ws) {
+            own_ws.grow(workspace_size(W));
+            ws = own_ws.p;
+        }
+        char *base = static_cast<char *>(ws);
+        double *cmat = reinterpret_cast<double *>(base + ((qf.workspace_size(W) + 255) & ~size_t(255)));
+        double *addend = cmat + (size_t)W * nb * ncl * (approx == 1 ? 1 : 0);
+        const bool use_add = log_cal_prior > 0 && cal_index >= 0;
+        const double *nu = nuis ? nuis : dl;   // never read when n_nuis == 0
+        timed_launch("cmbl_bin_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            hipExtLaunchKernelGGL(cmbl_bin_kernel, dim3(W), dim3(256), (uint32_t)lds_bytes, stream, e0, e1, 0, dev, dl,
+                                  ld_field, ld_walker, nu, ld_nuis, qf.x_rows(ws), cmat, use_add ? addend : nullptr,
+                                  qf.counters(ws, W), qf.n_counters(W));
+        });
+        HIP_CHECK(hipGetLastError());
+        if (approx == 1) {
+            timed_launch("cmbl_hl_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+                hipExtLaunchKernelGGL(cmbl_hl_kernel, dim3(W * nb), dim3(64), 0, stream, e0, e1, 0, hl,
+                                      (const double *)cmat, qf.x_rows(ws), W);
+            });
+            HIP_CHECK(hipGetLastError());
+        }
+        qf.launch(W, ws, use_add ? addend : nullptr, out, stream, "cmbl_quadform");
+    }
+};
+
+std::unique_ptr<Like> make_cmblikes(const Ini &ini, const std::string &tag) {
+    return std::unique_ptr<Like>(new CMBLikes(ini, tag));
+}
+
+}  // namespace cmamd

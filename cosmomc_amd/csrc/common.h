@@ -134,6 +134,7 @@ class Ini {
     std::string str(const std::string &key, const std::string &def = "") const;
     std::string str_required(const std::string &key) const;
     std::string relative_filename(const std::string &key, bool required) const;
+    std::string resolve_path(std::string value) const;     // the same rule for a value given directly
     const std::string &filename() const { return filename_; }
 
   private:
@@ -148,6 +149,8 @@ bool file_exists(const std::string &path);
 // File%LoadTxt: whitespace-separated numeric matrix, '#' comment lines skipped
 std::vector<std::vector<double>> load_txt(const std::string &path);
 std::vector<std::string> split_ws(const std::string &s);
+// .paramnames file -> space-separated names (derived '*' stripped), count
+std::string load_paramnames(const std::string &path, int *count);
 
 // ---------------- likelihood object ----------------
 struct Like {
@@ -166,6 +169,7 @@ struct Like {
 };
 
 std::unique_ptr<Like> make_plik_lite(const Ini &ini);
+std::unique_ptr<Like> make_cmblikes(const Ini &ini, const std::string &tag);
 
 }  // namespace cmamd
 

@@ -105,7 +105,10 @@ std::string Ini::str_required(const std::string &key) const {
 }
 
 std::string Ini::relative_filename(const std::string &key, bool required) const {
-    std::string v = required ? str_required(key) : str(key);
+    return resolve_path(required ? str_required(key) : str(key));
+}
+
+std::string Ini::resolve_path(std::string v) const {
     if (v.empty()) return v;
     // %DATASETDIR% / %LOCALDIR% (settings.f90:183-184): resolve against the
     // environment override or leave for the relative rule below

@@ -82,6 +82,12 @@ def base_theory(lmax: int = PLMAX) -> np.ndarray:
     m = L <= lmax
     for f, key in ((FIELD_TT, "TT"), (FIELD_TE, "TE"), (FIELD_EE, "EE"), (FIELD_BB, "BB"), (FIELD_PP, "PP")):
         out[f, L[m]] = z[key][m]
+        if lmax > L[-1]:
+            # beyond the file (l > 2508, e.g. SPT-SZ to 3300): damping-tail
+            # extrapolation D_l = D_2508 exp(-(l - 2508) / 600), (2508/l)^2 for PP
+            ell = np.arange(L[-1] + 1, lmax + 1, dtype=np.float64)
+            tail = (L[-1] / ell) ** 2 if key == "PP" else np.exp(-(ell - L[-1]) / 600.0)
+            out[f, L[-1] + 1:] = z[key][-1] * tail
     return out
 
 

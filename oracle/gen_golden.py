@@ -189,6 +189,76 @@ def gen_gr():
         json.dump(out, f, indent=0)
 
 
+# CMBlikes cases on the reference's own data (tests/golden/refdata.tar.xz):
+# (name, tag, dataset, overrides, walkers, lmax, nuisance kind)
+LENS = "planck_lensing_2018/smicadx12_Dec5_ftl_mv2_ndclpp_p_teb_consext8.dataset"
+BKP = "BKPlanck/BKPlanck_detset_comb_dust.dataset"
+CMBL_CASES = [
+    ("lensing_consext8", "lensing", LENS, {}, 6, 2500, "cal"),
+    ("bkplanck_3map_bins1to5", "BKPLANCK", BKP, {"maps_use": "B2K_B P217_B P353_B", "use_min": "1", "use_max": "5"},
+     5, 600, "bk_fid"),
+    ("bkplanck_all_maps", "BKPLANCK", BKP, {}, 4, 600, "bk_sync"),
+    ("bkplanck_decorr_lin_quad", "BKPLANCK", BKP, {"lform_dust_decorr": "lin", "lform_sync_decorr": "quad"},
+     3, 600, "bk_decorr"),
+    ("bkplanck_EB_4map", "BKPLANCK", BKP, {"maps_use": "B2K_E B2K_B P353_E P353_B", "use_max": "7"}, 3, 600, "bk_sync"),
+    ("sptsz_aberration_calprior", "SPT", "sptsz_2500d_tt/spt_s13_margfg.dataset", {}, 5, 3300, "cal_spt"),
+]
+BK_FID = [3.0, 0.0, -0.42, 1.59, 19.6, -0.6, -3.3, 0.0, 2.0, 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0]
+
+
+def cmbl_nuisance(kind, W, seed):
+    g = syn.gaussians(seed, W * 16).reshape(W, 16)
+    if kind == "cal":
+        return 1.0 + 0.0025 * g[:, :1]
+    if kind == "cal_spt":
+        return 1.0 + 0.0017 * g[:, :1]
+    P = np.tile(np.array(BK_FID), (W, 1))
+    P[:, 0] = 3.0 + 0.5 * g[:, 0]
+    P[:, 3] = 1.59 + 0.05 * g[:, 3]
+    if kind in ("bk_sync", "bk_decorr"):
+        P[:, 1] = 1.0 + 0.2 * np.abs(g[:, 1])
+        P[:, 2] = -0.42 + 0.05 * g[:, 2]
+        P[:, 4] = 19.6 + 0.5 * g[:, 4]
+        P[:, 7] = 0.2 + 0.05 * g[:, 7]
+    if kind == "bk_decorr":
+        P[:, 7] = 0.0
+        P[:, 10] = 0.85 + 0.02 * g[:, 10]
+        P[:, 11] = 0.9 + 0.02 * g[:, 11]
+    return P
+
+
+def refdata_dir(td):
+    import lzma
+    import tarfile
+    import io
+    d = os.path.join(td, "refdata")
+    with open(os.path.join(GOLDEN, "refdata.tar.xz"), "rb") as f:
+        tar = tarfile.open(fileobj=io.BytesIO(lzma.decompress(f.read())))
+        try:
+            tar.extractall(d, filter="data")
+        except TypeError:
+            tar.extractall(d)
+    return d
+
+
+def gen_cmblikes():
+    out = {"theory_seed": 0xC05A0C, "cases": {}}
+    with tempfile.TemporaryDirectory() as td:
+        data = refdata_dir(td)
+        for ci, (name, tag, ds, over, W, lmax, kind) in enumerate(CMBL_CASES):
+            th = syn.walker_theory(W, seed=out["theory_seed"] + 1000 * ci, lmax=lmax)
+            nu = cmbl_nuisance(kind, W, 4242 + ci)
+            ini = f"cmb_dataset[{tag}] = {os.path.join(data, ds)}\n" + \
+                "".join(f"cmb_dataset[{tag},{k}] = {v}\n" for k, v in over.items())
+            ref = run_cmb_harness(ini, th, nu, td)
+            out["cases"][name] = {"tag": tag, "dataset": ds, "overrides": over, "walkers": W, "lmax": lmax,
+                                  "theory_seed": out["theory_seed"] + 1000 * ci, "nuis": nu.tolist(),
+                                  "minus_lnL": ref.tolist()}
+            print(f"{name:28s} -lnL[0] = {ref[0]:.10f}")
+    with open(os.path.join(GOLDEN, "cmblikes_ref.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
     if not os.path.exists(os.path.join(REF_DIR, "plik_harness")):
         sys.exit("build the reference first: make -C oracle ref")
@@ -199,3 +269,5 @@ if __name__ == "__main__":
         gen_rng()
     if not only or "gr" in only:
         gen_gr()
+    if not only or "cmblikes" in only:
+        gen_cmblikes()

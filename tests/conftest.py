@@ -32,3 +32,25 @@ def rng_golden():
 @pytest.fixture(scope="session")
 def gr_golden():
     return load_golden("gr_ref.json")
+
+
+@pytest.fixture(scope="session")
+def cmbl_golden():
+    return load_golden("cmblikes_ref.json")
+
+
+@pytest.fixture(scope="session")
+def refdata(tmp_path_factory):
+    """The reference's own CMBlikes data files (tests/golden/refdata.tar.xz,
+    packed by oracle/pack_refdata.py) extracted to a temporary directory."""
+    import io
+    import lzma
+    import tarfile
+    d = str(tmp_path_factory.mktemp("refdata"))
+    with open(os.path.join(GOLDEN, "refdata.tar.xz"), "rb") as f:
+        tar = tarfile.open(fileobj=io.BytesIO(lzma.decompress(f.read())))
+        try:
+            tar.extractall(d, filter="data")
+        except TypeError:
+            tar.extractall(d)
+    return d

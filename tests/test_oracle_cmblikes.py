@@ -1,0 +1,24 @@
+"""CMBlikes oracle (oracle/cmblikes_oracle.py) against the compiled reference
+(tests/golden/cmblikes_ref.json) on the reference's own datasets: Planck 2018
+lensing (gaussian + linear correction + calPlanck), BICEP2/Keck/Planck (HL +
+foregrounds, decorrelation), SPT-SZ (aberration + log-calibration prior)."""
+import os
+
+import numpy as np
+import pytest
+
+import cmblikes_oracle as co
+from cosmomc_amd import synthetic as syn
+
+CASES = ["lensing_consext8", "bkplanck_3map_bins1to5", "bkplanck_all_maps", "bkplanck_decorr_lin_quad",
+         "bkplanck_EB_4map", "sptsz_aberration_calprior"]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_cmblikes_oracle_vs_reference(cmbl_golden, refdata, case):
+    c = cmbl_golden["cases"][case]
+    o = co.CMBLikesOracle(os.path.join(refdata, c["dataset"]), c["overrides"], c["tag"])
+    th = syn.walker_theory(c["walkers"], seed=c["theory_seed"], lmax=c["lmax"])
+    nu = np.array(c["nuis"])
+    got = np.array([o.loglike(th[w], nu[w]) for w in range(c["walkers"])])
+    np.testing.assert_allclose(got, c["minus_lnL"], rtol=1e-11, atol=1e-9)
