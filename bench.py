@@ -8,13 +8,15 @@ BlockedProposer GetProposalFast (propose.f90:283-289) -> native plik_lite
 binning + 613x613 quadratic form every step, as the reference) + calPlanck
 prior -> Metropolis accept.  Each step is W likelihood evaluations.
 
-Workload: BASELINE.json configs[2] (plik_lite_TTTEEE, 1024 walkers on one
-MI355X, cached slow block) without its lowl (clik commander: unavailable,
-parity-unpinned) and lensing terms.  Synthetic inputs of the Planck l_max
-shape (cosmomc_amd.synthetic).  Multi-GPU: walkers are sharded across ranks
-with no per-step collective ("weak" scaling).
+Workload: BASELINE.json configs[2] -- plik_lite_TTTEEE + Planck 2018 lensing
+(the reference's own consext8 dataset, tests/golden/refdata.tar.xz), 1024
+walkers on one MI355X, cached slow block -- without its lowl term (clik
+commander: library unavailable, parity-unpinned).  Each evaluation is both
+likelihoods + the calPlanck prior.  Synthetic theory of the Planck l_max shape
+(cosmomc_amd.synthetic).  Multi-GPU: walkers are sharded across ranks with no
+per-step collective ("weak" scaling).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 1024]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 1024] [--no-lensing]
 """
 from __future__ import annotations
 
@@ -51,10 +53,29 @@ def parse():
                    help="walker groups stepped on concurrent streams (cmbs_set_groups)")
     p.add_argument("--cpu-seconds", type=float, default=1.5, help="per-process CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-lensing", action="store_true", help="plik_lite only (configs[2] minus lensing)")
     return p.parse_args()
 
 
-def build_problem(W, rank, tmpdir, groups=1):
+LENS_DATASET = "planck_lensing_2018/smicadx12_Dec5_ftl_mv2_ndclpp_p_teb_consext8.dataset"
+
+
+def extract_refdata(tmpdir):
+    """The reference's own lensing dataset files, from the committed fixture."""
+    import io
+    import lzma
+    import tarfile
+    d = os.path.join(tmpdir, "refdata")
+    with open(os.path.join(ROOT, "tests", "golden", "refdata.tar.xz"), "rb") as f:
+        tar = tarfile.open(fileobj=io.BytesIO(lzma.decompress(f.read())))
+        try:
+            tar.extractall(d, filter="data")
+        except TypeError:
+            tar.extractall(d)
+    return d
+
+
+def build_problem(W, rank, tmpdir, groups=1, lensing=True):
     import torch
     from cosmomc_amd import synthetic as syn
     from cosmomc_amd.likelihood import NativeCMBLikelihood
@@ -62,6 +83,11 @@ def build_problem(W, rank, tmpdir, groups=1):
     data = syn.make_plik_lite(12345)
     ds = data.write(tmpdir)
     like = NativeCMBLikelihood("PLIK_LITE", ds)
+    likes = [like]
+    if lensing:
+        lens = NativeCMBLikelihood("lensing", os.path.join(extract_refdata(tmpdir), LENS_DATASET))
+        lens.nuisance_indices = [7]                   # calPlanck, shared with plik_lite
+        likes.append(lens)
     # parameters: 6 slow cosmological parameters (fixed theory cached per walker)
     # + calPlanck (fast, nuisance of plik_lite); blocks slow | fast
     names = ["omegabh2", "omegach2", "theta", "tau", "logA", "ns"]
@@ -78,13 +104,15 @@ def build_problem(W, rank, tmpdir, groups=1):
                       propose_scale=2.4, seed_ij=1802 + rank, seed_kl=9373, first_walker=rank * W)
     smp.set_covariance(np.diag(sig ** 2))
     smp.set_groups(groups)
-    theory = torch.tensor(syn.walker_theory(W, first_walker=rank * W, n_fields=3, ld_field=2512), device="cuda")
-    smp.add_likelihood(like, theory)
+    nf = 10 if lensing else 3
+    theory = torch.tensor(syn.walker_theory(W, first_walker=rank * W, n_fields=nf, ld_field=2512), device="cuda")
+    for lk in likes:
+        smp.add_likelihood(lk, theory)
     smp.set_start(np.tile(P0, (W, 1)))
-    return smp, like, theory, names
+    return smp, likes, theory, names
 
 
-def cpu_baseline(seconds):
+def cpu_baseline(seconds, lensing=True):
     """The reference's own plik_lite LogLike (oracle/_ref/plik_bench, compiled
     from /root/reference) on this host's cores, one single-threaded process per
     core like CosmoMC's one-chain-per-MPI-rank; falls back to the C
@@ -106,21 +134,26 @@ def cpu_baseline(seconds):
             ini = os.path.join(td, "l.ini")
             with open(ini, "w") as f:
                 f.write(f"cmb_dataset[PLIK_LITE] = {ds}\n")
+                if lensing:
+                    f.write(f"cmb_dataset[lensing] = {os.path.join(extract_refdata(td), LENS_DATASET)}\n")
+            th = syn.walker_theory(Wc, n_fields=10 if lensing else 3)
             th.tofile(os.path.join(td, "t.bin"))
             cal.tofile(os.path.join(td, "n.bin"))
             env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
-            cmd = [exe, ini, os.path.join(td, "t.bin"), os.path.join(td, "n.bin"), str(Wc), "2508", "3", "1",
-                   str(seconds)]
+            cmd = [exe, ini, os.path.join(td, "t.bin"), os.path.join(td, "n.bin"), str(Wc), "2508",
+                   str(th.shape[1]), "1", str(seconds)]
             procs = [subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env) for _ in range(P)]
             rates = []
             for pr in procs:
                 out, _ = pr.communicate(timeout=120)
                 n, t, _s = out.split()
                 rates.append(float(n) / float(t))
+            what = "TPlikLiteLikelihood_LogLike + CMBLikes_LogLike (lensing)" if lensing else \
+                "TPlikLiteLikelihood_LogLike"
             return {"value": float(sum(rates)), "unit": "evals/s", "cores": P, "kind": "reference",
-                    "sample": f"reference TPlikLiteLikelihood_LogLike (amdflang -O2 + OpenBLAS 1 thread), "
+                    "sample": f"reference {what} (amdflang -O2 + OpenBLAS 1 thread), "
                               f"{P} concurrent single-thread processes x {seconds:g} s over {Wc} synthetic "
-                              f"TTTEEE walkers"}
+                              f"walkers"}
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle as po
         orc = po.PlikLite(data)
@@ -130,7 +163,7 @@ def cpu_baseline(seconds):
             n += 1
         dt = time.perf_counter() - t0
         return {"value": n / dt, "unit": "evals/s", "cores": 1, "kind": "port",
-                "sample": f"C restatement oracle/liboracle.so, 1 thread, {seconds:g} s"}
+                "sample": f"C restatement oracle/liboracle.so (plik_lite only), 1 thread, {seconds:g} s"}
 
 
 def pmc_traffic(kernel, W):
@@ -167,7 +200,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     W = args.walkers
     with tempfile.TemporaryDirectory() as td:
-        smp, like, theory, _ = build_problem(W, rank, td, args.groups)
+        smp, likes, theory, _ = build_problem(W, rank, td, args.groups, lensing=not args.no_lensing)
 
         def barrier():
             if world > 1:
@@ -195,8 +228,9 @@ def main():
         smp.step(args.steps, fast_only=True)
         torch.cuda.synchronize()
         N.profile_enable(False)
-        kern = {k: N.profile_read(k) for k in ("plik_bin_delta", "plik_quadform_ksplit",
-                                                "mh_kernel")}
+        kern = {k: N.profile_read(k) for k in ("plik_bin_delta", "plik_quadform_ksplit", "mh_kernel",
+                                                "cmbl_bin_kernel", "cmbl_quadform")}
+        kern = {k: v for k, v in kern.items() if v[1]}
         _, _, _, nacc = smp.state()
         acc_rate = float(nacc.sum()) / (W * (args.warmup + 2 * args.steps))
 
@@ -218,16 +252,21 @@ def main():
             "metric": METRIC, "value": evals / dt, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "plik_lite_TTTEEE fast-parameter Metropolis step (BASELINE configs[2] "
-                                   "minus lowl/lensing): GetProposalFast + native plik_lite (613 bins, "
-                                   "l<=2508, full binning + quadratic form) + calPlanck prior + accept",
+            "config": {"workload": ("plik_lite_TTTEEE + Planck2018 lensing" if not args.no_lensing else
+                                    "plik_lite_TTTEEE") +
+                                   " fast-parameter Metropolis step (BASELINE configs[2]" +
+                                   (" minus lowl" if not args.no_lensing else " minus lowl/lensing") +
+                                   "): GetProposalFast + native plik_lite (613 bins, l<=2508, full binning + "
+                                   "quadratic form)" + (" + CMBlikes lensing (9 bins, linear correction)"
+                                                        if not args.no_lensing else "") +
+                                   " + calPlanck prior + accept",
                        "walkers_per_gpu": W, "stream_groups": args.groups, "global_walkers": W * world, "nbins": N_B, "lmax": 2508,
                        "parallelism": f"walkers sharded over {world} rank(s), no per-step collective",
                        "accept_rate": acc_rate},
             "roofline": roof,
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, lensing=not args.no_lensing)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -21,7 +21,7 @@ program plik_bench
     Type(TCosmoTheoryPredictions), allocatable :: Th(:)
     Type(CMBParams) :: CMB
     character(LEN=1024) :: ini_name, th_name, nu_name, arg
-    integer :: W, lmax, nfield, n_nuis, w_i, f, u_th, u_nu
+    integer :: W, lmax, nfield, n_nuis, w_i, f, u_th, u_nu, k
     integer(8) :: c0, c1, rate, nev
     real(mcp), allocatable :: cl(:,:), nuis(:,:)
     real(mcp) :: secs, el, tot
@@ -53,16 +53,20 @@ program plik_bench
         end do
     end do
     close(u_th); close(u_nu)
-    DL => Likes%Item(1)
     tot = 0
     nev = 0
     call system_clock(c0, rate)
     do
         do w_i = 1, 64
-            select type (DL)
-            class is (TCMBLikelihood)
-                tot = tot + DL%LogLike(CMB, Th(mod(nev, int(W,8)) + 1), nuis(:, mod(nev, int(W,8)) + 1))
-            end select
+            ! one evaluation = every registered likelihood at this point (all
+            ! share the same nuisance vector here: calPlanck)
+            do k = 1, Likes%Count
+                DL => Likes%Item(k)
+                select type (DL)
+                class is (TCMBLikelihood)
+                    tot = tot + DL%LogLike(CMB, Th(mod(nev, int(W,8)) + 1), nuis(:, mod(nev, int(W,8)) + 1))
+                end select
+            end do
             nev = nev + 1
         end do
         call system_clock(c1)
