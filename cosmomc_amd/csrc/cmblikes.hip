@@ -35,50 +35,50 @@ namespace cmamd {
 static constexpr int CL_MAXMAPS = 16;          // HL matrices up to 16 x 16 in one wave
 static constexpr int CL_MAXREQ = 32;            // required maps
 static constexpr int BK_NPARAM = 16;            // BKPlanck.paramnames
+static constexpr int WK_COLS = 24;              // window columns per work item (register accumulators)
+static constexpr int WK_CHUNK = 128;            // l per work item
 
 struct CLPair {      // one required map pair (i >= j)
     int field;       // theory field index 0..9 (TT TE EE BT BE BB PT PE PB PP)
     int cmb;         // both theory indices <= B: aberration and calibration apply
     int fg;          // foregrounds: 0 none, 1 EE, 2 BB
     int mi, mj;      // required-map indices (0-based)
-    int lo, hi;      // l range needed by this pair's columns
-    int col0, ncol;  // its columns: col_of_pair[col0 .. col0+ncol)
 };
 
-struct CLCol {       // one window column (bin, window entry)
-    int lo, hi;      // nonzero l range of the window
-    long long off;   // offset of W(lo) in the packed window array
+struct WItem {       // one (map pair, l chunk, <= WK_COLS window columns) contraction
+    int pair;
+    int l0, l1;      // l range (inclusive)
+    int ncol;
+    int part;        // partial rows part .. part+ncol-1
+    int pad;
+    long long woff;  // dense weights [ncol][l1-l0+1]
 };
 
 struct BKMap {       // per required map: bandpass samples and constants (Read_Bandpass :72-105)
     int off, n;      // samples in bp_nu / bp_R / bp_dnu
     int bc;          // band-centre error slot: 0 none, 1 '95', 2 '150', 3 '220'
+    int pad;
     double th_dust, th_sync, nu_bar;
 };
 
 struct CLDev {
     int lmin, lmax;                 // pcl_lmin, pcl_lmax
-    int npair, ncol, nb, ncl, ncl_used, nX, Np;
-    int approx;                     // 1 HL, 2 gaussian
-    int has_corr;
+    int nitem;
+    const WItem *items;
+    const double *wdense;
+    const CLPair *pairs;
+    double aberration;
     int cal_index;                  // 0-based in DataParams, -1 none
     double log_cal_prior;           // > 0: add (ln cal / prior)^2 to chi^2
-    double aberration;
-    int lpair;                      // max pair l-range length (LDS buffer)
-    const CLPair *pairs;
-    const CLCol *cols;
-    const int *col_of_pair;         // columns grouped by pair
-    const double *wts;              // packed windows
-    const double *col_fixed;        // [ncol] constant dot with fixed spectra (fix_cl), used when fixed_mask
-    const unsigned char *col_is_fixed;
-    const int *sum_off;             // [nb*ncl+1] main windows of (bin, cl) in window order: sum_cols[...]
-    const int *sum_cols;
-    const int *corr_off;            // [nb*ncl+1] linear-correction windows
-    const int *corr_cols;
-    const double *fidcorr;          // [nb][ncl]
-    const double *noise;            // [nb][ncl] (HL)
-    const double *chat;             // [nb][ncl] lower-triangle elements of Chat (gaussian)
-    const int *cl_use;              // [ncl_used]
+    // reduction to binned spectra, per element e = bin * ncl + cl
+    int nE, ncl_used, nX, Np, approx, has_corr;
+    const int *e_main_off, *e_main_cols, *e_corr_off, *e_corr_cols;
+    const int *col_part_off, *col_parts;     // partial rows of each column, l-chunk order
+    const double *col_const;        // columns without partials: fixed spectra (fix_cl) or empty windows
+    const double *fidcorr;          // [nE]
+    const double *noise;            // [nE] (HL)
+    const double *chat;             // [nE] (gaussian)
+    const int *e_to_x;              // [nE] gaussian: index into bigX or -1
     // BK foregrounds
     int bk, nreq;
     const BKMap *bkmaps;
@@ -113,183 +113,195 @@ __device__ inline double bk_decorr(double Delta, double nu0, double nu1, const d
     return exp(log(Delta) * scl_nu * scl_ell);
 }
 
-__global__ __launch_bounds__(256) void cmbl_bin_kernel(CLDev c, const double *__restrict__ dl, long long ld_field,
-                                                      long long ld_walker, const double *__restrict__ nuis,
-                                                      long long ld_nuis, double *__restrict__ xrows,
-                                                      double *__restrict__ cmat, double *__restrict__ addend,
-                                                      unsigned int *__restrict__ counters, int n_counters)
+// BK per-walker foreground set-up (TBK_planck_AddForegrounds :250-285): the
+// SED factors of every map (one wave per map, bandpass integrals as wave
+// reductions) and the dust / sync / dust-sync l profiles.
+//   coef[w][3][nreq] = fdust, fsync, band-centre error;  prof[3][L][W] (walker fastest)
+__global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *__restrict__ nuis, long long ld_nuis,
+                                                       double *__restrict__ coef, double *__restrict__ prof, int W)
 {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int w = blockIdx.x;
-    if (w == 0)
-        for (int i = tid; i < n_counters; i += blockDim.x) counters[i] = 0u;
-    const int L = c.lmax - c.lmin + 1;
-    // LDS carve: buf[2][lpair] | colval[ncol] | cls[nb*ncl] | fg[3][L] | fd[nreq] fs[nreq]
-    double *buf = lds;
-    double *colval = buf + 2 * c.lpair;
-    double *cls = colval + c.ncol;
-    double *fgp = cls + c.nb * c.ncl;
-    double *fdust = fgp + (c.bk ? 3 * L : 0);
-    double *fsync = fdust + c.nreq;
-    const double *D = dl + (long long)w * ld_walker;
     const double *P = nuis + (long long)w * ld_nuis;
-    const double cal = c.cal_index >= 0 ? P[c.cal_index] : 1.0;
-    const double calsq = cal * cal;
+    const double Adust = P[0], Async = P[1], alphadust = P[2], betadust = P[3], Tdust = P[4];
+    const double alphasync = P[5], betasync = P[6], dustsync_corr = P[7];
+    const double G = ghz_kelvin();
+    double *cw = coef + (long long)w * 3 * c.nreq;
+    for (int i = wave; i < c.nreq; i += 4) {
+        const BKMap m = c.bkmaps[i];
+        double gb = 0.0, pl = 0.0;
+        for (int k = lane; k < m.n; k += 64) {
+            const double nu = c.bp_nu[m.off + k], R = c.bp_R[m.off + k], dn = c.bp_dnu[m.off + k];
+            gb += dn * R * pow(nu, 3 + betadust) / (exp(G * nu / Tdust) - 1);
+            pl += dn * R * pow(nu, 2 + betasync);
+        }
+        gb = wave_sum(gb);
+        pl = wave_sum(pl);
+        if (lane == 0) {
+            double bc = 1.0;
+            if (m.bc == 1) bc = P[12] + P[13] + 1.;
+            else if (m.bc == 2) bc = P[12] + P[14] + 1.;
+            else if (m.bc == 3) bc = P[12] + P[15] + 1.;
+            const double nu0d = c.fpivot_dust, nu0s = c.fpivot_sync;
+            const double gb0 = pow(nu0d, 3 + betadust) / (exp(G * nu0d / Tdust) - 1);
+            const double pl0 = pow(nu0s, 2 + betasync);
+            double th_err = 1.0, gb_err = 1.0, pl_err = 1.0;
+            if (bc != 1.) {                                   // DustScaling :130-141, SyncScaling :169-178
+                const double e1 = exp(G * m.nu_bar / BK_TCMB) - 1, e2 = exp(G * m.nu_bar * bc / BK_TCMB) - 1;
+                th_err = (bc * bc * bc * bc) * exp(G * m.nu_bar * (bc - 1) / BK_TCMB) * (e1 * e1) / (e2 * e2);
+                gb_err = pow(bc, 3 + betadust) * (exp(G * m.nu_bar / Tdust) - 1) / (exp(G * m.nu_bar * bc / Tdust) - 1);
+                pl_err = pow(bc, 2 + betasync);
+            }
+            cw[i] = (gb / gb0) / m.th_dust * (gb_err / th_err);
+            cw[c.nreq + i] = (pl / pl0) / m.th_sync * (pl_err / th_err);
+            cw[2 * c.nreq + i] = bc;
+        }
+    }
+    const double lpivot = 80.0;
+    const int L = c.lmax - c.lmin + 1;
+    for (int l = c.lmin + tid; l <= c.lmax; l += blockDim.x) {
+        const long long j = l - c.lmin;
+        prof[j * W + w] = Adust * pow(l / lpivot, alphadust);
+        prof[((long long)L + j) * W + w] = Async * pow(l / lpivot, alphasync);
+        prof[((long long)2 * L + j) * W + w] =
+            dustsync_corr * sqrt(Adust * Async) * pow(l / lpivot, (alphadust + alphasync) / 2);
+    }
+}
 
-    // ---- BK foreground SEDs and l profiles (TBK_planck_AddForegrounds :229-285)
-    double EEtoBB_dust = 0, EEtoBB_sync = 0, Delta_dust = 1, Delta_sync = 1;
-    bool need_dd = false, need_ds = false;
-    if (c.bk) {
-        const double Adust = P[0], Async = P[1], alphadust = P[2], betadust = P[3], Tdust = P[4];
-        const double alphasync = P[5], betasync = P[6], dustsync_corr = P[7];
-        EEtoBB_dust = P[8];
-        EEtoBB_sync = P[9];
+// Window contractions.  One wave = 64 walkers (lane = walker) x one work item:
+// the map spectrum MapCl_pair(l) of each lane's walker (GetTheoryMapCls +
+// AdaptTheoryForMaps, CMBlikes.f90:1022-1126: aberration, foregrounds,
+// calibration) is formed in registers one l at a time and multiplied into up
+// to WK_COLS window columns whose weights are wave-uniform (scalar loads), so
+// every window value is fetched once per 64 walkers.  Writes the partial dot
+// products partial[(item.part + col) * W + w].
+__global__ __launch_bounds__(64) void cmbl_window_kernel(CLDev c, const double *__restrict__ dl, long long ld_field,
+                                                        long long ld_walker, const double *__restrict__ nuis,
+                                                        long long ld_nuis, const double *__restrict__ coef,
+                                                        const double *__restrict__ prof, double *__restrict__ partial,
+                                                        int W)
+{
+    const int lane = threadIdx.x;
+    const int w = blockIdx.x * 64 + lane;
+    const WItem it = c.items[blockIdx.y];
+    if (w >= W) return;
+    const CLPair pr = c.pairs[it.pair];
+    const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
+    const double *P = nuis + (long long)w * ld_nuis;
+    const double calsq = c.cal_index >= 0 ? P[c.cal_index] * P[c.cal_index] : 1.0;
+    const bool cal = c.cal_index >= 0 && pr.cmb;
+    const bool aber = c.aberration != 0.0 && pr.cmb;
+    double dust = 0, sync = 0, dustsync = 0, dd_flat = 1, ds_flat = 1, nu_i = 0, nu_j = 0;
+    double Delta_dust = 1, Delta_sync = 1;
+    bool dd_l = false, ds_l = false;
+    const int L = c.lmax - c.lmin + 1;
+    if (pr.fg) {                                              // :296-328
+        const double *cw = coef + (long long)w * 3 * c.nreq;
+        const int i = pr.mi, j = pr.mj;
+        dust = cw[i] * cw[j];
+        sync = cw[c.nreq + i] * cw[c.nreq + j];
+        dustsync = cw[i] * cw[c.nreq + j] + cw[c.nreq + i] * cw[j];
+        if (pr.fg == 1) {
+            const double EEd = P[8], EEs = P[9];
+            dust = dust * EEd;
+            sync = sync * EEs;
+            dustsync = dustsync * sqrt(EEd * EEs);
+        }
         Delta_dust = P[10];
         Delta_sync = P[11];
-        need_dd = fabs(Delta_dust - 1) > 1e-5;
-        need_ds = fabs(Delta_sync - 1) > 1e-5;
-        const double G = ghz_kelvin();
-        for (int i = wave; i < c.nreq; i += 4) {           // one wave per map
-            const BKMap m = c.bkmaps[i];
-            double gb = 0.0, pl = 0.0;
-            for (int k = lane; k < m.n; k += 64) {
-                const double nu = c.bp_nu[m.off + k], R = c.bp_R[m.off + k], dn = c.bp_dnu[m.off + k];
-                gb += dn * R * pow(nu, 3 + betadust) / (exp(G * nu / Tdust) - 1);
-                pl += dn * R * pow(nu, 2 + betasync);
-            }
-            gb = wave_sum(gb);
-            pl = wave_sum(pl);
-            if (lane == 0) {
-                double bc = 1.0;
-                if (m.bc == 1) bc = P[12] + P[13] + 1.;
-                else if (m.bc == 2) bc = P[12] + P[14] + 1.;
-                else if (m.bc == 3) bc = P[12] + P[15] + 1.;
-                const double nu0d = c.fpivot_dust, nu0s = c.fpivot_sync;
-                const double gb0 = pow(nu0d, 3 + betadust) / (exp(G * nu0d / Tdust) - 1);
-                const double pl0 = pow(nu0s, 2 + betasync);
-                double th_err = 1.0, gb_err = 1.0, pl_err = 1.0;
-                if (bc != 1.) {                              // DustScaling :130-141, SyncScaling :169-178
-                    const double e1 = exp(G * m.nu_bar / BK_TCMB) - 1, e2 = exp(G * m.nu_bar * bc / BK_TCMB) - 1;
-                    th_err = (bc * bc * bc * bc) * exp(G * m.nu_bar * (bc - 1) / BK_TCMB) * (e1 * e1) / (e2 * e2);
-                    gb_err = pow(bc, 3 + betadust) * (exp(G * m.nu_bar / Tdust) - 1) /
-                             (exp(G * m.nu_bar * bc / Tdust) - 1);
-                    pl_err = pow(bc, 2 + betasync);
-                }
-                fdust[i] = (gb / gb0) / m.th_dust * (gb_err / th_err);
-                fsync[i] = (pl / pl0) / m.th_sync * (pl_err / th_err);
-                fsync[c.nreq + i] = bc;                      // band-centre error per map
-            }
+        nu_i = c.bkmaps[i].nu_bar * cw[2 * c.nreq + i];
+        nu_j = c.bkmaps[j].nu_bar * cw[2 * c.nreq + j];
+        if (fabs(Delta_dust - 1) > 1e-5 && i != j) {
+            if (c.lform_dust == 0) dd_flat = bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, 0, 0);
+            else dd_l = true;
         }
-        const double lpivot = 80.0;
-        for (int l = c.lmin + tid; l <= c.lmax; l += blockDim.x) {
-            const int j = l - c.lmin;
-            fgp[j] = Adust * pow(l / lpivot, alphadust);
-            fgp[L + j] = Async * pow(l / lpivot, alphasync);
-            fgp[2 * L + j] = dustsync_corr * sqrt(Adust * Async) * pow(l / lpivot, (alphadust + alphasync) / 2);
+        if (fabs(Delta_sync - 1) > 1e-5 && i != j) {
+            if (c.lform_sync == 0) ds_flat = bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, 0, 0);
+            else ds_l = true;
         }
-        __syncthreads();
     }
-    const double *bcerr = fsync + c.nreq;
+    double acc[WK_COLS];
+#pragma unroll
+    for (int k = 0; k < WK_COLS; k++) acc[k] = 0.0;
+    const int len = it.l1 - it.l0 + 1;
+    const double *wd = c.wdense + it.woff;
+    for (int l = it.l0; l <= it.l1; l++) {
+        double v = Df[l];
+        if (aber) {                                           // AddAberration :1062-1101
+            int la = l - 1, lb = l + 1;
+            if (l == c.lmin) { la = l; lb = l + 2; }
+            else if (l == c.lmax) { la = l - 2; lb = l; }
+            const double ea = la, eb = lb, el = l;
+            const double ca = Df[la] / (ea * (ea + 1)), cb = Df[lb] / (eb * (eb + 1));
+            const double deriv = 0.5 * (cb - ca);
+            v = v + c.aberration * (el * el * (el + 1) * deriv);
+        }
+        if (pr.fg) {                                          // :329-334
+            const long long j = l - c.lmin;
+            const double Dd = dd_l ? bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, l, c.lform_dust) : dd_flat;
+            const double Ds = ds_l ? bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, l, c.lform_sync) : ds_flat;
+            v = v + dust * prof[j * W + w] * Dd + sync * prof[((long long)L + j) * W + w] * Ds +
+                dustsync * prof[((long long)2 * L + j) * W + w];
+        }
+        if (cal) v = v / calsq;                               // AdaptTheoryForMaps :1113-1124
+        const double *wl = wd + (l - it.l0);
+#pragma unroll
+        for (int k = 0; k < WK_COLS; k++)
+            if (k < it.ncol) acc[k] += wl[(long long)k * len] * v;
+    }
+#pragma unroll
+    for (int k = 0; k < WK_COLS; k++)
+        if (k < it.ncol) partial[(long long)(it.part + k) * W + w] = acc[k];
+}
 
-    // ---- map spectra and window dot products, pair by pair; the spectrum
-    // buffers alternate per processed pair so one barrier per pair suffices
-    int nproc = 0;
-    for (int p = 0; p < c.npair; p++) {
-        const CLPair pr = c.pairs[p];
-        if (pr.ncol == 0) continue;
-        double *B = buf + (nproc++ & 1) * c.lpair - pr.lo;
-        const double *Df = D + (long long)pr.field * ld_field;
-        double dust = 0, sync = 0, dustsync = 0, dd_flat = 1, ds_flat = 1;
-        bool dd_l = false, ds_l = false;
-        double nu_i = 0, nu_j = 0;
-        if (pr.fg) {
-            const int i = pr.mi, j = pr.mj;
-            dust = fdust[i] * fdust[j];
-            sync = fsync[i] * fsync[j];
-            dustsync = fdust[i] * fsync[j] + fsync[i] * fdust[j];
-            if (pr.fg == 1) {
-                dust = dust * EEtoBB_dust;
-                sync = sync * EEtoBB_sync;
-                dustsync = dustsync * sqrt(EEtoBB_dust * EEtoBB_sync);
-            }
-            nu_i = c.bkmaps[i].nu_bar * bcerr[i];
-            nu_j = c.bkmaps[j].nu_bar * bcerr[j];
-            if (need_dd && i != j) {
-                if (c.lform_dust == 0) dd_flat = bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, 0, 0);
-                else dd_l = true;
-            }
-            if (need_ds && i != j) {
-                if (c.lform_sync == 0) ds_flat = bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, 0, 0);
-                else ds_l = true;
-            }
-        }
-        for (int l = pr.lo + tid; l <= pr.hi; l += blockDim.x) {
-            double v = Df[l];
-            if (c.aberration != 0.0 && pr.cmb) {              // AddAberration :1062-1101
-                int la = l - 1, lb = l + 1;
-                if (l == c.lmin) { la = l; lb = l + 2; }
-                else if (l == c.lmax) { la = l - 2; lb = l; }
-                const double ea = la, eb = lb, el = l;
-                const double ca = Df[la] / (ea * (ea + 1)), cb = Df[lb] / (eb * (eb + 1));
-                const double deriv = 0.5 * (cb - ca);
-                v = v + c.aberration * (el * el * (el + 1) * deriv);
-            }
-            if (pr.fg) {                                      // :329-334
-                const int j = l - c.lmin;
-                const double Dd = dd_l ? bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, l, c.lform_dust) : dd_flat;
-                const double Ds = ds_l ? bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, l, c.lform_sync) : ds_flat;
-                v = v + dust * fgp[j] * Dd + sync * fgp[L + j] * Ds + dustsync * fgp[2 * L + j];
-            }
-            if (c.cal_index >= 0 && pr.cmb) v = v / calsq;    // AdaptTheoryForMaps :1113-1124
-            B[l] = v;
-        }
-        __syncthreads();
-        for (int k = wave; k < pr.ncol; k += 4) {
-            const int ci = c.col_of_pair[pr.col0 + k];
-            const CLCol col = c.cols[ci];
-            const double *Wc = c.wts + col.off - col.lo;
-            double acc = 0.0;
-            for (int l = col.lo + lane; l <= col.hi; l += 64) acc += Wc[l] * B[l];
-            acc = wave_sum(acc);
-            if (lane == 0) colval[ci] = acc;
-        }
-        // the next pair writes the other buffer; the barrier at its top orders reuse
+// Binned spectra per (walker, element e = bin * ncl + cl): window columns in
+// window order (TBinWindows_bin :1230-1256), each column the l-chunk partials
+// in order, plus the linear correction (GetBinnedMapCls :981-995).  Gaussian:
+// writes bigX = C - Chat for the used spectra; HL: writes C (+ noise) for the
+// transform.  Block (0, 0) zeroes the quadratic-form tickets; element 0 also
+// pads the bigX row and writes the calibration-prior addend.
+__global__ __launch_bounds__(64) void cmbl_reduce_kernel(CLDev c, const double *__restrict__ partial,
+                                                        const double *__restrict__ nuis, long long ld_nuis,
+                                                        double *__restrict__ xrows, double *__restrict__ cmat,
+                                                        double *__restrict__ addend, unsigned int *__restrict__ counters,
+                                                        int n_counters, int W)
+{
+    const int e = blockIdx.y;
+    const int w = blockIdx.x * 64 + threadIdx.x;
+    if (blockIdx.x == 0 && e == 0)
+        for (int i = threadIdx.x; i < n_counters; i += 64) counters[i] = 0u;
+    if (w >= W) return;
+    auto colval = [&](int col) {
+        const int p0 = c.col_part_off[col], p1 = c.col_part_off[col + 1];
+        if (p0 == p1) return c.col_const[col];
+        double v = 0.0;
+        for (int q = p0; q < p1; q++) v += partial[(long long)c.col_parts[q] * W + w];
+        return v;
+    };
+    double s = 0.0;
+    for (int q = c.e_main_off[e]; q < c.e_main_off[e + 1]; q++) s = s + colval(c.e_main_cols[q]);
+    if (c.has_corr) {
+        double cs = 0.0;
+        for (int q = c.e_corr_off[e]; q < c.e_corr_off[e + 1]; q++) cs = cs + colval(c.e_corr_cols[q]);
+        s = s + (cs - c.fidcorr[e]);
     }
-    for (int ci = tid; ci < c.ncol; ci += blockDim.x)
-        if (c.col_is_fixed[ci]) colval[ci] = c.col_fixed[ci];
-    __syncthreads();
-
-    // ---- binned spectra per (bin, cl): window order, then the linear correction
-    for (int e = tid; e < c.nb * c.ncl; e += blockDim.x) {
-        double s = 0.0;
-        for (int q = c.sum_off[e]; q < c.sum_off[e + 1]; q++) s = s + colval[c.sum_cols[q]];
-        if (c.has_corr) {
-            double cs = 0.0;
-            for (int q = c.corr_off[e]; q < c.corr_off[e + 1]; q++) cs = cs + colval[c.corr_cols[q]];
-            s = s + (cs - c.fidcorr[e]);
-        }
-        cls[e] = s;
-    }
-    __syncthreads();
     double *x = xrows + (long long)w * c.Np;
-    for (int k = c.nX + tid; k < c.Np; k += blockDim.x) x[k] = 0.0;
     if (c.approx == 2) {
-        for (int e = tid; e < c.nX; e += blockDim.x) {
-            const int b = e / c.ncl_used, u = c.cl_use[e % c.ncl_used];
-            x[e] = cls[b * c.ncl + u] - c.chat[b * c.ncl + u];
-        }
+        const int ix = c.e_to_x[e];
+        if (ix >= 0) x[ix] = s - c.chat[e];
     } else {
-        double *cm = cmat + (long long)w * c.nb * c.ncl;
-        for (int e = tid; e < c.nb * c.ncl; e += blockDim.x) cm[e] = cls[e] + c.noise[e];
+        cmat[(long long)w * c.nE + e] = s + c.noise[e];
     }
-    if (addend && tid == 0) {
-        double a = 0.0;
-        if (c.log_cal_prior > 0 && c.cal_index >= 0) {
-            const double t = log(cal) / c.log_cal_prior;
-            a = t * t / 2;
+    if (e == 0) {
+        for (int k = c.nX; k < c.Np; k++) x[k] = 0.0;
+        if (addend) {
+            double a = 0.0;
+            if (c.log_cal_prior > 0 && c.cal_index >= 0) {
+                const double t = log(nuis[(long long)w * ld_nuis + c.cal_index]) / c.log_cal_prior;
+                a = t * t / 2;
+            }
+            addend[w] = a;
         }
-        addend[w] = a;
     }
 }
 
@@ -551,10 +563,9 @@ struct CMBLikes final : Like {
     // device tables
     CLDev dev{};
     HLDev hl{};
-    DevBuf d_pairs, d_cols, d_colpair, d_wts, d_colfixed, d_isfixed, d_sumoff, d_sumcols, d_corroff, d_corrcols,
-        d_fidcorr, d_noise, d_chat, d_cluse, d_bkmaps, d_bpnu, d_bpR, d_bpdnu, d_hlchat, d_hlcf;
-    size_t lds_bytes = 0;
-    int max_field = 0;
+    DevBuf d_pairs, d_items, d_wts, d_colpartoff, d_colparts, d_colconst, d_sumoff, d_sumcols, d_corroff, d_corrcols,
+        d_etox, d_fidcorr, d_noise, d_chat, d_cluse, d_bkmaps, d_bpnu, d_bpR, d_bpdnu, d_hlchat, d_hlcf;
+    int max_field = 0, n_part_rows = 0;
 
     std::string cl_name(const std::vector<std::string> &names, int i, int j) const {   // Cl_i_j_name (:328-343)
         return has_map_names ? names[i - 1] + "x" + names[j - 1] : names[i - 1] + names[j - 1];
@@ -969,71 +980,80 @@ struct CMBLikes final : Like {
                 p.fg = bk ? ((f1 == 2 && f2 == 2) ? 1 : (f1 == 3 && f2 == 3) ? 2 : 0) : 0;
                 p.mi = i - 1;
                 p.mj = j - 1;
-                p.lo = 1 << 30;
-                p.hi = -1;
                 pairs.push_back(p);
             }
-        // window columns: main (bins x windows) then correction
-        std::vector<CLCol> cols;
-        std::vector<double> wpack, colfixed;
-        std::vector<unsigned char> isfixed;
-        std::vector<int> colpair;
-        std::vector<std::vector<int>> sum_lists((size_t)nb * ncl), corr_lists((size_t)nb * ncl);
+        // window columns: one per (bin, window entry with an output); main then correction
+        struct HCol { int pair, lo, hi; const double *W; double cst; bool fixed; };
+        std::vector<HCol> cols;
+        const int nE = nb * ncl;
+        std::vector<std::vector<int>> e_main(nE), e_corr(nE);
         auto add_windows = [&](const Windows &wn, std::vector<std::vector<int>> &lists) {
             const int norder = (int)wn.in_i.size();
             for (int b = 0; b < nb; b++)
                 for (int k = 0; k < norder; k++) {
                     if (wn.out[k] <= 0) continue;
                     const double *Wk = &wn.W[((size_t)b * norder + k) * L];
-                    int lo = L, hi = -1;
+                    HCol c{-1, L, -1, Wk, 0.0, false};
                     for (int l = 0; l < L; l++)
-                        if (Wk[l] != 0.0) { lo = std::min(lo, l); hi = l; }
-                    CLCol c{};
-                    int pid = -1;
-                    double fixed = 0.0;
-                    bool fx = !wn.fix[k].empty();
-                    if (fx) {
-                        for (int l = 0; l < L; l++) fixed += Wk[l] * wn.fix[k][l];
+                        if (Wk[l] != 0.0) { c.lo = std::min(c.lo, l); c.hi = l; }
+                    if (!wn.fix[k].empty()) {              // fix_cl: walker-independent dot
+                        c.fixed = true;
+                        for (int l = 0; l < L; l++) c.cst += Wk[l] * wn.fix[k][l];
                     } else {
                         if (wn.in_i[k] == 0 || wn.in_j[k] == 0)
                             fail(CMBL_ERR_FORMAT, "CMBlikes: bin window uses a spectrum of a map that is not required");
-                        pid = pair_index(wn.in_i[k], wn.in_j[k]);
+                        c.pair = pair_index(wn.in_i[k], wn.in_j[k]);
                     }
-                    if (hi < lo) { lo = 0; hi = -1; }
-                    c.lo = lo + lmin;
-                    c.hi = hi + lmin;
-                    c.off = (long long)wpack.size();
-                    for (int l = lo; l <= hi; l++) wpack.push_back(Wk[l]);
-                    const int ci = (int)cols.size();
+                    lists[(size_t)b * ncl + (wn.out[k] - 1)].push_back((int)cols.size());
                     cols.push_back(c);
-                    colfixed.push_back(fixed);
-                    isfixed.push_back(fx ? 1 : 0);
-                    colpair.push_back(pid);
-                    if (pid >= 0 && hi >= lo) {
-                        pairs[pid].lo = std::min(pairs[pid].lo, c.lo);
-                        pairs[pid].hi = std::max(pairs[pid].hi, c.hi);
-                    }
-                    lists[(size_t)b * ncl + (wn.out[k] - 1)].push_back(ci);
                 }
         };
-        add_windows(bw, sum_lists);
-        if (cw.present) add_windows(cw, corr_lists);
-        // group columns by pair
-        std::vector<int> col_of_pair;
-        int lpair = 2;
-        for (size_t p = 0; p < pairs.size(); p++) {
-            pairs[p].col0 = (int)col_of_pair.size();
-            for (size_t ci = 0; ci < cols.size(); ci++)
-                if (colpair[ci] == (int)p && cols[ci].hi >= cols[ci].lo) col_of_pair.push_back((int)ci);
-            pairs[p].ncol = (int)col_of_pair.size() - pairs[p].col0;
-            if (pairs[p].ncol == 0) { pairs[p].lo = 0; pairs[p].hi = -1; }
-            else lpair = std::max(lpair, pairs[p].hi - pairs[p].lo + 1);
+        add_windows(bw, e_main);
+        if (cw.present) add_windows(cw, e_corr);
+        // work items: per pair, per l chunk, the overlapping columns in groups of WK_COLS
+        std::vector<WItem> items;
+        std::vector<double> wdense;
+        std::vector<std::vector<int>> col_parts(cols.size());
+        int nrows = 0;
+        const int nchunk = (L + WK_CHUNK - 1) / WK_CHUNK;
+        for (size_t p = 0; p < pairs.size(); p++)
+            for (int ch = 0; ch < nchunk; ch++) {
+                const int c0 = ch * WK_CHUNK, c1 = std::min(L - 1, c0 + WK_CHUNK - 1);
+                std::vector<int> sel;
+                for (size_t ci = 0; ci < cols.size(); ci++)
+                    if (!cols[ci].fixed && cols[ci].pair == (int)p && cols[ci].hi >= c0 && cols[ci].lo <= c1)
+                        sel.push_back((int)ci);
+                for (size_t g0 = 0; g0 < sel.size(); g0 += WK_COLS) {
+                    const size_t g1 = std::min(sel.size(), g0 + WK_COLS);
+                    int lo = c1, hi = c0;
+                    for (size_t g = g0; g < g1; g++) {
+                        lo = std::min(lo, std::max(c0, cols[sel[g]].lo));
+                        hi = std::max(hi, std::min(c1, cols[sel[g]].hi));
+                    }
+                    WItem it{};
+                    it.pair = (int)p;
+                    it.l0 = lo + lmin;
+                    it.l1 = hi + lmin;
+                    it.ncol = (int)(g1 - g0);
+                    it.part = nrows;
+                    it.woff = (long long)wdense.size();
+                    for (size_t g = g0; g < g1; g++) {
+                        for (int l = lo; l <= hi; l++) wdense.push_back(cols[sel[g]].W[l]);
+                        col_parts[sel[g]].push_back(nrows++);
+                    }
+                    items.push_back(it);
+                }
+            }
+        n_part_rows = nrows;
+        std::vector<int> col_part_off(cols.size() + 1, 0), col_part_all;
+        std::vector<double> col_const(cols.size(), 0.0);
+        for (size_t ci = 0; ci < cols.size(); ci++) {
+            col_part_off[ci] = (int)col_part_all.size();
+            col_part_all.insert(col_part_all.end(), col_parts[ci].begin(), col_parts[ci].end());
+            col_const[ci] = cols[ci].cst;
         }
-        for (auto &p : pairs)
-            if (p.ncol > 0) max_field = std::max(max_field, p.field);
-        // columns with an empty window contribute 0 (mark fixed with value 0)
-        for (size_t ci = 0; ci < cols.size(); ci++)
-            if (cols[ci].hi < cols[ci].lo) isfixed[ci] = 1;
+        col_part_off[cols.size()] = (int)col_part_all.size();
+        for (auto &it : items) max_field = std::max(max_field, pairs[it.pair].field);
         auto flatten = [&](const std::vector<std::vector<int>> &lists, std::vector<int> &off, std::vector<int> &all) {
             off.assign(lists.size() + 1, 0);
             for (size_t e = 0; e < lists.size(); e++) {
@@ -1042,13 +1062,13 @@ struct CMBLikes final : Like {
             }
             off[lists.size()] = (int)all.size();
         };
-        std::vector<int> sum_off, sum_cols, corr_off, corr_cols;
-        flatten(sum_lists, sum_off, sum_cols);
-        flatten(corr_lists, corr_off, corr_cols);
-        if (sum_cols.empty()) sum_cols.push_back(0);
-        if (corr_cols.empty()) corr_cols.push_back(0);
-        if (wpack.empty()) wpack.push_back(0.0);
-        std::vector<double> fc((size_t)nb * ncl, 0.0), noise((size_t)nb * ncl, 0.0);
+        std::vector<int> main_off, main_cols, corr_off, corr_cols;
+        flatten(e_main, main_off, main_cols);
+        flatten(e_corr, corr_off, corr_cols);
+        std::vector<int> e_to_x(nE, -1);
+        for (int b = 0; b < nb; b++)
+            for (int u = 0; u < ncl_used; u++) e_to_x[b * ncl + cl_use[u]] = b * ncl_used + u;
+        std::vector<double> fc(nE, 0.0), noise(nE, 0.0);
         if (cw.present) fc = fidcorr;
         if (have_noise) noise = clnoise;
 
@@ -1057,15 +1077,16 @@ struct CMBLikes final : Like {
             if (bytes) d.upload(p, bytes);
         };
         up(d_pairs, pairs.data(), pairs.size() * sizeof(CLPair));
-        up(d_cols, cols.data(), cols.size() * sizeof(CLCol));
-        up(d_colpair, col_of_pair.data(), col_of_pair.size() * 4);
-        up(d_wts, wpack.data(), wpack.size() * 8);
-        up(d_colfixed, colfixed.data(), colfixed.size() * 8);
-        up(d_isfixed, isfixed.data(), isfixed.size());
-        up(d_sumoff, sum_off.data(), sum_off.size() * 4);
-        up(d_sumcols, sum_cols.data(), sum_cols.size() * 4);
+        up(d_items, items.data(), items.size() * sizeof(WItem));
+        up(d_wts, wdense.data(), wdense.size() * 8);
+        up(d_colpartoff, col_part_off.data(), col_part_off.size() * 4);
+        up(d_colparts, col_part_all.data(), col_part_all.size() * 4);
+        up(d_colconst, col_const.data(), col_const.size() * 8);
+        up(d_sumoff, main_off.data(), main_off.size() * 4);
+        up(d_sumcols, main_cols.data(), main_cols.size() * 4);
         up(d_corroff, corr_off.data(), corr_off.size() * 4);
         up(d_corrcols, corr_cols.data(), corr_cols.size() * 4);
+        up(d_etox, e_to_x.data(), e_to_x.size() * 4);
         up(d_fidcorr, fc.data(), fc.size() * 8);
         up(d_noise, noise.data(), noise.size() * 8);
         up(d_chat, clhat.data(), clhat.size() * 8);
@@ -1081,47 +1102,38 @@ struct CMBLikes final : Like {
         qf.init(invcov, nX);
         dev.lmin = lmin;
         dev.lmax = lmax;
-        dev.npair = (int)pairs.size();
-        dev.ncol = (int)cols.size();
-        dev.nb = nb;
-        dev.ncl = ncl;
+        dev.nitem = (int)items.size();
+        dev.items = d_items.as<WItem>();
+        dev.wdense = d_wts.as<double>();
+        dev.pairs = d_pairs.as<CLPair>();
+        dev.aberration = aberration;
+        dev.cal_index = cal_index;
+        dev.log_cal_prior = log_cal_prior;
+        dev.nE = nE;
         dev.ncl_used = ncl_used;
         dev.nX = nX;
         dev.Np = qf.Np;
         dev.approx = approx;
         dev.has_corr = cw.present ? 1 : 0;
-        dev.cal_index = cal_index;
-        dev.log_cal_prior = log_cal_prior;
-        dev.aberration = aberration;
-        dev.lpair = (lpair + 1) & ~1;
-        dev.pairs = d_pairs.as<CLPair>();
-        dev.cols = d_cols.as<CLCol>();
-        dev.col_of_pair = d_colpair.as<int>();
-        dev.wts = d_wts.as<double>();
-        dev.col_fixed = d_colfixed.as<double>();
-        dev.col_is_fixed = d_isfixed.as<unsigned char>();
-        dev.sum_off = d_sumoff.as<int>();
-        dev.sum_cols = d_sumcols.as<int>();
-        dev.corr_off = d_corroff.as<int>();
-        dev.corr_cols = d_corrcols.as<int>();
+        dev.e_main_off = d_sumoff.as<int>();
+        dev.e_main_cols = d_sumcols.as<int>();
+        dev.e_corr_off = d_corroff.as<int>();
+        dev.e_corr_cols = d_corrcols.as<int>();
+        dev.col_part_off = d_colpartoff.as<int>();
+        dev.col_parts = d_colparts.as<int>();
+        dev.col_const = d_colconst.as<double>();
         dev.fidcorr = d_fidcorr.as<double>();
         dev.noise = d_noise.as<double>();
         dev.chat = d_chat.as<double>();
-        dev.cl_use = d_cluse.as<int>();
+        dev.e_to_x = d_etox.as<int>();
         dev.bk = bk ? 1 : 0;
         dev.nreq = nreq;
         dev.bkmaps = bk ? d_bkmaps.as<BKMap>() : nullptr;
         dev.bp_nu = bk ? d_bpnu.as<double>() : nullptr;
         dev.bp_R = bk ? d_bpR.as<double>() : nullptr;
         dev.bp_dnu = bk ? d_bpdnu.as<double>() : nullptr;
-        lds_bytes = (size_t)(2 * dev.lpair + dev.ncol + nb * ncl + (bk ? 3 * L : 0) + 3 * nreq + 2) * 8;
-        if (lds_bytes > 160 * 1024) fail(CMBL_ERR_UNSUPPORTED, "CMBlikes: dataset needs %zu bytes of LDS", lds_bytes);
-        if (lds_bytes > 64 * 1024)
-            HIP_CHECK(hipFuncSetAttribute((const void *)cmbl_bin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)lds_bytes));
         hl.n = nmaps;
-        hl.m = (nmaps + 1) & ~1;
-        if (hl.m < 2) hl.m = 2;
+        hl.m = std::max(2, (nmaps + 1) & ~1);
         hl.nb = nb;
         hl.ncl = ncl;
         hl.ncl_used = ncl_used;
@@ -1132,10 +1144,22 @@ struct CMBLikes final : Like {
         hl.cl_use = d_cluse.as<int>();
     }
 
-    size_t cmat_bytes(int W) const { return approx == 1 ? (size_t)W * nb * ncl * 8 : 0; }
-    size_t workspace_size(int W) const override {
-        return qf.workspace_size(W) + ((cmat_bytes(W) + (size_t)W * 8 + 255) & ~size_t(255)) + 256;
+    // workspace: quadratic form | partial dots [rows][W] | C matrices [W][nE] (HL) |
+    //            BK coef [W][3 nreq] + profiles [3][L][W] | addend [W]
+    struct WsLayout { size_t part, cmat, coef, prof, add, total; };
+    WsLayout layout(int W) const {
+        auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+        WsLayout o{};
+        const int L = lmax - lmin + 1;
+        o.part = al(qf.workspace_size(W));
+        o.cmat = o.part + al((size_t)n_part_rows * W * 8);
+        o.coef = o.cmat + al(approx == 1 ? (size_t)W * nb * ncl * 8 : 0);
+        o.prof = o.coef + al(bk ? (size_t)W * 3 * nreq * 8 : 0);
+        o.add = o.prof + al(bk ? (size_t)3 * L * W * 8 : 0);
+        o.total = o.add + al((size_t)W * 8);
+        return o;
     }
+    size_t workspace_size(int W) const override { return layout(W).total; }
 
     void loglike_batch(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis,
                        long long ld_nuis, double *out, void *ws, hipStream_t stream) override {
@@ -1148,15 +1172,33 @@ struct CMBLikes final : Like {
             own_ws.grow(workspace_size(W));
             ws = own_ws.p;
         }
+        const WsLayout o = layout(W);
         char *base = static_cast<char *>(ws);
-        double *cmat = reinterpret_cast<double *>(base + ((qf.workspace_size(W) + 255) & ~size_t(255)));
-        double *addend = cmat + (size_t)W * nb * ncl * (approx == 1 ? 1 : 0);
+        double *partial = reinterpret_cast<double *>(base + o.part);
+        double *cmat = reinterpret_cast<double *>(base + o.cmat);
+        double *coef = reinterpret_cast<double *>(base + o.coef);
+        double *prof = reinterpret_cast<double *>(base + o.prof);
+        double *addend = reinterpret_cast<double *>(base + o.add);
         const bool use_add = log_cal_prior > 0 && cal_index >= 0;
         const double *nu = nuis ? nuis : dl;   // never read when n_nuis == 0
-        timed_launch("cmbl_bin_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(cmbl_bin_kernel, dim3(W), dim3(256), (uint32_t)lds_bytes, stream, e0, e1, 0, dev, dl,
-                                  ld_field, ld_walker, nu, ld_nuis, qf.x_rows(ws), cmat, use_add ? addend : nullptr,
-                                  qf.counters(ws, W), qf.n_counters(W));
+        const int tiles = (W + 63) / 64;
+        if (bk) {
+            timed_launch("cmbl_bk_prologue", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+                hipExtLaunchKernelGGL(cmbl_bk_prologue, dim3(W), dim3(256), 0, stream, e0, e1, 0, dev, nu, ld_nuis,
+                                      coef, prof, W);
+            });
+            HIP_CHECK(hipGetLastError());
+        }
+        timed_launch("cmbl_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            hipExtLaunchKernelGGL(cmbl_window_kernel, dim3(tiles, dev.nitem), dim3(64), 0, stream, e0, e1, 0, dev,
+                                  dl, ld_field, ld_walker, nu, ld_nuis, (const double *)coef, (const double *)prof,
+                                  partial, W);
+        });
+        HIP_CHECK(hipGetLastError());
+        timed_launch("cmbl_reduce_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            hipExtLaunchKernelGGL(cmbl_reduce_kernel, dim3(tiles, dev.nE), dim3(64), 0, stream, e0, e1, 0, dev,
+                                  (const double *)partial, nu, ld_nuis, qf.x_rows(ws), cmat, use_add ? addend : nullptr,
+                                  qf.counters(ws, W), qf.n_counters(W), W);
         });
         HIP_CHECK(hipGetLastError());
         if (approx == 1) {
