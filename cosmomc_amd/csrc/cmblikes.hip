@@ -37,6 +37,7 @@ static constexpr int CL_MAXREQ = 32;            // required maps
 static constexpr int BK_NPARAM = 16;            // BKPlanck.paramnames
 static constexpr int WK_COLS = 24;              // window columns per work item (register accumulators)
 static constexpr int WK_CHUNK = 128;            // l per work item
+static constexpr int WK_BATCH = 16;             // l per load batch
 
 struct CLPair {      // one required map pair (i >= j)
     int field;       // theory field index 0..9 (TT TE EE BT BE BB PT PE PB PP)
@@ -225,29 +226,55 @@ __global__ __launch_bounds__(64) void cmbl_window_kernel(CLDev c, const double *
     for (int k = 0; k < WK_COLS; k++) acc[k] = 0.0;
     const int len = it.l1 - it.l0 + 1;
     const double *wd = c.wdense + it.woff;
-    for (int l = it.l0; l <= it.l1; l++) {
-        double v = Df[l];
-        if (aber) {                                           // AddAberration :1062-1101
-            int la = l - 1, lb = l + 1;
-            if (l == c.lmin) { la = l; lb = l + 2; }
-            else if (l == c.lmax) { la = l - 2; lb = l; }
-            const double ea = la, eb = lb, el = l;
-            const double ca = Df[la] / (ea * (ea + 1)), cb = Df[lb] / (eb * (eb + 1));
-            const double deriv = 0.5 * (cb - ca);
-            v = v + c.aberration * (el * el * (el + 1) * deriv);
-        }
-        if (pr.fg) {                                          // :329-334
-            const long long j = l - c.lmin;
-            const double Dd = dd_l ? bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, l, c.lform_dust) : dd_flat;
-            const double Ds = ds_l ? bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, l, c.lform_sync) : ds_flat;
-            v = v + dust * prof[j * W + w] * Dd + sync * prof[((long long)L + j) * W + w] * Ds +
-                dustsync * prof[((long long)2 * L + j) * W + w];
-        }
-        if (cal) v = v / calsq;                               // AdaptTheoryForMaps :1113-1124
-        const double *wl = wd + (l - it.l0);
+    // l in batches of WK_BATCH: every load of a batch is issued before the
+    // first use (one memory latency per batch); a lane's theory values of a
+    // batch are 128 contiguous bytes of its own row
+    for (int lb0 = it.l0; lb0 <= it.l1; lb0 += WK_BATCH) {
+        double t[WK_BATCH], ta[WK_BATCH], tb[WK_BATCH], pd[WK_BATCH], ps[WK_BATCH], pds[WK_BATCH];
 #pragma unroll
-        for (int k = 0; k < WK_COLS; k++)
-            if (k < it.ncol) acc[k] += wl[(long long)k * len] * v;
+        for (int q = 0; q < WK_BATCH; q++) {
+            const int l = lb0 + q;
+            const bool in = l <= it.l1;
+            t[q] = in ? Df[l] : 0.0;
+            if (aber) {
+                int la = l - 1, lb = l + 1;
+                if (l == c.lmin) { la = l; lb = l + 2; }
+                else if (l >= c.lmax) { la = l - 2; lb = l; }
+                ta[q] = in ? Df[la] : 0.0;
+                tb[q] = in ? Df[lb] : 0.0;
+            }
+            if (pr.fg) {
+                const long long j = in ? l - c.lmin : 0;
+                pd[q] = prof[j * W + w];
+                ps[q] = prof[((long long)L + j) * W + w];
+                pds[q] = prof[((long long)2 * L + j) * W + w];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < WK_BATCH; q++) {
+            const int l = lb0 + q;
+            if (l > it.l1) break;
+            double v = t[q];
+            if (aber) {                                       // AddAberration :1062-1101
+                int la = l - 1, lb = l + 1;
+                if (l == c.lmin) { la = l; lb = l + 2; }
+                else if (l == c.lmax) { la = l - 2; lb = l; }
+                const double ea = la, eb = lb, el = l;
+                const double ca = ta[q] / (ea * (ea + 1)), cb = tb[q] / (eb * (eb + 1));
+                const double deriv = 0.5 * (cb - ca);
+                v = v + c.aberration * (el * el * (el + 1) * deriv);
+            }
+            if (pr.fg) {                                      // :329-334
+                const double Dd = dd_l ? bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, l, c.lform_dust) : dd_flat;
+                const double Ds = ds_l ? bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, l, c.lform_sync) : ds_flat;
+                v = v + dust * pd[q] * Dd + sync * ps[q] * Ds + dustsync * pds[q];
+            }
+            if (cal) v = v / calsq;                           // AdaptTheoryForMaps :1113-1124
+            const double *wl = wd + (l - it.l0);
+#pragma unroll
+            for (int k = 0; k < WK_COLS; k++)
+                if (k < it.ncol) acc[k] += wl[(long long)k * len] * v;
+        }
     }
 #pragma unroll
     for (int k = 0; k < WK_COLS; k++)

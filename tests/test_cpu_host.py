@@ -29,12 +29,16 @@ def test_open_missing_file_returns_error_code():
     assert not h.value
 
 
-def test_open_unknown_tag_returns_unsupported(tmp_path):
+def test_open_tag_dispatch(tmp_path):
+    """CMBLikelihood_Add (CMB.f90:80-97): unknown tags are CMBlikes datasets;
+    SPTpol / SMICA / WMAP are not built yet."""
     p = tmp_path / "a.dataset"
     p.write_text("name = x\n")
     h = C.c_void_p()
     err = C.create_string_buffer(256)
-    assert N.lib().cmbl_open(b"WHATEVER", str(p).encode(), None, C.byref(h), err, 256) == -6
+    assert N.lib().cmbl_open(b"WHATEVER", str(p).encode(), None, C.byref(h), err, 256) == -3   # not a CMBlikes dataset
+    assert b"fields_use" in err.value
+    assert N.lib().cmbl_open(b"SPTPOL_TEEE", str(p).encode(), None, C.byref(h), err, 256) == -6
 
 
 def test_null_arguments_rejected():
