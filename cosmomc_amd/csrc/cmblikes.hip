@@ -52,7 +52,7 @@ struct WItem {       // one (map pair, l chunk, <= WK_COLS window columns) contr
     int ncol;
     int part;        // partial rows part .. part+ncol-1
     int pad;
-    long long woff;  // dense weights [ncol][l1-l0+1]
+    long long woff;  // dense weights [l1-l0+1][WK_COLS] (zero-padded columns), 16-byte aligned
 };
 
 struct BKMap {       // per required map: bandpass samples and constants (Read_Bandpass :72-105)
@@ -73,9 +73,8 @@ struct CLDev {
     double log_cal_prior;           // > 0: add (ln cal / prior)^2 to chi^2
     // reduction to binned spectra, per element e = bin * ncl + cl
     int nE, ncl_used, nX, Np, approx, has_corr;
-    const int *e_main_off, *e_main_cols, *e_corr_off, *e_corr_cols;
-    const int *col_part_off, *col_parts;     // partial rows of each column, l-chunk order
-    const double *col_const;        // columns without partials: fixed spectra (fix_cl) or empty windows
+    const int *e_main_off, *e_main_rows, *e_corr_off, *e_corr_rows;   // partial rows per element
+    const double *e_main_const, *e_corr_const;   // fixed-spectrum (fix_cl) window dots per element
     const double *fidcorr;          // [nE]
     const double *noise;            // [nE] (HL)
     const double *chat;             // [nE] (gaussian)
@@ -182,9 +181,16 @@ __global__ __launch_bounds__(64) void cmbl_window_kernel(CLDev c, const double *
                                                         const double *__restrict__ prof, double *__restrict__ partial,
                                                         int W)
 {
+    __shared__ __attribute__((aligned(16))) double wsh[WK_CHUNK * WK_COLS];   // weights [l][col]
     const int lane = threadIdx.x;
     const int w = blockIdx.x * 64 + lane;
     const WItem it = c.items[blockIdx.y];
+    {   // stage this item's weights (zero-padded to WK_COLS columns): coalesced 16-byte loads
+        const int n2 = (it.l1 - it.l0 + 1) * WK_COLS / 2;
+        const double2 *src = reinterpret_cast<const double2 *>(c.wdense + it.woff);
+        for (int i = lane; i < n2; i += 64) reinterpret_cast<double2 *>(wsh)[i] = src[i];
+    }
+    __syncthreads();
     if (w >= W) return;
     const CLPair pr = c.pairs[it.pair];
     const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
@@ -224,8 +230,6 @@ __global__ __launch_bounds__(64) void cmbl_window_kernel(CLDev c, const double *
     double acc[WK_COLS];
 #pragma unroll
     for (int k = 0; k < WK_COLS; k++) acc[k] = 0.0;
-    const int len = it.l1 - it.l0 + 1;
-    const double *wd = c.wdense + it.woff;
     // l in batches of WK_BATCH: every load of a batch is issued before the
     // first use (one memory latency per batch); a lane's theory values of a
     // batch are 128 contiguous bytes of its own row
@@ -270,10 +274,13 @@ __global__ __launch_bounds__(64) void cmbl_window_kernel(CLDev c, const double *
                 v = v + dust * pd[q] * Dd + sync * ps[q] * Ds + dustsync * pds[q];
             }
             if (cal) v = v / calsq;                           // AdaptTheoryForMaps :1113-1124
-            const double *wl = wd + (l - it.l0);
+            const double2 *wl = reinterpret_cast<const double2 *>(wsh + (l - it.l0) * WK_COLS);   // LDS broadcast
 #pragma unroll
-            for (int k = 0; k < WK_COLS; k++)
-                if (k < it.ncol) acc[k] += wl[(long long)k * len] * v;
+            for (int k = 0; k < WK_COLS / 2; k++) {
+                const double2 ww = wl[k];
+                acc[2 * k] += ww.x * v;
+                acc[2 * k + 1] += ww.y * v;
+            }
         }
     }
 #pragma unroll
@@ -298,20 +305,22 @@ __global__ __launch_bounds__(64) void cmbl_reduce_kernel(CLDev c, const double *
     if (blockIdx.x == 0 && e == 0)
         for (int i = threadIdx.x; i < n_counters; i += 64) counters[i] = 0u;
     if (w >= W) return;
-    auto colval = [&](int col) {
-        const int p0 = c.col_part_off[col], p1 = c.col_part_off[col + 1];
-        if (p0 == p1) return c.col_const[col];
-        double v = 0.0;
-        for (int q = p0; q < p1; q++) v += partial[(long long)c.col_parts[q] * W + w];
+    // window columns in window order, each the l-chunk partials in order (flattened
+    // on the host); loads issued eight at a time
+    auto rows_sum = [&](const int *off, const int *rows, const double *cst) {
+        double v = cst[e];
+        const int q0 = off[e], q1 = off[e + 1];
+        for (int q = q0; q < q1; q += 8) {
+            double t[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) t[u] = (q + u < q1) ? partial[(long long)rows[q + u] * W + w] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; u++) v += t[u];
+        }
         return v;
     };
-    double s = 0.0;
-    for (int q = c.e_main_off[e]; q < c.e_main_off[e + 1]; q++) s = s + colval(c.e_main_cols[q]);
-    if (c.has_corr) {
-        double cs = 0.0;
-        for (int q = c.e_corr_off[e]; q < c.e_corr_off[e + 1]; q++) cs = cs + colval(c.e_corr_cols[q]);
-        s = s + (cs - c.fidcorr[e]);
-    }
+    double s = rows_sum(c.e_main_off, c.e_main_rows, c.e_main_const);
+    if (c.has_corr) s = s + (rows_sum(c.e_corr_off, c.e_corr_rows, c.e_corr_const) - c.fidcorr[e]);
     double *x = xrows + (long long)w * c.Np;
     if (c.approx == 2) {
         const int ix = c.e_to_x[e];
@@ -590,7 +599,7 @@ struct CMBLikes final : Like {
     // device tables
     CLDev dev{};
     HLDev hl{};
-    DevBuf d_pairs, d_items, d_wts, d_colpartoff, d_colparts, d_colconst, d_sumoff, d_sumcols, d_corroff, d_corrcols,
+    DevBuf d_pairs, d_items, d_wts, d_sumoff, d_sumcols, d_sumconst, d_corroff, d_corrcols, d_corrconst,
         d_etox, d_fidcorr, d_noise, d_chat, d_cluse, d_bkmaps, d_bpnu, d_bpR, d_bpdnu, d_hlchat, d_hlcf;
     int max_field = 0, n_part_rows = 0;
 
@@ -1064,34 +1073,34 @@ struct CMBLikes final : Like {
                     it.ncol = (int)(g1 - g0);
                     it.part = nrows;
                     it.woff = (long long)wdense.size();
-                    for (size_t g = g0; g < g1; g++) {
-                        for (int l = lo; l <= hi; l++) wdense.push_back(cols[sel[g]].W[l]);
-                        col_parts[sel[g]].push_back(nrows++);
-                    }
+                    for (int l = lo; l <= hi; l++)
+                        for (int g = 0; g < WK_COLS; g++)
+                            wdense.push_back(g0 + g < g1 ? cols[sel[g0 + g]].W[l] : 0.0);
+                    if ((hi - lo + 1) % 2) wdense.insert(wdense.end(), WK_COLS, 0.0);   // keep 16-byte alignment
+                    for (size_t g = g0; g < g1; g++) col_parts[sel[g]].push_back(nrows++);
                     items.push_back(it);
                 }
             }
         n_part_rows = nrows;
-        std::vector<int> col_part_off(cols.size() + 1, 0), col_part_all;
-        std::vector<double> col_const(cols.size(), 0.0);
-        for (size_t ci = 0; ci < cols.size(); ci++) {
-            col_part_off[ci] = (int)col_part_all.size();
-            col_part_all.insert(col_part_all.end(), col_parts[ci].begin(), col_parts[ci].end());
-            col_const[ci] = cols[ci].cst;
-        }
-        col_part_off[cols.size()] = (int)col_part_all.size();
         for (auto &it : items) max_field = std::max(max_field, pairs[it.pair].field);
-        auto flatten = [&](const std::vector<std::vector<int>> &lists, std::vector<int> &off, std::vector<int> &all) {
+        // per element: the partial rows of its columns in window order, and the fixed-spectrum constants
+        auto flatten = [&](const std::vector<std::vector<int>> &lists, std::vector<int> &off, std::vector<int> &rows,
+                           std::vector<double> &cst) {
             off.assign(lists.size() + 1, 0);
+            cst.assign(lists.size(), 0.0);
             for (size_t e = 0; e < lists.size(); e++) {
-                off[e] = (int)all.size();
-                all.insert(all.end(), lists[e].begin(), lists[e].end());
+                off[e] = (int)rows.size();
+                for (int ci : lists[e]) {
+                    rows.insert(rows.end(), col_parts[ci].begin(), col_parts[ci].end());
+                    cst[e] += cols[ci].cst;
+                }
             }
-            off[lists.size()] = (int)all.size();
+            off[lists.size()] = (int)rows.size();
         };
-        std::vector<int> main_off, main_cols, corr_off, corr_cols;
-        flatten(e_main, main_off, main_cols);
-        flatten(e_corr, corr_off, corr_cols);
+        std::vector<int> main_off, main_rows, corr_off, corr_rows;
+        std::vector<double> main_cst, corr_cst;
+        flatten(e_main, main_off, main_rows, main_cst);
+        flatten(e_corr, corr_off, corr_rows, corr_cst);
         std::vector<int> e_to_x(nE, -1);
         for (int b = 0; b < nb; b++)
             for (int u = 0; u < ncl_used; u++) e_to_x[b * ncl + cl_use[u]] = b * ncl_used + u;
@@ -1106,13 +1115,12 @@ struct CMBLikes final : Like {
         up(d_pairs, pairs.data(), pairs.size() * sizeof(CLPair));
         up(d_items, items.data(), items.size() * sizeof(WItem));
         up(d_wts, wdense.data(), wdense.size() * 8);
-        up(d_colpartoff, col_part_off.data(), col_part_off.size() * 4);
-        up(d_colparts, col_part_all.data(), col_part_all.size() * 4);
-        up(d_colconst, col_const.data(), col_const.size() * 8);
         up(d_sumoff, main_off.data(), main_off.size() * 4);
-        up(d_sumcols, main_cols.data(), main_cols.size() * 4);
+        up(d_sumcols, main_rows.data(), main_rows.size() * 4);
+        up(d_sumconst, main_cst.data(), main_cst.size() * 8);
         up(d_corroff, corr_off.data(), corr_off.size() * 4);
-        up(d_corrcols, corr_cols.data(), corr_cols.size() * 4);
+        up(d_corrcols, corr_rows.data(), corr_rows.size() * 4);
+        up(d_corrconst, corr_cst.data(), corr_cst.size() * 8);
         up(d_etox, e_to_x.data(), e_to_x.size() * 4);
         up(d_fidcorr, fc.data(), fc.size() * 8);
         up(d_noise, noise.data(), noise.size() * 8);
@@ -1143,12 +1151,11 @@ struct CMBLikes final : Like {
         dev.approx = approx;
         dev.has_corr = cw.present ? 1 : 0;
         dev.e_main_off = d_sumoff.as<int>();
-        dev.e_main_cols = d_sumcols.as<int>();
+        dev.e_main_rows = d_sumcols.as<int>();
+        dev.e_main_const = d_sumconst.as<double>();
         dev.e_corr_off = d_corroff.as<int>();
-        dev.e_corr_cols = d_corrcols.as<int>();
-        dev.col_part_off = d_colpartoff.as<int>();
-        dev.col_parts = d_colparts.as<int>();
-        dev.col_const = d_colconst.as<double>();
+        dev.e_corr_rows = d_corrcols.as<int>();
+        dev.e_corr_const = d_corrconst.as<double>();
         dev.fidcorr = d_fidcorr.as<double>();
         dev.noise = d_noise.as<double>();
         dev.chat = d_chat.as<double>();
