@@ -35,9 +35,11 @@ namespace cmamd {
 static constexpr int CL_MAXMAPS = 16;          // HL matrices up to 16 x 16 in one wave
 static constexpr int CL_MAXREQ = 32;            // required maps
 static constexpr int BK_NPARAM = 16;            // BKPlanck.paramnames
-static constexpr int WK_COLS = 24;              // window columns per work item (register accumulators)
-static constexpr int WK_CHUNK = 128;            // l per work item
-static constexpr int WK_BATCH = 16;             // l per load batch
+static constexpr int WK_COLS = 32;              // window columns per work item (two 16-row MFMA blocks)
+static constexpr int WK_CHUNK = 64;             // l per work item
+static constexpr int WK_TS = WK_CHUNK + 2;      // LDS row stride of the spectrum tile (doubles)
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 struct CLPair {      // one required map pair (i >= j)
     int field;       // theory field index 0..9 (TT TE EE BT BE BB PT PE PB PP)
@@ -116,7 +118,7 @@ __device__ inline double bk_decorr(double Delta, double nu0, double nu1, const d
 // BK per-walker foreground set-up (TBK_planck_AddForegrounds :250-285): the
 // SED factors of every map (one wave per map, bandpass integrals as wave
 // reductions) and the dust / sync / dust-sync l profiles.
-//   coef[w][3][nreq] = fdust, fsync, band-centre error;  prof[3][L][W] (walker fastest)
+//   coef[w][3][nreq] = fdust, fsync, band-centre error;  prof[w][3][L]
 __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *__restrict__ nuis, long long ld_nuis,
                                                        double *__restrict__ coef, double *__restrict__ prof, int W)
 {
@@ -161,131 +163,138 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
     const int L = c.lmax - c.lmin + 1;
     for (int l = c.lmin + tid; l <= c.lmax; l += blockDim.x) {
         const long long j = l - c.lmin;
-        prof[j * W + w] = Adust * pow(l / lpivot, alphadust);
-        prof[((long long)L + j) * W + w] = Async * pow(l / lpivot, alphasync);
-        prof[((long long)2 * L + j) * W + w] =
+        double *pw = prof + (long long)w * 3 * L;
+        pw[j] = Adust * pow(l / lpivot, alphadust);
+        pw[L + j] = Async * pow(l / lpivot, alphasync);
+        pw[2 * L + j] =
             dustsync_corr * sqrt(Adust * Async) * pow(l / lpivot, (alphadust + alphasync) / 2);
     }
 }
 
-// Window contractions.  One wave = 64 walkers (lane = walker) x one work item:
-// the map spectrum MapCl_pair(l) of each lane's walker (GetTheoryMapCls +
-// AdaptTheoryForMaps, CMBlikes.f90:1022-1126: aberration, foregrounds,
-// calibration) is formed in registers one l at a time and multiplied into up
-// to WK_COLS window columns whose weights are wave-uniform (scalar loads), so
-// every window value is fetched once per 64 walkers.  Writes the partial dot
-// products partial[(item.part + col) * W + w].
-__global__ __launch_bounds__(64) void cmbl_window_kernel(CLDev c, const double *__restrict__ dl, long long ld_field,
-                                                        long long ld_walker, const double *__restrict__ nuis,
-                                                        long long ld_nuis, const double *__restrict__ coef,
-                                                        const double *__restrict__ prof, double *__restrict__ partial,
-                                                        int W)
+// Window contractions on the f64 MFMA.  One workgroup = 64 walkers x one work
+// item (map pair, WK_CHUNK l, <= WK_COLS window columns):
+//   partial[col][w] = sum_l Wt[l][col] MapCl_w(l)
+// The walkers' map spectra MapCl_w(l) (GetTheoryMapCls + AdaptTheoryForMaps,
+// CMBlikes.f90:1022-1126: aberration, foregrounds, calibration) are formed
+// while staging the theory tile into LDS with coalesced 16-byte row loads;
+// the weights are staged once per 64 walkers.  Each wave then owns 16
+// walkers: v_mfma_f64_16x16x4f64 over (column block, walker block, 4 l).
+__global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double *__restrict__ dl, long long ld_field,
+                                                         long long ld_walker, const double *__restrict__ nuis,
+                                                         long long ld_nuis, const double *__restrict__ coef,
+                                                         const double *__restrict__ prof, double *__restrict__ partial,
+                                                         int W, int vec_ok)
 {
     __shared__ __attribute__((aligned(16))) double wsh[WK_CHUNK * WK_COLS];   // weights [l][col]
-    const int lane = threadIdx.x;
-    const int w = blockIdx.x * 64 + lane;
+    __shared__ __attribute__((aligned(16))) double tsh[64 * WK_TS];           // spectra [walker][l]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int w0 = blockIdx.x * 64;
     const WItem it = c.items[blockIdx.y];
-    {   // stage this item's weights (zero-padded to WK_COLS columns): coalesced 16-byte loads
-        const int n2 = (it.l1 - it.l0 + 1) * WK_COLS / 2;
+    const int len = it.l1 - it.l0 + 1;
+    {   // weights (zero-padded to WK_COLS columns and WK_CHUNK l by the host)
         const double2 *src = reinterpret_cast<const double2 *>(c.wdense + it.woff);
-        for (int i = lane; i < n2; i += 64) reinterpret_cast<double2 *>(wsh)[i] = src[i];
+        for (int i = tid; i < WK_CHUNK * WK_COLS / 2; i += 256) reinterpret_cast<double2 *>(wsh)[i] = src[i];
+    }
+    const CLPair pr = c.pairs[it.pair];
+    const bool aber = c.aberration != 0.0 && pr.cmb;
+    const int L = c.lmax - c.lmin + 1;
+    // staging: thread -> (walker row r, l pair q); 32 threads cover one row's 64 l
+    for (int i = tid; i < 64 * (WK_CHUNK / 2); i += 256) {
+        const int r = i / (WK_CHUNK / 2), q = i % (WK_CHUNK / 2);
+        const int w = w0 + r;
+        double v2[2] = {0.0, 0.0};
+        const int lq = it.l0 + 2 * q;
+        if (w < W && lq <= it.l1) {
+            const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
+            const double *P = nuis + (long long)w * ld_nuis;
+            if (vec_ok) {
+                const double2 d = *reinterpret_cast<const double2 *>(Df + lq);
+                v2[0] = d.x;
+                v2[1] = d.y;
+            } else {
+                v2[0] = Df[lq];
+                if (lq + 1 <= it.l1) v2[1] = Df[lq + 1];
+            }
+            double dust = 0, sync = 0, dustsync = 0, dd_flat = 1, ds_flat = 1, nu_i = 0, nu_j = 0;
+            double Delta_dust = 1, Delta_sync = 1;
+            bool dd_l = false, ds_l = false;
+            if (pr.fg) {                                      // :296-328
+                const double *cw = coef + (long long)w * 3 * c.nreq;
+                const int a = pr.mi, b = pr.mj;
+                dust = cw[a] * cw[b];
+                sync = cw[c.nreq + a] * cw[c.nreq + b];
+                dustsync = cw[a] * cw[c.nreq + b] + cw[c.nreq + a] * cw[b];
+                if (pr.fg == 1) {
+                    const double EEd = P[8], EEs = P[9];
+                    dust = dust * EEd;
+                    sync = sync * EEs;
+                    dustsync = dustsync * sqrt(EEd * EEs);
+                }
+                Delta_dust = P[10];
+                Delta_sync = P[11];
+                nu_i = c.bkmaps[a].nu_bar * cw[2 * c.nreq + a];
+                nu_j = c.bkmaps[b].nu_bar * cw[2 * c.nreq + b];
+                if (fabs(Delta_dust - 1) > 1e-5 && a != b) {
+                    if (c.lform_dust == 0) dd_flat = bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, 0, 0);
+                    else dd_l = true;
+                }
+                if (fabs(Delta_sync - 1) > 1e-5 && a != b) {
+                    if (c.lform_sync == 0) ds_flat = bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, 0, 0);
+                    else ds_l = true;
+                }
+            }
+            const double calsq = c.cal_index >= 0 ? P[c.cal_index] * P[c.cal_index] : 1.0;
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int l = lq + u;
+                if (l > it.l1) break;
+                double v = v2[u];
+                if (aber) {                                   // AddAberration :1062-1101
+                    int la = l - 1, lb = l + 1;
+                    if (l == c.lmin) { la = l; lb = l + 2; }
+                    else if (l == c.lmax) { la = l - 2; lb = l; }
+                    const double ea = la, eb = lb, el = l;
+                    const double ca = Df[la] / (ea * (ea + 1)), cb = Df[lb] / (eb * (eb + 1));
+                    const double deriv = 0.5 * (cb - ca);
+                    v = v + c.aberration * (el * el * (el + 1) * deriv);
+                }
+                if (pr.fg) {                                  // :329-334
+                    const double *pw = prof + (long long)w * 3 * L + (l - c.lmin);
+                    const double Dd = dd_l ? bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, l, c.lform_dust) : dd_flat;
+                    const double Ds = ds_l ? bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, l, c.lform_sync) : ds_flat;
+                    v = v + dust * pw[0] * Dd + sync * pw[L] * Ds + dustsync * pw[2 * L];
+                }
+                if (c.cal_index >= 0 && pr.cmb) v = v / calsq;   // AdaptTheoryForMaps :1113-1124
+                v2[u] = v;
+            }
+        }
+        tsh[r * WK_TS + 2 * q] = v2[0];
+        tsh[r * WK_TS + 2 * q + 1] = v2[1];
     }
     __syncthreads();
-    if (w >= W) return;
-    const CLPair pr = c.pairs[it.pair];
-    const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
-    const double *P = nuis + (long long)w * ld_nuis;
-    const double calsq = c.cal_index >= 0 ? P[c.cal_index] * P[c.cal_index] : 1.0;
-    const bool cal = c.cal_index >= 0 && pr.cmb;
-    const bool aber = c.aberration != 0.0 && pr.cmb;
-    double dust = 0, sync = 0, dustsync = 0, dd_flat = 1, ds_flat = 1, nu_i = 0, nu_j = 0;
-    double Delta_dust = 1, Delta_sync = 1;
-    bool dd_l = false, ds_l = false;
-    const int L = c.lmax - c.lmin + 1;
-    if (pr.fg) {                                              // :296-328
-        const double *cw = coef + (long long)w * 3 * c.nreq;
-        const int i = pr.mi, j = pr.mj;
-        dust = cw[i] * cw[j];
-        sync = cw[c.nreq + i] * cw[c.nreq + j];
-        dustsync = cw[i] * cw[c.nreq + j] + cw[c.nreq + i] * cw[j];
-        if (pr.fg == 1) {
-            const double EEd = P[8], EEs = P[9];
-            dust = dust * EEd;
-            sync = sync * EEs;
-            dustsync = dustsync * sqrt(EEd * EEs);
-        }
-        Delta_dust = P[10];
-        Delta_sync = P[11];
-        nu_i = c.bkmaps[i].nu_bar * cw[2 * c.nreq + i];
-        nu_j = c.bkmaps[j].nu_bar * cw[2 * c.nreq + j];
-        if (fabs(Delta_dust - 1) > 1e-5 && i != j) {
-            if (c.lform_dust == 0) dd_flat = bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, 0, 0);
-            else dd_l = true;
-        }
-        if (fabs(Delta_sync - 1) > 1e-5 && i != j) {
-            if (c.lform_sync == 0) ds_flat = bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, 0, 0);
-            else ds_l = true;
+    // f64 16x16x4: A = Wt[col][k] (lane: col = lane&15, k = lane>>4), B = MapCl[k][walker]
+    // (lane: walker = lane&15, k = lane>>4); D: walker = lane&15, col = (lane>>4) + 4 r
+    const int li = lane & 15, lk = lane >> 4;
+    f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    const double *trow = tsh + (16 * wave + li) * WK_TS;
+    const int nk = (len + 3) / 4;
+    for (int s = 0; s < nk; s++) {
+        const int k = 4 * s + lk;
+        const double b = trow[k];
+        const double a0 = wsh[k * WK_COLS + li];
+        const double a1 = wsh[k * WK_COLS + 16 + li];
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, acc1, 0, 0, 0);
+    }
+    const int w = w0 + 16 * wave + li;
+    if (w < W) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int c0 = lk + 4 * r, c1 = 16 + lk + 4 * r;
+            if (c0 < it.ncol) partial[(long long)(it.part + c0) * W + w] = acc0[r];
+            if (c1 < it.ncol) partial[(long long)(it.part + c1) * W + w] = acc1[r];
         }
     }
-    double acc[WK_COLS];
-#pragma unroll
-    for (int k = 0; k < WK_COLS; k++) acc[k] = 0.0;
-    // l in batches of WK_BATCH: every load of a batch is issued before the
-    // first use (one memory latency per batch); a lane's theory values of a
-    // batch are 128 contiguous bytes of its own row
-    for (int lb0 = it.l0; lb0 <= it.l1; lb0 += WK_BATCH) {
-        double t[WK_BATCH], ta[WK_BATCH], tb[WK_BATCH], pd[WK_BATCH], ps[WK_BATCH], pds[WK_BATCH];
-#pragma unroll
-        for (int q = 0; q < WK_BATCH; q++) {
-            const int l = lb0 + q;
-            const bool in = l <= it.l1;
-            t[q] = in ? Df[l] : 0.0;
-            if (aber) {
-                int la = l - 1, lb = l + 1;
-                if (l == c.lmin) { la = l; lb = l + 2; }
-                else if (l >= c.lmax) { la = l - 2; lb = l; }
-                ta[q] = in ? Df[la] : 0.0;
-                tb[q] = in ? Df[lb] : 0.0;
-            }
-            if (pr.fg) {
-                const long long j = in ? l - c.lmin : 0;
-                pd[q] = prof[j * W + w];
-                ps[q] = prof[((long long)L + j) * W + w];
-                pds[q] = prof[((long long)2 * L + j) * W + w];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < WK_BATCH; q++) {
-            const int l = lb0 + q;
-            if (l > it.l1) break;
-            double v = t[q];
-            if (aber) {                                       // AddAberration :1062-1101
-                int la = l - 1, lb = l + 1;
-                if (l == c.lmin) { la = l; lb = l + 2; }
-                else if (l == c.lmax) { la = l - 2; lb = l; }
-                const double ea = la, eb = lb, el = l;
-                const double ca = ta[q] / (ea * (ea + 1)), cb = tb[q] / (eb * (eb + 1));
-                const double deriv = 0.5 * (cb - ca);
-                v = v + c.aberration * (el * el * (el + 1) * deriv);
-            }
-            if (pr.fg) {                                      // :329-334
-                const double Dd = dd_l ? bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, l, c.lform_dust) : dd_flat;
-                const double Ds = ds_l ? bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, l, c.lform_sync) : ds_flat;
-                v = v + dust * pd[q] * Dd + sync * ps[q] * Ds + dustsync * pds[q];
-            }
-            if (cal) v = v / calsq;                           // AdaptTheoryForMaps :1113-1124
-            const double2 *wl = reinterpret_cast<const double2 *>(wsh + (l - it.l0) * WK_COLS);   // LDS broadcast
-#pragma unroll
-            for (int k = 0; k < WK_COLS / 2; k++) {
-                const double2 ww = wl[k];
-                acc[2 * k] += ww.x * v;
-                acc[2 * k + 1] += ww.y * v;
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < WK_COLS; k++)
-        if (k < it.ncol) partial[(long long)(it.part + k) * W + w] = acc[k];
 }
 
 // Binned spectra per (walker, element e = bin * ncl + cl): window columns in
@@ -602,6 +611,7 @@ struct CMBLikes final : Like {
     DevBuf d_pairs, d_items, d_wts, d_sumoff, d_sumcols, d_sumconst, d_corroff, d_corrcols, d_corrconst,
         d_etox, d_fidcorr, d_noise, d_chat, d_cluse, d_bkmaps, d_bpnu, d_bpR, d_bpdnu, d_hlchat, d_hlcf;
     int max_field = 0, n_part_rows = 0;
+    bool items_even = true;
 
     std::string cl_name(const std::vector<std::string> &names, int i, int j) const {   // Cl_i_j_name (:328-343)
         return has_map_names ? names[i - 1] + "x" + names[j - 1] : names[i - 1] + names[j - 1];
@@ -1066,6 +1076,7 @@ struct CMBLikes final : Like {
                         lo = std::min(lo, std::max(c0, cols[sel[g]].lo));
                         hi = std::max(hi, std::min(c1, cols[sel[g]].hi));
                     }
+                    if ((lo + lmin) % 2 == 1 && lo > c0) lo--;     // even l0: 16-byte theory loads
                     WItem it{};
                     it.pair = (int)p;
                     it.l0 = lo + lmin;
@@ -1073,15 +1084,16 @@ struct CMBLikes final : Like {
                     it.ncol = (int)(g1 - g0);
                     it.part = nrows;
                     it.woff = (long long)wdense.size();
-                    for (int l = lo; l <= hi; l++)
+                    for (int l = lo; l < lo + WK_CHUNK; l++)           // [WK_CHUNK][WK_COLS], zero padded
                         for (int g = 0; g < WK_COLS; g++)
-                            wdense.push_back(g0 + g < g1 ? cols[sel[g0 + g]].W[l] : 0.0);
-                    if ((hi - lo + 1) % 2) wdense.insert(wdense.end(), WK_COLS, 0.0);   // keep 16-byte alignment
+                            wdense.push_back(l <= hi && g0 + g < g1 ? cols[sel[g0 + g]].W[l] : 0.0);
                     for (size_t g = g0; g < g1; g++) col_parts[sel[g]].push_back(nrows++);
                     items.push_back(it);
                 }
             }
         n_part_rows = nrows;
+        items_even = true;
+        for (auto &it : items) items_even = items_even && (it.l0 % 2 == 0);
         for (auto &it : items) max_field = std::max(max_field, pairs[it.pair].field);
         // per element: the partial rows of its columns in window order, and the fixed-spectrum constants
         auto flatten = [&](const std::vector<std::vector<int>> &lists, std::vector<int> &off, std::vector<int> &rows,
@@ -1189,7 +1201,7 @@ struct CMBLikes final : Like {
         o.cmat = o.part + al((size_t)n_part_rows * W * 8);
         o.coef = o.cmat + al(approx == 1 ? (size_t)W * nb * ncl * 8 : 0);
         o.prof = o.coef + al(bk ? (size_t)W * 3 * nreq * 8 : 0);
-        o.add = o.prof + al(bk ? (size_t)3 * L * W * 8 : 0);
+        o.add = o.prof + al(bk ? (size_t)3 * L * W * 8 : 0);   // prof [W][3][L]
         o.total = o.add + al((size_t)W * 8);
         return o;
     }
@@ -1223,10 +1235,13 @@ struct CMBLikes final : Like {
             });
             HIP_CHECK(hipGetLastError());
         }
+        // 16-byte theory loads need aligned rows and even chunk starts
+        bool vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0 &&
+                      items_even && (lmax + 1 < ld_field || (lmax % 2 == 1 && lmax + 1 <= ld_field));
         timed_launch("cmbl_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(cmbl_window_kernel, dim3(tiles, dev.nitem), dim3(64), 0, stream, e0, e1, 0, dev,
+            hipExtLaunchKernelGGL(cmbl_window_kernel, dim3(tiles, dev.nitem), dim3(256), 0, stream, e0, e1, 0, dev,
                                   dl, ld_field, ld_walker, nu, ld_nuis, (const double *)coef, (const double *)prof,
-                                  partial, W);
+                                  partial, W, (int)vec_ok);
         });
         HIP_CHECK(hipGetLastError());
         timed_launch("cmbl_reduce_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
