@@ -198,57 +198,45 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
     const CLPair pr = c.pairs[it.pair];
     const bool aber = c.aberration != 0.0 && pr.cmb;
     const int L = c.lmax - c.lmin + 1;
-    // staging: thread -> (walker row r, l pair q); 32 threads cover one row's 64 l
-    for (int i = tid; i < 64 * (WK_CHUNK / 2); i += 256) {
+    // staging: thread -> (walker row r, l pair q); 32 threads cover one row's 64 l.
+    // All of a thread's loads are issued before any is used (one memory latency).
+    constexpr int PER = 64 * (WK_CHUNK / 2) / 256;
+    double2 raw[PER];
+    double cal2[PER];
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+        const int i = tid + 256 * u;
+        const int r = i / (WK_CHUNK / 2), q = i % (WK_CHUNK / 2);
+        const int w = w0 + r, lq = it.l0 + 2 * q;
+        raw[u] = make_double2(0.0, 0.0);
+        cal2[u] = 1.0;
+        if (w < W && lq <= it.l1) {
+            const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
+            if (vec_ok) {
+                raw[u] = *reinterpret_cast<const double2 *>(Df + lq);
+            } else {
+                raw[u].x = Df[lq];
+                if (lq + 1 <= it.l1) raw[u].y = Df[lq + 1];
+            }
+            if (c.cal_index >= 0) cal2[u] = nuis[(long long)w * ld_nuis + c.cal_index];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+        const int i = tid + 256 * u;
         const int r = i / (WK_CHUNK / 2), q = i % (WK_CHUNK / 2);
         const int w = w0 + r;
-        double v2[2] = {0.0, 0.0};
+        double v2[2] = {raw[u].x, raw[u].y};
         const int lq = it.l0 + 2 * q;
         if (w < W && lq <= it.l1) {
             const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
             const double *P = nuis + (long long)w * ld_nuis;
-            if (vec_ok) {
-                const double2 d = *reinterpret_cast<const double2 *>(Df + lq);
-                v2[0] = d.x;
-                v2[1] = d.y;
-            } else {
-                v2[0] = Df[lq];
-                if (lq + 1 <= it.l1) v2[1] = Df[lq + 1];
-            }
-            double dust = 0, sync = 0, dustsync = 0, dd_flat = 1, ds_flat = 1, nu_i = 0, nu_j = 0;
-            double Delta_dust = 1, Delta_sync = 1;
-            bool dd_l = false, ds_l = false;
-            if (pr.fg) {                                      // :296-328
-                const double *cw = coef + (long long)w * 3 * c.nreq;
-                const int a = pr.mi, b = pr.mj;
-                dust = cw[a] * cw[b];
-                sync = cw[c.nreq + a] * cw[c.nreq + b];
-                dustsync = cw[a] * cw[c.nreq + b] + cw[c.nreq + a] * cw[b];
-                if (pr.fg == 1) {
-                    const double EEd = P[8], EEs = P[9];
-                    dust = dust * EEd;
-                    sync = sync * EEs;
-                    dustsync = dustsync * sqrt(EEd * EEs);
-                }
-                Delta_dust = P[10];
-                Delta_sync = P[11];
-                nu_i = c.bkmaps[a].nu_bar * cw[2 * c.nreq + a];
-                nu_j = c.bkmaps[b].nu_bar * cw[2 * c.nreq + b];
-                if (fabs(Delta_dust - 1) > 1e-5 && a != b) {
-                    if (c.lform_dust == 0) dd_flat = bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, 0, 0);
-                    else dd_l = true;
-                }
-                if (fabs(Delta_sync - 1) > 1e-5 && a != b) {
-                    if (c.lform_sync == 0) ds_flat = bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, 0, 0);
-                    else ds_l = true;
-                }
-            }
-            const double calsq = c.cal_index >= 0 ? P[c.cal_index] * P[c.cal_index] : 1.0;
+            const double calsq = cal2[u] * cal2[u];
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const int l = lq + u;
+            for (int h = 0; h < 2; h++) {
+                const int l = lq + h;
                 if (l > it.l1) break;
-                double v = v2[u];
+                double v = v2[h];
                 if (aber) {                                   // AddAberration :1062-1101
                     int la = l - 1, lb = l + 1;
                     if (l == c.lmin) { la = l; lb = l + 2; }
@@ -265,7 +253,7 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
                     v = v + dust * pw[0] * Dd + sync * pw[L] * Ds + dustsync * pw[2 * L];
                 }
                 if (c.cal_index >= 0 && pr.cmb) v = v / calsq;   // AdaptTheoryForMaps :1113-1124
-                v2[u] = v;
+                v2[h] = v;
             }
         }
         tsh[r * WK_TS + 2 * q] = v2[0];
@@ -303,33 +291,45 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
 // writes bigX = C - Chat for the used spectra; HL: writes C (+ noise) for the
 // transform.  Block (0, 0) zeroes the quadratic-form tickets; element 0 also
 // pads the bigX row and writes the calibration-prior addend.
-__global__ __launch_bounds__(64) void cmbl_reduce_kernel(CLDev c, const double *__restrict__ partial,
-                                                        const double *__restrict__ nuis, long long ld_nuis,
-                                                        double *__restrict__ xrows, double *__restrict__ cmat,
-                                                        double *__restrict__ addend, unsigned int *__restrict__ counters,
-                                                        int n_counters, int W)
+__global__ __launch_bounds__(256) void cmbl_reduce_kernel(CLDev c, const double *__restrict__ partial,
+                                                         const double *__restrict__ nuis, long long ld_nuis,
+                                                         double *__restrict__ xrows, double *__restrict__ cmat,
+                                                         double *__restrict__ addend, unsigned int *__restrict__ counters,
+                                                         int n_counters, int W)
 {
+    __shared__ double red[2][4][64];
     const int e = blockIdx.y;
-    const int w = blockIdx.x * 64 + threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int w = blockIdx.x * 64 + lane;
     if (blockIdx.x == 0 && e == 0)
-        for (int i = threadIdx.x; i < n_counters; i += 64) counters[i] = 0u;
-    if (w >= W) return;
-    // window columns in window order, each the l-chunk partials in order (flattened
-    // on the host); loads issued eight at a time
-    auto rows_sum = [&](const int *off, const int *rows, const double *cst) {
-        double v = cst[e];
-        const int q0 = off[e], q1 = off[e + 1];
-        for (int q = q0; q < q1; q += 8) {
-            double t[8];
+        for (int i = threadIdx.x; i < n_counters; i += 256) counters[i] = 0u;
+    // window columns in window order, each the l-chunk partials in order (flattened on
+    // the host); wave v sums rows v, v+4, ... eight loads at a time, the four wave sums
+    // are combined in fixed order: deterministic
+    auto rows_sum = [&](const int *off, const int *rows) {
+        double v = 0.0;
+        if (w < W) {
+            const int q0 = off[e], q1 = off[e + 1];
+            for (int q = q0 + wave; q < q1; q += 32) {
+                double t[8];
 #pragma unroll
-            for (int u = 0; u < 8; u++) t[u] = (q + u < q1) ? partial[(long long)rows[q + u] * W + w] : 0.0;
+                for (int u = 0; u < 8; u++)
+                    t[u] = (q + 4 * u < q1) ? partial[(long long)rows[q + 4 * u] * W + w] : 0.0;
 #pragma unroll
-            for (int u = 0; u < 8; u++) v += t[u];
+                for (int u = 0; u < 8; u++) v += t[u];
+            }
         }
         return v;
     };
-    double s = rows_sum(c.e_main_off, c.e_main_rows, c.e_main_const);
-    if (c.has_corr) s = s + (rows_sum(c.e_corr_off, c.e_corr_rows, c.e_corr_const) - c.fidcorr[e]);
+    red[0][wave][lane] = rows_sum(c.e_main_off, c.e_main_rows);
+    red[1][wave][lane] = c.has_corr ? rows_sum(c.e_corr_off, c.e_corr_rows) : 0.0;
+    __syncthreads();
+    if (wave != 0 || w >= W) return;
+    double s = c.e_main_const[e] + (((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane]);
+    if (c.has_corr) {
+        const double cs = c.e_corr_const[e] + (((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane]);
+        s = s + (cs - c.fidcorr[e]);
+    }
     double *x = xrows + (long long)w * c.Np;
     if (c.approx == 2) {
         const int ix = c.e_to_x[e];
@@ -1245,7 +1245,7 @@ struct CMBLikes final : Like {
         });
         HIP_CHECK(hipGetLastError());
         timed_launch("cmbl_reduce_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(cmbl_reduce_kernel, dim3(tiles, dev.nE), dim3(64), 0, stream, e0, e1, 0, dev,
+            hipExtLaunchKernelGGL(cmbl_reduce_kernel, dim3(tiles, dev.nE), dim3(256), 0, stream, e0, e1, 0, dev,
                                   (const double *)partial, nu, ld_nuis, qf.x_rows(ws), cmat, use_add ? addend : nullptr,
                                   qf.counters(ws, W), qf.n_counters(W), W);
         });
