@@ -232,6 +232,34 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
             const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
             const double *P = nuis + (long long)w * ld_nuis;
             const double calsq = cal2[u] * cal2[u];
+            double dust = 0, sync = 0, dustsync = 0, dd_flat = 1, ds_flat = 1, nu_i = 0, nu_j = 0;
+            double Delta_dust = 1, Delta_sync = 1;
+            bool dd_l = false, ds_l = false;
+            if (pr.fg) {                                      // :296-328
+                const double *cw = coef + (long long)w * 3 * c.nreq;
+                const int a = pr.mi, b = pr.mj;
+                dust = cw[a] * cw[b];
+                sync = cw[c.nreq + a] * cw[c.nreq + b];
+                dustsync = cw[a] * cw[c.nreq + b] + cw[c.nreq + a] * cw[b];
+                if (pr.fg == 1) {
+                    const double EEd = P[8], EEs = P[9];
+                    dust = dust * EEd;
+                    sync = sync * EEs;
+                    dustsync = dustsync * sqrt(EEd * EEs);
+                }
+                Delta_dust = P[10];
+                Delta_sync = P[11];
+                nu_i = c.bkmaps[a].nu_bar * cw[2 * c.nreq + a];
+                nu_j = c.bkmaps[b].nu_bar * cw[2 * c.nreq + b];
+                if (fabs(Delta_dust - 1) > 1e-5 && a != b) {
+                    if (c.lform_dust == 0) dd_flat = bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, 0, 0);
+                    else dd_l = true;
+                }
+                if (fabs(Delta_sync - 1) > 1e-5 && a != b) {
+                    if (c.lform_sync == 0) ds_flat = bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, 0, 0);
+                    else ds_l = true;
+                }
+            }
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int l = lq + h;
