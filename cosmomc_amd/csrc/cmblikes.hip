@@ -179,6 +179,7 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
 // while staging the theory tile into LDS with coalesced 16-byte row loads;
 // the weights are staged once per 64 walkers.  Each wave then owns 16
 // walkers: v_mfma_f64_16x16x4f64 over (column block, walker block, 4 l).
+template <bool ABER, bool FG>
 __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double *__restrict__ dl, long long ld_field,
                                                          long long ld_walker, const double *__restrict__ nuis,
                                                          long long ld_nuis, const double *__restrict__ coef,
@@ -196,7 +197,11 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
         for (int i = tid; i < WK_CHUNK * WK_COLS / 2; i += 256) reinterpret_cast<double2 *>(wsh)[i] = src[i];
     }
     const CLPair pr = c.pairs[it.pair];
-    const bool aber = c.aberration != 0.0 && pr.cmb;
+    // ABER / FG are the dataset's aberration and foreground switches as template
+    // parameters: the per-pair flags below are then wave-uniform branches over
+    // code that exists only in the variants that need it
+    const bool aber = ABER && c.aberration != 0.0 && pr.cmb;
+    const bool fg = FG && pr.fg;
     const int L = c.lmax - c.lmin + 1;
     // staging: thread -> (walker row r, l pair q); 32 threads cover one row's 64 l.
     // All of a thread's loads are issued before any is used (one memory latency).
@@ -235,7 +240,7 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
             double dust = 0, sync = 0, dustsync = 0, dd_flat = 1, ds_flat = 1, nu_i = 0, nu_j = 0;
             double Delta_dust = 1, Delta_sync = 1;
             bool dd_l = false, ds_l = false;
-            if (pr.fg) {                                      // :296-328
+            if (fg) {                                      // :296-328
                 const double *cw = coef + (long long)w * 3 * c.nreq;
                 const int a = pr.mi, b = pr.mj;
                 dust = cw[a] * cw[b];
@@ -274,7 +279,7 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
                     const double deriv = 0.5 * (cb - ca);
                     v = v + c.aberration * (el * el * (el + 1) * deriv);
                 }
-                if (pr.fg) {                                  // :329-334
+                if (fg) {                                  // :329-334
                     const double *pw = prof + (long long)w * 3 * L + (l - c.lmin);
                     const double Dd = dd_l ? bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, l, c.lform_dust) : dd_flat;
                     const double Ds = ds_l ? bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, l, c.lform_sync) : ds_flat;
@@ -1267,9 +1272,19 @@ struct CMBLikes final : Like {
         bool vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0 &&
                       items_even && (lmax + 1 < ld_field || (lmax % 2 == 1 && lmax + 1 <= ld_field));
         timed_launch("cmbl_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(cmbl_window_kernel, dim3(tiles, dev.nitem), dim3(256), 0, stream, e0, e1, 0, dev,
-                                  dl, ld_field, ld_walker, nu, ld_nuis, (const double *)coef, (const double *)prof,
-                                  partial, W, (int)vec_ok);
+#define CMBL_WINDOW(A, F)                                                                                        \
+    hipExtLaunchKernelGGL(cmbl_window_kernel<A, F>, dim3(tiles, dev.nitem), dim3(256), 0, stream, e0, e1, 0, dev, dl, \
+                          ld_field, ld_walker, nu, ld_nuis, (const double *)coef, (const double *)prof, partial, W,    \
+                          (int)vec_ok)
+            const bool ab = aberration != 0.0;
+            if (bk) {
+                if (ab) CMBL_WINDOW(true, true);
+                else CMBL_WINDOW(false, true);
+            } else {
+                if (ab) CMBL_WINDOW(true, false);
+                else CMBL_WINDOW(false, false);
+            }
+#undef CMBL_WINDOW
         });
         HIP_CHECK(hipGetLastError());
         timed_launch("cmbl_reduce_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
