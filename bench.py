@@ -229,7 +229,8 @@ def main():
         torch.cuda.synchronize()
         N.profile_enable(False)
         kern = {k: N.profile_read(k) for k in ("plik_bin_delta", "plik_quadform_ksplit", "mh_kernel",
-                                                "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_quadform")}
+                                                "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_gauss_small_kernel",
+                                                "cmbl_quadform")}
         kern = {k: v for k, v in kern.items() if v[1]}
         _, _, _, nacc = smp.state()
         acc_rate = float(nacc.sum()) / (W * (args.warmup + 2 * args.steps))

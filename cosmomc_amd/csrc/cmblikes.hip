@@ -36,7 +36,8 @@ static constexpr int CL_MAXMAPS = 16;          // HL matrices up to 16 x 16 in o
 static constexpr int CL_MAXREQ = 32;            // required maps
 static constexpr int BK_NPARAM = 16;            // BKPlanck.paramnames
 static constexpr int WK_COLS = 32;              // window columns per work item (two 16-row MFMA blocks)
-static constexpr int WK_CHUNK = 64;             // l per work item
+static constexpr int WK_CHUNK = 64;             // l per chunk
+static constexpr int WK_NCH = 4;                // chunks per work item
 static constexpr int WK_TS = WK_CHUNK + 2;      // LDS row stride of the spectrum tile (doubles)
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -48,13 +49,13 @@ struct CLPair {      // one required map pair (i >= j)
     int mi, mj;      // required-map indices (0-based)
 };
 
-struct WItem {       // one (map pair, l chunk, <= WK_COLS window columns) contraction
+struct WItem {       // one (map pair, <= WK_NCH l chunks, <= WK_COLS window columns) contraction
     int pair;
-    int l0, l1;      // l range (inclusive)
+    int l0, l1;      // l range (inclusive), l0 even when possible
     int ncol;
     int part;        // partial rows part .. part+ncol-1
-    int pad;
-    long long woff;  // dense weights [l1-l0+1][WK_COLS] (zero-padded columns), 16-byte aligned
+    int nch;         // chunks of WK_CHUNK l
+    long long woff;  // dense weights [nch][WK_CHUNK][WK_COLS] (zero padded)
 };
 
 struct BKMap {       // per required map: bandpass samples and constants (Read_Bandpass :72-105)
@@ -172,13 +173,15 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
 }
 
 // Window contractions on the f64 MFMA.  One workgroup = 64 walkers x one work
-// item (map pair, WK_CHUNK l, <= WK_COLS window columns):
+// item (map pair, up to WK_NCH chunks of WK_CHUNK l, <= WK_COLS window columns):
 //   partial[col][w] = sum_l Wt[l][col] MapCl_w(l)
 // The walkers' map spectra MapCl_w(l) (GetTheoryMapCls + AdaptTheoryForMaps,
 // CMBlikes.f90:1022-1126: aberration, foregrounds, calibration) are formed
-// while staging the theory tile into LDS with coalesced 16-byte row loads;
-// the weights are staged once per 64 walkers.  Each wave then owns 16
-// walkers: v_mfma_f64_16x16x4f64 over (column block, walker block, 4 l).
+// while staging each theory chunk into LDS from coalesced 16-byte row loads;
+// the next chunk's loads are in flight during the current chunk's MFMAs.
+// Each wave owns 16 walkers: v_mfma_f64_16x16x4f64 over (column block, 4 l).
+// ABER / FG (the dataset's aberration / foreground switches) are template
+// parameters so the lensing variant carries no foreground code.
 template <bool ABER, bool FG>
 __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double *__restrict__ dl, long long ld_field,
                                                          long long ld_walker, const double *__restrict__ nuis,
@@ -191,122 +194,138 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int w0 = blockIdx.x * 64;
     const WItem it = c.items[blockIdx.y];
-    const int len = it.l1 - it.l0 + 1;
-    {   // weights (zero-padded to WK_COLS columns and WK_CHUNK l by the host)
-        const double2 *src = reinterpret_cast<const double2 *>(c.wdense + it.woff);
-        for (int i = tid; i < WK_CHUNK * WK_COLS / 2; i += 256) reinterpret_cast<double2 *>(wsh)[i] = src[i];
-    }
     const CLPair pr = c.pairs[it.pair];
-    // ABER / FG are the dataset's aberration and foreground switches as template
-    // parameters: the per-pair flags below are then wave-uniform branches over
-    // code that exists only in the variants that need it
     const bool aber = ABER && c.aberration != 0.0 && pr.cmb;
     const bool fg = FG && pr.fg;
     const int L = c.lmax - c.lmin + 1;
-    // staging: thread -> (walker row r, l pair q); 32 threads cover one row's 64 l.
-    // All of a thread's loads are issued before any is used (one memory latency).
+    // staging map: thread -> l pair q = tid % 32 of rows r_u = tid / 32 + 8 u (u < 8)
     constexpr int PER = 64 * (WK_CHUNK / 2) / 256;
-    double2 raw[PER];
-    double cal2[PER];
+    const int q = tid % (WK_CHUNK / 2), rbase = tid / (WK_CHUNK / 2);
+    // per-walker constants of the thread's rows
+    double calsq[PER];
+    double dust[FG ? PER : 1], sync[FG ? PER : 1], dsync[FG ? PER : 1], ddf[FG ? PER : 1], dsf[FG ? PER : 1],
+        nui[FG ? PER : 1], nuj[FG ? PER : 1];
+    bool dd_l = false, ds_l = false;
+    double Delta_dust = 1, Delta_sync = 1;
 #pragma unroll
     for (int u = 0; u < PER; u++) {
-        const int i = tid + 256 * u;
-        const int r = i / (WK_CHUNK / 2), q = i % (WK_CHUNK / 2);
-        const int w = w0 + r, lq = it.l0 + 2 * q;
-        raw[u] = make_double2(0.0, 0.0);
-        cal2[u] = 1.0;
-        if (w < W && lq <= it.l1) {
-            const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
-            if (vec_ok) {
-                raw[u] = *reinterpret_cast<const double2 *>(Df + lq);
-            } else {
-                raw[u].x = Df[lq];
-                if (lq + 1 <= it.l1) raw[u].y = Df[lq + 1];
-            }
-            if (c.cal_index >= 0) cal2[u] = nuis[(long long)w * ld_nuis + c.cal_index];
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < PER; u++) {
-        const int i = tid + 256 * u;
-        const int r = i / (WK_CHUNK / 2), q = i % (WK_CHUNK / 2);
-        const int w = w0 + r;
-        double v2[2] = {raw[u].x, raw[u].y};
-        const int lq = it.l0 + 2 * q;
-        if (w < W && lq <= it.l1) {
-            const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
-            const double *P = nuis + (long long)w * ld_nuis;
-            const double calsq = cal2[u] * cal2[u];
-            double dust = 0, sync = 0, dustsync = 0, dd_flat = 1, ds_flat = 1, nu_i = 0, nu_j = 0;
-            double Delta_dust = 1, Delta_sync = 1;
-            bool dd_l = false, ds_l = false;
-            if (fg) {                                      // :296-328
+        const int w = min(w0 + rbase + 8 * u, W - 1);
+        const double *P = nuis + (long long)w * ld_nuis;
+        const double cl = c.cal_index >= 0 ? P[c.cal_index] : 1.0;
+        calsq[u] = cl * cl;
+        if constexpr (FG) {
+            dust[u] = sync[u] = dsync[u] = nui[u] = nuj[u] = 0.0;
+            ddf[u] = dsf[u] = 1.0;
+            if (fg) {                                         // :296-328
                 const double *cw = coef + (long long)w * 3 * c.nreq;
                 const int a = pr.mi, b = pr.mj;
-                dust = cw[a] * cw[b];
-                sync = cw[c.nreq + a] * cw[c.nreq + b];
-                dustsync = cw[a] * cw[c.nreq + b] + cw[c.nreq + a] * cw[b];
+                double d = cw[a] * cw[b], sy = cw[c.nreq + a] * cw[c.nreq + b];
+                double ds = cw[a] * cw[c.nreq + b] + cw[c.nreq + a] * cw[b];
                 if (pr.fg == 1) {
                     const double EEd = P[8], EEs = P[9];
-                    dust = dust * EEd;
-                    sync = sync * EEs;
-                    dustsync = dustsync * sqrt(EEd * EEs);
+                    d = d * EEd;
+                    sy = sy * EEs;
+                    ds = ds * sqrt(EEd * EEs);
                 }
+                dust[u] = d;
+                sync[u] = sy;
+                dsync[u] = ds;
                 Delta_dust = P[10];
                 Delta_sync = P[11];
-                nu_i = c.bkmaps[a].nu_bar * cw[2 * c.nreq + a];
-                nu_j = c.bkmaps[b].nu_bar * cw[2 * c.nreq + b];
+                nui[u] = c.bkmaps[a].nu_bar * cw[2 * c.nreq + a];
+                nuj[u] = c.bkmaps[b].nu_bar * cw[2 * c.nreq + b];
                 if (fabs(Delta_dust - 1) > 1e-5 && a != b) {
-                    if (c.lform_dust == 0) dd_flat = bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, 0, 0);
+                    if (c.lform_dust == 0) ddf[u] = bk_decorr(Delta_dust, nui[u], nuj[u], c.decorr_dust, 0, 0);
                     else dd_l = true;
                 }
                 if (fabs(Delta_sync - 1) > 1e-5 && a != b) {
-                    if (c.lform_sync == 0) ds_flat = bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, 0, 0);
+                    if (c.lform_sync == 0) dsf[u] = bk_decorr(Delta_sync, nui[u], nuj[u], c.decorr_sync, 0, 0);
                     else ds_l = true;
                 }
             }
+        }
+    }
+    double2 raw[PER];
+    auto load_chunk = [&](int ch) {
+        const int lq = it.l0 + ch * WK_CHUNK + 2 * q;
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int l = lq + h;
-                if (l > it.l1) break;
-                double v = v2[h];
-                if (aber) {                                   // AddAberration :1062-1101
-                    int la = l - 1, lb = l + 1;
-                    if (l == c.lmin) { la = l; lb = l + 2; }
-                    else if (l == c.lmax) { la = l - 2; lb = l; }
-                    const double ea = la, eb = lb, el = l;
-                    const double ca = Df[la] / (ea * (ea + 1)), cb = Df[lb] / (eb * (eb + 1));
-                    const double deriv = 0.5 * (cb - ca);
-                    v = v + c.aberration * (el * el * (el + 1) * deriv);
+        for (int u = 0; u < PER; u++) {
+            const int w = w0 + rbase + 8 * u;
+            raw[u] = make_double2(0.0, 0.0);
+            if (w < W && lq <= it.l1) {
+                const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
+                if (vec_ok) {
+                    raw[u] = *reinterpret_cast<const double2 *>(Df + lq);
+                } else {
+                    raw[u].x = Df[lq];
+                    if (lq + 1 <= it.l1) raw[u].y = Df[lq + 1];
                 }
-                if (fg) {                                  // :329-334
-                    const double *pw = prof + (long long)w * 3 * L + (l - c.lmin);
-                    const double Dd = dd_l ? bk_decorr(Delta_dust, nu_i, nu_j, c.decorr_dust, l, c.lform_dust) : dd_flat;
-                    const double Ds = ds_l ? bk_decorr(Delta_sync, nu_i, nu_j, c.decorr_sync, l, c.lform_sync) : ds_flat;
-                    v = v + dust * pw[0] * Dd + sync * pw[L] * Ds + dustsync * pw[2 * L];
-                }
-                if (c.cal_index >= 0 && pr.cmb) v = v / calsq;   // AdaptTheoryForMaps :1113-1124
-                v2[h] = v;
             }
         }
-        tsh[r * WK_TS + 2 * q] = v2[0];
-        tsh[r * WK_TS + 2 * q + 1] = v2[1];
-    }
-    __syncthreads();
-    // f64 16x16x4: A = Wt[col][k] (lane: col = lane&15, k = lane>>4), B = MapCl[k][walker]
-    // (lane: walker = lane&15, k = lane>>4); D: walker = lane&15, col = (lane>>4) + 4 r
-    const int li = lane & 15, lk = lane >> 4;
+    };
     f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    const int li = lane & 15, lk = lane >> 4;
     const double *trow = tsh + (16 * wave + li) * WK_TS;
-    const int nk = (len + 3) / 4;
-    for (int s = 0; s < nk; s++) {
-        const int k = 4 * s + lk;
-        const double b = trow[k];
-        const double a0 = wsh[k * WK_COLS + li];
-        const double a1 = wsh[k * WK_COLS + 16 + li];
-        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, acc1, 0, 0, 0);
+    load_chunk(0);
+    for (int ch = 0; ch < it.nch; ch++) {
+        {   // weights of this chunk (zero-padded to WK_COLS columns and WK_CHUNK l by the host)
+            const double2 *src = reinterpret_cast<const double2 *>(c.wdense + it.woff) + ch * (WK_CHUNK * WK_COLS / 2);
+            for (int i = tid; i < WK_CHUNK * WK_COLS / 2; i += 256) reinterpret_cast<double2 *>(wsh)[i] = src[i];
+        }
+        const int lq = it.l0 + ch * WK_CHUNK + 2 * q;
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int r = rbase + 8 * u, w = w0 + r;
+            double v2[2] = {raw[u].x, raw[u].y};
+            if (w < W && lq <= it.l1) {
+                const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int l = lq + h;
+                    if (l > it.l1) break;
+                    double v = v2[h];
+                    if (aber) {                               // AddAberration :1062-1101
+                        int la = l - 1, lb = l + 1;
+                        if (l == c.lmin) { la = l; lb = l + 2; }
+                        else if (l == c.lmax) { la = l - 2; lb = l; }
+                        const double ea = la, eb = lb, el = l;
+                        const double ca = Df[la] / (ea * (ea + 1)), cb = Df[lb] / (eb * (eb + 1));
+                        const double deriv = 0.5 * (cb - ca);
+                        v = v + c.aberration * (el * el * (el + 1) * deriv);
+                    }
+                    if constexpr (FG) {
+                        if (fg) {                             // :329-334
+                            const double *pw = prof + (long long)w * 3 * L + (l - c.lmin);
+                            const double Dd = dd_l ? bk_decorr(Delta_dust, nui[u], nuj[u], c.decorr_dust, l, c.lform_dust)
+                                                   : ddf[u];
+                            const double Ds = ds_l ? bk_decorr(Delta_sync, nui[u], nuj[u], c.decorr_sync, l, c.lform_sync)
+                                                   : dsf[u];
+                            v = v + dust[u] * pw[0] * Dd + sync[u] * pw[L] * Ds + dsync[u] * pw[2 * L];
+                        }
+                    }
+                    if (c.cal_index >= 0 && pr.cmb) v = v / calsq[u];   // AdaptTheoryForMaps :1113-1124
+                    v2[h] = v;
+                }
+            }
+            tsh[r * WK_TS + 2 * q] = v2[0];
+            tsh[r * WK_TS + 2 * q + 1] = v2[1];
+        }
+        if (ch + 1 < it.nch) load_chunk(ch + 1);          // in flight during this chunk's MFMAs
+        __syncthreads();
+        // A = Wt[col][k] (lane: col = lane&15, k = lane>>4); B = MapCl[k][walker] (walker = lane&15)
+        const int clen = min(WK_CHUNK, it.l1 - (it.l0 + ch * WK_CHUNK) + 1);
+        const int nk = (clen + 3) / 4;
+        for (int s = 0; s < nk; s++) {
+            const int k = 4 * s + lk;
+            const double b = trow[k];
+            const double a0 = wsh[k * WK_COLS + li];
+            const double a1 = wsh[k * WK_COLS + 16 + li];
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, acc1, 0, 0, 0);
+        }
+        __syncthreads();
     }
+    // D: walker = lane&15, col = (lane>>4) + 4 r
     const int w = w0 + 16 * wave + li;
     if (w < W) {
 #pragma unroll
@@ -380,6 +399,59 @@ __global__ __launch_bounds__(256) void cmbl_reduce_kernel(CLDev c, const double 
             }
             addend[w] = a;
         }
+    }
+}
+
+// Small gaussian likelihoods (nX <= 64, e.g. lensing 9, SPT-SZ 47): binned
+// spectra, bigX = C - Chat and chi^2 = bigX^T C^-1 bigX in one kernel
+// (CMBlikes.f90:1183-1225; Matrix_QuadForm as row sums y = M x, then x.y).
+// 64 walkers per workgroup; wave v handles elements v, v+4, ... and rows of M.
+static constexpr int SMALL_NX = 64;
+__global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, const double *__restrict__ partial,
+                                                              const double *__restrict__ nuis, long long ld_nuis,
+                                                              const double *__restrict__ M, double *__restrict__ out,
+                                                              int W)
+{
+    __shared__ double xs[SMALL_NX][65];
+    __shared__ double red[4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int w = blockIdx.x * 64 + lane;
+    const bool act = w < W;
+    auto rows_sum = [&](const int *off, const int *rows, int e) {
+        double v = 0.0;
+        const int q0 = off[e], q1 = off[e + 1];
+        for (int q = q0; q < q1; q += 8) {
+            double t[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) t[u] = (act && q + u < q1) ? partial[(long long)rows[q + u] * W + w] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; u++) v += t[u];
+        }
+        return v;
+    };
+    for (int e = wave; e < c.nE; e += 4) {
+        const int ix = c.e_to_x[e];
+        if (ix < 0) continue;
+        double s = c.e_main_const[e] + rows_sum(c.e_main_off, c.e_main_rows, e);
+        if (c.has_corr) s = s + ((c.e_corr_const[e] + rows_sum(c.e_corr_off, c.e_corr_rows, e)) - c.fidcorr[e]);
+        xs[ix][lane] = s - c.chat[e];
+    }
+    __syncthreads();
+    double part = 0.0;
+    for (int i = wave; i < c.nX; i += 4) {
+        double y = 0.0;
+        for (int j = 0; j < c.nX; j++) y += M[i * c.nX + j] * xs[j][lane];
+        part += xs[i][lane] * y;
+    }
+    red[wave][lane] = part;
+    __syncthreads();
+    if (wave == 0 && act) {
+        double chisq = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+        if (c.log_cal_prior > 0 && c.cal_index >= 0) {
+            const double t = log(nuis[(long long)w * ld_nuis + c.cal_index]) / c.log_cal_prior;
+            chisq = chisq + t * t;
+        }
+        out[w] = chisq / 2;
     }
 }
 
@@ -644,7 +716,8 @@ struct CMBLikes final : Like {
     DevBuf d_pairs, d_items, d_wts, d_sumoff, d_sumcols, d_sumconst, d_corroff, d_corrcols, d_corrconst,
         d_etox, d_fidcorr, d_noise, d_chat, d_cluse, d_bkmaps, d_bpnu, d_bpR, d_bpdnu, d_hlchat, d_hlcf;
     int max_field = 0, n_part_rows = 0;
-    bool items_even = true;
+    bool items_even = true, small_gauss = false;
+    DevBuf d_invcov;
 
     std::string cl_name(const std::vector<std::string> &names, int i, int j) const {   // Cl_i_j_name (:328-343)
         return has_map_names ? names[i - 1] + "x" + names[j - 1] : names[i - 1] + names[j - 1];
@@ -1094,10 +1167,11 @@ struct CMBLikes final : Like {
         std::vector<double> wdense;
         std::vector<std::vector<int>> col_parts(cols.size());
         int nrows = 0;
-        const int nchunk = (L + WK_CHUNK - 1) / WK_CHUNK;
+        const int SEG = WK_CHUNK * WK_NCH;
+        const int nseg = (L + SEG - 1) / SEG;
         for (size_t p = 0; p < pairs.size(); p++)
-            for (int ch = 0; ch < nchunk; ch++) {
-                const int c0 = ch * WK_CHUNK, c1 = std::min(L - 1, c0 + WK_CHUNK - 1);
+            for (int sg = 0; sg < nseg; sg++) {
+                const int c0 = sg * SEG, c1 = std::min(L - 1, c0 + SEG - 1);
                 std::vector<int> sel;
                 for (size_t ci = 0; ci < cols.size(); ci++)
                     if (!cols[ci].fixed && cols[ci].pair == (int)p && cols[ci].hi >= c0 && cols[ci].lo <= c1)
@@ -1116,8 +1190,9 @@ struct CMBLikes final : Like {
                     it.l1 = hi + lmin;
                     it.ncol = (int)(g1 - g0);
                     it.part = nrows;
+                    it.nch = (hi - lo + WK_CHUNK) / WK_CHUNK;
                     it.woff = (long long)wdense.size();
-                    for (int l = lo; l < lo + WK_CHUNK; l++)           // [WK_CHUNK][WK_COLS], zero padded
+                    for (int l = lo; l < lo + it.nch * WK_CHUNK; l++)   // [nch][WK_CHUNK][WK_COLS], zero padded
                         for (int g = 0; g < WK_COLS; g++)
                             wdense.push_back(l <= hi && g0 + g < g1 ? cols[sel[g0 + g]].W[l] : 0.0);
                     for (size_t g = g0; g < g1; g++) col_parts[sel[g]].push_back(nrows++);
@@ -1180,6 +1255,8 @@ struct CMBLikes final : Like {
             up(d_bpdnu, bdnu.data(), bdnu.size() * 8);
         }
         qf.init(invcov, nX);
+        small_gauss = approx == 2 && nX <= SMALL_NX;
+        up(d_invcov, invcov.data(), invcov.size() * 8);
         dev.lmin = lmin;
         dev.lmax = lmax;
         dev.nitem = (int)items.size();
@@ -1287,6 +1364,14 @@ struct CMBLikes final : Like {
 #undef CMBL_WINDOW
         });
         HIP_CHECK(hipGetLastError());
+        if (small_gauss) {
+            timed_launch("cmbl_gauss_small_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+                hipExtLaunchKernelGGL(cmbl_gauss_small_kernel, dim3(tiles), dim3(256), 0, stream, e0, e1, 0, dev,
+                                      (const double *)partial, nu, ld_nuis, d_invcov.as<double>(), out, W);
+            });
+            HIP_CHECK(hipGetLastError());
+            return;
+        }
         timed_launch("cmbl_reduce_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
             hipExtLaunchKernelGGL(cmbl_reduce_kernel, dim3(tiles, dev.nE), dim3(256), 0, stream, e0, e1, 0, dev,
                                   (const double *)partial, nu, ld_nuis, qf.x_rows(ws), cmat, use_add ? addend : nullptr,

@@ -45,7 +45,8 @@ if __name__ == "__main__":
             like.loglike_batch(th, nu, out, ws)
         torch.cuda.synchronize()
         N.profile_enable(False)
-        for k in ("cmbl_bk_prologue", "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_hl_kernel", "cmbl_quadform"):
+        for k in ("cmbl_bk_prologue", "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_gauss_small_kernel",
+                  "cmbl_hl_kernel", "cmbl_quadform"):
             t, n = N.profile_read(k)
             if n:
                 print(f"{k:22s} {t / n * 1e3:9.2f} us")
