@@ -204,9 +204,8 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
     // per-walker constants of the thread's rows
     double calsq[PER];
     double dust[FG ? PER : 1], sync[FG ? PER : 1], dsync[FG ? PER : 1], ddf[FG ? PER : 1], dsf[FG ? PER : 1],
-        nui[FG ? PER : 1], nuj[FG ? PER : 1];
-    bool dd_l = false, ds_l = false;
-    double Delta_dust = 1, Delta_sync = 1;
+        nui[FG ? PER : 1], nuj[FG ? PER : 1], Ddust[FG ? PER : 1], Dsync[FG ? PER : 1];
+    bool dd_l = false, ds_l = false;     // l-dependent decorrelation (lform lin / quad) in use
 #pragma unroll
     for (int u = 0; u < PER; u++) {
         const int w = min(w0 + rbase + 8 * u, W - 1);
@@ -215,7 +214,7 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
         calsq[u] = cl * cl;
         if constexpr (FG) {
             dust[u] = sync[u] = dsync[u] = nui[u] = nuj[u] = 0.0;
-            ddf[u] = dsf[u] = 1.0;
+            ddf[u] = dsf[u] = Ddust[u] = Dsync[u] = 1.0;
             if (fg) {                                         // :296-328
                 const double *cw = coef + (long long)w * 3 * c.nreq;
                 const int a = pr.mi, b = pr.mj;
@@ -230,17 +229,23 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
                 dust[u] = d;
                 sync[u] = sy;
                 dsync[u] = ds;
-                Delta_dust = P[10];
-                Delta_sync = P[11];
+                const double Delta_dust = P[10], Delta_sync = P[11];
+                Ddust[u] = Delta_dust;
+                Dsync[u] = Delta_sync;
                 nui[u] = c.bkmaps[a].nu_bar * cw[2 * c.nreq + a];
                 nuj[u] = c.bkmaps[b].nu_bar * cw[2 * c.nreq + b];
+                // need_dust_decorr .and. i /= j (:288-289, :312); flat l-scaling is one factor per pair
                 if (fabs(Delta_dust - 1) > 1e-5 && a != b) {
                     if (c.lform_dust == 0) ddf[u] = bk_decorr(Delta_dust, nui[u], nuj[u], c.decorr_dust, 0, 0);
                     else dd_l = true;
+                } else {
+                    Ddust[u] = 1.0;   // marks "no decorrelation" for this walker
                 }
                 if (fabs(Delta_sync - 1) > 1e-5 && a != b) {
                     if (c.lform_sync == 0) dsf[u] = bk_decorr(Delta_sync, nui[u], nuj[u], c.decorr_sync, 0, 0);
                     else ds_l = true;
+                } else {
+                    Dsync[u] = 1.0;
                 }
             }
         }
@@ -296,10 +301,12 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
                     if constexpr (FG) {
                         if (fg) {                             // :329-334
                             const double *pw = prof + (long long)w * 3 * L + (l - c.lmin);
-                            const double Dd = dd_l ? bk_decorr(Delta_dust, nui[u], nuj[u], c.decorr_dust, l, c.lform_dust)
-                                                   : ddf[u];
-                            const double Ds = ds_l ? bk_decorr(Delta_sync, nui[u], nuj[u], c.decorr_sync, l, c.lform_sync)
-                                                   : dsf[u];
+                            const double Dd = (dd_l && Ddust[u] != 1.0)
+                                                  ? bk_decorr(Ddust[u], nui[u], nuj[u], c.decorr_dust, l, c.lform_dust)
+                                                  : ddf[u];
+                            const double Ds = (ds_l && Dsync[u] != 1.0)
+                                                  ? bk_decorr(Dsync[u], nui[u], nuj[u], c.decorr_sync, l, c.lform_sync)
+                                                  : dsf[u];
                             v = v + dust[u] * pw[0] * Dd + sync[u] * pw[L] * Ds + dsync[u] * pw[2 * L];
                         }
                     }
