@@ -412,48 +412,68 @@ __global__ __launch_bounds__(256) void cmbl_reduce_kernel(CLDev c, const double 
 // Small gaussian likelihoods (nX <= 64, e.g. lensing 9, SPT-SZ 47): binned
 // spectra, bigX = C - Chat and chi^2 = bigX^T C^-1 bigX in one kernel
 // (CMBlikes.f90:1183-1225; Matrix_QuadForm as row sums y = M x, then x.y).
-// 64 walkers per workgroup; wave v handles elements v, v+4, ... and rows of M.
+// Workgroup = 8 walkers x 32 thread groups.  The partial rows of every
+// element are cut into tasks of <= 8 rows (host); groups take tasks
+// round-robin with all loads of a task in flight, then combine them per
+// element in task order (deterministic), then split the rows of M.
 static constexpr int SMALL_NX = 64;
-__global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, const double *__restrict__ partial,
+static constexpr int SMALL_WT = 8;          // walkers per workgroup
+static constexpr int SMALL_MAXTASK = 256;   // tasks per dataset
+struct SmallTask { int first, count; };      // rows e_*_rows[first .. first+count)
+struct SmallDev {
+    int ntask;
+    const SmallTask *tasks;                  // main tasks then corr tasks, element order
+    const int *rows;                         // e_main_rows ++ e_corr_rows
+    const int *e_main_t, *e_corr_t;          // [nE+1] task ranges per element
+};
+
+__global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev sd, const double *__restrict__ partial,
                                                               const double *__restrict__ nuis, long long ld_nuis,
                                                               const double *__restrict__ M, double *__restrict__ out,
                                                               int W)
 {
-    __shared__ double xs[SMALL_NX][65];
-    __shared__ double red[4][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int w = blockIdx.x * 64 + lane;
+    __shared__ double tp[SMALL_MAXTASK][SMALL_WT];
+    __shared__ double xs[SMALL_NX][SMALL_WT];
+    __shared__ double red[32][SMALL_WT];
+    const int wl = threadIdx.x % SMALL_WT, g = threadIdx.x / SMALL_WT;
+    const int w = blockIdx.x * SMALL_WT + wl;
     const bool act = w < W;
-    auto rows_sum = [&](const int *off, const int *rows, int e) {
-        double v = 0.0;
-        const int q0 = off[e], q1 = off[e + 1];
-        for (int q = q0; q < q1; q += 8) {
-            double t[8];
+    for (int t = g; t < sd.ntask; t += 32) {
+        const SmallTask tk = sd.tasks[t];
+        double v[8];
 #pragma unroll
-            for (int u = 0; u < 8; u++) t[u] = (act && q + u < q1) ? partial[(long long)rows[q + u] * W + w] : 0.0;
+        for (int u = 0; u < 8; u++)
+            v[u] = (act && u < tk.count) ? partial[(long long)sd.rows[tk.first + u] * W + w] : 0.0;
+        double s = 0.0;
 #pragma unroll
-            for (int u = 0; u < 8; u++) v += t[u];
-        }
-        return v;
-    };
-    for (int e = wave; e < c.nE; e += 4) {
+        for (int u = 0; u < 8; u++) s += v[u];
+        tp[t][wl] = s;
+    }
+    __syncthreads();
+    for (int e = g; e < c.nE; e += 32) {
         const int ix = c.e_to_x[e];
         if (ix < 0) continue;
-        double s = c.e_main_const[e] + rows_sum(c.e_main_off, c.e_main_rows, e);
-        if (c.has_corr) s = s + ((c.e_corr_const[e] + rows_sum(c.e_corr_off, c.e_corr_rows, e)) - c.fidcorr[e]);
-        xs[ix][lane] = s - c.chat[e];
+        double s = c.e_main_const[e];
+        for (int t = sd.e_main_t[e]; t < sd.e_main_t[e + 1]; t++) s += tp[t][wl];
+        if (c.has_corr) {
+            double cs = c.e_corr_const[e];
+            for (int t = sd.e_corr_t[e]; t < sd.e_corr_t[e + 1]; t++) cs += tp[t][wl];
+            s = s + (cs - c.fidcorr[e]);
+        }
+        xs[ix][wl] = s - c.chat[e];
     }
     __syncthreads();
     double part = 0.0;
-    for (int i = wave; i < c.nX; i += 4) {
+    for (int i = g; i < c.nX; i += 32) {
         double y = 0.0;
-        for (int j = 0; j < c.nX; j++) y += M[i * c.nX + j] * xs[j][lane];
-        part += xs[i][lane] * y;
+        for (int j = 0; j < c.nX; j++) y += M[i * c.nX + j] * xs[j][wl];
+        part += xs[i][wl] * y;
     }
-    red[wave][lane] = part;
+    red[g][wl] = part;
     __syncthreads();
-    if (wave == 0 && act) {
-        double chisq = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    if (g == 0 && act) {
+        double chisq = 0.0;
+        for (int k = 0; k < 32; k++) chisq += red[k][wl];
         if (c.log_cal_prior > 0 && c.cal_index >= 0) {
             const double t = log(nuis[(long long)w * ld_nuis + c.cal_index]) / c.log_cal_prior;
             chisq = chisq + t * t;
@@ -724,7 +744,9 @@ struct CMBLikes final : Like {
         d_etox, d_fidcorr, d_noise, d_chat, d_cluse, d_bkmaps, d_bpnu, d_bpR, d_bpdnu, d_hlchat, d_hlcf;
     int max_field = 0, n_part_rows = 0;
     bool items_even = true, small_gauss = false;
-    DevBuf d_invcov;
+    int small_ntask = 0;
+    SmallDev sdev{};
+    DevBuf d_invcov, d_stasks, d_srows, d_smt, d_sct;
 
     std::string cl_name(const std::vector<std::string> &names, int i, int j) const {   // Cl_i_j_name (:328-343)
         return has_map_names ? names[i - 1] + "x" + names[j - 1] : names[i - 1] + names[j - 1];
@@ -1228,6 +1250,34 @@ struct CMBLikes final : Like {
         std::vector<double> main_cst, corr_cst;
         flatten(e_main, main_off, main_rows, main_cst);
         flatten(e_corr, corr_off, corr_rows, corr_cst);
+        {   // small-gaussian tasks: each element's rows in runs of <= 8 (main rows, then corr rows)
+            std::vector<SmallTask> tasks;
+            std::vector<int> rows_all(main_rows);
+            rows_all.insert(rows_all.end(), corr_rows.begin(), corr_rows.end());
+            std::vector<int> mt(nE + 1), ct(nE + 1);
+            for (int e = 0; e < nE; e++) {
+                mt[e] = (int)tasks.size();
+                for (int q = main_off[e]; q < main_off[e + 1]; q += 8)
+                    tasks.push_back({q, std::min(8, main_off[e + 1] - q)});
+            }
+            mt[nE] = (int)tasks.size();
+            const int base = (int)main_rows.size();
+            for (int e = 0; e < nE; e++) {
+                ct[e] = (int)tasks.size();
+                for (int q = corr_off[e]; q < corr_off[e + 1]; q += 8)
+                    tasks.push_back({base + q, std::min(8, corr_off[e + 1] - q)});
+            }
+            ct[nE] = (int)tasks.size();
+            small_ntask = (int)tasks.size();
+            auto up2 = [](DevBuf &d, const void *p, size_t bytes) {
+                d.alloc(std::max<size_t>(bytes, 16));
+                if (bytes) d.upload(p, bytes);
+            };
+            up2(d_stasks, tasks.data(), tasks.size() * sizeof(SmallTask));
+            up2(d_srows, rows_all.data(), rows_all.size() * 4);
+            up2(d_smt, mt.data(), mt.size() * 4);
+            up2(d_sct, ct.data(), ct.size() * 4);
+        }
         std::vector<int> e_to_x(nE, -1);
         for (int b = 0; b < nb; b++)
             for (int u = 0; u < ncl_used; u++) e_to_x[b * ncl + cl_use[u]] = b * ncl_used + u;
@@ -1262,7 +1312,12 @@ struct CMBLikes final : Like {
             up(d_bpdnu, bdnu.data(), bdnu.size() * 8);
         }
         qf.init(invcov, nX);
-        small_gauss = approx == 2 && nX <= SMALL_NX;
+        small_gauss = approx == 2 && nX <= SMALL_NX && small_ntask <= SMALL_MAXTASK;
+        sdev.ntask = small_ntask;
+        sdev.tasks = d_stasks.as<SmallTask>();
+        sdev.rows = d_srows.as<int>();
+        sdev.e_main_t = d_smt.as<int>();
+        sdev.e_corr_t = d_sct.as<int>();
         up(d_invcov, invcov.data(), invcov.size() * 8);
         dev.lmin = lmin;
         dev.lmax = lmax;
@@ -1373,8 +1428,9 @@ struct CMBLikes final : Like {
         HIP_CHECK(hipGetLastError());
         if (small_gauss) {
             timed_launch("cmbl_gauss_small_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                hipExtLaunchKernelGGL(cmbl_gauss_small_kernel, dim3(tiles), dim3(256), 0, stream, e0, e1, 0, dev,
-                                      (const double *)partial, nu, ld_nuis, d_invcov.as<double>(), out, W);
+                hipExtLaunchKernelGGL(cmbl_gauss_small_kernel, dim3((W + SMALL_WT - 1) / SMALL_WT), dim3(256), 0,
+                                      stream, e0, e1, 0, dev, sdev, (const double *)partial, nu, ld_nuis,
+                                      d_invcov.as<double>(), out, W);
             });
             HIP_CHECK(hipGetLastError());
             return;
