@@ -166,6 +166,28 @@ def cpu_baseline(seconds, lensing=True):
                 "sample": f"C restatement oracle/liboracle.so (plik_lite only), 1 thread, {seconds:g} s"}
 
 
+def lensing_window_bytes(refdir):
+    """Algorithmic bytes of one lensing window-contraction launch, split into
+    per-walker theory bytes (each field's D_l over the union of its windows'
+    nonzero l ranges, read once) and per-launch window bytes (nonzero weights,
+    read once): CMBlikes.f90:1230-1256 over the consext8 windows."""
+    base = os.path.join(refdir, LENS_DATASET.replace(".dataset", ""))
+    ranges = {}
+    wbytes = 0
+    for sub, fields in (("_window", ["PP"]), ("_lens_delta_window", ["TT", "EE", "TE", "PP"])):
+        for b in range(1, 10):
+            a = np.loadtxt(f"{base}{sub}/window{b}.dat", ndmin=2)
+            for k, f in enumerate(fields):
+                nz = np.nonzero(a[:, 1 + k])[0]
+                if len(nz):
+                    lo, hi = int(a[nz[0], 0]), int(a[nz[-1], 0])
+                    r = ranges.get(f, (lo, hi))
+                    ranges[f] = (min(r[0], lo), max(r[1], hi))
+                    wbytes += 8 * len(nz)
+    per_walker = 8 * sum(hi - lo + 1 for lo, hi in ranges.values())
+    return per_walker, wbytes
+
+
 def pmc_traffic(kernel, W):
     """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC pass
     (tools/gpu_pmc.sh -> tools/pmc_summary.py, FETCH_SIZE x2 + WRITE_SIZE per the
@@ -178,7 +200,8 @@ def pmc_traffic(kernel, W):
         return None, None
     if d.get("walkers") != W:
         return None, None
-    symbol = {"plik_quadform_ksplit": "quadform_ksplit"}.get(kernel, kernel)   # profiler label -> kernel
+    symbol = {"plik_quadform_ksplit": "quadform_ksplit",                    # profiler label -> kernel
+              "cmbl_window_kernel": "cmbl_window_kernel<false, false>"}.get(kernel, kernel)
     t = d["per_launch"].get(symbol)
     if not t:
         return None, None
@@ -201,6 +224,7 @@ def main():
     W = args.walkers
     with tempfile.TemporaryDirectory() as td:
         smp, likes, theory, _ = build_problem(W, rank, td, args.groups, lensing=not args.no_lensing)
+        lens_bytes = lensing_window_bytes(os.path.join(td, "refdata")) if not args.no_lensing else (0, 0)
 
         def barrier():
             if world > 1:
@@ -242,7 +266,11 @@ def main():
         roof = {"kernel": dom, "bound": "mfma", "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / PEAK_FP64_TFLOPS, "traffic": None}
     else:
-        ach = W * BYTES_BIN / (avg_ms[dom] * 1e-3) / 1e9 if dom == "plik_bin_delta" else None
+        ach = None
+        if dom == "plik_bin_delta":
+            ach = W * BYTES_BIN / (avg_ms[dom] * 1e-3) / 1e9
+        elif dom == "cmbl_window_kernel":
+            ach = (W * lens_bytes[0] + lens_bytes[1]) / (avg_ms[dom] * 1e-3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": (ach / PEAK_HBM_GBS) if ach else None, "traffic": None}
     roof["avg_kernel_us"] = {k: (v * 1e3 if v else None) for k, v in avg_ms.items()}
