@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=1.5, help="per-process CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-lensing", action="store_true", help="plik_lite only (configs[2] minus lensing)")
+    p.add_argument("--converge-seconds", type=float, default=20.0,
+                   help="R-1 vs wall-clock run after the throughput timing (0 = skip)")
     return p.parse_args()
 
 
@@ -110,6 +112,61 @@ def build_problem(W, rank, tmpdir, groups=1, lensing=True):
         smp.add_likelihood(lk, theory)
     smp.set_start(np.tile(P0, (W, 1)))
     return smp, likes, theory, names
+
+
+def convergence_run(W, rank, world, tmpdir, seconds, lensing=True):
+    """R-1 vs wall-clock (the metric's second half): every walker samples the
+    same posterior -- one shared cached slow point (theory stride 0), calPlanck
+    fast, plik_lite (+ lensing) + the calPlanck prior -- from an overdispersed
+    start; every MPI_Sample_update_freq samples the GPUs exchange chain moments
+    (ConvergenceExchange: all_reduce over RCCL) and learn the proposal,
+    until R-1 < 0.01 twice in a row (SampleCollector.f90:289-299) or time out."""
+    import torch
+    from cosmomc_amd import synthetic as syn
+    from cosmomc_amd.converge import CollectorSettings, ConvergenceExchange, reference_window
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    likes = [NativeCMBLikelihood("PLIK_LITE", syn.make_plik_lite(12345).write(tmpdir))]
+    if lensing:
+        likes.append(NativeCMBLikelihood("lensing", os.path.join(extract_refdata(tmpdir), LENS_DATASET)))
+    for lk in likes:
+        lk.nuisance_indices = [7]
+    P0 = np.array([0.02237, 0.1200, 1.04092, 0.0544, 3.044, 0.9649, 1.0])
+    pmin, pmax = P0.copy(), P0.copy()
+    pmin[6], pmax[6] = 0.9, 1.1
+    pm, ps = np.zeros(7), np.zeros(7)
+    pm[6], ps[6] = 1.0, 0.0025
+    steps_block = 40                                   # MPI_Sample_update_freq x num_params_used (1)
+    cap = 20000
+    smp = BatchedMCMC(W, 7, [7], [[1]], 0, pmin, pmax, pm, ps, propose_scale=2.4, seed_ij=2002 + rank,
+                      seed_kl=9373, first_walker=rank * W)
+    smp.set_covariance(np.array([[0.0025 ** 2]]))
+    th = torch.tensor(syn.walker_theory(1, n_fields=10 if lensing else 3, ld_field=2512), device="cuda")
+    th = th.expand(W, th.shape[1], th.shape[2])       # ld_walker = 0: one slow point for everyone
+    for lk in likes:
+        smp.add_likelihood(lk, th)
+    start = np.tile(P0, (W, 1))
+    start[:, 6] = 1.0 + 0.01 * syn.gaussians(77 + rank, W)
+    smp.set_start(start)
+    smp.enable_history(cap)
+    ex = ConvergenceExchange(1, CollectorSettings(MPI_R_Stop=0.01, MPI_Min_Sample_Update=55))
+    trace, t0, done_at = [], time.perf_counter(), None
+    while smp.history_count() + steps_block <= cap:
+        smp.step(steps_block, fast_only=True)
+        r = ex.update_cov_and_check_converge(smp, *reference_window(smp.history_count()))
+        el = time.perf_counter() - t0
+        trace.append([round(el, 4), smp.history_count(), r.R])
+        if r.update_proposal:
+            smp.set_covariance(r.propose_cov)
+        if r.converged:
+            done_at = el
+            break
+        if el > seconds:
+            break
+    return {"workload": "plik_lite_TTTEEE" + (" + lensing" if lensing else "") + " on one shared slow point, "
+                        "calPlanck fast, overdispersed start (1 +- 0.01)",
+            "walkers_total": W * world, "target_r_minus_1": 0.01, "exchange_every_steps": steps_block,
+            "converged_wall_s": done_at, "trace_wall_s_steps_R": trace}
 
 
 def cpu_baseline(seconds, lensing=True):
@@ -258,6 +315,9 @@ def main():
         kern = {k: v for k, v in kern.items() if v[1]}
         _, _, _, nacc = smp.state()
         acc_rate = float(nacc.sum()) / (W * (args.warmup + 2 * args.steps))
+        conv = None
+        if args.converge_seconds > 0:
+            conv = convergence_run(W, rank, world, td, args.converge_seconds, lensing=not args.no_lensing)
 
     dom = max(kern, key=lambda k: kern[k][0])
     avg_ms = {k: (v[0] / v[1] if v[1] else None) for k, v in kern.items()}
@@ -294,6 +354,8 @@ def main():
                        "accept_rate": acc_rate},
             "roofline": roof,
         }
+        if conv is not None:
+            out["convergence"] = conv
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, lensing=not args.no_lensing)
         print(json.dumps(out), flush=True)

@@ -1384,7 +1384,7 @@ struct CMBLikes final : Like {
         if (W <= 0) return;
         if (n_nuis > 0 && !nuis) fail(CMBL_ERR_ARG, "%s needs its %d nuisance parameters", name.c_str(), n_nuis);
         if (ld_field < lmax + 1) fail(CMBL_ERR_ARG, "ld_field %lld < cl_lmax+1 = %d", ld_field, lmax + 1);
-        if (W > 1 && ld_walker < (long long)(max_field + 1) * ld_field)
+        if (W > 1 && ld_walker != 0 && ld_walker < (long long)(max_field + 1) * ld_field)
             fail(CMBL_ERR_ARG, "ld_walker must cover theory fields 0..%d", max_field);
         if (!ws) {
             own_ws.grow(workspace_size(W));

@@ -315,7 +315,8 @@ struct PlikLite final : Like {
         if (W <= 0) return;
         if (n_nuis < 1 || !nuis) fail(CMBL_ERR_ARG, "plik_lite needs the calibration nuisance parameter");
         if (ld_field < lmax_needed + 1) fail(CMBL_ERR_ARG, "ld_field %lld < lmax+1 = %d", ld_field, lmax_needed + 1);
-        if (ld_walker < 3 * ld_field) fail(CMBL_ERR_ARG, "ld_walker must cover the TT, TE, EE fields");
+        // ld_walker == 0: every walker reads the same theory (a shared slow point)
+        if (ld_walker != 0 && ld_walker < 3 * ld_field) fail(CMBL_ERR_ARG, "ld_walker must cover the TT, TE, EE fields");
         if (!ws) {
             own_ws.grow(workspace_size(W));
             ws = own_ws.p;

@@ -49,7 +49,11 @@ enum {
 
 typedef struct cmbl cmbl_t;
 
-/* tag: "PLIK_LITE" (native plik_lite); other tags return CMBL_ERR_UNSUPPORTED.
+/* tag -> likelihood class as CMBLikelihood_Add (source/CMB.f90:80-97):
+ * "PLIK_LITE" native plik_lite (CMB.f90:30-329), "BKPLANCK" CMBlikes with the
+ * BICEP/Keck/Planck foregrounds (CMB_BK_Planck.f90), "WMAP" / "SPTPOL_TEEE" /
+ * "SPTPOL_BB" / "SMICA" CMBL_ERR_UNSUPPORTED, any other tag a CMBlikes
+ * dataset (CMBlikes.f90; like_approx HL or gaussian, binned).
  * override_ini: "key = value" lines applied over the dataset file, as
  * cmb_dataset[TAG,key] = value (source/CMB.f90:71-74); may be NULL. */
 int  cmbl_open(const char *tag, const char *dataset_path, const char *override_ini,
@@ -68,7 +72,8 @@ int  cmbl_info(const cmbl_t *h, int *n_nuis, int *cl_lmax, int *speed,
 size_t cmbl_workspace_size(const cmbl_t *h, int W);
 
 /* -lnL for W walkers (device pointers, asynchronous on `stream`):
- *   dl    [W] x [10 fields] x [l]  (strides ld_walker, ld_field, 1)
+ *   dl    [W] x [10 fields] x [l]  (strides ld_walker, ld_field, 1);
+ *         ld_walker = 0 gives every walker the same theory (one slow point)
  *   nuis  [W] x n_nuis (stride ld_nuis)   -- DataParams of each walker
  *   out   [W]
  * workspace: cmbl_workspace_size(h, W) bytes of device memory, or NULL to use
