@@ -606,6 +606,75 @@ int orc_mh_step(orc_proposer_t *prop, orc_rng_t *r, const orc_target_t *t,
     return acc;
 }
 
+int orc_drag_step(orc_proposer_t *prop, orc_rng_t *r, const orc_target_t *t, orc_drag_state_t *st,
+                  double *P, double *cur_like)
+{   /* TFastDraggingSampler_GetNewSample, MCMC.f90:338-452 */
+    const int np = t->num_params;
+    double tend[256], tstart[256], cend[256], cstart[256], delta[256];
+    if (*cur_like == ORC_LOGZERO || orc_proposer_fast_n(prop) == 0 || orc_proposer_slow_n(prop) == 0) {
+        double tl;                                            /* :351-354 */
+        int acc = orc_mh_step(prop, r, t, P, cur_like, 0, &tl);
+        st->mult = acc ? 1.0 : st->mult + 1.0;
+        return acc;
+    }
+    st->num_drag++;
+    if (st->num_drag % st->oversample_fast != 0) {            /* :357-361 FastParameterSample */
+        double tl;
+        int acc = orc_mh_step(prop, r, t, P, cur_like, 1, &tl);
+        st->mult = acc ? 1.0 : st->mult + 1.0;
+        return acc;
+    }
+    memcpy(tend, P, sizeof(double) * (size_t)np);
+    orc_proposer_get_proposal_slow(prop, r, tend);            /* :367-368 */
+    double cend_like = orc_target_loglike(t, tend);
+    if (cend_like == ORC_LOGZERO) {                           /* :370-374 */
+        st->mult += 1.0;
+        return 0;
+    }
+    double cstart_like = *cur_like;
+    double sum_e = cend_like, sum_s = cstart_like;
+    memcpy(cstart, P, sizeof(double) * (size_t)np);
+    memcpy(cend, tend, sizeof(double) * (size_t)np);
+    const int nfast = orc_proposer_fast_n(prop);
+    int interp = (int)lround(st->dragging_steps * nfast) + 1;   /* :386, nint */
+    if (interp < 2) interp = 2;
+    for (int is = 1; is <= interp - 1; is++) {
+        orc_proposer_get_proposal_fast_delta(prop, r, delta, np);
+        for (int i = 0; i < np; i++) tend[i] = cend[i] + delta[i];
+        double elike = orc_target_loglike(t, tend), slike = 0.0;
+        int acc = elike != ORC_LOGZERO;
+        if (acc) {
+            for (int i = 0; i < np; i++) tstart[i] = cstart[i] + delta[i];
+            slike = orc_target_loglike(t, tstart);
+            acc = slike != ORC_LOGZERO;
+            if (acc) {
+                const double frac = (double)is / interp;
+                const double cint = cstart_like * (1 - frac) + frac * cend_like;
+                const double ilike = slike * (1 - frac) + frac * elike;
+                acc = orc_metropolis_accept(r, ilike, cint);
+            }
+        }
+        if (acc) {
+            memcpy(cend, tend, sizeof(double) * (size_t)np);
+            memcpy(cstart, tstart, sizeof(double) * (size_t)np);
+            cend_like = elike;
+            cstart_like = slike;
+        }
+        sum_s = sum_s + cstart_like;
+        sum_e = sum_e + cend_like;
+    }
+    const double cur_drag = sum_s / interp, drag = sum_e / interp;
+    int acc = orc_metropolis_accept(r, drag, cur_drag);       /* :436 */
+    if (acc) {
+        memcpy(P, cend, sizeof(double) * (size_t)np);
+        *cur_like = cend_like;
+        st->mult = 1.0;
+    } else {
+        st->mult += 1.0;
+    }
+    return acc;
+}
+
 /* ======================= samples.f90 ======================= */
 
 static void jacobi_eigenvalues(double *A, int n, double *ev)

@@ -96,6 +96,15 @@ int    orc_metropolis_accept(orc_rng_t *r, double like, double cur_like); /* MCM
 int orc_mh_step(orc_proposer_t *prop, orc_rng_t *r, const orc_target_t *t,
                 double *P, double *cur_like, int fast_only, double *trial_like_out);
 
+/* TFastDraggingSampler_GetNewSample (MCMC.f90:338-452): num_drag / mult are
+ * the sampler's counters (in/out); dragging_steps as settings.f90:82 (3).
+ * Every oversample_fast-th call drags (slow proposal + interp_steps-1
+ * fast-delta steps on the start/end interpolated likelihood), the others
+ * are FastParameterSample.  Returns 1 if the move was accepted. */
+typedef struct { int num_drag; double mult; double dragging_steps; int oversample_fast; } orc_drag_state_t;
+int orc_drag_step(orc_proposer_t *prop, orc_rng_t *r, const orc_target_t *t, orc_drag_state_t *st,
+                  double *P, double *cur_like);
+
 /* ---------------- samples.f90 GelmanRubinEvalues ---------------- */
 /* samples.f90:41-67 restated: cov = mean of per-chain covs, meanscov = cov of
  * the chain means (normalisations as SampleCollector.f90:257-274 pass them);

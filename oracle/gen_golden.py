@@ -100,6 +100,10 @@ CHAIN_CASES = [
     ("gauss6_fast_only", 6, [[1, 2], [3, 4, 5], [6]], 1, 1, 1.9, 1, 400),
     # 1-D block of calPlanck-like width (sign flip RotMatrix branch, n=1)
     ("gauss3_n1_blocks", 3, [[1], [2], [3]], 1, 3, 2.4, 0, 300),
+    # fast dragging (TFastDraggingSampler, fast_only = 2): slow 2 + fast 3 + fast 1, drag every 2nd step
+    ("gauss6_drag", 6, [[1, 2], [3, 4, 5], [6]], 1, 2, 2.4, 2, 240),
+    # dragging every step (oversample_fast 1), one fast parameter (interp_steps 4)
+    ("gauss4_drag_every_step", 4, [[1, 2, 3], [4]], 1, 1, 2.0, 2, 200),
 ]
 
 

@@ -24,6 +24,11 @@ class Rng(C.Structure):
                 ("i97", C.c_int), ("j97", C.c_int), ("iset", C.c_int), ("gset", C.c_double)]
 
 
+class DragState(C.Structure):
+    _fields_ = [("num_drag", C.c_int), ("mult", C.c_double), ("dragging_steps", C.c_double),
+                ("oversample_fast", C.c_int)]
+
+
 class Target(C.Structure):
     _fields_ = [("num_params", C.c_int), ("pmin", C.c_void_p), ("pmax", C.c_void_p),
                 ("prior_mean", C.c_void_p), ("prior_std", C.c_void_p), ("temperature", C.c_double),
@@ -73,6 +78,9 @@ def lib():
         L.orc_mh_step.argtypes = [C.c_void_p, C.POINTER(Rng), C.POINTER(Target), _dp, C.POINTER(C.c_double),
                                   C.c_int, C.POINTER(C.c_double)]
         L.orc_mh_step.restype = C.c_int
+        L.orc_drag_step.argtypes = [C.c_void_p, C.POINTER(Rng), C.POINTER(Target), C.POINTER(DragState), _dp,
+                                    C.POINTER(C.c_double)]
+        L.orc_drag_step.restype = C.c_int
         L.orc_gelman_rubin.argtypes = [_dp, _dp, C.c_int]
         L.orc_gelman_rubin.restype = C.c_double
         _LIB = L

@@ -8,7 +8,10 @@
 !   mode "stream" : ranmar / Gaussian1 / randexp1 / RandIndices / RandRotationD
 !   mode "gr"     : GelmanRubinEvalues (samples.f90:41-67) on a given
 !                   (mean-of-covariances, covariance-of-means) pair
-!   mode "chain"  : BlockedProposer + Metropolis chain on the test_likelihood
+!   mode "chain"  : (fast_only = 2: TFastDraggingSampler_GetNewSample,
+!                   MCMC.f90:338-452, restated inline on the reference's
+!                   BlockedProposer GetProposalSlow / GetProposalFastDelta)
+!                   BlockedProposer + Metropolis chain on the test_likelihood
 !                   Gaussian (calclike.f90:180-199) with hard bounds
 !                   (calclike.f90:97-109) and Gaussian priors (:111-134).
 !                   The three-line MetropolisAccept of MCMC.f90:119-131 and the
@@ -37,6 +40,9 @@ program rng_harness
     logical :: accpt
     real :: e
     real(mcp), allocatable :: mcov(:,:), evals(:)
+    real(mcp), allocatable :: cend(:), cstart(:), tend(:), tstart(:), delta(:)
+    real(mcp) :: cendlike, cstartlike, elike, slike, sum_s, sum_e, frac, cintlike, intlike, mult
+    integer :: num_drag, num_fast, interp, istep
 
     call get_command_argument(1, mode)
     call get_command_argument(2, cfg)
@@ -121,9 +127,80 @@ program rng_harness
         call Prop%SetCovariance(cov)
         curlike = target(P)
         write(u_out, '(ES25.17)') curlike
+        num_fast = 0
+        do k = slow_block_max + 1, nblocks
+            num_fast = num_fast + bsize(k)
+        end do
+        allocate(cend(n), cstart(n), tend(n), tstart(n), delta(n))
+        num_drag = 0
+        mult = 1
         do k = 1, nsteps
+            if (fast_only == 2) then
+                num_drag = num_drag + 1
+                if (mod(num_drag, oversample) == 0) then
+                    ! --- TFastDraggingSampler_GetNewSample drag branch (MCMC.f90:364-452)
+                    tend = P
+                    call Prop%GetProposalSlow(tend)
+                    cendlike = target(tend)
+                    if (cendlike == LogZero) then
+                        mult = mult + 1
+                        write(u_out, '(I2,*(ES25.17))') 0, cendlike, curlike, P
+                        cycle
+                    end if
+                    cstartlike = curlike
+                    sum_e = cendlike
+                    sum_s = cstartlike
+                    cstart = P
+                    cend = tend
+                    interp = max(2, nint(dragging_steps * num_fast) + 1)
+                    do istep = 1, interp - 1
+                        call Prop%GetProposalFastDelta(delta)
+                        tend = cend
+                        tend(1:n) = tend(1:n) + delta
+                        elike = target(tend)
+                        accpt = elike /= LogZero
+                        if (accpt) then
+                            tstart = cstart
+                            tstart(1:n) = tstart(1:n) + delta
+                            slike = target(tstart)
+                            accpt = slike /= LogZero
+                            if (accpt) then
+                                frac = real(istep, mcp)/interp
+                                cintlike = cstartlike*(1-frac) + frac*cendlike
+                                intlike = slike*(1-frac) + frac*elike
+                                accpt = cintlike > intlike                 ! MetropolisAccept :119-131
+                                if (.not. accpt) accpt = randexp1() > intlike - cintlike
+                            end if
+                        end if
+                        if (accpt) then
+                            cend = tend
+                            cstart = tstart
+                            cendlike = elike
+                            cstartlike = slike
+                        end if
+                        sum_s = sum_s + cstartlike
+                        sum_e = sum_e + cendlike
+                    end do
+                    like = sum_e/interp                     ! DragLike
+                    if (like /= LogZero) then
+                        accpt = sum_s/interp > like
+                        if (.not. accpt) accpt = randexp1() > like - sum_s/interp
+                    else
+                        accpt = .false.
+                    end if
+                    if (accpt) then
+                        P = cend
+                        curlike = cendlike
+                        mult = 1
+                    else
+                        mult = mult + 1
+                    end if
+                    write(u_out, '(I2,*(ES25.17))') merge(1, 0, accpt), like, curlike, P
+                    cycle
+                end if
+            end if
             trial = P
-            if (fast_only == 1) then
+            if (fast_only >= 1) then
                 call Prop%GetProposalFast(trial)
             else
                 call Prop%GetProposal(trial)

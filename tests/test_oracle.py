@@ -109,3 +109,22 @@ def test_gelman_rubin_identity():
     assert po.lib().orc_gelman_rubin(cov, np.zeros((n, n)), n) == pytest.approx(0.0, abs=1e-15)
     # between-chain covariance equal to within -> largest eigenvalue 1
     assert po.lib().orc_gelman_rubin(cov, cov.copy(), n) == pytest.approx(1.0, rel=1e-12)
+
+
+@pytest.mark.parametrize("name", ["gauss6_drag", "gauss4_drag_every_step"])
+def test_oracle_dragging_vs_reference(rng_golden, name):
+    """TFastDraggingSampler_GetNewSample (MCMC.f90:338-452) step by step."""
+    import ctypes as C
+    ch = rng_golden["chains"][name]
+    t, keep = _target(ch)
+    h = make_oracle_proposer(ch)
+    r = po.Ranmar(ch["ij"], ch["kl"])
+    P = np.array(ch["P0"], dtype=np.float64)
+    cur = C.c_double(po.lib().orc_target_loglike(C.byref(t), P))
+    st = po.DragState(0, 1.0, 3.0, ch["oversample_fast"])
+    for k in range(ch["steps"]):
+        acc = po.lib().orc_drag_step(h, C.byref(r.s), C.byref(t), C.byref(st), P, C.byref(cur))
+        assert acc == ch["accept"][k], f"accept mismatch at step {k}"
+        assert cur.value == pytest.approx(ch["cur_like"][k], rel=1e-10, abs=1e-12)
+        np.testing.assert_allclose(P, ch["P"][k], rtol=1e-11, atol=1e-12)
+    po.lib().orc_proposer_free(h)
