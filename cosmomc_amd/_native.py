@@ -42,6 +42,18 @@ class CmbsConfig(C.Structure):
 
 _lib = None
 
+# cmbs_theory_fn: int (*)(void *user, int W, const double *P_end, long long ld, void *stream)
+THEORY_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_longlong, C.c_void_p)
+
+
+class DeviceRows:
+    """__cuda_array_interface__ view of device rows [n][ld] (walker-minor), for
+    torch.as_tensor without a copy."""
+
+    def __init__(self, ptr, n, W, ld):
+        self.__cuda_array_interface__ = {"shape": (n, W), "typestr": "<f8", "data": (ptr, True),
+                                         "strides": (ld * 8, 8), "version": 2}
+
 
 def build(force: bool = False) -> str:
     """Compile the HIP library in-tree (hipcc --offload-arch=gfx950)."""
@@ -81,6 +93,8 @@ def lib():
         L.cmbs_set_start.argtypes = [vp, vp, vp]
         L.cmbs_step.argtypes = [vp, i, i, vp]
         L.cmbs_set_groups.argtypes = [vp, i]
+        L.cmbs_set_drag_theory.argtypes = [vp, i, vp, ll, ll]
+        L.cmbs_step_drag.argtypes = [vp, i, d, THEORY_FN, vp, vp]
         L.cmbs_chain_moments.argtypes = [vp, i, i, vp, vp, vp]
         L.cmbs_enable_history.argtypes = [vp, i]
         L.cmbs_history_stats.argtypes = [vp, i, i, vp, vp, vp]

@@ -234,6 +234,20 @@ int cmbs_chain_moments(cmbs_t *s, int first, int last, const double *gmean, doub
                    [&] { cmamd::sampler_chain_moments(s, first, last, gmean, out, (hipStream_t)stream); });
 }
 
+int cmbs_set_drag_theory(cmbs_t *s, int like_index, double *dl_end, long long ld_field, long long ld_walker) {
+    if (!s || !dl_end) return CMBL_ERR_ARG;
+    return guarded(&s->last_error,
+                   [&] { cmamd::sampler_set_drag_theory(s, like_index, dl_end, ld_field, ld_walker); });
+}
+
+int cmbs_step_drag(cmbs_t *s, int n_steps, double dragging_steps, cmbs_theory_fn theory_fn, void *user,
+                   void *stream) {
+    if (!s) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] {
+        cmamd::sampler_step_drag(s, n_steps, dragging_steps, theory_fn, user, (hipStream_t)stream);
+    });
+}
+
 int cmbs_set_groups(cmbs_t *s, int n_groups) {
     if (!s) return CMBL_ERR_ARG;
     return guarded(&s->last_error, [&] { cmamd::sampler_set_groups(s, n_groups); });

@@ -90,6 +90,12 @@ struct cmbs {
     hipStream_t streams[cmamd::MAXGROUPS] = {};
     hipEvent_t events[cmamd::MAXGROUPS + 1] = {};
     cmamd::DevBuf ws_g[cmamd::MAXGROUPS];
+    // fast dragging (cmbs_step_drag): scratch rows, second likelihood set, end-point theories
+    cmamd::DevBuf drag_dd, drag_di, like_terms2;
+    cmamd::DevBuf nuis_bufs2[cmamd::MAXLIKE];
+    struct EndTheory { double *dl = nullptr; long long ld_field = 0, ld_walker = 0; };
+    EndTheory end_theory[cmamd::MAXLIKE];
+    long long num_drag = 0;
     ~cmbs() {
         for (auto &st : streams)
             if (st) (void)hipStreamDestroy(st);
@@ -101,4 +107,6 @@ struct cmbs {
 namespace cmamd {
 void sampler_set_groups(cmbs *s, int n_groups);
 void sampler_chain_moments(cmbs *s, int first, int last, const double *gmean, double *out, hipStream_t stream);
+void sampler_set_drag_theory(cmbs *s, int like_index, double *dl_end, long long ld_field, long long ld_walker);
+void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_fn fn, void *user, hipStream_t stream);
 }

@@ -464,6 +464,187 @@ __global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double 
 #undef SROW
 }
 
+// ---------------------------------------------------------------- fast dragging
+// TFastDraggingSampler_GetNewSample (MCMC.f90:338-452) in four launch stages,
+// one thread per walker on the walker state in HBM (the drag scratch lives in
+// separate rows, DragCfg::dd / di, so the Metropolis kernel's LDS image is
+// unchanged).  Between stages the host evaluates the likelihoods:
+//   set 1 at the trial-end rows T on the END slow point's theory,
+//   set 2 at the trial-start rows T2 on the walker's current theory.
+//   stage 0  TrialEnd = Cur + GetProposalSlow                        (:367-368)
+//   stage 1  CurEndLike; abort on logZero (:370-374); first delta    (:386-394)
+//   stage 2  interpolated Metropolis on (start, end) likes, sums; next delta,
+//            or (last step) the drag accept + MoveDone                (:395-452)
+// dst: 0 idle, 1 dragging, 2 aborted, 3 skipped (CurLike == logZero),
+//      4 accepted (the walker's theory must become the end theory)
+struct DragCfg {
+    double *dd;      // [3 np + 4 + max_blk][ld]: CE, CS, T2, (cel, csl, ss, se), vec scratch
+    int *di;         // [1 + all_n][ld]: dst, RandIndices scratch
+    int interp, istep;
+    const double *like_terms2;            // [n_like][ld] at T2
+    double *like_nuis2[MAXLIKE];          // [W][nn] DataParams at T2
+};
+
+template <int STAGE>
+__global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *hist_row)
+{
+    const int w = blockIdx.x * 64 + threadIdx.x;
+    if (w >= c.W) return;
+    const size_t ld = c.ld;
+    const Rows &R = c.rows;
+    const int np = c.np;
+    auto drow = [&](double *b, int r) { return Col<double>{b + (size_t)r * ld + w, (int)ld}; };
+    auto irow = [&](int *b, int r) { return Col<int>{b + (size_t)r * ld + w, (int)ld}; };
+    const Tabs t = make_tabs(c, c.tab_i, c.tab_d);
+    Walker k;
+    k.r.u = drow(c.sd, R.U);
+    k.r.c = c.sd[(size_t)R.C * ld + w];
+    k.r.gset = c.sd[(size_t)R.G * ld + w];
+    k.r.i97 = c.si[(size_t)R.I97 * ld + w];
+    k.r.j97 = c.si[(size_t)R.J97 * ld + w];
+    k.r.iset = c.si[(size_t)R.ISET * ld + w];
+    k.R = drow(c.sd, R.R);
+    k.P = drow(c.sd, R.P);
+    k.trial = drow(c.sd, R.T);
+    k.vec = drow(g.dd, 3 * np + 4);
+    k.cyc = irow(c.si, R.CYC);
+    k.cyclp = irow(c.si, R.CYCLP);
+    k.blklp = irow(c.si, R.BLKLP);
+    k.itmp = irow(g.di, 1);
+    k.fast_ix = c.si[(size_t)R.FASTIX * ld + w];
+    const Col<double> T = k.trial, CE = drow(g.dd, 0), CS = drow(g.dd, np), T2 = drow(g.dd, 2 * np);
+    double &cur = c.sd[(size_t)R.L * ld + w];
+    double &mult = c.sd[(size_t)R.M * ld + w];
+    int &nacc = c.si[(size_t)R.NACC * ld + w];
+    double &cel = g.dd[(size_t)(3 * np + 0) * ld + w];
+    double &csl = g.dd[(size_t)(3 * np + 1) * ld + w];
+    double &ss = g.dd[(size_t)(3 * np + 2) * ld + w];
+    double &se = g.dd[(size_t)(3 * np + 3) * ld + w];
+    int &dst = g.di[w];
+    const Col<double> lk1{const_cast<double *>(c.like_terms) + w, (int)ld};
+    const Col<double> lk2{const_cast<double *>(g.like_terms2) + w, (int)ld};
+
+    auto scatter = [&]() {            // DataParams of both trial points
+        for (int l = 0; l < c.n_like; l++)
+            for (int q = 0; q < c.like_nn[l]; q++) {
+                c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = T[c.like_nuis0[l] + q];
+                g.like_nuis2[l][(size_t)w * c.like_nn[l] + q] = T2[c.like_nuis0[l] + q];
+            }
+    };
+    auto next_delta = [&]() {         // GetProposalFastDelta (propose.f90:291-298) on both ends
+        Col<double> keep = k.trial;
+        for (int i = 0; i < np; i++) T2[i] = 0.0;
+        k.trial = T2;
+        proposal_fast(c, t, k);
+        k.trial = keep;
+        for (int i = 0; i < np; i++) {
+            const double d = T2[i];
+            T[i] = CE[i] + d;
+            T2[i] = CS[i] + d;
+        }
+    };
+    auto metropolis = [&](double like, double curl) {   // MCMC.f90:119-131
+        if (like == LOGZERO) return false;
+        bool a = curl > like;
+        if (!a) a = (double)randexp1(k.r) > like - curl;
+        return a;
+    };
+
+    if (STAGE == 0) {
+        if (cur == LOGZERO) {
+            dst = 3;
+        } else {
+            dst = 1;
+            for (int i = 0; i < np; i++) {
+                T[i] = k.P[i];
+                CS[i] = k.P[i];
+                T2[i] = k.P[i];
+            }
+            csl = cur;
+            proposal_slow(c, t, k);
+        }
+        scatter();
+    } else if (STAGE == 1) {
+        if (dst == 1) {
+            cel = target_like(c, t, T, lk1);
+            if (cel == LOGZERO) {
+                dst = 2;
+                mult += 1.0;
+            } else {
+                for (int i = 0; i < np; i++) CE[i] = T[i];
+                ss = csl;
+                se = cel;
+                next_delta();
+            }
+        }
+        scatter();
+    } else {
+        if (dst == 1) {
+            const double el = target_like(c, t, T, lk1);
+            bool acc = el != LOGZERO;
+            double sl = 0.0;
+            if (acc) {
+                sl = target_like(c, t, T2, lk2);
+                acc = sl != LOGZERO;
+                if (acc) {
+                    const double frac = (double)g.istep / g.interp;
+                    const double cint = csl * (1 - frac) + frac * cel;
+                    const double ilike = sl * (1 - frac) + frac * el;
+                    acc = metropolis(ilike, cint);
+                }
+            }
+            if (acc) {
+                for (int i = 0; i < np; i++) {
+                    CE[i] = T[i];
+                    CS[i] = T2[i];
+                }
+                cel = el;
+                csl = sl;
+            }
+            ss = ss + csl;
+            se = se + cel;
+            if (g.istep < g.interp - 1) {
+                next_delta();
+            } else {
+                const double cur_drag = ss / g.interp, drag = se / g.interp;
+                if (metropolis(drag, cur_drag)) {        // MoveDone :166-190 + :437-445
+                    if (mult > 0) nacc += 1;
+                    mult = 1.0;
+                    for (int i = 0; i < np; i++) k.P[i] = CE[i];
+                    cur = cel;
+                    dst = 4;
+                } else {
+                    mult += 1.0;
+                    dst = 0;
+                }
+            }
+        }
+        if (g.istep < g.interp - 1) {
+            scatter();
+        } else {
+            if (dst == 2 || dst == 3) dst = 0;
+            if (hist_row)
+                for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = k.P[t.params_used[i]];
+        }
+    }
+    c.sd[(size_t)R.C * ld + w] = k.r.c;
+    c.sd[(size_t)R.G * ld + w] = k.r.gset;
+    c.si[(size_t)R.I97 * ld + w] = k.r.i97;
+    c.si[(size_t)R.J97 * ld + w] = k.r.j97;
+    c.si[(size_t)R.ISET * ld + w] = k.r.iset;
+    c.si[(size_t)R.FASTIX * ld + w] = k.fast_ix;
+}
+
+// accepted drags: the end slow point's theory becomes the walker's theory
+__global__ void drag_swap_theory(const int *dst, int W, const double *src, long long src_ld, double *dstth,
+                                 long long dst_ld, long long n)
+{
+    const int w = blockIdx.y;
+    if (w >= W || dst[w] != 4) return;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        dstth[(long long)w * dst_ld + i] = src[(long long)w * src_ld + i];
+}
+
 // Starting point: -lnL of P = trial (likelihood terms already evaluated)
 __global__ void start_kernel(DevCfg c)
 {
@@ -929,6 +1110,122 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     for (int g = 0; g < G; g++) {
         HIP_CHECK(hipEventRecord(s->events[g], s->streams[g]));
         HIP_CHECK(hipStreamWaitEvent(stream, s->events[g], 0));
+    }
+}
+
+void sampler_set_drag_theory(cmbs *s, int like_index, double *dl_end, long long ld_field, long long ld_walker) {
+    if (like_index < 0 || like_index >= (int)s->likes.size()) fail(CMBL_ERR_ARG, "no likelihood %d", like_index);
+    auto &e = s->end_theory[like_index];
+    e.dl = dl_end;
+    e.ld_field = ld_field;
+    e.ld_walker = ld_walker;
+}
+
+// likelihood terms of set 1 (T rows, end theory) or set 2 (T2 rows, walker theory)
+static void eval_likes_drag(cmbs *s, int set, hipStream_t stream) {
+    for (size_t i = 0; i < s->likes.size(); i++) {
+        auto &l = s->likes[i];
+        const int nn = l.like->like->n_nuis;
+        const double *dl = l.dl;
+        long long ldf = l.ld_field, ldw = l.ld_walker;
+        double *nb = s->dc.like_nuis[i];
+        double *out = s->like_terms.as<double>() + i * (size_t)s->dc.ld;
+        if (set == 1) {
+            dl = s->end_theory[i].dl;
+            ldf = s->end_theory[i].ld_field;
+            ldw = s->end_theory[i].ld_walker;
+        } else {
+            nb = s->nuis_bufs2[i].as<double>();
+            out = s->like_terms2.as<double>() + i * (size_t)s->dc.ld;
+        }
+        l.like->like->loglike_batch(s->W, dl, ldf, ldw, nb, nn, out, s->ws.p, stream);
+    }
+}
+
+void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_fn fn, void *user,
+                       hipStream_t stream) {
+    if (!s->started) fail(CMBL_ERR_ARG, "cmbs_set_start must be called before cmbs_step_drag");
+    if (n_steps <= 0) return;
+    if (s->fast_n == 0 || s->slow_n == 0) {   // MCMC.f90:351-354: plain Metropolis
+        sampler_step(s, n_steps, 0, stream);
+        return;
+    }
+    const int nl = (int)s->likes.size();
+    for (int i = 0; i < nl; i++)
+        if (!s->end_theory[i].dl) fail(CMBL_ERR_ARG, "dragging needs an end-point theory buffer for likelihood %d", i);
+    if (nl > 0 && !fn) fail(CMBL_ERR_ARG, "dragging with data likelihoods needs a theory function");
+    const size_t ld = s->dc.ld;
+    const int np = s->np;
+    if (!s->drag_dd.p) {
+        s->drag_dd.alloc((size_t)(3 * np + 4 + s->dc.max_blk) * ld * 8);
+        s->drag_di.alloc((size_t)(1 + s->all_n) * ld * 4);
+        HIP_CHECK(hipMemset(s->drag_dd.p, 0, s->drag_dd.bytes));
+        HIP_CHECK(hipMemset(s->drag_di.p, 0, s->drag_di.bytes));
+        s->like_terms2.alloc(std::max<size_t>(1, s->likes.size()) * ld * 8);
+        HIP_CHECK(hipMemset(s->like_terms2.p, 0, s->like_terms2.bytes));
+        for (int i = 0; i < nl; i++)
+            s->nuis_bufs2[i].alloc((size_t)std::max(s->likes[i].like->like->n_nuis, 1) * s->W * 8);
+    }
+    DragCfg g{};
+    g.dd = s->drag_dd.as<double>();
+    g.di = s->drag_di.as<int>();
+    g.like_terms2 = s->like_terms2.as<double>();
+    for (int i = 0; i < nl; i++) g.like_nuis2[i] = s->nuis_bufs2[i].as<double>();
+    int interp = (int)std::lround(dragging_steps * s->fast_n) + 1;   // MCMC.f90:386
+    if (interp < 2) interp = 2;
+    g.interp = interp;
+    auto next_row = [&]() -> double * {
+        if (s->hist_cap == 0) return nullptr;
+        double *row = s->hist.as<double>() + (size_t)(s->hist_count % s->hist_cap) * s->n_used * s->W;
+        s->hist_count++;
+        return row;
+    };
+    const dim3 grid((s->W + 63) / 64), blk(64);
+    for (int step = 0; step < n_steps; step++) {
+        s->num_drag++;
+        if (s->num_drag % s->dc.oversample_fast != 0) {   // FastParameterSample (:357-361)
+            launch_mh(s, false, true, 1, nullptr, stream, 0, s->W);
+            eval_likes(s, stream, false, 0, s->W, s->ws.p);
+            launch_mh(s, true, false, 1, next_row(), stream, 0, s->W);
+            continue;
+        }
+        g.istep = 0;
+        timed_launch("drag_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            hipExtLaunchKernelGGL(drag_kernel<0>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, (double *)nullptr);
+        });
+        HIP_CHECK(hipGetLastError());
+        if (nl > 0) {
+            const double *Pend = s->dc.sd + (size_t)s->dc.rows.T * ld;
+            if (fn(user, s->W, Pend, (long long)ld, stream) != 0) fail(CMBL_ERR_ARG, "theory function failed");
+            eval_likes_drag(s, 1, stream);
+        }
+        timed_launch("drag_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            hipExtLaunchKernelGGL(drag_kernel<1>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, (double *)nullptr);
+        });
+        HIP_CHECK(hipGetLastError());
+        for (int is = 1; is <= interp - 1; is++) {
+            if (nl > 0) {
+                eval_likes_drag(s, 1, stream);
+                eval_likes_drag(s, 2, stream);
+            }
+            g.istep = is;
+            double *row = is == interp - 1 ? next_row() : nullptr;
+            timed_launch("drag_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+                hipExtLaunchKernelGGL(drag_kernel<2>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, row);
+            });
+            HIP_CHECK(hipGetLastError());
+        }
+        for (int i = 0; i < nl; i++) {               // accepted drags keep the end theory
+            const auto &e = s->end_theory[i];
+            const auto &l = s->likes[i];
+            const long long n = std::min(e.ld_walker, l.ld_walker) > 0 ? std::min(e.ld_walker, l.ld_walker)
+                                                                        : 10 * l.ld_field;
+            if (l.ld_walker == 0) fail(CMBL_ERR_ARG, "dragging needs per-walker theory rows (ld_walker > 0)");
+            hipLaunchKernelGGL(drag_swap_theory, dim3(16, s->W), dim3(256), 0, stream, g.di, s->W, e.dl,
+                               e.ld_walker, const_cast<double *>(l.dl), l.ld_walker, n);
+            HIP_CHECK(hipGetLastError());
+        }
+        HIP_CHECK(hipMemsetAsync(g.di, 0, (size_t)s->W * 4, stream));
     }
 }
 

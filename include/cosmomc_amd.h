@@ -161,6 +161,25 @@ int  cmbs_set_start(cmbs_t *s, const double *P0, void *stream);
  * Asynchronous on stream. */
 int  cmbs_step(cmbs_t *s, int n_steps, int fast_only, void *stream);
 
+/* Fast dragging, TFastDraggingSampler_GetNewSample (MCMC.f90:338-452;
+ * sampling_method = fast_dragging): n_steps GetNewSample calls for every
+ * walker; every oversample_fast-th call drags the fast parameters (Neal) along
+ * a slow proposal over interp_steps = max(2, nint(dragging_steps * num_fast) + 1)
+ * interpolation steps (dragging_steps 3 by default, settings.f90:82), the
+ * others are FastParameterSample.  Each drag needs the likelihoods at the
+ * proposed slow point: `theory_fn` is called once per drag (synchronously,
+ * after the slow proposal) with the device trial rows P_end [num_params][ld]
+ * (walker-minor) and must fill every likelihood's end-theory buffer
+ * registered with cmbs_set_drag_theory; it returns 0 on success.  Walkers
+ * whose drag is accepted get their end theory copied into their theory rows
+ * (the dl buffer passed to cmbs_add_likelihood).  With no likelihoods (the
+ * analytic test target) theory_fn may be NULL.  Walkers whose CurLike is
+ * logZero skip the drag (the reference makes a full Metropolis step there). */
+typedef int (*cmbs_theory_fn)(void *user, int W, const double *P_end, long long ld, void *stream);
+int  cmbs_set_drag_theory(cmbs_t *s, int like_index, double *dl_end, long long ld_field, long long ld_walker);
+int  cmbs_step_drag(cmbs_t *s, int n_steps, double dragging_steps, cmbs_theory_fn theory_fn, void *user,
+                    void *stream);
+
 /* Execution tuning (no reference counterpart; results are unchanged): split the
  * walkers into n_groups 64-aligned slices, each stepped on an internal stream
  * forked from / joined to the caller's, so the Metropolis kernel of one slice

@@ -217,3 +217,33 @@ def test_convergence_exchange_on_device():
     s.set_covariance(r.propose_cov)                   # learnt proposal (SetCovariance, :317)
     s.step(5)
     assert np.all(np.isfinite(s.state()[1]))
+
+
+@pytest.mark.parametrize("name", ["gauss6_drag", "gauss4_drag_every_step"])
+def test_walker0_follows_reference_dragging(rng_golden, name):
+    """cmbs_step_drag: walker 0 (seeded as the reference chain) follows the
+    reference TFastDraggingSampler chain step by step; every walker follows
+    the C oracle's dragging chain with its own seed."""
+    from cosmomc_amd.sampler import walker_seed
+    from test_oracle import _target, make_oracle_proposer
+    ch = rng_golden["chains"][name]
+    W = 70
+    s = _make_sampler(ch, W)
+    for k in range(ch["steps"]):
+        s.step_drag(1)
+        P, like, mult, nacc = s.state()
+        np.testing.assert_allclose(P[0], ch["P"][k], rtol=1e-11, atol=1e-12, err_msg=f"step {k}")
+        assert like[0] == pytest.approx(ch["cur_like"][k], rel=1e-10, abs=1e-12)
+    t, keep = _target(ch)
+    for w in (1, 37, 69):
+        ij, kl = walker_seed(ch["ij"], ch["kl"], w)
+        h = make_oracle_proposer(ch)
+        r = po.Ranmar(ij, kl)
+        Q = np.array(ch["P0"], dtype=np.float64)
+        cur = C.c_double(po.lib().orc_target_loglike(C.byref(t), Q))
+        st = po.DragState(0, 0.0, 3.0, ch["oversample_fast"])   # SampleFrom starts with mult = 0 (MCMC.f90:141)
+        for _ in range(ch["steps"]):
+            po.lib().orc_drag_step(h, C.byref(r.s), C.byref(t), C.byref(st), Q, C.byref(cur))
+        po.lib().orc_proposer_free(h)
+        np.testing.assert_allclose(P[w], Q, rtol=1e-10, atol=1e-12)
+        assert mult[w] == st.mult
