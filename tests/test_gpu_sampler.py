@@ -247,3 +247,40 @@ def test_walker0_follows_reference_dragging(rng_golden, name):
         po.lib().orc_proposer_free(h)
         np.testing.assert_allclose(P[w], Q, rtol=1e-10, atol=1e-12)
         assert mult[w] == st.mult
+
+
+def test_dragging_with_plik_theory_callback(tmp_path):
+    """Dragging over a slow amplitude A (theory = A x base D_l, supplied by a
+    theory function at every drag) with calPlanck fast and plik_lite: after the
+    run every walker's theory row is A_w x base (accepted drags swapped it in)
+    and its CurLike is the oracle's -lnL there plus the calPlanck prior."""
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    data = syn.make_plik_lite(12345)
+    like = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    like.nuisance_indices = [2]
+    W = 64
+    base = torch.tensor(syn.base_theory(2508)[:3], device="cuda")
+    theory = base.unsqueeze(0).repeat(W, 1, 1).contiguous()
+    end = torch.empty_like(theory)
+    pmin, pmax = np.array([0.9, 0.9]), np.array([1.1, 1.1])
+    pm, ps = np.array([0.0, 1.0]), np.array([0.0, 0.0025])
+    s = BatchedMCMC(W, 2, [1, 2], [[1], [2]], 1, pmin, pmax, pm, ps, oversample_fast=2, propose_scale=2.4,
+                    seed_ij=91, seed_kl=92)
+    s.set_covariance(np.diag([0.003 ** 2, 0.0025 ** 2]))
+    s.add_likelihood(like, theory)
+    s.set_drag_theory(0, end)
+    s.set_start(np.tile([1.0, 1.0], (W, 1)))
+
+    def theory_fn(P_end):
+        end.copy_(base.unsqueeze(0) * P_end[0].reshape(-1, 1, 1))
+    s.step_drag(40, theory_fn=theory_fn)
+    P, lk, mult, nacc = s.state()
+    assert np.any(np.abs(P[:, 0] - 1.0) > 1e-6), "no drag was accepted"
+    th = theory.cpu().numpy()
+    b = base.cpu().numpy()
+    orc = po.PlikLite(data)
+    for w in range(0, W, 9):
+        np.testing.assert_allclose(th[w], P[w, 0] * b, rtol=1e-15, atol=0)
+        ref = orc.loglike(th[w], P[w, 1]) + 0.5 * ((P[w, 1] - 1.0) / 0.0025) ** 2
+        assert lk[w] == pytest.approx(ref, rel=1e-9)
