@@ -51,7 +51,7 @@ class DeviceRows:
     torch.as_tensor without a copy."""
 
     def __init__(self, ptr, n, W, ld):
-        self.__cuda_array_interface__ = {"shape": (n, W), "typestr": "<f8", "data": (ptr, True),
+        self.__cuda_array_interface__ = {"shape": (n, W), "typestr": "<f8", "data": (ptr, False),
                                          "strides": (ld * 8, 8), "version": 2}
 
 
