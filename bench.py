@@ -161,7 +161,13 @@ def convergence_run(W, rank, world, tmpdir, seconds, lensing=True):
         if r.converged:
             done_at = el
             break
-        if el > seconds:
+        if world > 1:                                  # every rank must leave the exchange loop together
+            import torch.distributed as dist
+            flag = torch.tensor([1.0 if el > seconds else 0.0], dtype=torch.float64, device="cuda")
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            if flag.item() > 0:
+                break
+        elif el > seconds:
             break
     return {"workload": "plik_lite_TTTEEE" + (" + lensing" if lensing else "") + " on one shared slow point, "
                         "calPlanck fast, overdispersed start (1 +- 0.01)",
