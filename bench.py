@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=1.5, help="per-process CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-lensing", action="store_true", help="plik_lite only (configs[2] minus lensing)")
+    p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse ranks")
     p.add_argument("--converge-seconds", type=float, default=20.0,
                    help="R-1 vs wall-clock run after the throughput timing (0 = skip)")
     return p.parse_args()
@@ -281,9 +282,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     N.require_gpu()
-    torch.cuda.set_device(local)
+    dev = local % max(1, torch.cuda.device_count())   # rehearsals may put several ranks on one GPU
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.dist_backend)
     W = args.walkers
     with tempfile.TemporaryDirectory() as td:
         smp, likes, theory, _ = build_problem(W, rank, td, args.groups, lensing=not args.no_lensing)
