@@ -1022,25 +1022,45 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, int nuis_index0, const double
     size_t maxws = 0;
     for (auto &l : s->likes) maxws = std::max(maxws, l.like->like->workspace_size(s->W));
     s->ws.alloc(maxws);
+    s->ws_like[li].alloc(like->like->workspace_size(s->W));
+    if (li > 0 && !s->like_streams[li]) {
+        HIP_CHECK(hipStreamCreateWithFlags(&s->like_streams[li], hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&s->like_join[li], hipEventDisableTiming));
+    }
+    if (!s->like_fork) HIP_CHECK(hipEventCreateWithFlags(&s->like_fork, hipEventDisableTiming));
     if (s->n_groups > 1) sampler_set_groups(s, s->n_groups);   // resize the group workspaces
 }
 
 // likelihood terms of walkers [g0, g1) at their trial points
 static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1, void *ws) {
     const int Wg = g1 - g0;
-    for (size_t i = 0; i < s->likes.size(); i++) {
+    const size_t nl = s->likes.size();
+    // one walker group: the likelihoods are independent, run them side by side
+    const bool fork = nl > 1 && g0 == 0 && g1 == s->W;
+    if (fork) {
+        HIP_CHECK(hipEventRecord(s->like_fork, stream));
+        for (size_t i = 1; i < nl; i++) HIP_CHECK(hipStreamWaitEvent(s->like_streams[i], s->like_fork, 0));
+    }
+    for (size_t i = 0; i < nl; i++) {
+        hipStream_t st = (fork && i > 0) ? s->like_streams[i] : stream;
+        void *wsi = fork ? s->ws_like[i].p : ws;
         auto &l = s->likes[i];
         const int nn = l.like->like->n_nuis;
         double *nb = s->dc.like_nuis[i];
         if (gather) {   // mh_kernel scatters the nuisance slices itself on every step
-            hipLaunchKernelGGL(gather_nuis, dim3((s->W + 255) / 256), dim3(256), 0, stream,
+            hipLaunchKernelGGL(gather_nuis, dim3((s->W + 255) / 256), dim3(256), 0, st,
                                s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld, s->W, s->dc.ld, l.nuis0, nn, nb);
             HIP_CHECK(hipGetLastError());
         }
         l.like->like->loglike_batch(Wg, l.dl + (size_t)g0 * l.ld_walker, l.ld_field, l.ld_walker,
                                     nb + (size_t)g0 * nn, nn, s->like_terms.as<double>() + i * (size_t)s->dc.ld + g0,
-                                    ws, stream);
+                                    wsi, st);
     }
+    if (fork)
+        for (size_t i = 1; i < nl; i++) {
+            HIP_CHECK(hipEventRecord(s->like_join[i], s->like_streams[i]));
+            HIP_CHECK(hipStreamWaitEvent(stream, s->like_join[i], 0));
+        }
 }
 
 static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, double *row, hipStream_t stream, int g0,
