@@ -27,7 +27,8 @@ namespace cmamd {
 static constexpr double LOGZERO = CMBL_LOGZERO;
 static constexpr int MAXP = 64;        // max parameters per chain
 static constexpr int MAXBLK = 32;      // max block size
-static constexpr int NB = 64;          // walkers per mh_kernel block (one wavefront)
+static constexpr int NB = 64;          // walkers per mh_kernel block (one wavefront of chain logic)
+static constexpr int MH_WAVES = 4;     // waves per mh_kernel block sharing the state staging
 
 // strided per-walker column view (LDS: stride NB; HBM: stride W)
 template <class T> struct Col {
@@ -315,27 +316,28 @@ typedef __attribute__((address_space(1))) const void gbl_void_t;
 // One wave instruction moves two 512-byte rows; nothing passes through VGPRs,
 // so every piece of the walker state is in flight at once.
 __device__ inline void dma_rows_f64(double *dst, int d0, const double *src, int r0, int n, size_t ld, int wb,
-                                    int lane)
+                                    int lane, int wave = 0, int nw = 1)
 {
-    for (int r = 0; r < n; r += 2) {
+    for (int r = 2 * wave; r < n; r += 2 * nw) {
         const double *g = src + (size_t)(r0 + r + (lane >> 5)) * ld + wb + 2 * (lane & 31);
         __builtin_amdgcn_global_load_lds((gbl_void_t *)g, (lds_void_t *)(dst + (size_t)(d0 + r) * NB), 16, 0, 0);
     }
 }
 
 // same for int rows (n multiple of 4): one instruction moves four 256-byte rows
-__device__ inline void dma_rows_i32(int *dst, const int *src, int n, size_t ld, int wb, int lane)
+__device__ inline void dma_rows_i32(int *dst, const int *src, int n, size_t ld, int wb, int lane, int wave = 0,
+                                    int nw = 1)
 {
-    for (int r = 0; r < n; r += 4) {
+    for (int r = 4 * wave; r < n; r += 4 * nw) {
         const int *g = src + (size_t)(r + (lane >> 4)) * ld + wb + 4 * (lane & 15);
         __builtin_amdgcn_global_load_lds((gbl_void_t *)g, (lds_void_t *)(dst + (size_t)r * NB), 16, 0, 0);
     }
 }
 
 // flat copy of n 4-byte words (source allocation padded to a multiple of 64 words)
-__device__ inline void dma_words(void *dst, const void *src, int n, int lane)
+__device__ inline void dma_words(void *dst, const void *src, int n, int lane, int wave = 0, int nw = 1)
 {
-    for (int i = 0; i < n; i += 64) {
+    for (int i = 64 * wave; i < n; i += 64 * nw) {
         const unsigned *g = reinterpret_cast<const unsigned *>(src) + i + lane;
         __builtin_amdgcn_global_load_lds((gbl_void_t *)g, (lds_void_t *)(reinterpret_cast<unsigned *>(dst) + i), 4,
                                          0, 0);
@@ -343,9 +345,10 @@ __device__ inline void dma_words(void *dst, const void *src, int n, int lane)
 }
 
 template <class T>
-__device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size_t ld, int w, int lane)
+__device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size_t ld, int w, int lane, int wave = 0,
+                          int nw = 1)
 {
-    for (int r = r0; r < r1; r++) dst[(size_t)r * ld + w] = src[(size_t)(src_r0 + r - r0) * NB + lane];
+    for (int r = r0 + wave; r < r1; r += nw) dst[(size_t)r * ld + w] = src[(size_t)(src_r0 + r - r0) * NB + lane];
 }
 
 // One launch per Metropolis step boundary: accept/reject the pending trial
@@ -353,11 +356,11 @@ __device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size
 // next trial (GetProposal / GetProposalFast) and scatter its nuisance
 // parameters for the likelihood kernels.  One wavefront per 64 walkers.
 template <bool ACCEPT, bool PROPOSE>
-__global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double *hist_row, int blk0)
+__global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_only, double *hist_row, int blk0)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Rows &R = c.rows;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & (NB - 1), wave = threadIdx.x / NB;
     const int wb = (blk0 + blockIdx.x) * NB;
     const int w = wb + lane;
     const bool act = w < c.W;
@@ -377,22 +380,25 @@ __global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double 
 #define SROW(r) ((skipR && (r) >= R.R) ? (r) - R.RR : (r))
 
     STAMP(0);
+    // all MH_WAVES waves issue the LDS-DMA of the state image (row pairs
+    // interleaved across waves); wave 0 alone runs the chain logic; all waves
+    // write the image back
     const int rEnd = R.R + R.RR;
     if (skipR) {
-        dma_rows_f64(sd, 0, c.sd, 0, R.R, W, wb, lane);
-        dma_rows_f64(sd, R.R, c.sd, rEnd, R.ND - rEnd, W, wb, lane);
+        dma_rows_f64(sd, 0, c.sd, 0, R.R, W, wb, lane, wave, MH_WAVES);
+        dma_rows_f64(sd, R.R, c.sd, rEnd, R.ND - rEnd, W, wb, lane, wave, MH_WAVES);
     } else {
-        dma_rows_f64(sd, 0, c.sd, 0, R.ND, W, wb, lane);
+        dma_rows_f64(sd, 0, c.sd, 0, R.ND, W, wb, lane, wave, MH_WAVES);
     }
-    dma_rows_f64(lk, 0, c.like_terms, 0, nlk, W, wb, lane);
-    dma_rows_i32(si, c.si, R.NI, W, wb, lane);
-    dma_words(td, c.tab_d, 2 * c.tl.n_dbl, lane);
-    dma_words(ti, c.tab_i, c.tl.n_int, lane);
+    dma_rows_f64(lk, 0, c.like_terms, 0, nlk, W, wb, lane, wave, MH_WAVES);
+    dma_rows_i32(si, c.si, R.NI, W, wb, lane, wave, MH_WAVES);
+    dma_words(td, c.tab_d, 2 * c.tl.n_dbl, lane, wave, MH_WAVES);
+    dma_words(ti, c.tab_i, c.tl.n_int, lane, wave, MH_WAVES);
     STAMP(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     STAMP(2);
-    if (!act) return;
+    if (wave == 0 && act) {
 
     const Tabs t = make_tabs(c, ti, td);
     Walker k;
@@ -449,13 +455,16 @@ __global__ __launch_bounds__(NB) void mh_kernel(DevCfg c, int fast_only, double 
     si[(size_t)R.J97 * NB + lane] = k.r.j97;
     si[(size_t)R.ISET * NB + lane] = k.r.iset;
     si[(size_t)R.FASTIX * NB + lane] = k.fast_ix;
-    if (skipR) {
-        stage_out(c.sd, sd, 0, 0, R.R, W, w, lane);
-        stage_out(c.sd, sd, R.R, rEnd, R.ND, W, w, lane);
-    } else {
-        stage_out(c.sd, sd, 0, 0, R.ND, W, w, lane);
     }
-    stage_out(c.si, si, 0, 0, R.NI, W, w, lane);
+    __syncthreads();
+    if (!act) return;
+    if (skipR) {
+        stage_out(c.sd, sd, 0, 0, R.R, W, w, lane, wave, MH_WAVES);
+        stage_out(c.sd, sd, R.R, rEnd, R.ND, W, w, lane, wave, MH_WAVES);
+    } else {
+        stage_out(c.sd, sd, 0, 0, R.ND, W, w, lane, wave, MH_WAVES);
+    }
+    stage_out(c.si, si, 0, 0, R.NI, W, w, lane, wave, MH_WAVES);
     STAMP(5);
 #ifdef CMAMD_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1065,7 +1074,7 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
 
 static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, double *row, hipStream_t stream, int g0,
                       int g1) {
-    const dim3 g((g1 - g0 + NB - 1) / NB), b(NB);
+    const dim3 g((g1 - g0 + NB - 1) / NB), b(NB * MH_WAVES);
     const int blk0 = g0 / NB;
     const size_t lds = s->mh_lds;
     timed_launch("mh_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
