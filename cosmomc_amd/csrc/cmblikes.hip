@@ -271,12 +271,20 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
     f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     const int li = lane & 15, lk = lane >> 4;
     const double *trow = tsh + (16 * wave + li) * WK_TS;
+    // weights (zero-padded to WK_COLS columns and WK_CHUNK l by the host): the
+    // next chunk's are prefetched into registers with its theory
+    constexpr int WPER = WK_CHUNK * WK_COLS / 2 / 256;
+    double2 wreg[WPER];
+    auto load_weights = [&](int ch) {
+        const double2 *src = reinterpret_cast<const double2 *>(c.wdense + it.woff) + ch * (WK_CHUNK * WK_COLS / 2);
+#pragma unroll
+        for (int u = 0; u < WPER; u++) wreg[u] = src[tid + 256 * u];
+    };
     load_chunk(0);
+    load_weights(0);
     for (int ch = 0; ch < it.nch; ch++) {
-        {   // weights of this chunk (zero-padded to WK_COLS columns and WK_CHUNK l by the host)
-            const double2 *src = reinterpret_cast<const double2 *>(c.wdense + it.woff) + ch * (WK_CHUNK * WK_COLS / 2);
-            for (int i = tid; i < WK_CHUNK * WK_COLS / 2; i += 256) reinterpret_cast<double2 *>(wsh)[i] = src[i];
-        }
+#pragma unroll
+        for (int u = 0; u < WPER; u++) reinterpret_cast<double2 *>(wsh)[tid + 256 * u] = wreg[u];
         const int lq = it.l0 + ch * WK_CHUNK + 2 * q;
 #pragma unroll
         for (int u = 0; u < PER; u++) {
@@ -317,18 +325,28 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
             tsh[r * WK_TS + 2 * q] = v2[0];
             tsh[r * WK_TS + 2 * q + 1] = v2[1];
         }
-        if (ch + 1 < it.nch) load_chunk(ch + 1);          // in flight during this chunk's MFMAs
+        if (ch + 1 < it.nch) {                              // in flight during this chunk's MFMAs
+            load_chunk(ch + 1);
+            load_weights(ch + 1);
+        }
         __syncthreads();
         // A = Wt[col][k] (lane: col = lane&15, k = lane>>4); B = MapCl[k][walker] (walker = lane&15)
         const int clen = min(WK_CHUNK, it.l1 - (it.l0 + ch * WK_CHUNK) + 1);
         const int nk = (clen + 3) / 4;
-        for (int s = 0; s < nk; s++) {
-            const int k = 4 * s + lk;
-            const double b = trow[k];
-            const double a0 = wsh[k * WK_COLS + li];
-            const double a1 = wsh[k * WK_COLS + 16 + li];
-            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, acc1, 0, 0, 0);
+        if (it.ncol > 16) {
+            for (int s = 0; s < nk; s++) {
+                const int k = 4 * s + lk;
+                const double b = trow[k];
+                const double a0 = wsh[k * WK_COLS + li];
+                const double a1 = wsh[k * WK_COLS + 16 + li];
+                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, acc1, 0, 0, 0);
+            }
+        } else {                                            // one 16-column block suffices
+            for (int s = 0; s < nk; s++) {
+                const int k = 4 * s + lk;
+                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wsh[k * WK_COLS + li], trow[k], acc0, 0, 0, 0);
+            }
         }
         __syncthreads();
     }
