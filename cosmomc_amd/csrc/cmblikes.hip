@@ -271,20 +271,12 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
     f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     const int li = lane & 15, lk = lane >> 4;
     const double *trow = tsh + (16 * wave + li) * WK_TS;
-    // weights (zero-padded to WK_COLS columns and WK_CHUNK l by the host): the
-    // next chunk's are prefetched into registers with its theory
-    constexpr int WPER = WK_CHUNK * WK_COLS / 2 / 256;
-    double2 wreg[WPER];
-    auto load_weights = [&](int ch) {
-        const double2 *src = reinterpret_cast<const double2 *>(c.wdense + it.woff) + ch * (WK_CHUNK * WK_COLS / 2);
-#pragma unroll
-        for (int u = 0; u < WPER; u++) wreg[u] = src[tid + 256 * u];
-    };
     load_chunk(0);
-    load_weights(0);
     for (int ch = 0; ch < it.nch; ch++) {
-#pragma unroll
-        for (int u = 0; u < WPER; u++) reinterpret_cast<double2 *>(wsh)[tid + 256 * u] = wreg[u];
+        {   // weights of this chunk (zero-padded to WK_COLS columns and WK_CHUNK l by the host)
+            const double2 *src = reinterpret_cast<const double2 *>(c.wdense + it.woff) + ch * (WK_CHUNK * WK_COLS / 2);
+            for (int i = tid; i < WK_CHUNK * WK_COLS / 2; i += 256) reinterpret_cast<double2 *>(wsh)[i] = src[i];
+        }
         const int lq = it.l0 + ch * WK_CHUNK + 2 * q;
 #pragma unroll
         for (int u = 0; u < PER; u++) {
@@ -325,10 +317,7 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
             tsh[r * WK_TS + 2 * q] = v2[0];
             tsh[r * WK_TS + 2 * q + 1] = v2[1];
         }
-        if (ch + 1 < it.nch) {                              // in flight during this chunk's MFMAs
-            load_chunk(ch + 1);
-            load_weights(ch + 1);
-        }
+        if (ch + 1 < it.nch) load_chunk(ch + 1);          // in flight during this chunk's MFMAs
         __syncthreads();
         // A = Wt[col][k] (lane: col = lane&15, k = lane>>4); B = MapCl[k][walker] (walker = lane&15)
         const int clen = min(WK_CHUNK, it.l1 - (it.l0 + ch * WK_CHUNK) + 1);

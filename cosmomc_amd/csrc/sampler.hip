@@ -20,6 +20,8 @@
 #include <cmath>
 #include <cstring>
 
+#include <cstdlib>
+
 #include "sampler.h"
 
 namespace cmamd {
@@ -1045,7 +1047,8 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
     const int Wg = g1 - g0;
     const size_t nl = s->likes.size();
     // one walker group: the likelihoods are independent, run them side by side
-    const bool fork = nl > 1 && g0 == 0 && g1 == s->W;
+    static const bool serial = std::getenv("CMBS_SERIAL_LIKES") != nullptr;   // A/B switch for measurement
+    const bool fork = nl > 1 && g0 == 0 && g1 == s->W && !serial;
     if (fork) {
         HIP_CHECK(hipEventRecord(s->like_fork, stream));
         for (size_t i = 1; i < nl; i++) HIP_CHECK(hipStreamWaitEvent(s->like_streams[i], s->like_fork, 0));
