@@ -37,7 +37,10 @@ static constexpr int CL_MAXREQ = 32;            // required maps
 static constexpr int BK_NPARAM = 16;            // BKPlanck.paramnames
 static constexpr int WK_COLS = 32;              // window columns per work item (two 16-row MFMA blocks)
 static constexpr int WK_CHUNK = 64;             // l per chunk
-static constexpr int WK_NCH = 4;                // chunks per work item
+#ifndef CMAMD_WK_NCH
+#define CMAMD_WK_NCH 4
+#endif
+static constexpr int WK_NCH = CMAMD_WK_NCH;     // chunks per work item
 static constexpr int WK_TS = WK_CHUNK + 2;      // LDS row stride of the spectrum tile (doubles)
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));

@@ -1047,8 +1047,11 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
     const int Wg = g1 - g0;
     const size_t nl = s->likes.size();
     // one walker group: the likelihoods are independent, run them side by side
-    static const bool serial = std::getenv("CMBS_SERIAL_LIKES") != nullptr;   // A/B switch for measurement
-    const bool fork = nl > 1 && g0 == 0 && g1 == s->W && !serial;
+    // measured on MI355X (W = 1024, plik_lite + lensing): side by side the memory-bound
+    // likelihood kernels slow each other more than they overlap (91.7 vs 89.7 us/step),
+    // so the default is in order; CMBS_CONCURRENT_LIKES=1 forks them onto streams
+    static const bool concurrent = std::getenv("CMBS_CONCURRENT_LIKES") != nullptr;
+    const bool fork = nl > 1 && g0 == 0 && g1 == s->W && concurrent;
     if (fork) {
         HIP_CHECK(hipEventRecord(s->like_fork, stream));
         for (size_t i = 1; i < nl; i++) HIP_CHECK(hipStreamWaitEvent(s->like_streams[i], s->like_fork, 0));
