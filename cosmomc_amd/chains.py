@@ -1,0 +1,108 @@
+"""CosmoMC / GetDist chain files from the batched sampler.
+
+Reference: every accepted move writes the previous point with its
+multiplicity, ``mult like values`` (IO_OutputChainRow, source/IO.f90:85-93,
+via TChainSampler_MoveDone -> AddNewWeightedPoint, source/MCMC.f90:166-190),
+in Fortran ``'(*(E17.7))'`` (source/FileUtils.f90:75), one ``root_N.txt`` per
+chain, plus ``root.paramnames`` and ``root.ranges``.
+
+Here every walker is a chain: the sampler's history ring holds each walker's
+current point and -lnL after every step (``cmbs_history_host``); runs of
+identical consecutive points are the reference's weighted rows.  A run that is
+still open at the end of a block stays pending until it closes (or ``close``).
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+
+
+def fortran_e(x: float, w: int = 17, d: int = 7) -> str:
+    """Fortran Ew.d edit descriptor (e.g. E17.7: '   0.1234567E+01')."""
+    if x == 0.0 or not math.isfinite(x):
+        body = f"0.{'0' * d}E+00" if x == 0.0 else str(x)
+        return body.rjust(w)
+    e = math.floor(math.log10(abs(x))) + 1
+    m = abs(x) / 10.0 ** e
+    digits = round(m * 10 ** d)
+    if digits >= 10 ** d:                         # rounding carried into the next decade
+        digits //= 10
+        e += 1
+    if digits < 10 ** (d - 1):                    # log10 rounding below the decade
+        digits = round(abs(x) / 10.0 ** (e - 1) * 10 ** d)
+        e -= 1
+    s = f"{'-' if x < 0 else ''}0.{digits:0{d}d}E{'+' if e >= 0 else '-'}{abs(e):02d}"
+    return s.rjust(w)
+
+
+class ChainWriter:
+    """Chain files for walkers ``walkers`` (default all) of a BatchedMCMC.
+
+    names / labels / ranges are for the used parameters (params_used order);
+    ranges: list of (min, max) or None."""
+
+    def __init__(self, root: str, names, labels=None, ranges=None, walkers=None, first_chain: int = 1):
+        self.root = root
+        self.names = list(names)
+        self.labels = list(labels) if labels is not None else list(names)
+        self.ranges = ranges
+        self.walkers = walkers
+        self.first_chain = first_chain
+        self.pending = {}                          # walker -> [point values (like, P...), count]
+        self.next_step = None
+        d = os.path.dirname(root)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        with open(root + ".paramnames", "w") as f:
+            for n, lab in zip(self.names, self.labels):
+                f.write(f"{n}\t{lab}\n")
+        if ranges is not None:
+            with open(root + ".ranges", "w") as f:
+                for n, r in zip(self.names, ranges):
+                    f.write(f"{n}\t{r[0]!r}\t{r[1]!r}\n")
+
+    def _file(self, w):
+        return f"{self.root}_{w + self.first_chain}.txt"
+
+    def _emit(self, fh, point, count):
+        fh.write("".join(fortran_e(v) for v in [float(count), point[0], *point[1:]]) + "\n")
+
+    def add_rows(self, rows):
+        """rows: [steps, n_used + 1, W] history block (params_used..., CurLike)."""
+        rows = np.asarray(rows)
+        steps, n1, W = rows.shape
+        walkers = range(W) if self.walkers is None else self.walkers
+        for w in walkers:
+            pts = np.concatenate([rows[:, n1 - 1:n1, w], rows[:, :n1 - 1, w]], axis=1)   # like, P...
+            with open(self._file(w), "a") as fh:
+                cur = self.pending.get(w)
+                for t in range(steps):
+                    p = pts[t]
+                    if cur is not None and np.array_equal(cur[0], p):
+                        cur[1] += 1
+                    else:
+                        if cur is not None:
+                            self._emit(fh, cur[0], cur[1])
+                        cur = [p.copy(), 1]
+                self.pending[w] = cur
+
+    def append(self, sampler, first: int = None, count: int = None):
+        """Write the history steps [first, first + count) of ``sampler``
+        (default: everything recorded since the last call)."""
+        total = sampler.history_count()
+        if first is None:
+            first = self.next_step if self.next_step is not None else 0
+        if count is None:
+            count = total - first
+        if count > 0:
+            self.add_rows(sampler.history_host(first, count))
+        self.next_step = first + max(count, 0)
+
+    def close(self):
+        for w, cur in self.pending.items():
+            if cur is not None:
+                with open(self._file(w), "a") as fh:
+                    self._emit(fh, cur[0], cur[1])
+        self.pending = {}

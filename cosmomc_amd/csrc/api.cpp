@@ -248,6 +248,11 @@ int cmbs_step_drag(cmbs_t *s, int n_steps, double dragging_steps, cmbs_theory_fn
     });
 }
 
+int cmbs_history_host(cmbs_t *s, int first, int count, double *out) {
+    if (!s || !out || count < 0) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_history_host(s, first, count, out); });
+}
+
 int cmbs_set_groups(cmbs_t *s, int n_groups) {
     if (!s) return CMBL_ERR_ARG;
     return guarded(&s->last_error, [&] { cmamd::sampler_set_groups(s, n_groups); });

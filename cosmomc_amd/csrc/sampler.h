@@ -118,6 +118,7 @@ struct cmbs {
 namespace cmamd {
 void sampler_set_groups(cmbs *s, int n_groups);
 void sampler_chain_moments(cmbs *s, int first, int last, const double *gmean, double *out, hipStream_t stream);
+void sampler_history_host(cmbs *s, int first, int count, double *out);
 void sampler_set_drag_theory(cmbs *s, int like_index, double *dl_end, long long ld_field, long long ld_walker);
 void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_fn fn, void *user, hipStream_t stream);
 }

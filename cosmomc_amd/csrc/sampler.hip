@@ -438,8 +438,10 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
         } else {
             mult += 1.0;
         }
-        if (hist_row)
+        if (hist_row) {
             for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = k.P[t.params_used[i]];
+            hist_row[(size_t)c.n_used * c.W + w] = cur;
+        }
     }
     STAMP(3);
     if (PROPOSE) {
@@ -635,7 +637,10 @@ __global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *h
         } else {
             if (dst == 2 || dst == 3) dst = 0;
             if (hist_row)
+            {
                 for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = k.P[t.params_used[i]];
+                hist_row[(size_t)c.n_used * c.W + w] = cur;
+            }
         }
     }
     c.sd[(size_t)R.C * ld + w] = k.r.c;
@@ -688,14 +693,14 @@ __global__ void hist_stats_kernel(const double *hist, int cap, int W, int n, int
     double *m = means + (size_t)w * n;
     for (int i = 0; i < n; i++) m[i] = 0.0;
     for (int tt = first; tt <= last; tt++) {
-        const double *row = hist + (size_t)(tt % cap) * n * W;
+        const double *row = hist + (size_t)(tt % cap) * (n + 1) * W;
         for (int i = 0; i < n; i++) m[i] += row[(size_t)i * W + w];
     }
     for (int i = 0; i < n; i++) m[i] /= cnt;
     double *C = covs + (size_t)w * n * n;
     for (int i = 0; i < n * n; i++) C[i] = 0.0;
     for (int tt = first; tt <= last; tt++) {
-        const double *row = hist + (size_t)(tt % cap) * n * W;
+        const double *row = hist + (size_t)(tt % cap) * (n + 1) * W;
         for (int j = 0; j < n; j++) {
             const double dj = row[(size_t)j * W + w] - m[j];
             for (int i = 0; i < n; i++) C[i * n + j] += (row[(size_t)i * W + w] - m[i]) * dj;
@@ -1114,7 +1119,7 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (n_steps <= 0) return;
     auto next_row = [&]() -> double * {
         if (s->hist_cap == 0) return nullptr;
-        double *row = s->hist.as<double>() + (size_t)(s->hist_count % s->hist_cap) * s->n_used * s->W;
+        double *row = s->hist.as<double>() + (size_t)(s->hist_count % s->hist_cap) * (s->n_used + 1) * s->W;
         s->hist_count++;
         return row;
     };
@@ -1211,7 +1216,7 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
     g.interp = interp;
     auto next_row = [&]() -> double * {
         if (s->hist_cap == 0) return nullptr;
-        double *row = s->hist.as<double>() + (size_t)(s->hist_count % s->hist_cap) * s->n_used * s->W;
+        double *row = s->hist.as<double>() + (size_t)(s->hist_count % s->hist_cap) * (s->n_used + 1) * s->W;
         s->hist_count++;
         return row;
     };
@@ -1282,7 +1287,7 @@ void sampler_set_groups(cmbs *s, int n_groups) {
 }
 
 void sampler_enable_history(cmbs *s, int capacity) {
-    s->hist.alloc((size_t)capacity * s->n_used * s->W * 8);
+    s->hist.alloc((size_t)capacity * (s->n_used + 1) * s->W * 8);   // per step: P(params_used) rows, CurLike row
     s->hist_cap = capacity;
     s->hist_count = 0;
 }
@@ -1305,6 +1310,20 @@ void sampler_chain_moments(cmbs *s, int first, int last, const double *gmean, do
     hipLaunchKernelGGL(chain_moments_kernel, dim3(1), dim3(256), 0, stream, means, covs, s->W, n,
                        (double)(last - first + 1), gmean, out);
     HIP_CHECK(hipGetLastError());
+}
+
+void sampler_history_host(cmbs *s, int first, int count, double *out) {
+    if (s->hist_cap == 0) fail(CMBL_ERR_ARG, "history not enabled");
+    const int oldest = std::max(0, s->hist_count - s->hist_cap);
+    if (first < oldest || first + count > s->hist_count)
+        fail(CMBL_ERR_ARG, "history rows [%d, %d) not kept (rows %d..%d)", first, first + count, oldest, s->hist_count - 1);
+    HIP_CHECK(hipDeviceSynchronize());
+    const size_t blk = (size_t)(s->n_used + 1) * s->W;
+    for (int k = 0; k < count; k++) {
+        const int slot = (first + k) % s->hist_cap;
+        HIP_CHECK(hipMemcpy(out + (size_t)k * blk, s->hist.as<double>() + (size_t)slot * blk, blk * 8,
+                            hipMemcpyDeviceToHost));
+    }
 }
 
 void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, int *num_accept) {

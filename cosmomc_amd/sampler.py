@@ -132,6 +132,13 @@ class BatchedMCMC:
     def history_count(self) -> int:
         return N.lib().cmbs_history_count(self._h)
 
+    def history_host(self, first: int, count: int):
+        """History rows [first, first+count) on the host: [count, n_used + 1, W]
+        (used parameters, then CurLike)."""
+        out = np.empty((count, len(self.params_used) + 1, self.W))
+        self._check(N.lib().cmbs_history_host(self._h, first, count, out.ctypes.data))
+        return out
+
     def history_stats(self, first: int, last: int):
         """Per-walker means [W, n_used] and covariances [W, n_used, n_used] (cuda tensors)."""
         import torch

@@ -187,14 +187,20 @@ int  cmbs_step_drag(cmbs_t *s, int n_steps, double dragging_steps, cmbs_theory_f
 int  cmbs_set_groups(cmbs_t *s, int n_groups);
 
 /* Optional history capture for convergence statistics: every step appends
- * each walker's current used-parameter vector to a device ring of `capacity`
- * steps (SampleCollector AddNewPoint, SampleCollector.f90:324-456). */
+ * each walker's current used-parameter vector and CurLike to a device ring of
+ * `capacity` steps (SampleCollector AddNewPoint, SampleCollector.f90:324-456). */
 int  cmbs_enable_history(cmbs_t *s, int capacity);
-/* Per-walker statistics over history rows [first, last] (inclusive, oldest
- * row = 0): counts[W], means[W][n_used], covs[W][n_used][n_used], device ptrs
+/* Per-walker statistics over history rows [first, last] (inclusive; row k is
+ * the k-th step recorded since cmbs_enable_history, the ring keeps the last
+ * `capacity`): means[W][n_used], covs[W][n_used][n_used], device ptrs
  * (SampleCollector.f90:235-246 "second half" window is first = count/2). */
 int  cmbs_history_stats(cmbs_t *s, int first, int last, double *means, double *covs, void *stream);
 int  cmbs_history_count(const cmbs_t *s);
+/* Synchronising copy of history rows [first, first+count) (step indices as
+ * cmbs_history_stats; the ring keeps the last `capacity`) to HOST memory: out[count][n_used + 1][W], per step the used parameters
+ * then CurLike of every walker (the chain-file writer's input,
+ * IO_OutputChainRow IO.f90:85-93). */
+int  cmbs_history_host(cmbs_t *s, int first, int count, double *out);
 /* This GPU's partial sums for the convergence / proposal-learning exchange
  * (TMpiChainCollector_UpdateCovAndCheckConverge, SampleCollector.f90:212-322):
  * each walker is one chain whose samples are history rows [first, last].

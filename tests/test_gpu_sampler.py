@@ -284,3 +284,28 @@ def test_dragging_with_plik_theory_callback(tmp_path):
         np.testing.assert_allclose(th[w], P[w, 0] * b, rtol=1e-15, atol=0)
         ref = orc.loglike(th[w], P[w, 1]) + 0.5 * ((P[w, 1] - 1.0) / 0.0025) ** 2
         assert lk[w] == pytest.approx(ref, rel=1e-9)
+
+
+def test_chain_files_from_history(tmp_path):
+    """ChainWriter on a GPU run: per walker the weights add up to the steps,
+    consecutive rows are distinct points, and the last row is the final state."""
+    from cosmomc_amd.chains import ChainWriter
+    from cosmomc_amd.sampler import BatchedMCMC
+    n, W, T = 2, 8, 90
+    s = BatchedMCMC(W, n, [1, 2], [[1, 2]], 1, [-10, -10], [10, 10], seed_ij=5, seed_kl=6)
+    s.set_covariance(np.eye(2))
+    s.set_test_gaussian(np.array([[1.0, 0.3], [0.3, 2.0]]), np.zeros(2))
+    s.set_start(np.zeros((W, n)))
+    s.enable_history(40)
+    cw = ChainWriter(str(tmp_path / "run"), ["x", "y"])
+    for _ in range(3):
+        s.step(30)
+        cw.append(s)
+    cw.close()
+    P, like, _, _ = s.state()
+    for w in range(W):
+        c = np.loadtxt(tmp_path / f"run_{w + 1}.txt", ndmin=2)
+        assert c[:, 0].sum() == T
+        assert np.all(np.any(np.diff(c[:, 2:], axis=0) != 0, axis=1))
+        np.testing.assert_allclose(c[-1, 2:], P[w], rtol=1e-6)
+        assert c[-1, 1] == pytest.approx(like[w], rel=1e-6)
