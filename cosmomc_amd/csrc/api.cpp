@@ -234,10 +234,10 @@ int cmbs_chain_moments(cmbs_t *s, int first, int last, const double *gmean, doub
                    [&] { cmamd::sampler_chain_moments(s, first, last, gmean, out, (hipStream_t)stream); });
 }
 
-int cmbs_set_drag_theory(cmbs_t *s, int like_index, double *dl_end, long long ld_field, long long ld_walker) {
+int cmbs_set_trial_theory(cmbs_t *s, int like_index, double *dl_end, long long ld_field, long long ld_walker) {
     if (!s || !dl_end) return CMBL_ERR_ARG;
     return guarded(&s->last_error,
-                   [&] { cmamd::sampler_set_drag_theory(s, like_index, dl_end, ld_field, ld_walker); });
+                   [&] { cmamd::sampler_set_trial_theory(s, like_index, dl_end, ld_field, ld_walker); });
 }
 
 int cmbs_step_drag(cmbs_t *s, int n_steps, double dragging_steps, cmbs_theory_fn theory_fn, void *user,
@@ -251,6 +251,12 @@ int cmbs_step_drag(cmbs_t *s, int n_steps, double dragging_steps, cmbs_theory_fn
 int cmbs_history_host(cmbs_t *s, int first, int count, double *out) {
     if (!s || !out || count < 0) return CMBL_ERR_ARG;
     return guarded(&s->last_error, [&] { cmamd::sampler_history_host(s, first, count, out); });
+}
+
+int cmbs_step_theory(cmbs_t *s, int n_steps, cmbs_theory_fn theory_fn, void *user, void *stream) {
+    if (!s) return CMBL_ERR_ARG;
+    return guarded(&s->last_error,
+                   [&] { cmamd::sampler_step_theory(s, n_steps, theory_fn, user, (hipStream_t)stream); });
 }
 
 int cmbs_set_groups(cmbs_t *s, int n_groups) {

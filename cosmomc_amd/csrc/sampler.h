@@ -27,6 +27,7 @@ struct Rows {
     int CYCLP = 5;      // 3 rows: All, Slow, Fast CyclicIndexRandomizer%loopix
     int BLKLP = 8;      // nblocks rows: RandDirectionProposer%loopix
     int CYC;            // all_n + slow_n + fast_n rows: the three index permutations
+    int ACCF;           // 1 if the last accept of this walker moved it (theory swap for slow steps)
     int NI;             // multiple of 4: rows are moved four at a time
 };
 
@@ -119,6 +120,7 @@ namespace cmamd {
 void sampler_set_groups(cmbs *s, int n_groups);
 void sampler_chain_moments(cmbs *s, int first, int last, const double *gmean, double *out, hipStream_t stream);
 void sampler_history_host(cmbs *s, int first, int count, double *out);
-void sampler_set_drag_theory(cmbs *s, int like_index, double *dl_end, long long ld_field, long long ld_walker);
+void sampler_set_trial_theory(cmbs *s, int like_index, double *dl_end, long long ld_field, long long ld_walker);
 void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_fn fn, void *user, hipStream_t stream);
+void sampler_step_theory(cmbs *s, int n_steps, cmbs_theory_fn fn, void *user, hipStream_t stream);
 }

@@ -438,6 +438,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
         } else {
             mult += 1.0;
         }
+        si[(size_t)R.ACCF * NB + lane] = acc ? 1 : 0;
         if (hist_row) {
             for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = k.P[t.params_used[i]];
             hist_row[(size_t)c.n_used * c.W + w] = cur;
@@ -651,12 +652,13 @@ __global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *h
     c.si[(size_t)R.FASTIX * ld + w] = k.fast_ix;
 }
 
-// accepted drags: the end slow point's theory becomes the walker's theory
-__global__ void drag_swap_theory(const int *dst, int W, const double *src, long long src_ld, double *dstth,
-                                 long long dst_ld, long long n)
+// accepted moves: the trial (end) slow point's theory becomes the walker's theory
+// (flag[w] == value: drag_kernel dst 4, or the Metropolis accept flag row)
+__global__ void drag_swap_theory(const int *flag, int value, int W, const double *src, long long src_ld,
+                                 double *dstth, long long dst_ld, long long n)
 {
     const int w = blockIdx.y;
-    if (w >= W || dst[w] != 4) return;
+    if (w >= W || flag[w] != value) return;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
         dstth[(long long)w * dst_ld + i] = src[(long long)w * src_ld + i];
 }
@@ -912,7 +914,8 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     R.M = R.L + 1;
     R.ND = (R.M + 2) & ~1;
     R.CYC = R.BLKLP + nb;
-    R.NI = (R.CYC + s->all_n + s->slow_n + s->fast_n + 3) & ~3;
+    R.ACCF = R.CYC + s->all_n + s->slow_n + s->fast_n;
+    R.NI = (R.ACCF + 1 + 3) & ~3;
     d.ld = (W + NB - 1) / NB * NB;
     s->sd.alloc((size_t)R.ND * d.ld * 8);
     s->si.alloc((size_t)R.NI * d.ld * 4);
@@ -1116,6 +1119,8 @@ void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream) {
 void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (!s->started) fail(CMBL_ERR_ARG, "cmbs_set_start must be called before cmbs_step");
     if (fast_only && s->fast_n == 0) fail(CMBL_ERR_ARG, "no fast parameters");
+    if (!fast_only && s->slow_n > 0 && !s->likes.empty())
+        fail(CMBL_ERR_ARG, "slow proposals need the theory at the trial point: use cmbs_step_theory");
     if (n_steps <= 0) return;
     auto next_row = [&]() -> double * {
         if (s->hist_cap == 0) return nullptr;
@@ -1153,7 +1158,7 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     }
 }
 
-void sampler_set_drag_theory(cmbs *s, int like_index, double *dl_end, long long ld_field, long long ld_walker) {
+void sampler_set_trial_theory(cmbs *s, int like_index, double *dl_end, long long ld_field, long long ld_walker) {
     if (like_index < 0 || like_index >= (int)s->likes.size()) fail(CMBL_ERR_ARG, "no likelihood %d", like_index);
     auto &e = s->end_theory[like_index];
     e.dl = dl_end;
@@ -1261,12 +1266,62 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
             const long long n = std::min(e.ld_walker, l.ld_walker) > 0 ? std::min(e.ld_walker, l.ld_walker)
                                                                         : 10 * l.ld_field;
             if (l.ld_walker == 0) fail(CMBL_ERR_ARG, "dragging needs per-walker theory rows (ld_walker > 0)");
-            hipLaunchKernelGGL(drag_swap_theory, dim3(16, s->W), dim3(256), 0, stream, g.di, s->W, e.dl,
+            hipLaunchKernelGGL(drag_swap_theory, dim3(16, s->W), dim3(256), 0, stream, g.di, 4, s->W, e.dl,
                                e.ld_walker, const_cast<double *>(l.dl), l.ld_walker, n);
             HIP_CHECK(hipGetLastError());
         }
         HIP_CHECK(hipMemsetAsync(g.di, 0, (size_t)s->W * 4, stream));
     }
+}
+
+// full TMetropolisSampler_GetNewSample steps (MCMC.f90:269-307) with the
+// theory recomputed at every trial point: the caller's theory function fills
+// the trial-theory buffers, the likelihoods run on them, and accepted walkers
+// take the trial theory as their own
+static void swap_accepted_theory(cmbs *s, hipStream_t stream) {
+    const int *flag = s->dc.si + (size_t)s->dc.rows.ACCF * s->dc.ld;
+    for (size_t i = 0; i < s->likes.size(); i++) {
+        const auto &e = s->end_theory[i];
+        const auto &l = s->likes[i];
+        const long long n = std::min(e.ld_walker, l.ld_walker);
+        hipLaunchKernelGGL(drag_swap_theory, dim3(16, s->W), dim3(256), 0, stream, flag, 1, s->W, e.dl, e.ld_walker,
+                           const_cast<double *>(l.dl), l.ld_walker, n);
+        HIP_CHECK(hipGetLastError());
+    }
+}
+
+void sampler_step_theory(cmbs *s, int n_steps, cmbs_theory_fn fn, void *user, hipStream_t stream) {
+    if (!s->started) fail(CMBL_ERR_ARG, "cmbs_set_start must be called before cmbs_step_theory");
+    if (n_steps <= 0) return;
+    if (s->likes.empty()) {
+        sampler_step(s, n_steps, 0, stream);
+        return;
+    }
+    if (!fn) fail(CMBL_ERR_ARG, "cmbs_step_theory needs a theory function");
+    for (size_t i = 0; i < s->likes.size(); i++) {
+        if (!s->end_theory[i].dl) fail(CMBL_ERR_ARG, "likelihood %zu has no trial-theory buffer", i);
+        if (s->likes[i].ld_walker == 0) fail(CMBL_ERR_ARG, "slow steps need per-walker theory rows");
+    }
+    auto next_row = [&]() -> double * {
+        if (s->hist_cap == 0) return nullptr;
+        double *row = s->hist.as<double>() + (size_t)(s->hist_count % s->hist_cap) * (s->n_used + 1) * s->W;
+        s->hist_count++;
+        return row;
+    };
+    const double *Ptrial = s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld;
+    auto trial_likes = [&]() {
+        if (fn(user, s->W, Ptrial, (long long)s->dc.ld, stream) != 0) fail(CMBL_ERR_ARG, "theory function failed");
+        eval_likes_drag(s, 1, stream);
+    };
+    launch_mh(s, false, true, 0, nullptr, stream, 0, s->W);
+    trial_likes();
+    for (int k = 1; k < n_steps; k++) {
+        launch_mh(s, true, true, 0, next_row(), stream, 0, s->W);
+        swap_accepted_theory(s, stream);
+        trial_likes();
+    }
+    launch_mh(s, true, false, 0, next_row(), stream, 0, s->W);
+    swap_accepted_theory(s, stream);
 }
 
 void sampler_set_groups(cmbs *s, int n_groups) {

@@ -97,33 +97,48 @@ class BatchedMCMC:
             stream = N.current_stream_ptr()
         self._check(N.lib().cmbs_step(self._h, n_steps, int(fast_only), stream))
 
-    def set_drag_theory(self, like_index: int, dl_end):
-        """End-point theory buffer of likelihood ``like_index`` for dragging
-        (cuda float64 tensor shaped like the theory given to add_likelihood)."""
+    def set_trial_theory(self, like_index: int, dl_end):
+        """Trial-point theory buffer of likelihood ``like_index`` (cuda float64
+        tensor shaped like the theory given to add_likelihood), filled by the
+        theory function of step_drag / step_theory."""
         self._drag_keep = getattr(self, "_drag_keep", {})
         self._drag_keep[like_index] = dl_end
-        self._check(N.lib().cmbs_set_drag_theory(self._h, like_index, dl_end.data_ptr(), dl_end.stride(1),
-                                                 dl_end.stride(0)))
+        self._check(N.lib().cmbs_set_trial_theory(self._h, like_index, dl_end.data_ptr(), dl_end.stride(1),
+                                                  dl_end.stride(0)))
+
+    set_drag_theory = set_trial_theory
+
+    def _theory_cb(self, theory_fn):
+        import torch
+        if theory_fn is None:
+            return N.THEORY_FN()
+
+        def _cb(user, W, ptr, ld, strm):
+            try:
+                theory_fn(torch.as_tensor(N.DeviceRows(ptr, self.np, W, ld), device="cuda"))
+                return 0
+            except Exception:                        # reported as a failed theory call
+                import traceback
+                traceback.print_exc()
+                return 1
+        return N.THEORY_FN(_cb)
+
+    def step_theory(self, n_steps: int = 1, theory_fn=None, stream=None):
+        """n_steps full GetNewSample steps (slow and fast proposals) with the
+        theory at every trial point from theory_fn(P_trial [num_params, W])."""
+        if stream is None:
+            stream = N.current_stream_ptr()
+        cb = self._theory_cb(theory_fn)
+        self._check(N.lib().cmbs_step_theory(self._h, n_steps, cb, None, stream))
 
     def step_drag(self, n_steps: int = 1, dragging_steps: float = 3.0, theory_fn=None, stream=None):
         """n_steps TFastDraggingSampler_GetNewSample calls (MCMC.f90:338-452).
 
         theory_fn(P_end) -> None fills every end-theory buffer (set_drag_theory)
         for the proposed points P_end, a cuda tensor view [num_params, W]."""
-        import torch
         if stream is None:
             stream = N.current_stream_ptr()
-        cb = N.THEORY_FN()
-        if theory_fn is not None:
-            def _cb(user, W, ptr, ld, strm):
-                try:
-                    theory_fn(torch.as_tensor(N.DeviceRows(ptr, self.np, W, ld), device="cuda"))
-                    return 0
-                except Exception:                    # reported as a failed theory call
-                    import traceback
-                    traceback.print_exc()
-                    return 1
-            cb = N.THEORY_FN(_cb)
+        cb = self._theory_cb(theory_fn)
         self._check(N.lib().cmbs_step_drag(self._h, n_steps, dragging_steps, cb, None, stream))
 
     def enable_history(self, capacity: int):

@@ -170,15 +170,25 @@ int  cmbs_step(cmbs_t *s, int n_steps, int fast_only, void *stream);
  * proposed slow point: `theory_fn` is called once per drag (synchronously,
  * after the slow proposal) with the device trial rows P_end [num_params][ld]
  * (walker-minor) and must fill every likelihood's end-theory buffer
- * registered with cmbs_set_drag_theory; it returns 0 on success.  Walkers
+ * registered with cmbs_set_trial_theory; it returns 0 on success.  Walkers
  * whose drag is accepted get their end theory copied into their theory rows
  * (the dl buffer passed to cmbs_add_likelihood).  With no likelihoods (the
  * analytic test target) theory_fn may be NULL.  Walkers whose CurLike is
  * logZero skip the drag (the reference makes a full Metropolis step there). */
 typedef int (*cmbs_theory_fn)(void *user, int W, const double *P_end, long long ld, void *stream);
-int  cmbs_set_drag_theory(cmbs_t *s, int like_index, double *dl_end, long long ld_field, long long ld_walker);
+/* Trial-point theory buffer of likelihood `like_index` (same layout as its
+ * theory rows), filled by the theory function for dragging end points and
+ * for cmbs_step_theory trial points. */
+int  cmbs_set_trial_theory(cmbs_t *s, int like_index, double *dl_end, long long ld_field, long long ld_walker);
 int  cmbs_step_drag(cmbs_t *s, int n_steps, double dragging_steps, cmbs_theory_fn theory_fn, void *user,
                     void *stream);
+/* Full TMetropolisSampler_GetNewSample steps (MCMC.f90:269-307; GetProposal
+ * slow and fast) when data likelihoods need the theory at the trial point
+ * (the reference recomputes it with CAMB, CalcLike_Cosmology.f90:59-94):
+ * theory_fn fills the trial-theory buffers from the trial rows every step and
+ * accepted walkers take the trial theory.  cmbs_step(fast_only = 0) refuses
+ * slow proposals when data likelihoods are registered. */
+int  cmbs_step_theory(cmbs_t *s, int n_steps, cmbs_theory_fn theory_fn, void *user, void *stream);
 
 /* Execution tuning (no reference counterpart; results are unchanged): split the
  * walkers into n_groups 64-aligned slices, each stepped on an internal stream

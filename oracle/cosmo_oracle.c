@@ -565,7 +565,16 @@ double orc_target_loglike(const orc_target_t *t, const double *P)
         for (int i = 0; i < n; i++) d += X[i] * y[i];
         main = d / 2.0;
     }
-    if (t->plik) main += orc_plik_loglike(t->plik, t->plik_dl, t->plik_ld_field, P[t->plik_nuis_index - 1]);
+    if (t->plik && t->plik_scale_index > 0) {
+        const long n = 3 * t->plik_ld_field;
+        double *dl = (double *)malloc((size_t)n * sizeof(double));
+        const double a = P[t->plik_scale_index - 1];
+        for (long i = 0; i < n; i++) dl[i] = a * t->plik_dl[i];
+        main += orc_plik_loglike(t->plik, dl, t->plik_ld_field, P[t->plik_nuis_index - 1]);
+        free(dl);
+    } else if (t->plik) {
+        main += orc_plik_loglike(t->plik, t->plik_dl, t->plik_ld_field, P[t->plik_nuis_index - 1]);
+    }
     add_like_temp(&like, main, t->temperature);
     if (like == ORC_LOGZERO) return like;
     double pri = 0.0;                                  /* GetLogPriors :111-134 */

@@ -85,6 +85,9 @@ typedef struct {
     int plik_nuis_index;                /* 1-based */
     const double *plik_dl;
     long plik_ld_field;
+    /* slow-theory test model: theory = P(plik_scale_index) x plik_dl (0: off),
+     * standing in for CAMB's recomputation at the trial point */
+    int plik_scale_index;               /* 1-based */
 } orc_target_t;
 
 double orc_target_loglike(const orc_target_t *t, const double *P); /* GetLogLike :136-151 */

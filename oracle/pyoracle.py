@@ -34,7 +34,8 @@ class Target(C.Structure):
                 ("prior_mean", C.c_void_p), ("prior_std", C.c_void_p), ("temperature", C.c_double),
                 ("test_like", C.c_int), ("n_used", C.c_int), ("params_used", C.c_void_p),
                 ("test_covinv", C.c_void_p), ("center", C.c_void_p), ("plik", C.c_void_p),
-                ("plik_nuis_index", C.c_int), ("plik_dl", C.c_void_p), ("plik_ld_field", C.c_long)]
+                ("plik_nuis_index", C.c_int), ("plik_dl", C.c_void_p), ("plik_ld_field", C.c_long),
+                ("plik_scale_index", C.c_int)]
 
 
 def lib():

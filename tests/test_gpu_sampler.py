@@ -286,6 +286,66 @@ def test_dragging_with_plik_theory_callback(tmp_path):
         assert lk[w] == pytest.approx(ref, rel=1e-9)
 
 
+@pytest.mark.parametrize("oversample", [1, 3])
+def test_full_steps_with_theory_callback(tmp_path, oversample):
+    """cmbs_step_theory: full GetNewSample steps (slow amplitude A and fast
+    calPlanck) with the theory A x base recomputed at every trial point by a
+    theory function.  Walkers follow the C oracle's chains (its slow-theory
+    model scales the cached theory by P(A)) and accepted walkers carry A x base."""
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC, walker_seed
+    from cosmomc_amd._native import NativeError
+    data = syn.make_plik_lite(12345)
+    like = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    like.nuisance_indices = [2]
+    W, steps = 80, 40
+    base = torch.tensor(syn.base_theory(2508)[:3], device="cuda")
+    theory = base.unsqueeze(0).repeat(W, 1, 1).contiguous()
+    trial = torch.empty_like(theory)
+    pmin, pmax = np.array([0.9, 0.9]), np.array([1.1, 1.1])
+    pm, ps = np.array([0.0, 1.0]), np.array([0.0, 0.0025])
+    cov = np.diag([0.002 ** 2, 0.0025 ** 2])
+    s = BatchedMCMC(W, 2, [1, 2], [[1], [2]], 1, pmin, pmax, pm, ps, oversample_fast=oversample,
+                    propose_scale=2.4, seed_ij=71, seed_kl=72)
+    s.set_covariance(cov)
+    s.add_likelihood(like, theory)
+    s.set_trial_theory(0, trial)
+    s.set_start(np.tile([1.0, 1.0], (W, 1)))
+    with pytest.raises(NativeError):
+        s.step(1, fast_only=False)              # slow proposals need the trial theory
+
+    def theory_fn(P_trial):
+        trial.copy_(base.unsqueeze(0) * P_trial[0].reshape(-1, 1, 1))
+    s.step_theory(steps, theory_fn=theory_fn)
+    P, lk, mult, nacc = s.state()
+    assert np.any(np.abs(P[:, 0] - 1.0) > 1e-6), "no slow move was accepted"
+    th, b = theory.cpu().numpy(), base.cpu().numpy()
+    orc = po.PlikLite(data)
+    bh = np.ascontiguousarray(syn.base_theory(2508)[:3])
+    for w in (0, 1, 41, 79):
+        np.testing.assert_allclose(th[w], P[w, 0] * b, rtol=1e-15, atol=0)
+        ij, kl = walker_seed(71, 72, w)
+        h = po.lib().orc_proposer_create(2, np.array([1, 1], dtype=np.int32), np.array([1, 2], dtype=np.int32),
+                                         1, oversample, 2.4, 2, np.array([1, 2], dtype=np.int32))
+        po.lib().orc_proposer_set_covariance(h, np.ascontiguousarray(cov))
+        t = po.Target()
+        keep = [np.ascontiguousarray(a) for a in (pmin, pmax, pm, ps)]
+        t.num_params = 2
+        t.pmin, t.pmax, t.prior_mean, t.prior_std = [a.ctypes.data for a in keep]
+        t.temperature = 1.0
+        t.plik, t.plik_nuis_index, t.plik_dl, t.plik_ld_field = orc.h, 2, bh.ctypes.data, bh.shape[1]
+        t.plik_scale_index = 1
+        r = po.Ranmar(ij, kl)
+        Q = np.array([1.0, 1.0])
+        cur = C.c_double(po.lib().orc_target_loglike(C.byref(t), Q))
+        acc = 0
+        for _ in range(steps):
+            acc += po.lib().orc_mh_step(h, C.byref(r.s), C.byref(t), Q, C.byref(cur), 0, None)
+        po.lib().orc_proposer_free(h)
+        np.testing.assert_allclose(P[w], Q, rtol=1e-11)
+        assert lk[w] == pytest.approx(cur.value, rel=1e-9)
+
+
 def test_chain_files_from_history(tmp_path):
     """ChainWriter on a GPU run: per walker the weights add up to the steps,
     consecutive rows are distinct points, and the last row is the final state."""
