@@ -265,7 +265,7 @@ def pmc_traffic(kernel, W):
     if d.get("walkers") != W:
         return None, None
     symbol = {"plik_quadform_ksplit": "quadform_ksplit",                    # profiler label -> kernel
-              "cmbl_window_kernel": "cmbl_window_kernel<false, false>"}.get(kernel, kernel)
+              "cmbl_window_kernel": "cmbl_window_direct"}.get(kernel, kernel)
     t = d["per_launch"].get(symbol)
     if not t:
         return None, None

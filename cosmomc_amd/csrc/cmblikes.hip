@@ -42,6 +42,9 @@ static constexpr int WK_CHUNK = 64;             // l per chunk
 #endif
 static constexpr int WK_NCH = CMAMD_WK_NCH;     // chunks per work item
 static constexpr int WK_TS = WK_CHUNK + 2;      // LDS row stride of the spectrum tile (doubles)
+static constexpr int SMALL_NX = 64;
+static constexpr int SMALL_WT = 4;          // walkers per workgroup (measured: 7.1 / 8.0 / 9.8 / 13.9 us for 4 / 2 / 8 / 16)
+static constexpr int SMALL_MAXTASK = 256;   // tasks per dataset
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
@@ -59,6 +62,7 @@ struct WItem {       // one (map pair, <= WK_NCH l chunks, <= WK_COLS window col
     int part;        // partial rows part .. part+ncol-1
     int nch;         // chunks of WK_CHUNK l
     long long woff;  // dense weights [nch][WK_CHUNK][WK_COLS] (zero padded)
+    long long woff2; // direct-kernel weights [nch][ncol blocks][16 columns][WK_CHUNK] (zero padded)
 };
 
 struct BKMap {       // per required map: bandpass samples and constants (Read_Bandpass :72-105)
@@ -73,6 +77,7 @@ struct CLDev {
     int nitem;
     const WItem *items;
     const double *wdense;
+    const double *wdirect;
     const CLPair *pairs;
     double aberration;
     int cal_index;                  // 0-based in DataParams, -1 none
@@ -354,6 +359,121 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
     }
 }
 
+// Window contraction without aberration or foregrounds (TBinWindows_bin
+// :1230-1256 on GetTheoryMapCls :1022-1052).  The spectrum operand comes
+// straight from global memory: lane (walker li, quarter kq) of a wave holds 8
+// consecutive l of its walker's spectrum, l = l0 + 32 st + 8 kq + s, and MFMA
+// step s contracts the four l {8 kq + s}; every load is a 16-byte vector and
+// the next step's spectra are in flight during this step's MFMAs.  The weights
+// (8 KB per 64 l) are shared by the block's four waves through a
+// double-buffered LDS tile: read per wave from L2 they cost 24.2 vs 17.7 us per
+// launch (lensing, W = 1024, MI355X).  The calibration (AdaptTheoryForMaps
+// :1113-1124, D_l / cal^2 for T/E/B pairs) is linear and is applied to the
+// sums.  Blocks are dealt to the 8 XCDs round-robin; the remap puts all walker
+// tiles of an item on one XCD so its weights are fetched into one L2 (17.9 vs
+// 18.7 us with the linear order).
+__global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double *__restrict__ dl, long long ld_field,
+                                                         long long ld_walker, const double *__restrict__ nuis,
+                                                         long long ld_nuis, double *__restrict__ partial, int W,
+                                                         int tiles, int vec_ok)
+{
+    constexpr int LPL = 8, STEP = 4 * LPL, NSUB = WK_CHUNK / STEP, WROW = STEP + 2;
+    __shared__ __attribute__((aligned(16))) double wsh[2 * 2 * 16 * WROW];   // [buf][col block][col][l]
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    const int item = xcd + 8 * (j / tiles), tile = j % tiles;
+    if (item >= c.nitem) return;
+    const WItem it = c.items[item];
+    const CLPair pr = c.pairs[it.pair];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, kq = lane >> 4;
+    const int w = tile * 64 + wave * 16 + li;
+    const int wl = min(w, W - 1);
+    const double *Df = dl + (long long)wl * ld_walker + (long long)pr.field * ld_field;
+    const int ncb = (it.ncol + 15) >> 4;
+    const int nstep = it.nch * NSUB;
+    double t[LPL], tn[LPL], a[LPL], a2[LPL];
+    auto load_t = [&](int st, double *dst) {
+        const int lb = it.l0 + st * STEP + LPL * kq;
+        if (vec_ok && lb + LPL - 1 <= it.l1) {
+            const double2 *src = reinterpret_cast<const double2 *>(Df + lb);
+#pragma unroll
+            for (int s = 0; s < LPL / 2; s++) {
+                const double2 v = src[s];
+                dst[2 * s] = v.x;
+                dst[2 * s + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < LPL; s++) dst[s] = (lb + s <= it.l1) ? Df[lb + s] : 0.0;
+        }
+    };
+    // weights [nch][ncb][16][WK_CHUNK]; thread tid moves column tid/16, l 2 (tid%16) .. +1
+    auto wsrc = [&](int st, int cb) {
+        const int ch = st / NSUB, sub = st % NSUB;
+        return c.wdirect + it.woff2 + ((long long)ch * ncb + cb) * 16 * WK_CHUNK + sub * STEP;
+    };
+    const int wc = tid >> 4, wp = 2 * (tid & 15);
+    double2 wr0, wr1;
+    auto fetch_w = [&](int st) {
+        wr0 = *reinterpret_cast<const double2 *>(wsrc(st, 0) + wc * WK_CHUNK + wp);
+        if (ncb > 1) wr1 = *reinterpret_cast<const double2 *>(wsrc(st, 1) + wc * WK_CHUNK + wp);
+    };
+    auto store_w = [&](int buf) {
+        *reinterpret_cast<double2 *>(wsh + ((buf * 2 + 0) * 16 + wc) * WROW + wp) = wr0;
+        if (ncb > 1) *reinterpret_cast<double2 *>(wsh + ((buf * 2 + 1) * 16 + wc) * WROW + wp) = wr1;
+    };
+    auto read_w = [&](int buf, int cb, double *dst) {   // A operand: column li, the lane's LPL l
+        const double *src = wsh + ((buf * 2 + cb) * 16 + li) * WROW + LPL * kq;
+#pragma unroll
+        for (int s = 0; s < LPL / 2; s++) {
+            const double2 v = *reinterpret_cast<const double2 *>(src + 2 * s);
+            dst[2 * s] = v.x;
+            dst[2 * s + 1] = v.y;
+        }
+    };
+    f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    load_t(0, t);
+    fetch_w(0);
+    store_w(0);
+    __syncthreads();
+    for (int st = 0; st < nstep; st++) {
+        const bool more = st + 1 < nstep;
+        const int cur = st & 1;
+        if (more) {                                    // in flight across this step's MFMAs
+            load_t(st + 1, tn);
+            fetch_w(st + 1);
+        }
+        read_w(cur, 0, a);
+        if (ncb > 1) read_w(cur, 1, a2);
+#pragma unroll
+        for (int s = 0; s < LPL; s++) acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], t[s], acc0, 0, 0, 0);
+        if (ncb > 1) {
+#pragma unroll
+            for (int s = 0; s < LPL; s++) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[s], t[s], acc1, 0, 0, 0);
+        }
+        if (more) {
+            store_w(cur ^ 1);      // buffer cur ^ 1 was last read before the previous barrier
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < LPL; s++) t[s] = tn[s];
+        }
+    }
+    if (w < W) {
+        double inv = 1.0;
+        if (c.cal_index >= 0 && pr.cmb) {
+            const double cl = nuis[(long long)w * ld_nuis + c.cal_index];
+            inv = cl * cl;
+        }
+        // D: walker = lane&15, column = (lane>>4) + 4 r
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int c0 = kq + 4 * r, c1 = 16 + kq + 4 * r;
+            if (c0 < it.ncol) partial[(long long)(it.part + c0) * W + w] = acc0[r] / inv;
+            if (c1 < it.ncol) partial[(long long)(it.part + c1) * W + w] = acc1[r] / inv;
+        }
+    }
+}
+
 // Binned spectra per (walker, element e = bin * ncl + cl): window columns in
 // window order (TBinWindows_bin :1230-1256), each column the l-chunk partials
 // in order, plus the linear correction (GetBinnedMapCls :981-995).  Gaussian:
@@ -426,9 +546,6 @@ __global__ __launch_bounds__(256) void cmbl_reduce_kernel(CLDev c, const double 
 // element are cut into tasks of <= 8 rows (host); groups take tasks
 // round-robin with all loads of a task in flight, then combine them per
 // element in task order (deterministic), then split the rows of M.
-static constexpr int SMALL_NX = 64;
-static constexpr int SMALL_WT = 8;          // walkers per workgroup
-static constexpr int SMALL_MAXTASK = 256;   // tasks per dataset
 struct SmallTask { int first, count; };      // rows e_*_rows[first .. first+count)
 struct SmallDev {
     int ntask;
@@ -437,18 +554,22 @@ struct SmallDev {
     const int *e_main_t, *e_corr_t;          // [nE+1] task ranges per element
 };
 
+template <int WT>
 __global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev sd, const double *__restrict__ partial,
                                                               const double *__restrict__ nuis, long long ld_nuis,
                                                               const double *__restrict__ M, double *__restrict__ out,
                                                               int W)
 {
-    __shared__ double tp[SMALL_MAXTASK][SMALL_WT];
-    __shared__ double xs[SMALL_NX][SMALL_WT];
-    __shared__ double red[32][SMALL_WT];
-    const int wl = threadIdx.x % SMALL_WT, g = threadIdx.x / SMALL_WT;
-    const int w = blockIdx.x * SMALL_WT + wl;
+    constexpr int NG = 256 / WT;             // thread groups of WT walkers
+    __shared__ double tp[SMALL_MAXTASK][WT];
+    __shared__ double xs[SMALL_NX][WT];
+    __shared__ double red[NG][WT];
+    __shared__ double Msh[SMALL_NX * SMALL_NX];
+    const int wl = threadIdx.x % WT, g = threadIdx.x / WT;
+    const int w = blockIdx.x * WT + wl;
+    for (int i = threadIdx.x; i < c.nX * c.nX; i += 256) Msh[i] = M[i];   // in flight with the partial loads
     const bool act = w < W;
-    for (int t = g; t < sd.ntask; t += 32) {
+    for (int t = g; t < sd.ntask; t += NG) {
         const SmallTask tk = sd.tasks[t];
         double v[8];
 #pragma unroll
@@ -460,7 +581,7 @@ __global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev
         tp[t][wl] = s;
     }
     __syncthreads();
-    for (int e = g; e < c.nE; e += 32) {
+    for (int e = g; e < c.nE; e += NG) {
         const int ix = c.e_to_x[e];
         if (ix < 0) continue;
         double s = c.e_main_const[e];
@@ -474,16 +595,16 @@ __global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev
     }
     __syncthreads();
     double part = 0.0;
-    for (int i = g; i < c.nX; i += 32) {
+    for (int i = g; i < c.nX; i += NG) {
         double y = 0.0;
-        for (int j = 0; j < c.nX; j++) y += M[i * c.nX + j] * xs[j][wl];
+        for (int j = 0; j < c.nX; j++) y += Msh[i * c.nX + j] * xs[j][wl];
         part += xs[i][wl] * y;
     }
     red[g][wl] = part;
     __syncthreads();
     if (g == 0 && act) {
         double chisq = 0.0;
-        for (int k = 0; k < 32; k++) chisq += red[k][wl];
+        for (int k = 0; k < NG; k++) chisq += red[k][wl];
         if (c.log_cal_prior > 0 && c.cal_index >= 0) {
             const double t = log(nuis[(long long)w * ld_nuis + c.cal_index]) / c.log_cal_prior;
             chisq = chisq + t * t;
@@ -750,7 +871,7 @@ struct CMBLikes final : Like {
     // device tables
     CLDev dev{};
     HLDev hl{};
-    DevBuf d_pairs, d_items, d_wts, d_sumoff, d_sumcols, d_sumconst, d_corroff, d_corrcols, d_corrconst,
+    DevBuf d_pairs, d_items, d_wts, d_wdir, d_sumoff, d_sumcols, d_sumconst, d_corroff, d_corrcols, d_corrconst,
         d_etox, d_fidcorr, d_noise, d_chat, d_cluse, d_bkmaps, d_bpnu, d_bpR, d_bpdnu, d_hlchat, d_hlcf;
     int max_field = 0, n_part_rows = 0;
     bool items_even = true, small_gauss = false;
@@ -1203,7 +1324,7 @@ struct CMBLikes final : Like {
         if (cw.present) add_windows(cw, e_corr);
         // work items: per pair, per l chunk, the overlapping columns in groups of WK_COLS
         std::vector<WItem> items;
-        std::vector<double> wdense;
+        std::vector<double> wdense, wdirect;
         std::vector<std::vector<int>> col_parts(cols.size());
         int nrows = 0;
         const int SEG = WK_CHUNK * WK_NCH;
@@ -1234,6 +1355,15 @@ struct CMBLikes final : Like {
                     for (int l = lo; l < lo + it.nch * WK_CHUNK; l++)   // [nch][WK_CHUNK][WK_COLS], zero padded
                         for (int g = 0; g < WK_COLS; g++)
                             wdense.push_back(l <= hi && g0 + g < g1 ? cols[sel[g0 + g]].W[l] : 0.0);
+                    it.woff2 = (long long)wdirect.size();
+                    const int ncb = (it.ncol + 15) / 16;
+                    for (int ch = 0; ch < it.nch; ch++)         // [nch][ncb][16][WK_CHUNK], zero padded
+                        for (int cb = 0; cb < ncb; cb++)
+                            for (int g = 16 * cb; g < 16 * cb + 16; g++)
+                                for (int k = 0; k < WK_CHUNK; k++) {
+                                    const int l = lo + ch * WK_CHUNK + k;
+                                    wdirect.push_back(l <= hi && g0 + g < g1 ? cols[sel[g0 + g]].W[l] : 0.0);
+                                }
                     for (size_t g = g0; g < g1; g++) col_parts[sel[g]].push_back(nrows++);
                     items.push_back(it);
                 }
@@ -1302,6 +1432,7 @@ struct CMBLikes final : Like {
         up(d_pairs, pairs.data(), pairs.size() * sizeof(CLPair));
         up(d_items, items.data(), items.size() * sizeof(WItem));
         up(d_wts, wdense.data(), wdense.size() * 8);
+        up(d_wdir, wdirect.data(), wdirect.size() * 8);
         up(d_sumoff, main_off.data(), main_off.size() * 4);
         up(d_sumcols, main_rows.data(), main_rows.size() * 4);
         up(d_sumconst, main_cst.data(), main_cst.size() * 8);
@@ -1334,6 +1465,7 @@ struct CMBLikes final : Like {
         dev.nitem = (int)items.size();
         dev.items = d_items.as<WItem>();
         dev.wdense = d_wts.as<double>();
+        dev.wdirect = d_wdir.as<double>();
         dev.pairs = d_pairs.as<CLPair>();
         dev.aberration = aberration;
         dev.cal_index = cal_index;
@@ -1402,6 +1534,7 @@ struct CMBLikes final : Like {
         }
         const WsLayout o = layout(W);
         char *base = static_cast<char *>(ws);
+        void *qws = ws;
         double *partial = reinterpret_cast<double *>(base + o.part);
         double *cmat = reinterpret_cast<double *>(base + o.cmat);
         double *coef = reinterpret_cast<double *>(base + o.coef);
@@ -1420,6 +1553,14 @@ struct CMBLikes final : Like {
         // 16-byte theory loads need aligned rows and even chunk starts
         bool vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0 &&
                       items_even && (lmax + 1 < ld_field || (lmax % 2 == 1 && lmax + 1 <= ld_field));
+        static const bool staged = std::getenv("CMAMD_WINDOW_STAGED") != nullptr;   // A/B measurement switch
+        if (!bk && aberration == 0.0 && !staged) {
+            const int nblk = 8 * tiles * ((dev.nitem + 7) / 8);
+            timed_launch("cmbl_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+                hipExtLaunchKernelGGL(cmbl_window_direct, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, dev, dl,
+                                      ld_field, ld_walker, nu, ld_nuis, partial, W, tiles, (int)vec_ok);
+            });
+        } else
         timed_launch("cmbl_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
 #define CMBL_WINDOW(A, F)                                                                                        \
     hipExtLaunchKernelGGL(cmbl_window_kernel<A, F>, dim3(tiles, dev.nitem), dim3(256), 0, stream, e0, e1, 0, dev, dl, \
@@ -1438,27 +1579,32 @@ struct CMBLikes final : Like {
         HIP_CHECK(hipGetLastError());
         if (small_gauss) {
             timed_launch("cmbl_gauss_small_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                hipExtLaunchKernelGGL(cmbl_gauss_small_kernel, dim3((W + SMALL_WT - 1) / SMALL_WT), dim3(256), 0,
-                                      stream, e0, e1, 0, dev, sdev, (const double *)partial, nu, ld_nuis,
-                                      d_invcov.as<double>(), out, W);
+                static const int wt = std::getenv("CMAMD_SMALL_WT") ? atoi(std::getenv("CMAMD_SMALL_WT")) : SMALL_WT;
+#define CMBL_SMALL(T)                                                                                             \
+    hipExtLaunchKernelGGL(cmbl_gauss_small_kernel<T>, dim3((W + T - 1) / T), dim3(256), 0, stream, e0, e1, 0, dev, \
+                          sdev, (const double *)partial, nu, ld_nuis, d_invcov.as<double>(), out, W)
+                if (wt == 2) CMBL_SMALL(2);
+                else if (wt == 8) CMBL_SMALL(8);
+                else CMBL_SMALL(4);
+#undef CMBL_SMALL
             });
             HIP_CHECK(hipGetLastError());
             return;
         }
         timed_launch("cmbl_reduce_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
             hipExtLaunchKernelGGL(cmbl_reduce_kernel, dim3(tiles, dev.nE), dim3(256), 0, stream, e0, e1, 0, dev,
-                                  (const double *)partial, nu, ld_nuis, qf.x_rows(ws), cmat, use_add ? addend : nullptr,
-                                  qf.counters(ws, W), qf.n_counters(W), W);
+                                  (const double *)partial, nu, ld_nuis, qf.x_rows(qws), cmat, use_add ? addend : nullptr,
+                                  qf.counters(qws, W), qf.n_counters(W), W);
         });
         HIP_CHECK(hipGetLastError());
         if (approx == 1) {
             timed_launch("cmbl_hl_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
                 hipExtLaunchKernelGGL(cmbl_hl_kernel, dim3(W * nb), dim3(64), 0, stream, e0, e1, 0, hl,
-                                      (const double *)cmat, qf.x_rows(ws), W);
+                                      (const double *)cmat, qf.x_rows(qws), W);
             });
             HIP_CHECK(hipGetLastError());
         }
-        qf.launch(W, ws, use_add ? addend : nullptr, out, stream, "cmbl_quadform");
+        qf.launch(W, qws, use_add ? addend : nullptr, out, stream, "cmbl_quadform");
     }
 };
 

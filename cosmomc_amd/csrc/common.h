@@ -50,7 +50,10 @@ struct DevBuf {
     ~DevBuf() { release(); }
     void alloc(size_t n) {
         release();
-        if (n) HIP_CHECK(hipMalloc(&p, n));
+        if (n) {
+            HIP_CHECK(hipMalloc(&p, n));
+            HIP_CHECK(hipMemset(p, 0, n));
+        }
         bytes = n;
     }
     void grow(size_t n) {

@@ -34,16 +34,20 @@ struct BinInfo {
     int pad;
 };
 
-struct FieldRanges {   // per used field: l range staged in LDS (even-aligned)
-    int lo[3], hi[3], off[3];
+struct FieldRanges {   // per used field: l range staged in LDS (even-aligned), its bins [b0, b1)
+    int lo[3], hi[3], b0[3], b1[3];
 };
 
-// Binning + residual.  One workgroup per walker: the walker's TT/TE/EE D_l
-// rows are read once (16-byte loads when the layout allows), multiplied by the
-// plik weights and kept in LDS; each thread then sums whole bins in l order
-// (the reference's dot_product order) and writes Delta = X - cl / cal^2.
-// Block 0 also zeroes the split-K arrival counters of the quadratic-form
-// kernel that follows on the same stream.
+// Binning + residual.  One workgroup per (walker, field): the field's D_l row
+// is read once (16-byte loads when the layout allows; issuing all of a thread's
+// loads up front measured no faster),
+// multiplied by the plik weights and kept in LDS; each thread then sums whole
+// bins in l order (the reference's dot_product order) and writes
+// Delta = X - cl / cal^2 for the field's bins.  Per-field blocks need at most
+// 20 KB of LDS, so a W = 1024 launch (3072 blocks) runs in even rounds (one
+// 51 KB block per walker: 768 resident, a 1.33-round tail).  Block (0, 0) also
+// zeroes the split-K arrival counters of the quadratic-form kernel that
+// follows on the same stream and the Delta padding.
 __global__ __launch_bounds__(256) void plik_bin_delta(
     const double *__restrict__ dl, long long ld_field, long long ld_walker,
     const double *__restrict__ nuis, long long ld_nuis,
@@ -53,45 +57,39 @@ __global__ __launch_bounds__(256) void plik_bin_delta(
     double *__restrict__ delta, unsigned int *__restrict__ counters, int n_counters)
 {
     extern __shared__ __attribute__((aligned(16))) double prod[];
-    const int w = blockIdx.x;
+    const int w = blockIdx.x, f = blockIdx.y;
     const int tid = threadIdx.x;
-    if (w == 0)
-        for (int i = tid; i < n_counters; i += blockDim.x) counters[i] = 0u;
-    const double *D = dl + (long long)w * ld_walker;
-#pragma unroll
-    for (int f = 0; f < 3; f++) {
-        const int lo = fr.lo[f], hi = fr.hi[f];
-        if (hi < lo) continue;
-        const double *Df = D + f * ld_field;
-        double *P = prod + fr.off[f] - lo;
-        if (vec_ok) {
-            // lo is even; pairs (l, l+1), l <= hi (hi odd after alignment)
+    double *out = delta + (long long)w * Np;
+    if (f == 0) {
+        if (w == 0)
+            for (int i = tid; i < n_counters; i += blockDim.x) counters[i] = 0u;
+        for (int i = nused + tid; i < Np; i += blockDim.x) out[i] = 0.0;
+    }
+    const int lo = fr.lo[f], hi = fr.hi[f];
+    if (hi < lo) return;
+    const double *Df = dl + (long long)w * ld_walker + f * ld_field;
+    double *P = prod - lo;
+    if (vec_ok) {
+        // lo is even, hi odd: pairs (l, l+1)
 #pragma unroll 4
-            for (int l = lo + 2 * tid; l <= hi; l += 2 * blockDim.x) {
-                const double2 d = *reinterpret_cast<const double2 *>(Df + l);
-                const double2 q = *reinterpret_cast<const double2 *>(wts + l);
-                *reinterpret_cast<double2 *>(P + l) = make_double2(d.x * q.x, d.y * q.y);
-            }
-        } else {
-            const int hs = hi < ld_field ? hi : (int)ld_field - 1;   // never read past the row
-#pragma unroll 4
-            for (int l = lo + tid; l <= hs; l += blockDim.x) P[l] = Df[l] * wts[l];
+        for (int l = lo + 2 * tid; l <= hi; l += 2 * blockDim.x) {
+            const double2 d = *reinterpret_cast<const double2 *>(Df + l);
+            const double2 q = *reinterpret_cast<const double2 *>(wts + l);
+            *reinterpret_cast<double2 *>(P + l) = make_double2(d.x * q.x, d.y * q.y);
         }
+    } else {
+        const int hs = hi < ld_field ? hi : (int)ld_field - 1;   // never read past the row
+#pragma unroll 4
+        for (int l = lo + tid; l <= hs; l += blockDim.x) P[l] = Df[l] * wts[l];
     }
     __syncthreads();
     const double cal = nuis[(long long)w * ld_nuis];
     const double c2 = cal * cal;
-    double *out = delta + (long long)w * Np;
-    for (int i = tid; i < Np; i += blockDim.x) {
-        double d = 0.0;
-        if (i < nused) {
-            const BinInfo b = bins[i];
-            const double *p = prod + fr.off[b.field] - fr.lo[b.field];
-            double acc = 0.0;
-            for (int l = b.lmin; l <= b.lmax; l++) acc += p[l];
-            d = X[i] - acc / c2;
-        }
-        out[i] = d;
+    for (int i = fr.b0[f] + tid; i < fr.b1[f]; i += blockDim.x) {
+        const BinInfo b = bins[i];
+        double acc = 0.0;
+        for (int l = b.lmin; l <= b.lmax; l++) acc += P[l];
+        out[i] = X[i] - acc / c2;
     }
 }
 
@@ -274,17 +272,20 @@ struct PlikLite final : Like {
         for (int f = 0; f < 3; f++) {
             fr.lo[f] = 1 << 30;
             fr.hi[f] = -1;
+            fr.b0[f] = fr.b1[f] = 0;
         }
-        for (auto &b : binfo) {
+        for (size_t i = 0; i < binfo.size(); i++) {   // bins are in field order
+            const auto &b = binfo[i];
+            if (fr.hi[b.field] < 0) fr.b0[b.field] = (int)i;
+            fr.b1[b.field] = (int)i + 1;
             fr.lo[b.field] = std::min(fr.lo[b.field], b.lmin);
             fr.hi[b.field] = std::max(fr.hi[b.field], b.lmax);
         }
         for (int f = 0; f < 3; f++) {
-            fr.off[f] = lds_doubles;
             if (fr.hi[f] >= fr.lo[f]) {
                 fr.lo[f] &= ~1;
                 fr.hi[f] |= 1;
-                lds_doubles += fr.hi[f] - fr.lo[f] + 1;
+                lds_doubles = std::max(lds_doubles, fr.hi[f] - fr.lo[f] + 1);
             } else {
                 fr.lo[f] = 0;
                 fr.hi[f] = -1;
@@ -328,7 +329,7 @@ struct PlikLite final : Like {
         for (int f = 0; f < 3; f++)
             if (fr.hi[f] >= fr.lo[f] && fr.hi[f] >= ld_field) vec_ok = 0;
         timed_launch("plik_bin_delta", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(plik_bin_delta, dim3(W), dim3(256), (size_t)lds_doubles * 8, stream, e0, e1, 0, dl, ld_field,
+            hipExtLaunchKernelGGL(plik_bin_delta, dim3(W, 3), dim3(256), (size_t)lds_doubles * 8, stream, e0, e1, 0, dl, ld_field,
                                ld_walker, nuis, ld_nuis, d_wts.as<double>(), d_bins.as<BinInfo>(), d_X.as<double>(),
                                nused, Np, fr, vec_ok, delta, counters, qf.n_counters(W));
         });

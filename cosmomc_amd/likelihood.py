@@ -88,6 +88,8 @@ class NativeCMBLikelihood(DataLikelihood):
         dl   : cuda float64 tensor [W, 10, L] (or [W, nf>=3, L] for plik_lite),
                D_l in muK^2 indexed from l = 0 (field order TT TE EE BT BE BB PT PE PB PP)
         nuis : cuda float64 tensor [W, n_nuis] (DataParams)
+        workspace : optional cuda tensor of >= workspace_bytes(W) bytes; default:
+               the handle's own
         """
         import torch
         W = dl.shape[0]
