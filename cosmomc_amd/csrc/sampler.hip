@@ -30,7 +30,10 @@ static constexpr double LOGZERO = CMBL_LOGZERO;
 static constexpr int MAXP = 64;        // max parameters per chain
 static constexpr int MAXBLK = 32;      // max block size
 static constexpr int NB = 64;          // walkers per mh_kernel block (one wavefront of chain logic)
-static constexpr int MH_WAVES = 4;     // waves per mh_kernel block sharing the state staging
+#ifndef CMAMD_MH_WAVES
+#define CMAMD_MH_WAVES 4
+#endif
+static constexpr int MH_WAVES = CMAMD_MH_WAVES;   // waves per mh_kernel block sharing the state staging
 
 // strided per-walker column view (LDS: stride NB; HBM: stride W)
 template <class T> struct Col {

@@ -19,7 +19,8 @@ OUT = os.path.join(ROOT, "tools", "_stamps")
 if __name__ == "__main__":
     if "--no-build" not in sys.argv:
         subprocess.run(["make", "-C", os.path.join(ROOT, "cosmomc_amd", "csrc"), "-j8", f"OUT={OUT}",
-                        "EXTRA=-DCMAMD_STAMPS"], check=True, stdout=subprocess.DEVNULL)
+                        "EXTRA=-DCMAMD_STAMPS " + os.environ.get("STAMP_EXTRA", "")], check=True,
+                       stdout=subprocess.DEVNULL)
     os.environ["COSMOMC_AMD_LIB"] = os.path.join(OUT, "libcosmomc_amd.so")
     sys.path.insert(0, ROOT)
     import torch
