@@ -90,7 +90,8 @@ int cmbl_open(const char *tag, const char *dataset_path, const char *override_in
         std::string t(tag);
         // tag -> likelihood class as CMBLikelihood_Add (source/CMB.f90:80-97)
         if (t == "PLIK_LITE") h->like = cmamd::make_plik_lite(ini);
-        else if (t == "WMAP" || t == "SPTPOL_TEEE" || t == "SPTPOL_BB" || t == "SMICA")
+        else if (t == "SPTPOL_TEEE" || t == "SPTPOL_BB") h->like = cmamd::make_sptpol(ini, t);   // CMB.f90:86-91
+        else if (t == "WMAP" || t == "SMICA")
             cmamd::fail(CMBL_ERR_UNSUPPORTED, "cmbl_open: dataset tag '%s' not supported yet", tag);
         else h->like = cmamd::make_cmblikes(ini, t);      // TCMBLikes, or TBK_planck for BKPLANCK
         *out = h.release();

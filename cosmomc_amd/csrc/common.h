@@ -173,6 +173,7 @@ struct Like {
 
 std::unique_ptr<Like> make_plik_lite(const Ini &ini);
 std::unique_ptr<Like> make_cmblikes(const Ini &ini, const std::string &tag);
+std::unique_ptr<Like> make_sptpol(const Ini &ini, const std::string &tag);   // SPTPOL_TEEE / SPTPOL_BB
 
 }  // namespace cmamd
 

@@ -240,3 +240,200 @@ def chain_ensemble(n_chains: int, n_samples: int, n: int, seed: int, spread: flo
     off = spread * g[n * n:n * n + n_chains * n].reshape(n_chains, n)
     z = g[n * n + n_chains * n:].reshape(n_chains, n_samples, n)
     return (off[:, None, :] + z) @ L.T
+
+
+# ---------------------------------------------------------------------------
+# SPTpol synthetic datasets.  The SPTpol 500d data files are not shipped with
+# the reference (no data/ directory or .ini refers to them), so the SPTPOL_TEEE
+# and SPTPOL_BB likelihoods are exercised on synthetic data written in the
+# exact on-disk formats their readers expect:
+#   SPTpol_TEEE_ReadIni / InitSPTpolData  source/CMB_SPTpol_TEEE_2017.f90:56-352
+#   SPTpol_BB_ReadIni / InitSPTpolBBData  source/CMB_SPTpol_BB_2019.f90:56-438
+# Shapes follow the published analyses (Henning et al. 2018: TE/EE, 56 bins,
+# 50 < l < 8000, two beam modes; Sayre et al. 2020: BB 150x150 / 95x150 /
+# 95x95, 7 bins, seven beam modes).
+
+def _smooth_windows(lmin: int, lmax: int, edges: list[tuple[int, int]]) -> np.ndarray:
+    """Dense window columns [lmax-lmin+1, nbin]: a sin^2-tapered top hat over
+    each bin widened by half a bin on both sides, normalised to unit sum."""
+    ell = np.arange(lmin, lmax + 1, dtype=np.float64)
+    out = np.zeros((ell.size, len(edges)))
+    for b, (lo, hi) in enumerate(edges):
+        w = hi - lo + 1
+        a, z = max(lmin, lo - w // 2), min(lmax, hi + w // 2)
+        m = (ell >= a) & (ell <= z)
+        x = (ell[m] - a + 0.5) / (z - a + 1.0)
+        v = np.sin(np.pi * x) ** 2
+        out[m, b] = v / v.sum()
+    return out
+
+
+def _spd_cov(vals: np.ndarray, g: np.ndarray, frac: float) -> np.ndarray:
+    n = vals.size
+    A = g[:n * n].reshape(n, n)
+    sig = frac * np.sqrt(vals ** 2 + (0.1 * np.sqrt(np.mean(vals ** 2))) ** 2)
+    M = np.eye(n) + 0.05 * (A @ A.T) / n
+    cov = sig[:, None] * M * sig[None, :]
+    return 0.5 * (cov + cov.T)
+
+
+@dataclass
+class SptpolTEEEData:
+    lmin: int
+    lmax: int
+    windows: np.ndarray     # [lmax-lmin+1, 2 nbin], TE columns then EE
+    spec: np.ndarray        # [3, nbin]  TE, EE, TT
+    cov: np.ndarray         # [2 nbin, 2 nbin]
+    beam_err: np.ndarray    # [2, 2 nbin]
+
+    PARAMS = ("kappa", "czero_psTE_150", "czero_psEE_150", "ADust_TE", "alphaDust_TE", "ADust_EE",
+              "alphaDust_EE", "mapTcal", "mapPcal", "beam1", "beam2")
+
+    @property
+    def nbin(self) -> int:
+        return self.spec.shape[1]
+
+    def write(self, directory: str, extra: dict | None = None) -> str:
+        d = os.path.abspath(directory)
+        os.makedirs(os.path.join(d, "sptpol_windows"), exist_ok=True)
+        nb, nall = self.nbin, 2 * self.nbin
+        with open(os.path.join(d, "sptpol_TEEE.desc"), "w") as f:
+            f.write(f"{nb} 1\n{self.lmin} {self.lmax}\n")
+        with open(os.path.join(d, "sptpol_TEEE_bp.txt"), "w") as f:
+            for i in range(3):
+                for j in range(nb):
+                    f.write(f"{j + 1} {self.spec[i, j]:.17e}\n")
+        # direct-access records of nall doubles, record i = cov(:, i)
+        np.ascontiguousarray(self.cov.T, dtype="<f8").tofile(os.path.join(d, "sptpol_TEEE_cov.bin"))
+        ell = np.arange(self.lmin, self.lmax + 1)
+        for i in range(nall):
+            np.savetxt(os.path.join(d, "sptpol_windows", f"window_{i + 1}"),
+                       np.column_stack([ell, self.windows[:, i]]), fmt=["%d", "%.17e"])
+        with open(os.path.join(d, "sptpol_TEEE_beam.txt"), "w") as f:
+            for t in range(self.beam_err.shape[0]):
+                for j in range(nall):
+                    f.write(f"{j + 1} {self.beam_err[t, j]:.17e}\n")
+        with open(os.path.join(d, "sptpol_TEEE.paramnames"), "w") as f:
+            for p in self.PARAMS:
+                f.write(f"{p}    {p}\n")
+        lines = [
+            "sptpol_TEEE_params_file = " + os.path.join(d, "sptpol_TEEE.paramnames"),
+            "sptpol_TEEE_desc_file = " + os.path.join(d, "sptpol_TEEE.desc"),
+            "sptpol_TEEE_bp_file = " + os.path.join(d, "sptpol_TEEE_bp.txt"),
+            "sptpol_TEEE_cov_file = " + os.path.join(d, "sptpol_TEEE_cov.bin"),
+            "sptpol_TEEE_window_dir = " + os.path.join(d, "sptpol_windows") + "/",
+            "sptpol_TEEE_beam_file = " + os.path.join(d, "sptpol_TEEE_beam.txt"),
+        ]
+        for k, v in (extra or {}).items():
+            lines.append(f"{k} = {v}")
+        path = os.path.join(d, "sptpol_TEEE.dataset")
+        with open(path, "w") as f:
+            f.write("\n".join(lines) + "\n")
+        return path
+
+
+def sptpol_teee_edges() -> list[tuple[int, int]]:
+    edges = [(51 + 50 * i, 100 + 50 * i) for i in range(50)]
+    edges += [(2551, 3000), (3001, 3500), (3501, 4000), (4001, 5000), (5001, 6500), (6501, 7950)]
+    return edges
+
+
+def make_sptpol_teee(seed: int = 2017) -> SptpolTEEEData:
+    lmin, lmax = 50, 8000
+    edges = sptpol_teee_edges()
+    nb = len(edges)
+    win1 = _smooth_windows(lmin, lmax, edges)
+    base = base_theory(lmax + 1)
+    g = gaussians(seed, 3 * nb + 4 * nb * nb + 4 * nb)
+    spec = np.zeros((3, nb))
+    for k, f in enumerate((FIELD_TE, FIELD_EE, FIELD_TT)):
+        spec[k] = (win1.T @ base[f, lmin:lmax + 1]) * (1.0 + 0.02 * g[k * nb:(k + 1) * nb])
+    cov = _spd_cov(spec[:2].ravel(), g[3 * nb:], 0.03)
+    beam = 0.01 * g[3 * nb + 4 * nb * nb:].reshape(2, 2 * nb)
+    return SptpolTEEEData(lmin, lmax, np.hstack([win1, win1]), spec, cov, beam)
+
+
+@dataclass
+class SptpolBBData:
+    lmin: int
+    lmax: int
+    eff_freqs: tuple        # eff dust frequencies (150 band first, decreasing)
+    edges: list
+    windows: np.ndarray     # [lmax-lmin+1, 3 nbin]: 150x150, 95x150, 95x95
+    spec: np.ndarray        # [3, nbin] same order
+    cov: np.ndarray         # [3 nbin, 3 nbin]
+    beam_err: np.ndarray    # [7, 3 nbin]
+    r_template: np.ndarray  # [lmax_t + 1] BB D_l of r = 1 tensors (l = 0..)
+
+    PARAMS = ("Abb", "r_sptpol", "const_bb", "Add_150", "Pois_150", "Pois_95x150", "Pois_95",
+              "MapBcal150", "MapBcal95") + tuple(f"bbbeam{i}" for i in range(1, 8))
+
+    @property
+    def nbin(self) -> int:
+        return self.spec.shape[1]
+
+    def write(self, directory: str, extra: dict | None = None, with_r_template: bool = True) -> str:
+        d = os.path.abspath(directory)
+        os.makedirs(d, exist_ok=True)
+        nb, nall = self.nbin, 3 * self.nbin
+        with open(os.path.join(d, "sptpol_BB.desc"), "w") as f:
+            f.write(f"{nb} 2\n{self.lmin} {self.lmax}\n{self.eff_freqs[0]!r}\n{self.eff_freqs[1]!r}\n")
+        with open(os.path.join(d, "sptpol_BB_bp.txt"), "w") as f:
+            f.write("# lcenter lmin lmax BB_95x95 BB_95x150 BB_150x150\n")
+            for b, (lo, hi) in enumerate(self.edges):
+                f.write(f"{(lo + hi) / 2:.1f} {lo} {hi} {self.spec[2, b]:.17e} {self.spec[1, b]:.17e} "
+                        f"{self.spec[0, b]:.17e}\n")
+        np.ascontiguousarray(self.cov.T, dtype="<f8").tofile(os.path.join(d, "sptpol_BB_cov.bin"))
+        with open(os.path.join(d, "sptpol_BB_windows.bin"), "wb") as f:
+            f.write(np.array([self.lmin, self.lmax], dtype="<i4").tobytes())
+            f.write(np.asfortranarray(self.windows, dtype="<f8").tobytes(order="F"))
+        with open(os.path.join(d, "sptpol_BB_beam.bin"), "wb") as f:
+            f.write(np.array([nall, self.beam_err.shape[0]], dtype="<i4").tobytes())
+            f.write(np.ascontiguousarray(self.beam_err, dtype="<f8").tobytes())
+        with open(os.path.join(d, "sptpol_BB.paramnames"), "w") as f:
+            for p in self.PARAMS:
+                f.write(f"{p}    {p}\n")
+        lines = [
+            "sptpol_BB_params_file = " + os.path.join(d, "sptpol_BB.paramnames"),
+            "sptpol_BB_desc_file = " + os.path.join(d, "sptpol_BB.desc"),
+            "sptpol_BB_bp_file = " + os.path.join(d, "sptpol_BB_bp.txt"),
+            "sptpol_BB_cov_file = " + os.path.join(d, "sptpol_BB_cov.bin"),
+            "sptpol_BB_window_file = " + os.path.join(d, "sptpol_BB_windows.bin"),
+            "sptpol_BB_beam_file = " + os.path.join(d, "sptpol_BB_beam.bin"),
+        ]
+        if with_r_template:
+            tp = os.path.join(d, "r_template_totcls.dat")
+            with open(tp, "w") as f:
+                f.write("#    L    TT             EE             BB             TE\n")
+                for l in range(2, self.r_template.size):
+                    t = self.r_template[l]
+                    f.write(f"{l:5d} {40 * t:.8e} {0.5 * t:.8e} {t:.8e} {3 * t:.8e}\n")
+            lines.append("r_template_file = " + tp)
+        with open(os.path.join(d, "sptpol_blind_abb.bin"), "wb") as f:
+            f.write(np.array([0.0125], dtype="<f8").tobytes())
+        for k, v in (extra or {}).items():
+            lines.append(f"{k} = {v}")
+        path = os.path.join(d, "sptpol_BB.dataset")
+        with open(path, "w") as f:
+            f.write("\n".join(lines) + "\n")
+        return path
+
+
+def make_sptpol_bb(seed: int = 2019) -> SptpolBBData:
+    lmin, lmax = 50, 2350
+    edges = [(51, 250), (251, 500), (501, 750), (751, 1000), (1001, 1350), (1351, 1800), (1801, 2300)]
+    nb = len(edges)
+    win1 = _smooth_windows(lmin, lmax, edges)
+    base = base_theory(lmax + 1)
+    g = gaussians(seed, 3 * nb + 9 * nb * nb + 21 * nb)
+    spec = np.zeros((3, nb))
+    fg = (0.06, 0.12, 0.25)                  # rough foreground excess per band
+    for k in range(3):
+        spec[k] = (win1.T @ base[FIELD_BB, lmin:lmax + 1]) * (1.0 + fg[k]) * (1.0 + 0.05 * g[k * nb:(k + 1) * nb])
+    cov = _spd_cov(spec.ravel(), g[3 * nb:], 0.08)
+    beam = 0.005 * g[3 * nb + 9 * nb * nb:].reshape(7, 3 * nb)
+    lt = 3000
+    ell = np.arange(lt + 1, dtype=np.float64)
+    rt = np.zeros(lt + 1)
+    rt[2:] = 0.06 * (ell[2:] / 80.0) ** 1.0 * np.exp(-(ell[2:] / 120.0) ** 1.5)
+    return SptpolBBData(lmin, lmax, (152.3, 96.2), edges, np.hstack([win1, win1, win1]), spec, cov, beam, rt)

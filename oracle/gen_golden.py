@@ -41,8 +41,13 @@ def run_cmb_harness(ini_text: str, theory: np.ndarray, nuis: np.ndarray, workdir
     cmd = [os.path.join(REF_DIR, "plik_harness"), ini, th, nu, str(W), str(nl - 1), str(nfield),
            str(nuis.shape[1]), out]
     env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
+    if os.path.exists(out):
+        os.remove(out)                # a Fortran STOP exits 0: never read a stale result
     subprocess.run(cmd, check=True, cwd=workdir, env=env, stdout=subprocess.DEVNULL)
-    return np.loadtxt(out, ndmin=1)
+    res = np.loadtxt(out, ndmin=1)
+    if res.size != W:
+        raise RuntimeError(f"reference harness wrote {res.size} of {W} results")
+    return res
 
 
 PLIK_CASES = [
@@ -263,6 +268,71 @@ def gen_cmblikes():
         json.dump(out, f, indent=1)
 
 
+# SPTpol cases on the synthetic datasets (cosmomc_amd.synthetic.make_sptpol_*):
+# (name, tag, dataset overrides, walkers)
+SPTPOL_CASES = [
+    ("teee_default", "SPTPOL_TEEE", {}, 4),
+    ("teee_aberration_priors", "SPTPOL_TEEE",
+     {"correct_aberration": "T", "sptpol_tcal_prior": "T", "sptpol_meanTcal": "1.001", "sptpol_sigmaTcal": "0.0034",
+      "sptpol_pcal_prior": "T", "sptpol_kappa_prior": "T", "sptpol_alphaEE_prior": "T", "sptpol_alphaTE_prior": "T",
+      "sptpol_meanAlphaTE": "-2.3"}, 4),
+    ("teee_EEonly", "SPTPOL_TEEE", {"sptpol_EEonly": "T"}, 3),
+    ("teee_TEonly", "SPTPOL_TEEE", {"sptpol_TEonly": "T", "correct_aberration": "T"}, 3),
+    ("bb_default", "SPTPOL_BB", {}, 4),
+    ("bb_priors_blind_abb", "SPTPOL_BB",
+     {"sptpol_cal_prior": "T", "sptpol_invCal_90x150": "0.0001", "sptpol_Add_prior": "T", "sptpol_blind_abb": "T",
+      "sptpol_blind_abb_file": "@DIR@/sptpol_blind_abb.bin"}, 4),
+    ("bb_drop_90x150", "SPTPOL_BB", {"sptpol_drop_90x150ghz": "T"}, 3),
+    ("bb_no_r_template", "SPTPOL_BB", {"r_template_file": ""}, 3),
+]
+SPTPOL_LMAX = {"SPTPOL_TEEE": 8001, "SPTPOL_BB": 2351}
+
+
+def sptpol_nuisance(tag, W, seed):
+    if tag == "SPTPOL_TEEE":
+        g = syn.gaussians(seed, W * 11).reshape(W, 11)
+        c = np.array([0.0, 0.1, 0.05, 0.1, -2.42, 0.05, -2.42, 1.0, 1.0, 0.0, 0.0])
+        s = np.array([0.001, 0.02, 0.02, 0.02, 0.05, 0.01, 0.05, 0.005, 0.02, 1.0, 1.0])
+        return c[None, :] + g * s[None, :]
+    g = syn.gaussians(seed, W * 16).reshape(W, 16)
+    c = np.array([1.0, 0.0, 0.0, 0.0132, 0.05, 0.03, 0.02, 1.0, 1.0] + [0.0] * 7)
+    s = np.array([0.05, 0.01, 0.001, 0.003, 0.01, 0.01, 0.01, 0.01, 0.01] + [1.0] * 7)
+    P = c[None, :] + g * s[None, :]
+    P[0, 0] = 1.0            # Abb == 1: no scaling branch
+    if W > 1:
+        P[1, 0] = 0.0        # Abb == 0: theory zeroed
+    return P
+
+
+def sptpol_dataset(tag, td):
+    d = os.path.join(td, tag)
+    if tag == "SPTPOL_TEEE":
+        return syn.make_sptpol_teee().write(d)
+    return syn.make_sptpol_bb().write(d)
+
+
+def gen_sptpol():
+    out = {"theory_seed": 0xC05A0C, "generator": "cosmomc_amd.synthetic.make_sptpol_teee / make_sptpol_bb",
+           "cases": {}}
+    with tempfile.TemporaryDirectory() as td:
+        paths = {t: sptpol_dataset(t, td) for t in SPTPOL_LMAX}
+        for ci, (name, tag, over, W) in enumerate(SPTPOL_CASES):
+            lmax = SPTPOL_LMAX[tag]
+            th = syn.walker_theory(W, seed=out["theory_seed"] + 100 * ci, lmax=lmax,
+                                   n_fields=3 if tag == "SPTPOL_TEEE" else 6)
+            nu = sptpol_nuisance(tag, W, 5150 + ci)
+            dsdir = os.path.dirname(paths[tag])
+            ini = f"cmb_dataset[{tag}] = {paths[tag]}\n" + \
+                "".join(f"cmb_dataset[{tag},{k}] = {v.replace('@DIR@', dsdir)}\n" for k, v in over.items())
+            ref = run_cmb_harness(ini, th, nu, td)
+            out["cases"][name] = {"tag": tag, "overrides": over, "walkers": W, "lmax": lmax,
+                                  "theory_seed": out["theory_seed"] + 100 * ci, "nuis": nu.tolist(),
+                                  "minus_lnL": ref.tolist()}
+            print(f"{name:28s} -lnL = {ref}")
+    with open(os.path.join(GOLDEN, "sptpol_ref.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
     if not os.path.exists(os.path.join(REF_DIR, "plik_harness")):
         sys.exit("build the reference first: make -C oracle ref")
@@ -275,3 +345,5 @@ if __name__ == "__main__":
         gen_gr()
     if not only or "cmblikes" in only:
         gen_cmblikes()
+    if not only or "sptpol" in only:
+        gen_sptpol()

@@ -54,3 +54,24 @@ def refdata(tmp_path_factory):
         except TypeError:
             tar.extractall(d)
     return d
+
+
+@pytest.fixture(scope="session")
+def sptpol_golden():
+    return load_golden("sptpol_ref.json")
+
+
+@pytest.fixture(scope="session")
+def sptpol_data(tmp_path_factory):
+    """The synthetic SPTpol TEEE / BB datasets (cosmomc_amd.synthetic) written
+    once per session: {tag: dataset path}."""
+    from cosmomc_amd import synthetic as syn
+    d = str(tmp_path_factory.mktemp("sptpol"))
+    return {"SPTPOL_TEEE": syn.make_sptpol_teee().write(os.path.join(d, "SPTPOL_TEEE")),
+            "SPTPOL_BB": syn.make_sptpol_bb().write(os.path.join(d, "SPTPOL_BB"))}
+
+
+def sptpol_overrides(case, dataset):
+    """Golden-case overrides with @DIR@ -> the dataset's directory."""
+    d = os.path.dirname(dataset)
+    return {k: v.replace("@DIR@", d) for k, v in case["overrides"].items()}

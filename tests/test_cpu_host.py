@@ -31,14 +31,26 @@ def test_open_missing_file_returns_error_code():
 
 def test_open_tag_dispatch(tmp_path):
     """CMBLikelihood_Add (CMB.f90:80-97): unknown tags are CMBlikes datasets;
-    SPTpol / SMICA / WMAP are not built yet."""
+    SPTpol datasets need their sptpol_* keys; SMICA / WMAP are not built."""
     p = tmp_path / "a.dataset"
     p.write_text("name = x\n")
     h = C.c_void_p()
     err = C.create_string_buffer(256)
     assert N.lib().cmbl_open(b"WHATEVER", str(p).encode(), None, C.byref(h), err, 256) == -3   # not a CMBlikes dataset
     assert b"fields_use" in err.value
-    assert N.lib().cmbl_open(b"SPTPOL_TEEE", str(p).encode(), None, C.byref(h), err, 256) == -6
+    assert N.lib().cmbl_open(b"SPTPOL_TEEE", str(p).encode(), None, C.byref(h), err, 256) == -3
+    assert b"sptpol_TEEE_params_file" in err.value
+    assert N.lib().cmbl_open(b"SMICA", str(p).encode(), None, C.byref(h), err, 256) == -6
+
+
+def test_sptpol_blind_r_rejected(tmp_path):
+    """sptpol_blind_r needs CMB%InitPower(amp_ratio_index) (CMB_SPTpol_BB_2019.f90:585-586),
+    which the batched interface does not carry: refused with CMBL_ERR_UNSUPPORTED."""
+    ds = syn.make_sptpol_bb().write(str(tmp_path))
+    h = C.c_void_p()
+    err = C.create_string_buffer(256)
+    rc = N.lib().cmbl_open(b"SPTPOL_BB", ds.encode(), b"sptpol_blind_r = T\n", C.byref(h), err, 256)
+    assert rc == -6 and b"sptpol_blind_r" in err.value
 
 
 def test_null_arguments_rejected():
