@@ -437,3 +437,61 @@ def make_sptpol_bb(seed: int = 2019) -> SptpolBBData:
     rt = np.zeros(lt + 1)
     rt[2:] = 0.06 * (ell[2:] / 80.0) ** 1.0 * np.exp(-(ell[2:] / 120.0) ** 1.5)
     return SptpolBBData(lmin, lmax, (152.3, 96.2), edges, np.hstack([win1, win1, win1]), spec, cov, beam, rt)
+
+
+# ---------------------------------------------------------------------------
+# BK15 (BASELINE configs[4]): the reference ships data/BK15 without its
+# bandpower covariance (BK15_dust.dataset: covmat_fiducial = BK15_covmat_dust.dat
+# is absent), so a synthetic SPD covariance of the file's shape is written next
+# to the real files: (300 spectra x 9 bins)^2, text, bin-major as ReadCovmat
+# expects (CMBlikes.f90:785-795).  The 78 B x B spectra (the BK15.ini B-only
+# selection) carry a dense correlated block across all bins; every other
+# spectrum is diagonal, so any map selection stays positive definite.
+
+def _bk15_order(dataset_path: str) -> list[str]:
+    with open(dataset_path) as f:
+        for line in f:
+            s = line.strip()
+            if s.startswith("covmat_cl"):
+                return s.split("=", 1)[1].split()
+    raise ValueError("covmat_cl missing in " + dataset_path)
+
+
+def write_bk15_covmat(bk15_dir: str, seed: int = 1515, rank: int = 24) -> str:
+    """Write BK15_covmat_dust.dat into ``bk15_dir`` (the extracted data/BK15)."""
+    order = _bk15_order(os.path.join(bk15_dir, "BK15_dust.dataset"))
+    ncl, nbin = len(order), 9
+    fid = np.loadtxt(os.path.join(bk15_dir, "BK15_fiducial_dust.dat"), ndmin=2)[:nbin, 1:ncl + 1]
+    noi = np.loadtxt(os.path.join(bk15_dir, "BK15_noise.dat"), ndmin=2)[:nbin, 1:ncl + 1]
+    # sigma of spectrum A x B ~ 0.15 sqrt((C_AA + N_AA)(C_BB + N_BB)) (Knox-like scaling)
+    auto = {c.split("x")[0]: i for i, c in enumerate(order) if c.split("x")[0] == c.split("x")[1]}
+    tot = np.abs(fid) + np.abs(noi)
+    scale = np.empty_like(tot)                                 # [bin][cl]
+    for i, c in enumerate(order):
+        a, b = c.split("x")
+        scale[:, i] = 0.15 * np.sqrt(tot[:, auto[a]] * tot[:, auto[b]]) + 1e-4
+    n = ncl * nbin
+    sig = scale.ravel()                                        # index (bin - 1) * ncl + cl
+    bb = [i for i, c in enumerate(order) if c.count("_B") == 2]
+    dense = np.array([b * ncl + c for b in range(nbin) for c in bb])
+    m = dense.size
+    g = gaussians(seed, m * rank)
+    B = g.reshape(m, rank)
+    corr = np.eye(m) + 0.3 * (B @ B.T) / rank
+    d = 1.0 / np.sqrt(np.diag(corr))
+    corr = corr * d[:, None] * d[None, :]
+    in_dense = np.full(n, -1)
+    in_dense[dense] = np.arange(m)
+    path = os.path.join(bk15_dir, "BK15_covmat_dust.dat")
+    with open(path, "w") as f:
+        for i in range(n):
+            row = ["0"] * n
+            if in_dense[i] >= 0:
+                vals = corr[in_dense[i]] * sig[i] * sig[dense]
+                for jj, j in enumerate(dense):
+                    row[j] = repr(float(vals[jj]))
+            else:
+                row[i] = repr(float(sig[i] * sig[i]))
+            f.write(" ".join(row))
+            f.write("\n")
+    return path

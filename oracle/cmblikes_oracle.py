@@ -83,7 +83,9 @@ def _content_rows(path):
         for line in f:
             s = line.strip()
             if s and not s.startswith("#"):
-                rows.append([float(x.replace("d", "e").replace("D", "e")) for x in s.split()])
+                if "d" in s or "D" in s:
+                    s = s.replace("d", "e").replace("D", "e")
+                rows.append(np.array(s.split(), dtype=np.float64))
     return rows
 
 
@@ -299,18 +301,17 @@ class CMBLikesOracle:
         self.cl_use = [c for c in cl_in if c]
         used = [i for i, c in enumerate(cl_in) if c]
         nin = len(cl_in)
-        cov = np.array(sum(_content_rows(ini.fname("covmat_fiducial")), [])).reshape(nin * self.nbins,
-                                                                                     nin * self.nbins)
+        cov = np.concatenate(_content_rows(ini.fname("covmat_fiducial"))).reshape(nin * self.nbins,
+                                                                                  nin * self.nbins)
         scale = float(ini.get("covmat_scale", 1.0))
         nu = len(self.cl_use)
         nb = len(self.bins)
         C = np.zeros((nb * nu, nb * nu))
+        used = np.array(used)
         for bx in self.bins:
             for by in self.bins:
-                for a in range(nu):
-                    for c in range(nu):
-                        C[(bx - self.bin_min) * nu + a, (by - self.bin_min) * nu + c] = \
-                            scale * cov[(bx - 1) * nin + used[a], (by - 1) * nin + used[c]]
+                C[(bx - self.bin_min) * nu:(bx - self.bin_min + 1) * nu, (by - self.bin_min) * nu:(by - self.bin_min + 1) * nu] = \
+                    scale * cov[np.ix_((bx - 1) * nin + used, (by - 1) * nin + used)]
         self.inv_cov = np.linalg.inv(C)
 
     def _read_bandpass(self, fn):                          # TBK_planck_Read_Bandpass :72-105

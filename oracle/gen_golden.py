@@ -202,6 +202,8 @@ def gen_gr():
 # (name, tag, dataset, overrides, walkers, lmax, nuisance kind)
 LENS = "planck_lensing_2018/smicadx12_Dec5_ftl_mv2_ndclpp_p_teb_consext8.dataset"
 BKP = "BKPlanck/BKPlanck_detset_comb_dust.dataset"
+BK15 = "BK15/BK15_dust.dataset"
+BK15_MAPS = "BK15_95_B BK15_150_B BK15_220_B W023_B P030_B W033_B P044_B P070_B P100_B P143_B P217_B P353_B"
 CMBL_CASES = [
     ("lensing_consext8", "lensing", LENS, {}, 6, 2500, "cal"),
     ("bkplanck_3map_bins1to5", "BKPLANCK", BKP, {"maps_use": "B2K_B P217_B P353_B", "use_min": "1", "use_max": "5"},
@@ -211,6 +213,9 @@ CMBL_CASES = [
      3, 600, "bk_decorr"),
     ("bkplanck_EB_4map", "BKPLANCK", BKP, {"maps_use": "B2K_E B2K_B P353_E P353_B", "use_max": "7"}, 3, 600, "bk_sync"),
     ("sptsz_aberration_calprior", "SPT", "sptsz_2500d_tt/spt_s13_margfg.dataset", {}, 5, 3300, "cal_spt"),
+    # BASELINE configs[4]: BK15 B-only, 12 maps x 9 bins (batch3/BK15.ini), synthetic covariance
+    ("bk15_B_12maps", "BKPLANCK", BK15, {"maps_use": BK15_MAPS, "use_min": "1", "use_max": "9"}, 3, 600, "bk_sync"),
+    ("bk15_B_decorr_bandcentre", "BKPLANCK", BK15, {"maps_use": BK15_MAPS}, 3, 600, "bk15_bc"),
 ]
 BK_FID = [3.0, 0.0, -0.42, 1.59, 19.6, -0.6, -3.3, 0.0, 2.0, 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0]
 
@@ -229,6 +234,12 @@ def cmbl_nuisance(kind, W, seed):
         P[:, 2] = -0.42 + 0.05 * g[:, 2]
         P[:, 4] = 19.6 + 0.5 * g[:, 4]
         P[:, 7] = 0.2 + 0.05 * g[:, 7]
+    if kind == "bk15_bc":
+        P[:, 1] = 1.0 + 0.2 * np.abs(g[:, 1])
+        P[:, 7] = 0.2 + 0.05 * g[:, 7]
+        P[:, 10] = 0.9 + 0.02 * g[:, 10]
+        P[:, 11] = 0.95 + 0.02 * g[:, 11]
+        P[:, 12:16] = 0.01 * g[:, 12:16]
     if kind == "bk_decorr":
         P[:, 7] = 0.0
         P[:, 10] = 0.85 + 0.02 * g[:, 10]
@@ -247,6 +258,8 @@ def refdata_dir(td):
             tar.extractall(d, filter="data")
         except TypeError:
             tar.extractall(d)
+    if os.path.isdir(os.path.join(d, "BK15")):
+        syn.write_bk15_covmat(os.path.join(d, "BK15"))
     return d
 
 

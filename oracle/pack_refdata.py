@@ -7,6 +7,8 @@ tests/golden/refdata.tar.xz, so the tests run where /root/reference is absent
   planck_lensing_2018/...consext8 (dataset, bandpowers, cov, fiducial correction, windows)
   BKPlanck/BKPlanck_detset_comb_* + BKPlanck.paramnames + the five used bandpasses + windows
   sptsz_2500d_tt/*
+  BK15/* (all but the bandpower covariance, which the reference does not ship;
+          cosmomc_amd.synthetic.write_bk15_covmat writes a synthetic one after extraction)
 
     python oracle/pack_refdata.py
 """
@@ -35,9 +37,10 @@ def members():
     for f in sorted(os.listdir(os.path.join(REF, "BKPlanck", "windows"))):
         if f.startswith("BKPlanck_detset_comb_bpwf_bin"):
             yield "BKPlanck/windows/" + f
-    for root, _, files in sorted(os.walk(os.path.join(REF, "sptsz_2500d_tt"))):
-        for f in sorted(files):
-            yield os.path.relpath(os.path.join(root, f), REF)
+    for d in ("sptsz_2500d_tt", "BK15"):
+        for root, _, files in sorted(os.walk(os.path.join(REF, d))):
+            for f in sorted(files):
+                yield os.path.relpath(os.path.join(root, f), REF)
 
 
 def main():

@@ -53,6 +53,9 @@ def refdata(tmp_path_factory):
             tar.extractall(d, filter="data")
         except TypeError:
             tar.extractall(d)
+    if os.path.isdir(os.path.join(d, "BK15")):        # configs[4]: synthetic BK15 covariance
+        from cosmomc_amd import synthetic as syn
+        syn.write_bk15_covmat(os.path.join(d, "BK15"))
     return d
 
 

@@ -1,7 +1,9 @@
 """CMBlikes oracle (oracle/cmblikes_oracle.py) against the compiled reference
 (tests/golden/cmblikes_ref.json) on the reference's own datasets: Planck 2018
 lensing (gaussian + linear correction + calPlanck), BICEP2/Keck/Planck (HL +
-foregrounds, decorrelation), SPT-SZ (aberration + log-calibration prior)."""
+foregrounds, decorrelation), SPT-SZ (aberration + log-calibration prior), BK15
+(12 B maps x 9 bins, band-centre errors; synthetic covariance, the one file the
+reference does not ship)."""
 import os
 
 import numpy as np
@@ -11,7 +13,7 @@ import cmblikes_oracle as co
 from cosmomc_amd import synthetic as syn
 
 CASES = ["lensing_consext8", "bkplanck_3map_bins1to5", "bkplanck_all_maps", "bkplanck_decorr_lin_quad",
-         "bkplanck_EB_4map", "sptsz_aberration_calprior"]
+         "bkplanck_EB_4map", "sptsz_aberration_calprior", "bk15_B_12maps", "bk15_B_decorr_bandcentre"]
 
 
 @pytest.mark.parametrize("case", CASES)
