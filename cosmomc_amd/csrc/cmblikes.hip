@@ -700,12 +700,15 @@ struct HLDev {
 __global__ __launch_bounds__(64) void cmbl_hl_kernel(HLDev h, const double *__restrict__ cmat, double *__restrict__ xrows,
                                                     int W)
 {
-    __shared__ double S[9 * CL_MAXMAPS * CL_MAXMAPS + 3 * CL_MAXMAPS];
+    // LDS sized by the padded matrix edge m (9 m^2 + 3 m doubles; 10.7 KB at
+    // m = 12 instead of 18.8 KB at the 16 x 16 maximum), so about twice as many
+    // of these latency-bound single-wave blocks are resident per CU
+    extern __shared__ double S[];
     __shared__ int partner[CL_MAXMAPS];
     const int lane = threadIdx.x;
     const int w = blockIdx.x / h.nb, b = blockIdx.x % h.nb;
     if (w >= W) return;
-    const int n = h.n, m = h.m, MM = CL_MAXMAPS * CL_MAXMAPS;
+    const int n = h.n, m = h.m, MM = m * m;
     double *A = S, *A2 = S + MM, *U = S + 2 * MM, *V2 = S + 3 * MM, *T = S + 4 * MM, *R = S + 5 * MM;
     double *Vb = S + 6 * MM, *Ch = S + 7 * MM, *Cf = S + 8 * MM;
     double *cs = S + 9 * MM, *dg = cs + 2 * CL_MAXMAPS;
@@ -1599,7 +1602,8 @@ struct CMBLikes final : Like {
         HIP_CHECK(hipGetLastError());
         if (approx == 1) {
             timed_launch("cmbl_hl_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                hipExtLaunchKernelGGL(cmbl_hl_kernel, dim3(W * nb), dim3(64), 0, stream, e0, e1, 0, hl,
+                const size_t lds = (size_t)(9 * hl.m * hl.m + 3 * hl.m) * sizeof(double);
+                hipExtLaunchKernelGGL(cmbl_hl_kernel, dim3(W * nb), dim3(64), lds, stream, e0, e1, 0, hl,
                                       (const double *)cmat, qf.x_rows(qws), W);
             });
             HIP_CHECK(hipGetLastError());

@@ -19,10 +19,10 @@
 //       consecutive l of its walker in registers (foregrounds, derivative and
 //       aberration from the l-1 / l+8 halo) and feeds v_mfma_f64_16x16x4f64.
 //       Theory for the next 32 l is in flight across the current MFMAs.
-//   sptpol_delta_kernel  sums each bandpower's item partials in fixed order,
-//       applies 1/Cal, the beam factors and the data, writes delta rows for
-//       the quadratic form (LDS transpose, coalesced row writes) and the
-//       log-det + prior addend; zeroes the quadratic-form tickets.
+//   sptpol_delta_kernel  sums each bandpower's item partials in fixed order
+//       (one wave per bandpower, 64 walkers per wave), applies 1/Cal, the beam
+//       factors and the data, writes delta rows for the quadratic form (LDS
+//       transpose) and the log-det + prior addend; zeroes the tickets.
 //   quadform_ksplit      delta^T C^-1 delta / 2 + addend (quadform.hip).
 #include <algorithm>
 #include <cmath>
@@ -38,7 +38,7 @@ namespace cmamd {
 static constexpr int SP_COLS = 16;      // window columns per item (one MFMA block)
 static constexpr int SP_STEP = 32;      // l per MFMA step (4 lane groups x 8 l)
 static constexpr int SP_CH = 256;       // l per item (8 steps)
-static constexpr int SP_WB = 16;        // walkers per delta-kernel block
+static constexpr int SP_DB = 8;         // bandpowers per delta-kernel block (one wave each)
 static constexpr double SP_TWOPI = 6.283185307179586476925286766559;
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -227,48 +227,58 @@ __global__ __launch_bounds__(256) void sptpol_window_kernel(SPDev c, const doubl
 }
 
 // tmpcb / Cal, * BeamFac, - spec -> delta rows [W][Np]; addend = log det + priors.
+// Block = 64 walkers x SP_DB bandpowers, one wave per bandpower: each lane sums
+// its walker's partial rows (coalesced across the wave, eight loads in flight,
+// added in row order), the block transposes through LDS and writes SP_DB
+// consecutive delta entries per walker row.  Block (0, 0) zeroes the
+// quadratic-form tickets; bandpower group 0 writes the addend.
 template <int KIND>
-__global__ __launch_bounds__(256) void sptpol_delta_kernel(SPDev c, const double *__restrict__ partial,
-                                                           const double *__restrict__ nuis, long long ld_nuis,
-                                                           double *__restrict__ xrows, double *__restrict__ addend,
-                                                           unsigned int *__restrict__ counters, int n_counters, int W)
+__global__ __launch_bounds__(64 * SP_DB) void sptpol_delta_kernel(SPDev c, const double *__restrict__ partial,
+                                                                  const double *__restrict__ nuis, long long ld_nuis,
+                                                                  double *__restrict__ xrows, double *__restrict__ addend,
+                                                                  unsigned int *__restrict__ counters, int n_counters,
+                                                                  int W)
 {
-    extern __shared__ double tile[];     // [SP_WB][Np + 1]
-    const int tid = threadIdx.x;
-    const int w0 = blockIdx.x * SP_WB;
-    const int ld = c.Np + 1;
-    if (blockIdx.x == 0)
-        for (int i = tid; i < n_counters; i += 256) counters[i] = 0u;
-    for (int q = tid; q < c.Np * SP_WB; q += 256) {
-        const int i = q / SP_WB, wl = q % SP_WB, w = w0 + wl;
-        double v = 0.0;
-        if (i < c.nall && w < W) {
-            const double *P = nuis + (long long)w * ld_nuis;
-            double s = 0.0;
-            for (int r = c.row_off[i]; r < c.row_off[i + 1]; r++) s += partial[(long long)c.rows[r] * W + w];
-            const int k = i / c.nbin;
-            double cal;
-            if (KIND == SP_TEEE) {
-                const double tc = P[7], pc = P[8];                 // CalFactors(k+1) = Tcal^2 Pcal^k (:455-457)
-                cal = (tc * tc) * (k == 0 ? pc : pc * pc);
-            } else {
-                const double b150 = P[7], b90 = P[8];              // :507-509
-                cal = k == 0 ? b150 * b150 : (k == 1 ? b90 * b150 : b90 * b90);
-            }
-            s = s / cal;
-            double bf = 1.0;                                       // BeamFac (:500-503)
-            for (int t = 0; t < c.nbeam; t++) bf = bf * (1 + c.beam_err[t * c.nall + i] * P[9 + t]);
-            v = s * bf - c.spec[i];
+    __shared__ double tile[64][SP_DB + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int w = blockIdx.x * 64 + lane;
+    const int i = blockIdx.y * SP_DB + wave;
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+        for (int q = tid; q < n_counters; q += 64 * SP_DB) counters[q] = 0u;
+    double v = 0.0;
+    if (i < c.nall && w < W) {
+        const double *P = nuis + (long long)w * ld_nuis;
+        const int r0 = c.row_off[i], r1 = c.row_off[i + 1];
+        double s = 0.0;
+        for (int r = r0; r < r1; r += 8) {
+            double t[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) t[u] = r + u < r1 ? partial[(long long)c.rows[r + u] * W + w] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; u++) s += t[u];
         }
-        tile[wl * ld + i] = v;
+        const int k = i / c.nbin;
+        double cal;
+        if (KIND == SP_TEEE) {
+            const double tc = P[7], pc = P[8];                 // CalFactors(k+1) = Tcal^2 Pcal^k (:455-457)
+            cal = (tc * tc) * (k == 0 ? pc : pc * pc);
+        } else {
+            const double b150 = P[7], b90 = P[8];              // :507-509
+            cal = k == 0 ? b150 * b150 : (k == 1 ? b90 * b150 : b90 * b90);
+        }
+        s = s / cal;
+        double bf = 1.0;                                       // BeamFac (:500-503)
+        for (int t = 0; t < c.nbeam; t++) bf = bf * (1 + c.beam_err[t * c.nall + i] * P[9 + t]);
+        v = s * bf - c.spec[i];
     }
+    tile[lane][wave] = v;
     __syncthreads();
-    for (int q = tid; q < c.Np * SP_WB; q += 256) {
-        const int wl = q / c.Np, i = q % c.Np, w = w0 + wl;
-        if (w < W) xrows[(long long)w * c.Np + i] = tile[wl * ld + i];
+    {
+        const int wl = tid / SP_DB, q = tid % SP_DB;
+        const int ww = blockIdx.x * 64 + wl, ii = blockIdx.y * SP_DB + q;
+        if (ww < W && ii < c.Np) xrows[(long long)ww * c.Np + ii] = tile[wl][q];
     }
-    if (tid < SP_WB && w0 + tid < W) {
-        const int w = w0 + tid;
+    if (blockIdx.y == 0 && wave == 0 && w < W) {
         const double *P = nuis + (long long)w * ld_nuis;
         double pr = 0.0;
         for (int t = 0; t < c.nbeam; t++) pr += P[9 + t] * P[9 + t];
@@ -783,16 +793,16 @@ struct SPTpol final : Like {
             });
             HIP_CHECK(hipGetLastError());
         }
-        const size_t lds = (size_t)SP_WB * (qf.Np + 1) * 8;
+        const dim3 dgrid((W + 63) / 64, (qf.Np + SP_DB - 1) / SP_DB);
         timed_launch("sptpol_delta_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
             if (kind == SP_BB)
-                hipExtLaunchKernelGGL(sptpol_delta_kernel<SP_BB>, dim3((W + SP_WB - 1) / SP_WB), dim3(256), lds, stream,
-                                      e0, e1, 0, dev, (const double *)partial, nuis, ld_nuis, qf.x_rows(ws), addend,
+                hipExtLaunchKernelGGL(sptpol_delta_kernel<SP_BB>, dgrid, dim3(64 * SP_DB), 0, stream, e0, e1, 0, dev,
+                                      (const double *)partial, nuis, ld_nuis, qf.x_rows(ws), addend,
                                       qf.counters(ws, W), qf.n_counters(W), W);
             else
-                hipExtLaunchKernelGGL(sptpol_delta_kernel<SP_TEEE>, dim3((W + SP_WB - 1) / SP_WB), dim3(256), lds,
-                                      stream, e0, e1, 0, dev, (const double *)partial, nuis, ld_nuis, qf.x_rows(ws),
-                                      addend, qf.counters(ws, W), qf.n_counters(W), W);
+                hipExtLaunchKernelGGL(sptpol_delta_kernel<SP_TEEE>, dgrid, dim3(64 * SP_DB), 0, stream, e0, e1, 0, dev,
+                                      (const double *)partial, nuis, ld_nuis, qf.x_rows(ws), addend,
+                                      qf.counters(ws, W), qf.n_counters(W), W);
         });
         HIP_CHECK(hipGetLastError());
         qf.launch(W, ws, addend, out, stream, "sptpol_quadform");
