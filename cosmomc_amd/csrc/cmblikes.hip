@@ -92,6 +92,7 @@ struct CLDev {
     const int *e_to_x;              // [nE] gaussian: index into bigX or -1
     // BK foregrounds
     int bk, nreq;
+    int LP;                         // profile row length: prof[w][3][LP], indexed by l (zero outside lmin..lmax)
     const BKMap *bkmaps;
     const double *bp_nu, *bp_R, *bp_dnu;
     double fpivot_dust, fpivot_sync, decorr_dust[2], decorr_sync[2];
@@ -169,13 +170,16 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
         }
     }
     const double lpivot = 80.0;
-    const int L = c.lmax - c.lmin + 1;
-    for (int l = c.lmin + tid; l <= c.lmax; l += blockDim.x) {
-        const long long j = l - c.lmin;
-        double *pw = prof + (long long)w * 3 * L;
-        pw[j] = Adust * pow(l / lpivot, alphadust);
-        pw[L + j] = Async * pow(l / lpivot, alphasync);
-        pw[2 * L + j] =
+    const int LP = c.LP;
+    double *pw = prof + (long long)w * 3 * LP;
+    for (int l = tid; l < LP; l += blockDim.x) {
+        if (l < c.lmin || l > c.lmax) {
+            pw[l] = pw[LP + l] = pw[2 * LP + l] = 0.0;
+            continue;
+        }
+        pw[l] = Adust * pow(l / lpivot, alphadust);
+        pw[LP + l] = Async * pow(l / lpivot, alphasync);
+        pw[2 * LP + l] =
             dustsync_corr * sqrt(Adust * Async) * pow(l / lpivot, (alphadust + alphasync) / 2);
     }
 }
@@ -205,7 +209,6 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
     const CLPair pr = c.pairs[it.pair];
     const bool aber = ABER && c.aberration != 0.0 && pr.cmb;
     const bool fg = FG && pr.fg;
-    const int L = c.lmax - c.lmin + 1;
     // staging map: thread -> l pair q = tid % 32 of rows r_u = tid / 32 + 8 u (u < 8)
     constexpr int PER = 64 * (WK_CHUNK / 2) / 256;
     const int q = tid % (WK_CHUNK / 2), rbase = tid / (WK_CHUNK / 2);
@@ -308,14 +311,14 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
                     }
                     if constexpr (FG) {
                         if (fg) {                             // :329-334
-                            const double *pw = prof + (long long)w * 3 * L + (l - c.lmin);
+                            const double *pw = prof + (long long)w * 3 * c.LP + l;
                             const double Dd = (dd_l && Ddust[u] != 1.0)
                                                   ? bk_decorr(Ddust[u], nui[u], nuj[u], c.decorr_dust, l, c.lform_dust)
                                                   : ddf[u];
                             const double Ds = (ds_l && Dsync[u] != 1.0)
                                                   ? bk_decorr(Dsync[u], nui[u], nuj[u], c.decorr_sync, l, c.lform_sync)
                                                   : dsf[u];
-                            v = v + dust[u] * pw[0] * Dd + sync[u] * pw[L] * Ds + dsync[u] * pw[2 * L];
+                            v = v + dust[u] * pw[0] * Dd + sync[u] * pw[c.LP] * Ds + dsync[u] * pw[2 * c.LP];
                         }
                     }
                     if (c.cal_index >= 0 && pr.cmb) v = v / calsq[u];   // AdaptTheoryForMaps :1113-1124
@@ -470,6 +473,209 @@ __global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double 
             const int c0 = kq + 4 * r, c1 = 16 + kq + 4 * r;
             if (c0 < it.ncol) partial[(long long)(it.part + c0) * W + w] = acc0[r] / inv;
             if (c1 < it.ncol) partial[(long long)(it.part + c1) * W + w] = acc1[r] / inv;
+        }
+    }
+}
+
+// BK foreground datasets (TBK_planck, CMB_BK_Planck.f90:229-340): every map pair
+// p of a theory field reads the same four per-walker rows -- the theory D_l and
+// the dust / sync / dust-sync l profiles of cmbl_bk_prologue -- and differs only
+// in per-(pair, walker) SED coefficients:
+//   MapCl_p(l) = D_l + (dust_p Pd(l) Dd_p(l) + sync_p Ps(l) Ds_p(l) + dsync_p Px(l))
+// (the expression of cmbl_window_kernel's staging, :329-334 of the reference).
+// A work item is (up to GP pairs of one field, <= GSEG l); the workgroup
+// (64 walkers, 16 per wave) loads each lane's 4 consecutive l of the four rows
+// once per 16-l step and forms every pair's MapCl in registers for
+// v_mfma_f64_16x16x4f64 against that pair's <= 16 window columns, so a row
+// element is read once per item instead of once per pair (78 B x B pairs for
+// BK15).  l-dependent decorrelation (lform lin / quad with Delta /= 1) is
+// evaluated per value, as in the staged kernel.
+static constexpr int GP = 8;        // pairs per grouped item
+static constexpr int GSEG = 256;    // l per grouped item
+
+struct GItem {
+    int field, npair, l0, nstep;
+    int pair[GP];       // CLPair index
+    int ncol[GP];       // columns of each pair (<= 16)
+    int part[GP];       // first partial row of each pair
+    long long woff;     // weights [GP][16][nstep * 32] (zero padded)
+};
+
+__global__ __launch_bounds__(256, 2) void cmbl_window_group(CLDev c, const GItem *__restrict__ gitems, int ngitem,
+                                                        const double *__restrict__ wts, const double *__restrict__ dl,
+                                                        long long ld_field, long long ld_walker,
+                                                        const double *__restrict__ nuis, long long ld_nuis,
+                                                        const double *__restrict__ coef, const double *__restrict__ prof,
+                                                        int LP, double *__restrict__ partial, int W, int tiles,
+                                                        int vec_ok)
+{
+    constexpr int LPL = 4, STEP = 4 * LPL;
+    // per-(pair, walker) SED coefficients: [GP][8][64] = dust, sync, dsync, ddf, dsf, nui, nuj, flags
+    __shared__ double cf[GP][8][64];
+    // the item's window weights of one step, double-buffered: [GP * 16 columns][STEP (+2 pad)]
+    constexpr int WR = STEP + 2;
+    __shared__ __attribute__((aligned(16))) double wsh[2][GP * 16 * WR];
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    const int item = xcd + 8 * (j / tiles), tile = j % tiles;   // all walker tiles of an item on one XCD
+    if (item >= ngitem) return;
+    const GItem &it = gitems[item];
+    const int np = it.npair;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    {   // staged kernel :226-258, one (walker, pair) per thread and pass
+        const int ws = min(tile * 64 + lane, W - 1);
+        const double *P = nuis + (long long)ws * ld_nuis;
+        const double *cw = coef + (long long)ws * 3 * c.nreq;
+        const double Delta_dust = P[10], Delta_sync = P[11];
+        for (int g = wave; g < np; g += 4) {
+            const CLPair pr = c.pairs[it.pair[g]];
+            double d = 0.0, sy = 0.0, ds = 0.0, ddf = 1.0, dsf = 1.0, nui = 0.0, nuj = 0.0;
+            int flags = 0;
+            if (pr.fg) {
+                const int a = pr.mi, bb = pr.mj;
+                d = cw[a] * cw[bb];
+                sy = cw[c.nreq + a] * cw[c.nreq + bb];
+                ds = cw[a] * cw[c.nreq + bb] + cw[c.nreq + a] * cw[bb];
+                if (pr.fg == 1) {
+                    const double EEd = P[8], EEs = P[9];
+                    d = d * EEd;
+                    sy = sy * EEs;
+                    ds = ds * sqrt(EEd * EEs);
+                }
+                nui = c.bkmaps[a].nu_bar * cw[2 * c.nreq + a];
+                nuj = c.bkmaps[bb].nu_bar * cw[2 * c.nreq + bb];
+                if (fabs(Delta_dust - 1) > 1e-5 && a != bb) {
+                    if (c.lform_dust == 0) ddf = bk_decorr(Delta_dust, nui, nuj, c.decorr_dust, 0, 0);
+                    else flags |= 1;
+                }
+                if (fabs(Delta_sync - 1) > 1e-5 && a != bb) {
+                    if (c.lform_sync == 0) dsf = bk_decorr(Delta_sync, nui, nuj, c.decorr_sync, 0, 0);
+                    else flags |= 2;
+                }
+            }
+            cf[g][0][lane] = d;
+            cf[g][1][lane] = sy;
+            cf[g][2][lane] = ds;
+            cf[g][3][lane] = ddf;
+            cf[g][4][lane] = dsf;
+            cf[g][5][lane] = nui;
+            cf[g][6][lane] = nuj;
+            cf[g][7][lane] = (double)flags;
+        }
+    }
+    const int li = lane & 15, kq = lane >> 4;
+    const int wr_ = wave * 16 + li;                // walker within the tile
+    const int w = tile * 64 + wr_;
+    const int wl = min(w, W - 1);
+    const double *P = nuis + (long long)wl * ld_nuis;
+    const double Delta_dust = P[10], Delta_sync = P[11];
+    const double *Df = dl + (long long)wl * ld_walker + (long long)it.field * ld_field;
+    const double *pw = prof + (long long)wl * 3 * LP;
+    double t[4][LPL], tn[4][LPL];
+    auto load = [&](int st, double (*dst)[LPL]) {
+        const int lb = it.l0 + st * STEP + LPL * kq;
+        if (vec_ok && lb + LPL - 1 <= c.lmax) {
+#pragma unroll
+            for (int s = 0; s < LPL / 2; s++) {
+                const double2 v0 = reinterpret_cast<const double2 *>(Df + lb)[s];
+                const double2 v1 = reinterpret_cast<const double2 *>(pw + lb)[s];
+                const double2 v2 = reinterpret_cast<const double2 *>(pw + LP + lb)[s];
+                const double2 v3 = reinterpret_cast<const double2 *>(pw + 2 * LP + lb)[s];
+                dst[0][2 * s] = v0.x; dst[0][2 * s + 1] = v0.y;
+                dst[1][2 * s] = v1.x; dst[1][2 * s + 1] = v1.y;
+                dst[2][2 * s] = v2.x; dst[2][2 * s + 1] = v2.y;
+                dst[3][2 * s] = v3.x; dst[3][2 * s + 1] = v3.y;
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < LPL; s++) {
+                const int l = lb + s;
+                const bool ok = l <= c.lmax;
+                dst[0][s] = ok ? Df[l] : 0.0;
+                dst[1][s] = ok ? pw[l] : 0.0;
+                dst[2][s] = ok ? pw[LP + l] : 0.0;
+                dst[3][s] = ok ? pw[2 * LP + l] : 0.0;
+            }
+        }
+    };
+    f64x4 acc[GP];
+#pragma unroll
+    for (int g = 0; g < GP; g++) acc[g] = f64x4{0.0, 0.0, 0.0, 0.0};
+    const int Lp = it.nstep * 32;
+    const int nst = it.nstep * (32 / STEP);
+    // weights of step st: GP*16 rows of STEP doubles; thread q moves rows q / (STEP/2) ...
+    constexpr int NW2 = GP * 16 * STEP / 2, PERT = NW2 / 256;
+    double2 wr[PERT];
+    auto fetch_w = [&](int st) {
+#pragma unroll
+        for (int u = 0; u < PERT; u++) {
+            const int q = tid + 256 * u, row = q / (STEP / 2), c2 = q % (STEP / 2);
+            wr[u] = row < np * 16 ? reinterpret_cast<const double2 *>(wts + it.woff + (long long)row * Lp + st * STEP)[c2]
+                                  : make_double2(0.0, 0.0);
+        }
+    };
+    auto store_w = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < PERT; u++) {
+            const int q = tid + 256 * u, row = q / (STEP / 2), c2 = q % (STEP / 2);
+            *reinterpret_cast<double2 *>(&wsh[buf][row * WR + 2 * c2]) = wr[u];
+        }
+    };
+    load(0, t);
+    fetch_w(0);
+    store_w(0);
+    __syncthreads();
+    for (int st = 0; st < nst; st++) {
+        const bool more = st + 1 < nst;
+        const int cur = st & 1;
+        if (more) {                                    // in flight across this step's MFMAs
+            load(st + 1, tn);
+            fetch_w(st + 1);
+        }
+        const int lr = st * STEP + LPL * kq;
+#pragma unroll
+        for (int g = 0; g < GP; g++) {
+            if (g >= np) break;
+            const double *src = &wsh[cur][(g * 16 + li) * WR + LPL * kq];
+            const double2 q0 = reinterpret_cast<const double2 *>(src)[0], q1 = reinterpret_cast<const double2 *>(src)[1];
+            const double a[LPL] = {q0.x, q0.y, q1.x, q1.y};
+            const double dg = cf[g][0][wr_], sg = cf[g][1][wr_], xg = cf[g][2][wr_];
+            const int flags = (int)cf[g][7][wr_];
+#pragma unroll
+            for (int s = 0; s < LPL; s++) {
+                double Dd = cf[g][3][wr_], Ds = cf[g][4][wr_];
+                if (flags) {
+                    const int l = it.l0 + lr + s;
+                    if (flags & 1) Dd = bk_decorr(Delta_dust, cf[g][5][wr_], cf[g][6][wr_], c.decorr_dust, l, c.lform_dust);
+                    if (flags & 2) Ds = bk_decorr(Delta_sync, cf[g][5][wr_], cf[g][6][wr_], c.decorr_sync, l, c.lform_sync);
+                }
+                const double v = t[0][s] + (dg * t[1][s] * Dd + sg * t[2][s] * Ds + xg * t[3][s]);
+                acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], v, acc[g], 0, 0, 0);
+            }
+        }
+        if (more) {
+            store_w(cur ^ 1);          // buffer cur ^ 1 was last read before the previous barrier
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+#pragma unroll
+                for (int s = 0; s < LPL; s++) t[q][s] = tn[q][s];
+        }
+    }
+    if (w < W) {
+#pragma unroll
+        for (int g = 0; g < GP; g++) {
+            if (g >= np) break;
+            double inv = 1.0;
+            if (c.cal_index >= 0 && c.pairs[it.pair[g]].cmb) {
+                const double cl = P[c.cal_index];
+                inv = cl * cl;
+            }
+            // D: walker = lane & 15, column = (lane >> 4) + 4 r
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int col = kq + 4 * r;
+                if (col < it.ncol[g]) partial[(long long)(it.part[g] + col) * W + w] = acc[g][r] / inv;
+            }
         }
     }
 }
@@ -878,6 +1084,9 @@ struct CMBLikes final : Like {
         d_etox, d_fidcorr, d_noise, d_chat, d_cluse, d_bkmaps, d_bpnu, d_bpR, d_bpdnu, d_hlchat, d_hlcf;
     int max_field = 0, n_part_rows = 0;
     bool items_even = true, small_gauss = false;
+    bool use_group = false;      // BK foregrounds: grouped-pair window kernel
+    int n_gitem = 0;
+    DevBuf d_gitems, d_gw;
     int small_ntask = 0;
     SmallDev sdev{};
     DevBuf d_invcov, d_stasks, d_srows, d_smt, d_sct;
@@ -1332,7 +1541,66 @@ struct CMBLikes final : Like {
         int nrows = 0;
         const int SEG = WK_CHUNK * WK_NCH;
         const int nseg = (L + SEG - 1) / SEG;
-        for (size_t p = 0; p < pairs.size(); p++)
+        // BK foregrounds without aberration: grouped-pair items (cmbl_window_group),
+        // when no pair has more than 16 window columns
+        use_group = bk && aberration == 0.0 && !std::getenv("CMAMD_BK_STAGED");
+        if (use_group) {
+            std::vector<int> per_pair(pairs.size(), 0);
+            for (auto &cc : cols)
+                if (!cc.fixed && ++per_pair[cc.pair] > 16) use_group = false;
+        }
+        std::vector<GItem> gitems;
+        std::vector<double> gw;
+        if (use_group) {
+            std::map<int, std::vector<int>> by_field;
+            for (size_t p = 0; p < pairs.size(); p++) by_field[pairs[p].field].push_back((int)p);
+            for (auto &fv : by_field)
+                for (size_t g0 = 0; g0 < fv.second.size(); g0 += GP) {
+                    const int npair = (int)std::min<size_t>(GP, fv.second.size() - g0);
+                    for (int sg = 0; sg < (L + GSEG - 1) / GSEG; sg++) {
+                        const int c0 = sg * GSEG, c1 = std::min(L - 1, c0 + GSEG - 1);
+                        std::vector<std::vector<int>> sel(npair);
+                        int lo = c1 + 1, hi = c0 - 1;
+                        for (int g = 0; g < npair; g++)
+                            for (size_t ci = 0; ci < cols.size(); ci++)
+                                if (!cols[ci].fixed && cols[ci].pair == fv.second[g0 + g] && cols[ci].hi >= c0 &&
+                                    cols[ci].lo <= c1) {
+                                    sel[g].push_back((int)ci);
+                                    lo = std::min(lo, std::max(c0, cols[ci].lo));
+                                    hi = std::max(hi, std::min(c1, cols[ci].hi));
+                                }
+                        if (hi < lo) continue;
+                        GItem it{};
+                        it.field = fv.first;
+                        it.npair = npair;
+                        it.l0 = (lo + lmin) & ~1;      // even: 16-byte loads (>= lmin - 1; profiles are 0 there)
+                        it.nstep = (hi + lmin - it.l0 + 32) / 32;
+                        it.woff = (long long)gw.size();
+                        const int Lp = it.nstep * 32;
+                        for (int g = 0; g < GP; g++) {
+                            it.pair[g] = g < npair ? fv.second[g0 + g] : 0;
+                            it.ncol[g] = g < npair ? (int)sel[g].size() : 0;
+                            it.part[g] = nrows;
+                            for (int cc = 0; cc < 16; cc++)
+                                for (int l = 0; l < Lp; l++) {
+                                    const int jl = it.l0 + l - lmin;
+                                    gw.push_back(g < npair && cc < it.ncol[g] && jl >= lo && jl <= hi
+                                                     ? cols[sel[g][cc]].W[jl] : 0.0);
+                                }
+                            if (g < npair)
+                                for (int ci : sel[g]) col_parts[ci].push_back(nrows++);
+                        }
+                        gitems.push_back(it);
+                    }
+                }
+            for (auto &p : pairs) max_field = std::max(max_field, p.field);
+        }
+        n_gitem = (int)gitems.size();
+        d_gitems.alloc(std::max<size_t>(16, gitems.size() * sizeof(GItem)));
+        if (!gitems.empty()) d_gitems.upload(gitems.data(), gitems.size() * sizeof(GItem));
+        d_gw.alloc(std::max<size_t>(16, gw.size() * 8));
+        if (!gw.empty()) d_gw.upload(gw.data(), gw.size() * 8);
+        for (size_t p = 0; p < (use_group ? 0 : pairs.size()); p++)
             for (int sg = 0; sg < nseg; sg++) {
                 const int c0 = sg * SEG, c1 = std::min(L - 1, c0 + SEG - 1);
                 std::vector<int> sel;
@@ -1491,6 +1759,7 @@ struct CMBLikes final : Like {
         dev.e_to_x = d_etox.as<int>();
         dev.bk = bk ? 1 : 0;
         dev.nreq = nreq;
+        dev.LP = (lmax + 2) & ~1;
         dev.bkmaps = bk ? d_bkmaps.as<BKMap>() : nullptr;
         dev.bp_nu = bk ? d_bpnu.as<double>() : nullptr;
         dev.bp_R = bk ? d_bpR.as<double>() : nullptr;
@@ -1513,12 +1782,11 @@ struct CMBLikes final : Like {
     WsLayout layout(int W) const {
         auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
         WsLayout o{};
-        const int L = lmax - lmin + 1;
         o.part = al(qf.workspace_size(W));
         o.cmat = o.part + al((size_t)n_part_rows * W * 8);
         o.coef = o.cmat + al(approx == 1 ? (size_t)W * nb * ncl * 8 : 0);
         o.prof = o.coef + al(bk ? (size_t)W * 3 * nreq * 8 : 0);
-        o.add = o.prof + al(bk ? (size_t)3 * L * W * 8 : 0);   // prof [W][3][L]
+        o.add = o.prof + al(bk ? (size_t)3 * dev.LP * W * 8 : 0);   // prof [W][3][LP]
         o.total = o.add + al((size_t)W * 8);
         return o;
     }
@@ -1557,7 +1825,16 @@ struct CMBLikes final : Like {
         bool vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0 &&
                       items_even && (lmax + 1 < ld_field || (lmax % 2 == 1 && lmax + 1 <= ld_field));
         static const bool staged = std::getenv("CMAMD_WINDOW_STAGED") != nullptr;   // A/B measurement switch
-        if (!bk && aberration == 0.0 && !staged) {
+        if (use_group) {
+            const bool gvec = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0;
+            const int nblk = 8 * tiles * ((n_gitem + 7) / 8);
+            timed_launch("cmbl_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+                hipExtLaunchKernelGGL(cmbl_window_group, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, dev,
+                                      d_gitems.as<GItem>(), n_gitem, d_gw.as<double>(), dl, ld_field, ld_walker, nu,
+                                      ld_nuis, (const double *)coef, (const double *)prof, dev.LP, partial, W, tiles,
+                                      (int)gvec);
+            });
+        } else if (!bk && aberration == 0.0 && !staged) {
             const int nblk = 8 * tiles * ((dev.nitem + 7) / 8);
             timed_launch("cmbl_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
                 hipExtLaunchKernelGGL(cmbl_window_direct, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, dev, dl,
