@@ -989,6 +989,261 @@ __global__ __launch_bounds__(64) void cmbl_hl_kernel(HLDev h, const double *__re
     }
 }
 
+// ------------------------------------------- HL, register-resident (16 lanes / matrix)
+// The same two cyclic-Jacobi eigensolves and HL transform as cmbl_hl_kernel
+// (CMBLikes_Transform :861-914), with the matrices in registers: lane r of a
+// 16-lane group owns row r of the working matrix and of the eigenvector
+// matrix, and a 64-lane block runs four (walker, bin) problems.  A Jacobi
+// round is a column rotation of the lane's own row (the round's (c, s) of
+// every column read from LDS) followed by the row rotation with the partner
+// row (one LDS exchange); rounds are unrolled over the compile-time matrix
+// edge M so every register index is static.  The matrix products go through
+// per-group LDS row buffers.
+template <int M>
+struct HLRowsLds {
+    double rows[4][3][16][M + 1];   // three row buffers per problem (odd stride: fewer bank conflicts)
+    double cs[4][16][2];            // (c, s) of each column in the current round
+    double dg[4][16];               // a diagonal / g(x) broadcast
+};
+
+template <int M>
+__device__ inline double hl_pick(const double (&a)[M], int k) {   // a[k] for a runtime k (no scratch)
+    double v = 0.0;
+#pragma unroll
+    for (int j = 0; j < M; j++) v = (j == k) ? a[j] : v;
+    return v;
+}
+
+template <int M>
+__device__ inline int hl_partner(int rr, int r) {   // round-robin pairing of round rr (circle method)
+    if (r == M - 1) return rr;
+    if (r == rr) return M - 1;
+    return ((2 * rr - r) % (M - 1) + (M - 1)) % (M - 1);
+}
+
+// cyclic Jacobi of the group's M x M matrix (row r in A), eigenvectors in V (row r).
+// The partner column of every column changes from round to round, so the
+// lane's own rows are mirrored into LDS (rows[.][1], rows[.][2]) to be read at
+// runtime indices instead of indexing registers.
+template <int M>
+__device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, int grp, int r, int lane,
+                               int max_sweeps)
+{
+#pragma unroll
+    for (int k = 0; k < M; k++) V[k] = (k == r) ? 1.0 : 0.0;
+    double *Aown = S.rows[grp][1][r < M ? r : 0];
+    double *Vown = S.rows[grp][2][r < M ? r : 0];
+    for (int sweep = 0; sweep < max_sweeps; sweep++) {
+        // convergence (as cmbl_hl_kernel): every off-diagonal |a_rk| <= 1e-18 sqrt(|a_rr a_kk|) or 0
+        if (r < M) S.dg[grp][r] = hl_pick<M>(A, r);
+        __syncthreads();
+        bool big = false;
+        if (r < M) {
+            const double arr = S.dg[grp][r];
+#pragma unroll
+            for (int k = 0; k < M; k++) {
+                const double a = A[k];
+                if (k != r && a != 0.0 && fabs(a) > 1e-18 * sqrt(fabs(arr * S.dg[grp][k]))) big = true;
+            }
+        }
+        __syncthreads();
+        if (!__any(big)) break;        // wave-uniform: converged groups keep rotating by ~0
+#pragma unroll 1
+        for (int rr = 0; rr < M - 1; rr++) {
+            // (1) this row's pair and rotation (the lower row's a_pq for both lanes)
+            double c = 1.0, s = 0.0;
+            int p = r;
+            if (r < M) {
+                p = hl_partner<M>(rr, r);
+                S.dg[grp][r] = hl_pick<M>(A, r);
+                S.rows[grp][0][r][0] = hl_pick<M>(A, p);
+#pragma unroll
+                for (int k = 0; k < M; k++) {
+                    Aown[k] = A[k];
+                    Vown[k] = V[k];
+                }
+            }
+            __syncthreads();
+            if (r < M) {
+                const int lo = r < p ? r : p, hi = r < p ? p : r;
+                const double apq = S.rows[grp][0][lo][0], app = S.dg[grp][lo], aqq = S.dg[grp][hi];
+                double cc = 1.0, ss = 0.0;
+                if (apq != 0.0 && fabs(apq) > 1e-300) {
+                    const double theta = (aqq - app) / (2.0 * apq);
+                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                    cc = 1.0 / sqrt(t * t + 1.0);
+                    ss = t * cc;
+                }
+                c = cc;
+                s = (r == lo) ? -ss : ss;      // J[r][r] = c, J[p][r] = s (column r of J)
+                S.cs[grp][r][0] = c;
+                S.cs[grp][r][1] = s;
+            }
+            __syncthreads();
+            // (2) B = A J, V = V J on this lane's row; (3) A' = J^T B: row r = c B_r + s B_p
+            if (r < M) {
+#pragma unroll
+                for (int k = 0; k < M; k++) {
+                    const int pk = hl_partner<M>(rr, k);
+                    const double ck = S.cs[grp][k][0], sk = S.cs[grp][k][1];
+                    A[k] = A[k] * ck + Aown[pk] * sk;     // B, kept in A
+                    V[k] = V[k] * ck + Vown[pk] * sk;
+                }
+#pragma unroll
+                for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = A[k];
+            }
+            __syncthreads();
+            if (r < M) {
+                const double *Bp = S.rows[grp][0][p];
+                // the rotated-away a_rp is exactly 0 (standard Jacobi; computing it leaves
+                // O(eps) noise that the convergence test would keep rotating)
+#pragma unroll
+                for (int k = 0; k < M; k++) A[k] = (k == p) ? 0.0 : c * A[k] + s * Bp[k];
+            }
+            __syncthreads();
+        }
+    }
+}
+
+template <int M>
+__global__ __launch_bounds__(64) void cmbl_hl_rows_kernel(HLDev h, const double *__restrict__ cmat,
+                                                         double *__restrict__ xrows, int W, int max_sweeps)
+{
+    __shared__ HLRowsLds<M> S;
+    const int lane = threadIdx.x, grp = lane >> 4, r = lane & 15;
+    const int prob = blockIdx.x * 4 + grp;
+    const int nprob = W * h.nb;
+    const bool live = prob < nprob;
+    const int w = live ? prob / h.nb : 0, b = live ? prob % h.nb : 0;
+    const int n = h.n;
+    const bool row_ok = r < n;
+    auto U_row = [&](int k, int j) { return S.rows[grp][0][k][j]; };
+    // C row r from its lower-triangle elements (ElementsToMatrix :950-965), zero padded to M
+    double A[M], V[M];
+    const double *cm = cmat + ((long long)w * h.nb + b) * h.ncl;
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        double v = 0.0;
+        if (live && row_ok && j < n) {
+            const int a = r > j ? r : j, bb = r > j ? j : r;
+            v = cm[a * (a + 1) / 2 + bb];
+        }
+        A[j] = v;
+    }
+    // (1) C = U diag U^T
+    hl_jacobi_rows<M>(A, V, S, grp, r, lane, max_sweeps);
+    const double dgr = hl_pick<M>(A, r < M ? r : 0);
+    if (r < M) {
+        S.dg[grp][r] = dgr;
+#pragma unroll
+        for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = V[k];     // U rows
+    }
+    __syncthreads();
+    // (2) T = Chat U ; R = U^T T scaled by 1/sqrt(diag) (:878-889)
+    double T[M];
+    const double *ch = h.chat + (long long)b * n * n;
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        double s = 0.0;
+        if (row_ok && j < n)
+            for (int k = 0; k < n; k++) s += ch[r * n + k] * U_row(k, j);
+        T[j] = s;
+    }
+    if (r < M)
+#pragma unroll
+        for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = T[k];
+    __syncthreads();
+    double R[M];
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        double s = 0.0;
+        if (row_ok && j < n) {
+            for (int k = 0; k < n; k++) s += U_row(k, r) * S.rows[grp][1][k][j];
+            const int lo = r < j ? r : j, hi = r < j ? j : r;
+            s = s / sqrt(S.dg[grp][lo]);
+            s = s / sqrt(S.dg[grp][hi]);
+        }
+        R[j] = s;
+    }
+    __syncthreads();
+    // (3) Rot = U R U^T (:891): T2 = R U^T (rows through LDS), A = U T2
+    if (r < M)
+#pragma unroll
+        for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = R[k];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < M; j++) {        // T2[r][j] = sum_k R[r][k] U[j][k]
+        double s = 0.0;
+        if (row_ok && j < n)
+#pragma unroll
+            for (int k = 0; k < M; k++)
+                if (k < n) s += R[k] * U_row(j, k);
+        T[j] = s;
+    }
+    __syncthreads();
+    if (r < M)
+#pragma unroll
+        for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = T[k];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < M; j++) {        // A[r][j] = sum_k U[r][k] T2[k][j]
+        double s = 0.0;
+        if (row_ok && j < n)
+            for (int k = 0; k < n; k++) s += U_row(r, k) * S.rows[grp][1][k][j];
+        A[j] = s;
+    }
+    __syncthreads();
+    // (4) Rot = V diag V^T; g(x) = sign(x - 1) sqrt(2 max(0, x - ln x - 1))  (:892-894)
+    hl_jacobi_rows<M>(A, V, S, grp, r, lane, max_sweeps);
+    if (r < M) {
+        const double x = hl_pick<M>(A, r);
+        const double g = sqrt(2 * fmax(0.0, x - log(x) - 1));
+        S.dg[grp][r] = (x - 1 >= 0) ? g : -g;
+#pragma unroll
+        for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = V[k];     // V rows
+    }
+    __syncthreads();
+    // (5) U = Cfhalf V ; C = U diag(g) U^T (:907-912)
+    const double *cf = h.cfhalf + (long long)b * n * n;
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        double s = 0.0;
+        if (row_ok && j < n)
+            for (int k = 0; k < n; k++) s += cf[r * n + k] * U_row(k, j);
+        T[j] = s;
+    }
+    __syncthreads();
+    if (r < M)
+#pragma unroll
+        for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = T[k];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < M; j++) {        // C[r][j] = sum_k (T[r][k] g_k) T[j][k]
+        double s = 0.0;
+        if (row_ok && j < n)
+#pragma unroll
+            for (int k = 0; k < M; k++)
+                if (k < n) s += (T[k] * S.dg[grp][k]) * S.rows[grp][1][j][k];
+        A[j] = s;
+    }
+    __syncthreads();
+    if (r < M)
+#pragma unroll
+        for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = A[k];
+    __syncthreads();
+    // vecp = lower-triangle elements (MatrixToElements :917-931); bigX entries of this bin
+    if (live) {
+        double *x = xrows + (long long)w * h.Np + (long long)b * h.ncl_used;
+        for (int u = r; u < h.ncl_used; u += 16) {
+            const int k = h.cl_use[u];
+            int i = 0;
+            while ((i + 1) * (i + 2) / 2 <= k) i++;
+            const int j = k - i * (i + 1) / 2;
+            x[u] = S.rows[grp][0][i][j];
+        }
+    }
+}
+
 // ------------------------------------------------------------------ host side
 
 static std::vector<std::string> split_list(const std::string &s) { return split_ws(s); }
@@ -1879,9 +2134,26 @@ struct CMBLikes final : Like {
         HIP_CHECK(hipGetLastError());
         if (approx == 1) {
             timed_launch("cmbl_hl_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                const size_t lds = (size_t)(9 * hl.m * hl.m + 3 * hl.m) * sizeof(double);
-                hipExtLaunchKernelGGL(cmbl_hl_kernel, dim3(W * nb), dim3(64), lds, stream, e0, e1, 0, hl,
-                                      (const double *)cmat, qf.x_rows(qws), W);
+                static const bool lds_hl = std::getenv("CMAMD_HL_LDS") != nullptr;   // A/B measurement switch
+                if (!lds_hl) {
+                    static const int sweeps = std::getenv("CMAMD_HL_SWEEPS") ? atoi(std::getenv("CMAMD_HL_SWEEPS")) : 40;
+                    const dim3 g((W * nb + 3) / 4), bl(64);
+                    switch (hl.m) {
+#define CMBL_HLR(MM)                                                                                              \
+    case MM:                                                                                                      \
+        hipExtLaunchKernelGGL(cmbl_hl_rows_kernel<MM>, g, bl, 0, stream, e0, e1, 0, hl, (const double *)cmat,      \
+                              qf.x_rows(qws), W, sweeps);                                                         \
+        break;
+                        CMBL_HLR(2) CMBL_HLR(4) CMBL_HLR(6) CMBL_HLR(8) CMBL_HLR(10) CMBL_HLR(12) CMBL_HLR(14)
+                        CMBL_HLR(16)
+#undef CMBL_HLR
+                        default: break;
+                    }
+                } else {
+                    const size_t lds = (size_t)(9 * hl.m * hl.m + 3 * hl.m) * sizeof(double);
+                    hipExtLaunchKernelGGL(cmbl_hl_kernel, dim3(W * nb), dim3(64), lds, stream, e0, e1, 0, hl,
+                                          (const double *)cmat, qf.x_rows(qws), W);
+                }
             });
             HIP_CHECK(hipGetLastError());
         }
