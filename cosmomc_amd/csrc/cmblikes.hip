@@ -95,6 +95,8 @@ struct CLDev {
     int LP;                         // profile row length: prof[w][3][LP], indexed by l (zero outside lmin..lmax)
     const BKMap *bkmaps;
     const double *bp_nu, *bp_R, *bp_dnu;
+    const double *bp_lnu;           // log(nu) of every bandpass sample
+    const double *log_l80;          // log(l / 80), l = 0 .. LP-1
     double fpivot_dust, fpivot_sync, decorr_dust[2], decorr_sync[2];
     int lform_dust, lform_sync;     // 0 flat, 1 lin, 2 quad
 };
@@ -144,8 +146,9 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
         double gb = 0.0, pl = 0.0;
         for (int k = lane; k < m.n; k += 64) {
             const double nu = c.bp_nu[m.off + k], R = c.bp_R[m.off + k], dn = c.bp_dnu[m.off + k];
-            gb += dn * R * pow(nu, 3 + betadust) / (exp(G * nu / Tdust) - 1);
-            pl += dn * R * pow(nu, 2 + betasync);
+            const double lnu = c.bp_lnu[m.off + k];          // nu^e as exp(e log nu): one exp instead of a pow
+            gb += dn * R * exp((3 + betadust) * lnu) / (exp(G * nu / Tdust) - 1);
+            pl += dn * R * exp((2 + betasync) * lnu);
         }
         gb = wave_sum(gb);
         pl = wave_sum(pl);
@@ -169,7 +172,6 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
             cw[2 * c.nreq + i] = bc;
         }
     }
-    const double lpivot = 80.0;
     const int LP = c.LP;
     double *pw = prof + (long long)w * 3 * LP;
     for (int l = tid; l < LP; l += blockDim.x) {
@@ -177,10 +179,10 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
             pw[l] = pw[LP + l] = pw[2 * LP + l] = 0.0;
             continue;
         }
-        pw[l] = Adust * pow(l / lpivot, alphadust);
-        pw[LP + l] = Async * pow(l / lpivot, alphasync);
-        pw[2 * LP + l] =
-            dustsync_corr * sqrt(Adust * Async) * pow(l / lpivot, (alphadust + alphasync) / 2);
+        const double ll = c.log_l80[l];                     // (l/80)^a as exp(a log(l/80))
+        pw[l] = Adust * exp(alphadust * ll);
+        pw[LP + l] = Async * exp(alphasync * ll);
+        pw[2 * LP + l] = dustsync_corr * sqrt(Adust * Async) * exp(((alphadust + alphasync) / 2) * ll);
     }
 }
 
@@ -1341,7 +1343,7 @@ struct CMBLikes final : Like {
     bool items_even = true, small_gauss = false;
     bool use_group = false;      // BK foregrounds: grouped-pair window kernel
     int n_gitem = 0;
-    DevBuf d_gitems, d_gw;
+    DevBuf d_gitems, d_gw, d_bplnu, d_logl80;
     int small_ntask = 0;
     SmallDev sdev{};
     DevBuf d_invcov, d_stasks, d_srows, d_smt, d_sct;
@@ -1977,6 +1979,11 @@ struct CMBLikes final : Like {
             up(d_bpnu, bnu.data(), bnu.size() * 8);
             up(d_bpR, bR.data(), bR.size() * 8);
             up(d_bpdnu, bdnu.data(), bdnu.size() * 8);
+            std::vector<double> blnu(bnu.size()), ll80((lmax + 2) & ~1, 0.0);
+            for (size_t k = 0; k < bnu.size(); k++) blnu[k] = std::log(bnu[k]);
+            for (int l = 1; l < (int)ll80.size(); l++) ll80[l] = std::log(l / 80.0);
+            up(d_bplnu, blnu.data(), blnu.size() * 8);
+            up(d_logl80, ll80.data(), ll80.size() * 8);
         }
         qf.init(invcov, nX);
         small_gauss = approx == 2 && nX <= SMALL_NX && small_ntask <= SMALL_MAXTASK;
@@ -2017,6 +2024,8 @@ struct CMBLikes final : Like {
         dev.LP = (lmax + 2) & ~1;
         dev.bkmaps = bk ? d_bkmaps.as<BKMap>() : nullptr;
         dev.bp_nu = bk ? d_bpnu.as<double>() : nullptr;
+        dev.bp_lnu = bk ? d_bplnu.as<double>() : nullptr;
+        dev.log_l80 = bk ? d_logl80.as<double>() : nullptr;
         dev.bp_R = bk ? d_bpR.as<double>() : nullptr;
         dev.bp_dnu = bk ? d_bpdnu.as<double>() : nullptr;
         hl.n = nmaps;
