@@ -51,8 +51,10 @@ typedef struct cmbl cmbl_t;
 
 /* tag -> likelihood class as CMBLikelihood_Add (source/CMB.f90:80-97):
  * "PLIK_LITE" native plik_lite (CMB.f90:30-329), "BKPLANCK" CMBlikes with the
- * BICEP/Keck/Planck foregrounds (CMB_BK_Planck.f90), "WMAP" / "SPTPOL_TEEE" /
- * "SPTPOL_BB" / "SMICA" CMBL_ERR_UNSUPPORTED, any other tag a CMBlikes
+ * BICEP/Keck/Planck foregrounds (CMB_BK_Planck.f90), "SPTPOL_TEEE" / "SPTPOL_BB"
+ * the SPTpol TE/EE 2017 and BB 2019 likelihoods (CMB_SPTpol_TEEE_2017.f90,
+ * CMB_SPTpol_BB_2019.f90; sptpol_blind_r is CMBL_ERR_UNSUPPORTED),
+ * "WMAP" / "SMICA" CMBL_ERR_UNSUPPORTED, any other tag a CMBlikes
  * dataset (CMBlikes.f90; like_approx HL or gaussian, binned).
  * override_ini: "key = value" lines applied over the dataset file, as
  * cmb_dataset[TAG,key] = value (source/CMB.f90:71-74); may be NULL. */
