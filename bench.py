@@ -17,6 +17,11 @@ likelihoods + the calPlanck prior.  Synthetic theory of the Planck l_max shape
 per-step collective ("weak" scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 1024] [--no-lensing]
+
+The JSON line also carries, outside the headline value: "convergence" (R-1 vs
+wall-clock for the headline workload) and "config5_bk15_plik" (BASELINE
+configs[4]: BK15 + plik_lite jointly, fast-step throughput and R-1 vs
+wall-clock with the cross-GPU exchange).
 """
 from __future__ import annotations
 
@@ -57,6 +62,8 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse ranks")
     p.add_argument("--converge-seconds", type=float, default=20.0,
                    help="R-1 vs wall-clock run after the throughput timing (0 = skip)")
+    p.add_argument("--config5-seconds", type=float, default=60.0,
+                   help="BK15 + plik_lite (BASELINE configs[4]) throughput and R-1 run (< 0 = skip)")
     return p.parse_args()
 
 
@@ -174,6 +181,100 @@ def convergence_run(W, rank, world, tmpdir, seconds, lensing=True):
                         "calPlanck fast, overdispersed start (1 +- 0.01)",
             "walkers_total": W * world, "target_r_minus_1": 0.01, "exchange_every_steps": steps_block,
             "converged_wall_s": done_at, "trace_wall_s_steps_R": trace}
+
+
+BK15_DATASET = "BK15/BK15_dust.dataset"
+BK15_MAPS = "BK15_95_B BK15_150_B BK15_220_B W023_B P030_B W033_B P044_B P070_B P100_B P143_B P217_B P353_B"
+
+
+def config5_run(W, rank, world, tmpdir, seconds, steps=100):
+    """BASELINE configs[4]: BK15 (12 B maps x 9 bins, HL, batch3/BK15.ini selection;
+    the reference does not ship its covariance, a synthetic one of the file's
+    shape is used) + plik_lite TTTEEE jointly, on one shared cached slow point.
+    Fast parameters: calPlanck and the seven BK15.ini foreground parameters
+    (BBdust, BBsync, BBalphadust, BBbetadust, BBalphasync, BBbetasync,
+    BBdustsynccorr, with its ranges and Gaussian priors); the rest of the 16 BK
+    nuisances fixed as in BK15.ini.  Reports fast-step throughput and R-1 vs
+    wall-clock with the cross-GPU exchange every 40 x n_used samples."""
+    import torch
+    from cosmomc_amd import synthetic as syn
+    from cosmomc_amd.converge import CollectorSettings, ConvergenceExchange, reference_window
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    rd = extract_refdata(os.path.join(tmpdir, "c5"))
+    syn.write_bk15_covmat(os.path.join(rd, "BK15"))
+    plik = NativeCMBLikelihood("PLIK_LITE", syn.make_plik_lite(12345).write(os.path.join(tmpdir, "c5p")))
+    bk = NativeCMBLikelihood("BKPLANCK", os.path.join(rd, BK15_DATASET), {"maps_use": BK15_MAPS})
+    plik.nuisance_indices = [1]
+    bk.nuisance_indices = list(range(2, 18))
+    #        calPlanck BBdust BBsync adust bdust  Tdust async  bsync  corr  EEd  EEs  Dd   Ds   gc   g95  g150 g220
+    P0 = np.array([1.0, 3.0, 1.0, -0.42, 1.59, 19.6, -0.6, -3.1, 0.2, 2.0, 2.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0])
+    pmin, pmax = P0.copy(), P0.copy()
+    for i, lo, hi in ((0, 0.9, 1.1), (1, 0.0, 15.0), (2, 0.0, 50.0), (3, -1.0, 0.0), (4, 1.04, 2.14),
+                      (6, -1.0, 0.0), (7, -4.5, -2.0), (8, -1.0, 1.0)):
+        pmin[i], pmax[i] = lo, hi
+    pm, ps = np.zeros(17), np.zeros(17)
+    pm[0], ps[0] = 1.0, 0.0025
+    pm[4], ps[4] = 1.59, 0.11
+    pm[7], ps[7] = -3.1, 0.3
+    used = [1, 2, 3, 4, 5, 7, 8, 9]
+    # starting proposal: a diagonal guess of the posterior widths (no covmat; the
+    # reference then learns the proposal freely, covariance_is_diagonal)
+    width = np.array([0.0025, 0.5, 1.0, 0.1, 0.1, 0.1, 0.3, 0.2])
+    smp = BatchedMCMC(W, 17, used, [[1], [2, 3, 4, 5, 6, 7, 8]], 0, pmin, pmax, pm, ps, propose_scale=2.4,
+                      seed_ij=3003 + rank, seed_kl=9373, first_walker=rank * W)
+    smp.set_covariance(np.diag(width ** 2))
+    th = torch.tensor(syn.walker_theory(1, n_fields=10, ld_field=2512), device="cuda")
+    th = th.expand(W, th.shape[1], th.shape[2])       # one cached slow point for everyone
+    smp.add_likelihood(plik, th)
+    smp.add_likelihood(bk, th)
+    start = np.tile(P0, (W, 1))
+    g = syn.gaussians(91 + rank, W * 8).reshape(W, 8)
+    for c, i in enumerate([u - 1 for u in used]):
+        start[:, i] = np.clip(P0[i] + 2 * width[c] * g[:, c], pmin[i] + 1e-9, pmax[i] - 1e-9)
+    smp.set_start(start)
+    smp.step(5, fast_only=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    smp.step(steps, fast_only=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    out = {"workload": "BK15 (12 B maps x 9 bins, HL, synthetic covariance) + plik_lite_TTTEEE joint, "
+                       "8 fast parameters (calPlanck + 7 BK15 foreground), one shared slow point",
+           "walkers_total": W * world, "evals_per_s": W * world * steps / dt, "ms_per_step": dt / steps * 1e3}
+    if seconds > 0:
+        steps_block = 40 * len(used)                   # MPI_Sample_update_freq (SampleCollector.f90:399-403)
+        cap = 100 * steps_block
+        smp.enable_history(cap)
+        ex = ConvergenceExchange(len(used), CollectorSettings(MPI_R_Stop=0.01, MPI_Min_Sample_Update=55,
+                                                              covariance_is_diagonal=True))
+        trace, t0, done_at = [], time.perf_counter(), None
+        while smp.history_count() + steps_block <= cap:
+            smp.step(steps_block, fast_only=True)
+            r = ex.update_cov_and_check_converge(smp, *reference_window(smp.history_count()))
+            el = time.perf_counter() - t0
+            trace.append([round(el, 3), smp.history_count(), r.R])
+            if r.update_proposal:
+                smp.set_covariance(r.propose_cov)
+            if r.converged:
+                done_at = el
+                break
+            stop = el > seconds
+            if world > 1:
+                import torch.distributed as dist
+                flag = torch.tensor([1.0 if stop else 0.0], dtype=torch.float64, device="cuda")
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                stop = flag.item() > 0
+            if stop:
+                break
+        out.update({"target_r_minus_1": 0.01, "exchange_every_steps": steps_block, "converged_wall_s": done_at,
+                    "trace_wall_s_steps_R": trace})
+    return out
 
 
 def cpu_baseline(seconds, lensing=True):
@@ -329,6 +430,9 @@ def main():
         conv = None
         if args.converge_seconds > 0:
             conv = convergence_run(W, rank, world, td, args.converge_seconds, lensing=not args.no_lensing)
+        c5 = None
+        if args.config5_seconds >= 0:
+            c5 = config5_run(W, rank, world, td, args.config5_seconds)
 
     dom = max(kern, key=lambda k: kern[k][0])
     avg_ms = {k: (v[0] / v[1] if v[1] else None) for k, v in kern.items()}
@@ -367,6 +471,8 @@ def main():
         }
         if conv is not None:
             out["convergence"] = conv
+        if c5 is not None:
+            out["config5_bk15_plik"] = c5
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, lensing=not args.no_lensing)
         print(json.dumps(out), flush=True)
