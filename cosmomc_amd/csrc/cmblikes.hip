@@ -998,12 +998,12 @@ __global__ __launch_bounds__(64) void cmbl_hl_kernel(HLDev h, const double *__re
 // matrix, and a 64-lane block runs four (walker, bin) problems.  A Jacobi
 // round is a column rotation of the lane's own row (the round's (c, s) of
 // every column read from LDS) followed by the row rotation with the partner
-// row (one LDS exchange); rounds are unrolled over the compile-time matrix
-// edge M so every register index is static.  The matrix products go through
-// per-group LDS row buffers.
+// row (one LDS exchange); the column rotation is dispatched per round to a
+// compile-time instance, so every register index is static.  The matrix
+// products go through per-group LDS row buffers.
 template <int M>
 struct HLRowsLds {
-    double rows[4][3][16][M + 1];   // three row buffers per problem (odd stride: fewer bank conflicts)
+    double rows[4][2][16][M + 1];   // two row buffers per problem (odd stride: fewer bank conflicts)
     double cs[4][16][2];            // (c, s) of each column in the current round
     double dg[4][16];               // a diagonal / g(x) broadcast
 };
@@ -1023,18 +1023,47 @@ __device__ inline int hl_partner(int rr, int r) {   // round-robin pairing of ro
     return ((2 * rr - r) % (M - 1) + (M - 1)) % (M - 1);
 }
 
-// cyclic Jacobi of the group's M x M matrix (row r in A), eigenvectors in V (row r).
-// The partner column of every column changes from round to round, so the
-// lane's own rows are mirrored into LDS (rows[.][1], rows[.][2]) to be read at
-// runtime indices instead of indexing registers.
+// column rotation of one row for round RR (compile-time, so the partner
+// column of every column is a static register index): B = A J, V = V J
+template <int M, int RR>
+__device__ __forceinline__ void hl_colrot(double (&A)[M], double (&V)[M], const double (*cs)[2])
+{
+    if constexpr (RR < M - 1) {
+        double An[M], Vn[M];
+#pragma unroll
+        for (int k = 0; k < M; k++) {
+            const int pk = (k == M - 1) ? RR : (k == RR ? M - 1 : ((2 * RR - k) % (M - 1) + (M - 1)) % (M - 1));
+            const double ck = cs[k][0], sk = cs[k][1];
+            An[k] = A[k] * ck + A[pk] * sk;
+            Vn[k] = V[k] * ck + V[pk] * sk;
+        }
+#pragma unroll
+        for (int k = 0; k < M; k++) {
+            A[k] = An[k];
+            V[k] = Vn[k];
+        }
+    }
+}
+
+template <int M>
+__device__ __forceinline__ void hl_colrot_round(int rr, double (&A)[M], double (&V)[M], const double (*cs)[2])
+{
+    switch (rr) {
+#define HLC(R) case R: hl_colrot<M, R>(A, V, cs); break;
+        HLC(0) HLC(1) HLC(2) HLC(3) HLC(4) HLC(5) HLC(6) HLC(7) HLC(8) HLC(9) HLC(10) HLC(11) HLC(12) HLC(13)
+        HLC(14)
+#undef HLC
+        default: break;
+    }
+}
+
+// cyclic Jacobi of the group's M x M matrix (row r in A), eigenvectors in V (row r)
 template <int M>
 __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, int grp, int r, int lane,
                                int max_sweeps)
 {
 #pragma unroll
     for (int k = 0; k < M; k++) V[k] = (k == r) ? 1.0 : 0.0;
-    double *Aown = S.rows[grp][1][r < M ? r : 0];
-    double *Vown = S.rows[grp][2][r < M ? r : 0];
     for (int sweep = 0; sweep < max_sweeps; sweep++) {
         // convergence (as cmbl_hl_kernel): every off-diagonal |a_rk| <= 1e-18 sqrt(|a_rr a_kk|) or 0
         if (r < M) S.dg[grp][r] = hl_pick<M>(A, r);
@@ -1059,11 +1088,6 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
                 p = hl_partner<M>(rr, r);
                 S.dg[grp][r] = hl_pick<M>(A, r);
                 S.rows[grp][0][r][0] = hl_pick<M>(A, p);
-#pragma unroll
-                for (int k = 0; k < M; k++) {
-                    Aown[k] = A[k];
-                    Vown[k] = V[k];
-                }
             }
             __syncthreads();
             if (r < M) {
@@ -1084,13 +1108,7 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
             __syncthreads();
             // (2) B = A J, V = V J on this lane's row; (3) A' = J^T B: row r = c B_r + s B_p
             if (r < M) {
-#pragma unroll
-                for (int k = 0; k < M; k++) {
-                    const int pk = hl_partner<M>(rr, k);
-                    const double ck = S.cs[grp][k][0], sk = S.cs[grp][k][1];
-                    A[k] = A[k] * ck + Aown[pk] * sk;     // B, kept in A
-                    V[k] = V[k] * ck + Vown[pk] * sk;
-                }
+                hl_colrot_round<M>(rr, A, V, S.cs[grp]);
 #pragma unroll
                 for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = A[k];
             }
