@@ -1126,7 +1126,7 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
 }
 
 template <int M>
-__global__ __launch_bounds__(64) void cmbl_hl_rows_kernel(HLDev h, const double *__restrict__ cmat,
+__global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLDev h, const double *__restrict__ cmat,
                                                          double *__restrict__ xrows, int W, int max_sweeps)
 {
     __shared__ HLRowsLds<M> S;
