@@ -112,13 +112,17 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
             for (int q = 0; q < 4; q++)
                 a[t][q] = *reinterpret_cast<const double2 *>(A + r * BK + (((lk * 4 + q) ^ swz(r)) * 2));
         }
+        // consecutive MFMAs go to different accumulators (dependency distance 4);
+        // each accumulator still sums k in the same order
 #pragma unroll
-        for (int q = 0; q < 4; q++)
+        for (int q = 0; q < 4; q++) {
 #pragma unroll
-            for (int t = 0; t < 4; t++) {
+            for (int t = 0; t < 4; t++)
                 acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][q].x, b[q].x, acc[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 4; t++)
                 acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][q].y, b[q].y, acc[t], 0, 0, 0);
-            }
+        }
     }
     __syncthreads();                                  // all waves done with the operand buffers
     // Delta_I tile: smem[n][i] (row stride QF_TILE+2)
