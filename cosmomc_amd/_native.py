@@ -103,6 +103,11 @@ def lib():
         L.cmbs_history_count.argtypes = [vp]
         L.cmbs_state.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
         L.cmbs_get_state_host.argtypes = [vp, vp, vp, vp, vp]
+        L.cmbs_state_bytes.argtypes = [vp]
+        L.cmbs_state_bytes.restype = sz
+        L.cmbs_save_state.argtypes = [vp, vp, sz]
+        L.cmbs_load_state.argtypes = [vp, vp, sz]
+        L.cmbs_history_restore.argtypes = [vp, i, i, vp]
         L.cmbl_profile_enable.argtypes = [i]
         L.cmbl_profile_reset.argtypes = []
         L.cmbl_profile_read.argtypes = [C.c_char_p, C.POINTER(d), C.POINTER(ll)]

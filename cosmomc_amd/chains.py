@@ -100,6 +100,26 @@ class ChainWriter:
             self.add_rows(sampler.history_host(first, count))
         self.next_step = first + max(count, 0)
 
+    def checkpoint_state(self) -> dict:
+        """What a resume needs: the open weighted rows, the next history step
+        and every chain file's length (rows written after the checkpoint are
+        cut off on resume, so the files continue as if never interrupted)."""
+        walkers = self.pending.keys()
+        return {"pending": {str(w): [np.asarray(c[0]).tolist(), int(c[1])]
+                            for w, c in self.pending.items() if c is not None},
+                "next_step": self.next_step,
+                "sizes": {str(w): (os.path.getsize(self._file(w)) if os.path.exists(self._file(w)) else 0)
+                          for w in walkers}}
+
+    def restore(self, state: dict):
+        for w, n in state.get("sizes", {}).items():
+            f = self._file(int(w))
+            if os.path.exists(f) and os.path.getsize(f) > n:
+                with open(f, "r+b") as fh:
+                    fh.truncate(n)
+        self.pending = {int(w): [np.asarray(p, dtype=np.float64), c] for w, (p, c) in state["pending"].items()}
+        self.next_step = state.get("next_step")
+
     def close(self):
         for w, cur in self.pending.items():
             if cur is not None:

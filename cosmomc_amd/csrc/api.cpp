@@ -15,6 +15,10 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream);
 void sampler_enable_history(cmbs *s, int capacity);
 void sampler_history_stats(cmbs *s, int first, int last, double *means, double *covs, hipStream_t stream);
 void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, int *num_accept);
+size_t sampler_state_bytes(const cmbs *s);
+void sampler_history_restore(cmbs *s, int first, int count, const double *in);
+void sampler_save_state(cmbs *s, void *buf, size_t bytes);
+void sampler_load_state(cmbs *s, const void *buf, size_t bytes);
 void launch_clik_to_dl(const double *clp, long long ld, const int *lm, double *dl, long long ld_field,
                        long long ld_walker, int lmax_out, int W, hipStream_t stream);
 }  // namespace cmamd
@@ -292,6 +296,23 @@ int cmbs_state(cmbs_t *s, double **P, double **cur_like, double **mult, int **nu
 int cmbs_get_state_host(cmbs_t *s, double *P, double *cur_like, double *mult, int *num_accept) {
     if (!s) return CMBL_ERR_ARG;
     return guarded(&s->last_error, [&] { cmamd::sampler_get_state_host(s, P, cur_like, mult, num_accept); });
+}
+
+size_t cmbs_state_bytes(const cmbs_t *s) { return s ? cmamd::sampler_state_bytes(s) : 0; }
+
+int cmbs_save_state(cmbs_t *s, void *buf, size_t bytes) {
+    if (!s || !buf) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_save_state(s, buf, bytes); });
+}
+
+int cmbs_history_restore(cmbs_t *s, int first, int count, const double *in) {
+    if (!s || (count > 0 && !in)) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_history_restore(s, first, count, in); });
+}
+
+int cmbs_load_state(cmbs_t *s, const void *buf, size_t bytes) {
+    if (!s || !buf) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_load_state(s, buf, bytes); });
 }
 
 }  // extern "C"

@@ -1384,6 +1384,25 @@ void sampler_history_host(cmbs *s, int first, int count, double *out) {
     }
 }
 
+// checkpoint resume of the history ring: rows [first, first + count) as
+// written by sampler_history_host go back to their ring slots, and the ring
+// continues at first + count (the samples the convergence test windows over,
+// TMpiChainCollector_ReadState's Samples%LoadState, SampleCollector.f90:167)
+void sampler_history_restore(cmbs *s, int first, int count, const double *in) {
+    if (s->hist_cap == 0) fail(CMBL_ERR_ARG, "history not enabled");
+    if (first < 0 || count < 0 || count > s->hist_cap)
+        fail(CMBL_ERR_ARG, "history rows [%d, %d) do not fit the ring (capacity %d)", first, first + count,
+             s->hist_cap);
+    HIP_CHECK(hipDeviceSynchronize());
+    const size_t blk = (size_t)(s->n_used + 1) * s->W;
+    for (int k = 0; k < count; k++) {
+        const int slot = (first + k) % s->hist_cap;
+        HIP_CHECK(hipMemcpy(s->hist.as<double>() + (size_t)slot * blk, in + (size_t)k * blk, blk * 8,
+                            hipMemcpyHostToDevice));
+    }
+    s->hist_count = first + count;
+}
+
 void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, int *num_accept) {
     HIP_CHECK(hipDeviceSynchronize());
     const int W = s->W, np = s->np;
@@ -1399,6 +1418,71 @@ void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, 
     if (mult) HIP_CHECK(hipMemcpy(mult, s->dc.sd + (size_t)R.M * ld, (size_t)W * 8, hipMemcpyDeviceToHost));
     if (num_accept)
         HIP_CHECK(hipMemcpy(num_accept, s->dc.si + (size_t)R.NACC * ld, (size_t)W * 4, hipMemcpyDeviceToHost));
+}
+
+// Checkpoint image of every walker's chain state: the reference's .chk holds
+// num_sample / MaxLike / num_accept (MCMC.f90:98-114, 199-218) and the
+// proposal matrix (propose.f90:308-325) and restarts from the last chain row
+// with a fresh RNG (GeneralSetup.f90:123-131); this image holds the complete
+// device state instead -- point, CurLike, multiplicity, accept count, RANMAR
+// table and Gaussian1 cache, cyclic-index and rotation state -- so a resumed
+// run continues each chain exactly.  Layout: StateHeader, double rows
+// [ND][W], int rows [NI][W].  The proposal covariance is the caller's part
+// (cmbs_set_covariance before cmbs_load_state).
+struct StateHeader {
+    unsigned magic, version;
+    int W, np, n_used, nblocks, all_n, slow_n, fast_n, R_total, ND, NI;
+    long long num_drag;
+};
+static constexpr unsigned STATE_MAGIC = 0x53424d43u;   // "CMBS"
+
+size_t sampler_state_bytes(const cmbs *s) {
+    const Rows &R = s->dc.rows;
+    return sizeof(StateHeader) + (size_t)R.ND * s->W * 8 + (size_t)R.NI * s->W * 4;
+}
+
+static StateHeader state_header(const cmbs *s) {
+    const Rows &R = s->dc.rows;
+    return StateHeader{STATE_MAGIC, 1u, s->W, s->np, s->n_used, s->nblocks, s->all_n, s->slow_n, s->fast_n,
+                       s->R_total, R.ND, R.NI, s->num_drag};
+}
+
+void sampler_save_state(cmbs *s, void *buf, size_t bytes) {
+    if (!s->started) fail(CMBL_ERR_ARG, "no chain state yet: cmbs_set_start first");
+    if (bytes < sampler_state_bytes(s)) fail(CMBL_ERR_ARG, "state buffer too small (%zu < %zu bytes)", bytes,
+                                            sampler_state_bytes(s));
+    HIP_CHECK(hipDeviceSynchronize());
+    const Rows &R = s->dc.rows;
+    const size_t ld = s->dc.ld, W = s->W;
+    char *p = static_cast<char *>(buf);
+    const StateHeader h = state_header(s);
+    std::memcpy(p, &h, sizeof h);
+    p += sizeof h;
+    HIP_CHECK(hipMemcpy2D(p, W * 8, s->dc.sd, ld * 8, W * 8, R.ND, hipMemcpyDeviceToHost));
+    p += (size_t)R.ND * W * 8;
+    HIP_CHECK(hipMemcpy2D(p, W * 4, s->dc.si, ld * 4, W * 4, R.NI, hipMemcpyDeviceToHost));
+}
+
+void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
+    if (bytes < sizeof(StateHeader)) fail(CMBL_ERR_ARG, "state image too short");
+    StateHeader h;
+    std::memcpy(&h, buf, sizeof h);
+    if (h.magic != STATE_MAGIC || h.version != 1u) fail(CMBL_ERR_FORMAT, "not a cmbs state image");
+    const StateHeader m = state_header(s);
+    if (h.W != m.W || h.np != m.np || h.n_used != m.n_used || h.nblocks != m.nblocks || h.all_n != m.all_n ||
+        h.slow_n != m.slow_n || h.fast_n != m.fast_n || h.R_total != m.R_total || h.ND != m.ND || h.NI != m.NI)
+        fail(CMBL_ERR_ARG, "state image is for a different sampler (W %d np %d blocks %d; this one W %d np %d blocks %d)",
+             h.W, h.np, h.nblocks, m.W, m.np, m.nblocks);
+    if (bytes < sampler_state_bytes(s)) fail(CMBL_ERR_FORMAT, "state image truncated");
+    const Rows &R = s->dc.rows;
+    const size_t ld = s->dc.ld, W = s->W;
+    const char *p = static_cast<const char *>(buf) + sizeof h;
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemcpy2D(s->dc.sd, ld * 8, p, W * 8, W * 8, R.ND, hipMemcpyHostToDevice));
+    p += (size_t)R.ND * W * 8;
+    HIP_CHECK(hipMemcpy2D(s->dc.si, ld * 4, p, W * 4, W * 4, R.NI, hipMemcpyHostToDevice));
+    s->num_drag = h.num_drag;
+    s->started = true;
 }
 
 }  // namespace cmamd

@@ -143,6 +143,7 @@ class BatchedMCMC:
 
     def enable_history(self, capacity: int):
         self._check(N.lib().cmbs_enable_history(self._h, capacity))
+        self._hist_cap = capacity
 
     def history_count(self) -> int:
         return N.lib().cmbs_history_count(self._h)
@@ -186,6 +187,24 @@ class BatchedMCMC:
         self._check(N.lib().cmbs_get_state_host(self._h, P.ctypes.data, like.ctypes.data, mult.ctypes.data,
                                                 nacc.ctypes.data))
         return P, like, mult, nacc
+
+    def save_state(self) -> bytes:
+        """Every walker's complete chain state (cmbs_save_state): point,
+        CurLike, multiplicity, accept count, RANMAR and proposer state."""
+        n = N.lib().cmbs_state_bytes(self._h)
+        buf = C.create_string_buffer(n)
+        self._check(N.lib().cmbs_save_state(self._h, buf, n))
+        return buf.raw
+
+    def load_state(self, image: bytes):
+        """Resume from save_state's image (set_covariance first); replaces set_start."""
+        buf = C.create_string_buffer(bytes(image), len(image))
+        self._check(N.lib().cmbs_load_state(self._h, buf, len(image)))
+
+    def history_restore(self, first: int, rows):
+        """Put history rows [first, first + len(rows)) back (layout of history_host)."""
+        r = np.ascontiguousarray(rows, dtype=np.float64)
+        self._check(N.lib().cmbs_history_restore(self._h, first, r.shape[0], r.ctypes.data))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -232,6 +232,25 @@ int  cmbs_state(cmbs_t *s, double **P, double **cur_like, double **mult, int **n
  * P [W][num_params], cur_like [W], mult [W], num_accept [W]. */
 int  cmbs_get_state_host(cmbs_t *s, double *P, double *cur_like, double *mult, int *num_accept);
 
+/* Checkpoint / resume (replaces TMpiChainCollector_SaveState / ReadState,
+ * SampleCollector.f90:139-202, and TChainSampler_SaveState / LoadState,
+ * MCMC.f90:199-218).  The image is every walker's complete chain state
+ * (point, CurLike, multiplicity, accept count, RANMAR state, proposer
+ * cycle/rotation state), so a resumed chain continues exactly where it
+ * stopped; the reference restarts from the last chain row with a new random
+ * sequence instead.  The proposal covariance is not in the image: restore it
+ * with cmbs_set_covariance first.  Loading checks the sampler shape and marks
+ * the sampler started (no cmbs_set_start needed). */
+size_t cmbs_state_bytes(const cmbs_t *s);
+int  cmbs_save_state(cmbs_t *s, void *host_buf, size_t bytes);
+int  cmbs_load_state(cmbs_t *s, const void *host_buf, size_t bytes);
+
+/* Put history rows [first, first + count) back (HOST array laid out as
+ * cmbs_history_host writes it; count <= capacity) and continue the ring at
+ * first + count: the samples the convergence exchange windows over survive a
+ * resume (Samples%LoadState, SampleCollector.f90:167). */
+int  cmbs_history_restore(cmbs_t *s, int first, int count, const double *rows);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,130 @@
+"""Checkpoint / resume on the GPU (cmbs_save_state / cmbs_load_state,
+cosmomc_amd.checkpoint): a run stopped at a checkpoint and resumed in a fresh
+sampler continues every chain exactly -- the same points, likelihoods,
+multiplicities and accept counts, the same chain files and history -- as the
+run that never stopped.  The reference (SampleCollector.f90:139-202,
+GeneralSetup.f90:123-131) restarts from the last chain row with a new random
+sequence, so there is no reference output to pin; the uninterrupted run is
+the oracle here."""
+import numpy as np
+import pytest
+
+from cosmomc_amd import synthetic as syn
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _gauss_sampler(ch, W):
+    from cosmomc_amd.sampler import BatchedMCMC
+    n = ch["n"]
+    s = BatchedMCMC(W, n, list(range(1, n + 1)), ch["blocks"], ch["slow_block_max"], ch["pmin"], ch["pmax"],
+                    ch["prior_mean"], ch["prior_std"], oversample_fast=ch["oversample_fast"],
+                    propose_scale=ch["propose_scale"], temperature=ch["temperature"], seed_ij=ch["ij"],
+                    seed_kl=ch["kl"])
+    s.set_test_gaussian(np.array(ch["cov"]), np.array(ch["center"]))
+    return s
+
+
+def _same_state(a, b):
+    for x, y in zip(a.state(), b.state()):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("name", ["gauss6_blocked", "gauss6_fast_only", "gauss3_n1_blocks"])
+def test_resume_continues_chains_exactly(rng_golden, tmp_path, name):
+    from cosmomc_amd.checkpoint import read_checkpoint, write_checkpoint
+    ch = rng_golden["chains"][name]
+    W, fast = 128, bool(ch["fast_only"])
+    a = _gauss_sampler(ch, W)
+    a.set_covariance(np.array(ch["cov"]))
+    a.set_start(np.tile(np.array(ch["P0"]), (W, 1)))
+    a.step(25, fast_only=fast)
+    root = str(tmp_path / "run")
+    write_checkpoint(root, a, np.array(ch["cov"]), collector={"num_sample": 25})
+    a.step(40, fast_only=fast)
+    b = _gauss_sampler(ch, W)
+    assert read_checkpoint(root, b) == {"num_sample": 25}
+    b.step(40, fast_only=fast)
+    _same_state(a, b)
+
+
+def test_resume_dragging(rng_golden, tmp_path):
+    from cosmomc_amd.checkpoint import read_checkpoint, write_checkpoint
+    ch = rng_golden["chains"]["gauss6_drag"]
+    W = 64
+    a = _gauss_sampler(ch, W)
+    a.set_covariance(np.array(ch["cov"]))
+    a.set_start(np.tile(np.array(ch["P0"]), (W, 1)))
+    a.step_drag(6, 3.0)
+    root = str(tmp_path / "drag")
+    write_checkpoint(root, a, np.array(ch["cov"]))
+    a.step_drag(6, 3.0)
+    b = _gauss_sampler(ch, W)
+    read_checkpoint(root, b)
+    b.step_drag(6, 3.0)
+    _same_state(a, b)
+
+
+def test_resume_plik_chain_files_and_history(tmp_path):
+    """plik_lite fast chains with chain files and the history ring: the run
+    that crashed after its checkpoint (rows already written past it) and was
+    resumed writes byte-identical chain files to the uninterrupted run, and
+    the convergence window statistics agree."""
+    from cosmomc_amd.chains import ChainWriter
+    from cosmomc_amd.checkpoint import read_checkpoint, write_checkpoint
+    from cosmomc_amd.converge import ConvergenceExchange
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    data = syn.make_plik_lite(12345)
+    like = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    like.nuisance_indices = [2]
+    W = 96
+    dl = torch.tensor(syn.walker_theory(W, seed=3, n_fields=3), device="cuda")
+    P0 = np.array([0.0222, 1.0, 3.05])
+    cov = np.array([[0.002 ** 2]])
+
+    def sampler():
+        s = BatchedMCMC(W, 3, [2], [[1]], 0, [0.0222, 0.9, 3.05], [0.0222, 1.1, 3.05], [0.0, 1.0, 0.0],
+                        [0.0, 0.0025, 0.0], seed_ij=55, seed_kl=66)
+        s.add_likelihood(like, dl)
+        s.enable_history(50)
+        return s
+
+    ref = sampler()
+    ref.set_covariance(cov)
+    ref.set_start(np.tile(P0, (W, 1)))
+    cw = ChainWriter(str(tmp_path / "ref"), ["calPlanck"])
+    for _ in range(3):
+        ref.step(30, fast_only=True)
+        cw.append(ref)
+    cw.close()
+
+    a = sampler()
+    a.set_covariance(cov)
+    a.set_start(np.tile(P0, (W, 1)))
+    ex = ConvergenceExchange(1)
+    ex.flukecheck = True
+    cwa = ChainWriter(str(tmp_path / "run"), ["calPlanck"])
+    for _ in range(2):
+        a.step(30, fast_only=True)
+        cwa.append(a)
+    write_checkpoint(str(tmp_path / "run"), a, cov, chains=cwa, exchange=ex)
+    a.step(30, fast_only=True)
+    cwa.append(a)                                   # written, then the job dies
+    del a, cwa
+
+    b = sampler()
+    ex2 = ConvergenceExchange(1)
+    cwb = ChainWriter(str(tmp_path / "run"), ["calPlanck"])
+    read_checkpoint(str(tmp_path / "run"), b, chains=cwb, exchange=ex2)
+    assert ex2.flukecheck
+    assert b.history_count() == 60
+    b.step(30, fast_only=True)
+    cwb.append(b)
+    cwb.close()
+    _same_state(ref, b)
+    for w in range(W):
+        assert (tmp_path / f"run_{w + 1}.txt").read_bytes() == (tmp_path / f"ref_{w + 1}.txt").read_bytes()
+    for x, y in zip(ref.history_stats(45, 89), b.history_stats(45, 89)):
+        assert torch.equal(x, y)
