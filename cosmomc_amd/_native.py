@@ -107,7 +107,8 @@ def lib():
         L.cmbs_state_bytes.restype = sz
         L.cmbs_save_state.argtypes = [vp, vp, sz]
         L.cmbs_load_state.argtypes = [vp, vp, sz]
-        L.cmbs_history_restore.argtypes = [vp, i, i, vp]
+        L.cmbs_history_restore.argtypes = [vp, i, i, vp, vp]
+        L.cmbs_history_terms_host.argtypes = [vp, i, i, vp]
         L.cmbl_profile_enable.argtypes = [i]
         L.cmbl_profile_reset.argtypes = []
         L.cmbl_profile_read.argtypes = [C.c_char_p, C.POINTER(d), C.POINTER(ll)]

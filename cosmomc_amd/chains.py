@@ -10,6 +10,13 @@ Here every walker is a chain: the sampler's history ring holds each walker's
 current point and -lnL after every step (``cmbs_history_host``); runs of
 identical consecutive points are the reference's weighted rows.  A run that is
 still open at the end of a block stays pending until it closes (or ``close``).
+
+With ``likelihoods`` given, rows carry the reference's likelihood-derived
+columns (AddOutputLikelihoodParams / addLikelihoodDerivedParams,
+source/GeneralTypes.f90:671-776): ``chi2_<tag>`` = 2 x each likelihood's -lnL
+at the point (``cmbs_history_terms_host``), ``chi2_prior`` = 2 x (like -
+sum of terms), and ``chi2_<type>`` sums for every likelihood type used more
+than once; ``root.likelihoods`` lists them (OutputDescription, :792-812).
 """
 from __future__ import annotations
 
@@ -43,25 +50,65 @@ class ChainWriter:
     names / labels / ranges are for the used parameters (params_used order);
     ranges: list of (min, max) or None."""
 
-    def __init__(self, root: str, names, labels=None, ranges=None, walkers=None, first_chain: int = 1):
+    def __init__(self, root: str, names, labels=None, ranges=None, walkers=None, first_chain: int = 1,
+                 likelihoods=None):
+        """likelihoods: one (tag, type, name, version) per sampler likelihood,
+        in add_likelihood order, to add the chi2_* columns."""
         self.root = root
         self.names = list(names)
         self.labels = list(labels) if labels is not None else list(names)
         self.ranges = ranges
         self.walkers = walkers
         self.first_chain = first_chain
-        self.pending = {}                          # walker -> [point values (like, P...), count]
+        self.likelihoods = [tuple(x) for x in likelihoods] if likelihoods else []
+        self.pending = {}                          # walker -> [point values (like, P..., chi2...), count]
         self.next_step = None
         d = os.path.dirname(root)
         if d:
             os.makedirs(d, exist_ok=True)
+        derived = self._chi2_names()
         with open(root + ".paramnames", "w") as f:
             for n, lab in zip(self.names, self.labels):
                 f.write(f"{n}\t{lab}\n")
+            for n, lab in derived:
+                f.write(f"{n}*\t{lab}\n")
         if ranges is not None:
             with open(root + ".ranges", "w") as f:
                 for n, r in zip(self.names, ranges):
                     f.write(f"{n}\t{r[0]!r}\t{r[1]!r}\n")
+                for n, _ in derived:                 # AddDerivedRange(name, mn=0) (ObjectParamNames.f90:480-508)
+                    f.write(f"{n:<22}{fortran_e(0.0)}{'    N':<17}\n")
+        if self.likelihoods:
+            with open(root + ".likelihoods", "w") as f:
+                for tag, typ, name, ver in self.likelihoods:
+                    f.write("\t".join(str(x).strip() for x in ("1", typ, tag, name, ver)) + "\n")
+
+    def _types(self):
+        """likelihood types used more than once, in first-use order, with their members"""
+        order, members = [], {}
+        for i, (_, typ, _, _) in enumerate(self.likelihoods):
+            if typ:
+                if typ not in members:
+                    order.append(typ)
+                    members[typ] = []
+                members[typ].append(i)
+        return [(t, members[t]) for t in order if len(members[t]) > 1]
+
+    def _chi2_names(self):
+        if not self.likelihoods:
+            return []
+        lab = "\\chi^2_{\\rm %s}"                     # chisq_label, settings.f90:127
+        out = [(f"chi2_{tag}", lab % tag.replace("_", "\\_")) for tag, _, _, _ in self.likelihoods]
+        out.append(("chi2_prior", lab % "prior"))
+        out += [(f"chi2_{t}", lab % t.replace("_", "\\_")) for t, _ in self._types()]
+        return out
+
+    def _derived(self, like, terms):
+        """chi2 columns [steps, n_derived] from CurLike [steps] and terms [steps, n_like]"""
+        cols = [2.0 * terms[:, i] for i in range(terms.shape[1])]
+        cols.append(2.0 * (like - terms.sum(axis=1)))
+        cols += [2.0 * terms[:, m].sum(axis=1) for _, m in self._types()]
+        return np.stack(cols, axis=1)
 
     def _file(self, w):
         return f"{self.root}_{w + self.first_chain}.txt"
@@ -69,13 +116,18 @@ class ChainWriter:
     def _emit(self, fh, point, count):
         fh.write("".join(fortran_e(v) for v in [float(count), point[0], *point[1:]]) + "\n")
 
-    def add_rows(self, rows):
-        """rows: [steps, n_used + 1, W] history block (params_used..., CurLike)."""
+    def add_rows(self, rows, terms=None):
+        """rows: [steps, n_used + 1, W] history block (params_used..., CurLike);
+        terms: [steps, n_like, W] (history_terms) when writing chi2 columns."""
         rows = np.asarray(rows)
         steps, n1, W = rows.shape
+        if self.likelihoods and (terms is None or np.shape(terms)[1] != len(self.likelihoods)):
+            raise ValueError("chi2 columns need the per-likelihood history terms of every likelihood")
         walkers = range(W) if self.walkers is None else self.walkers
         for w in walkers:
             pts = np.concatenate([rows[:, n1 - 1:n1, w], rows[:, :n1 - 1, w]], axis=1)   # like, P...
+            if self.likelihoods:
+                pts = np.concatenate([pts, self._derived(rows[:, n1 - 1, w], np.asarray(terms)[:, :, w])], axis=1)
             with open(self._file(w), "a") as fh:
                 cur = self.pending.get(w)
                 for t in range(steps):
@@ -97,7 +149,8 @@ class ChainWriter:
         if count is None:
             count = total - first
         if count > 0:
-            self.add_rows(sampler.history_host(first, count))
+            terms = sampler.history_terms(first, count) if self.likelihoods else None
+            self.add_rows(sampler.history_host(first, count), terms)
         self.next_step = first + max(count, 0)
 
     def checkpoint_state(self) -> dict:

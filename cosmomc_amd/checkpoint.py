@@ -49,6 +49,9 @@ def write_checkpoint(root: str, sampler, propose_cov, chains=None, exchange=None
         meta["history"] = {"first": first, "count": count - first, "capacity": sampler._hist_cap}
         if count > first:
             hist = np.ascontiguousarray(sampler.history_host(first, count - first)).tobytes()
+            if getattr(sampler, "_likes", None):
+                meta["history"]["terms"] = len(sampler._likes)
+                hist += np.ascontiguousarray(sampler.history_terms(first, count - first)).tobytes()
     js = json.dumps(meta).encode()
     tmp = root + ".chk_tmp"
     with open(tmp, "wb") as f:
@@ -84,11 +87,16 @@ def read_checkpoint(root: str, sampler, chains=None, exchange=None) -> dict:
     sampler.load_state(parts[1])
     h = meta.get("history")
     if h is not None and getattr(sampler, "_hist_cap", 0):
-        rows = np.frombuffer(parts[2], dtype=np.float64)
+        flat = np.frombuffer(parts[2], dtype=np.float64)
         if h["count"]:
-            rows = rows.reshape(h["count"], len(sampler.params_used) + 1, sampler.W)
+            nr = h["count"] * (len(sampler.params_used) + 1) * sampler.W
+            rows = flat[:nr].reshape(h["count"], len(sampler.params_used) + 1, sampler.W)
+            terms = None
+            if h.get("terms"):
+                terms = flat[nr:].reshape(h["count"], h["terms"], sampler.W)
             keep = min(h["count"], sampler._hist_cap)
-            sampler.history_restore(h["first"] + h["count"] - keep, rows[h["count"] - keep:])
+            sampler.history_restore(h["first"] + h["count"] - keep, rows[h["count"] - keep:],
+                                    None if terms is None else terms[h["count"] - keep:])
         else:
             sampler.history_restore(h["first"], rows.reshape(0, len(sampler.params_used) + 1, sampler.W))
     if chains is not None and meta.get("chains") is not None:

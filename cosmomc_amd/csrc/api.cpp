@@ -16,7 +16,8 @@ void sampler_enable_history(cmbs *s, int capacity);
 void sampler_history_stats(cmbs *s, int first, int last, double *means, double *covs, hipStream_t stream);
 void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, int *num_accept);
 size_t sampler_state_bytes(const cmbs *s);
-void sampler_history_restore(cmbs *s, int first, int count, const double *in);
+void sampler_history_restore(cmbs *s, int first, int count, const double *in, const double *terms);
+void sampler_history_terms_host(cmbs *s, int first, int count, double *out);
 void sampler_save_state(cmbs *s, void *buf, size_t bytes);
 void sampler_load_state(cmbs *s, const void *buf, size_t bytes);
 void launch_clik_to_dl(const double *clp, long long ld, const int *lm, double *dl, long long ld_field,
@@ -305,9 +306,14 @@ int cmbs_save_state(cmbs_t *s, void *buf, size_t bytes) {
     return guarded(&s->last_error, [&] { cmamd::sampler_save_state(s, buf, bytes); });
 }
 
-int cmbs_history_restore(cmbs_t *s, int first, int count, const double *in) {
+int cmbs_history_restore(cmbs_t *s, int first, int count, const double *in, const double *terms) {
     if (!s || (count > 0 && !in)) return CMBL_ERR_ARG;
-    return guarded(&s->last_error, [&] { cmamd::sampler_history_restore(s, first, count, in); });
+    return guarded(&s->last_error, [&] { cmamd::sampler_history_restore(s, first, count, in, terms); });
+}
+
+int cmbs_history_terms_host(cmbs_t *s, int first, int count, double *out) {
+    if (!s || (count > 0 && !out)) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_history_terms_host(s, first, count, out); });
 }
 
 int cmbs_load_state(cmbs_t *s, const void *buf, size_t bytes) {

@@ -53,6 +53,8 @@ struct DevCfg {
     int stage_R;            // R rows staged in LDS (else read in place, stride W)
     int n_like;
     const double *like_terms;       // [n_like (even)][ld] -lnL of each likelihood at the trial point
+    double *cur_terms;              // [n_like][ld] -lnL of each likelihood at the current point
+                                    //   (TCalculationAtParamPoint%Likelihoods, for chi2_* output)
     int like_nuis0[MAXLIKE], like_nn[MAXLIKE];
     double *like_nuis[MAXLIKE];     // [W][like_nn] DataParams buffers written by mh_kernel
 };
@@ -71,7 +73,7 @@ struct cmbs {
     int W = 0, np = 0, n_used = 0;
     std::vector<int> params_used;
     std::string last_error;
-    cmamd::DevBuf tab_i, tab_d, sd, si, like_terms, ws, hist, mom;
+    cmamd::DevBuf tab_i, tab_d, sd, si, like_terms, cur_terms, ws, hist, hist_terms, mom;
     cmamd::DevBuf nuis_bufs[cmamd::MAXLIKE];
     std::vector<int> h_tab_i;
     std::vector<double> h_tab_d;

@@ -361,7 +361,7 @@ __device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size
 // next trial (GetProposal / GetProposalFast) and scatter its nuisance
 // parameters for the likelihood kernels.  One wavefront per 64 walkers.
 template <bool ACCEPT, bool PROPOSE>
-__global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_only, double *hist_row, int blk0)
+__global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_only, double *hist_row, double *hist_terms, int blk0)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Rows &R = c.rows;
@@ -399,6 +399,13 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     dma_rows_i32(si, c.si, R.NI, W, wb, lane, wave, MH_WAVES);
     dma_words(td, c.tab_d, 2 * c.tl.n_dbl, lane, wave, MH_WAVES);
     dma_words(ti, c.tab_i, c.tl.n_int, lane, wave, MH_WAVES);
+    // per-likelihood terms of the current point, for the history (rejected walkers keep theirs)
+    double ct[MAXLIKE];
+    if (ACCEPT && hist_terms && wave == 0 && act) {
+#pragma unroll
+        for (int l = 0; l < MAXLIKE; l++)
+            if (l < c.n_like) ct[l] = c.cur_terms[(size_t)l * W + w];
+    }
     STAMP(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -438,6 +445,12 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
             mult = 1.0;
             for (int i = 0; i < c.np; i++) k.P[i] = k.trial[i];
             cur = like;
+#pragma unroll
+            for (int l = 0; l < MAXLIKE; l++)
+                if (l < c.n_like) {
+                    ct[l] = lk[(size_t)l * NB + lane];
+                    c.cur_terms[(size_t)l * W + w] = ct[l];
+                }
         } else {
             mult += 1.0;
         }
@@ -445,6 +458,11 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
         if (hist_row) {
             for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = k.P[t.params_used[i]];
             hist_row[(size_t)c.n_used * c.W + w] = cur;
+        }
+        if (hist_terms) {
+#pragma unroll
+            for (int l = 0; l < MAXLIKE; l++)
+                if (l < c.n_like) hist_terms[(size_t)l * c.W + w] = ct[l];
         }
     }
     STAMP(3);
@@ -495,7 +513,8 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
 // dst: 0 idle, 1 dragging, 2 aborted, 3 skipped (CurLike == logZero),
 //      4 accepted (the walker's theory must become the end theory)
 struct DragCfg {
-    double *dd;      // [3 np + 4 + max_blk][ld]: CE, CS, T2, (cel, csl, ss, se), vec scratch
+    double *dd;      // [3 np + 4 + max_blk + n_like][ld]: CE, CS, T2, (cel, csl, ss, se), vec scratch,
+                     //   per-likelihood terms at CE
     int *di;         // [1 + all_n][ld]: dst, RandIndices scratch
     int interp, istep;
     const double *like_terms2;            // [n_like][ld] at T2
@@ -503,7 +522,7 @@ struct DragCfg {
 };
 
 template <int STAGE>
-__global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *hist_row)
+__global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *hist_row, double *hist_terms)
 {
     const int w = blockIdx.x * 64 + threadIdx.x;
     if (w >= c.W) return;
@@ -540,6 +559,10 @@ __global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *h
     int &dst = g.di[w];
     const Col<double> lk1{const_cast<double *>(c.like_terms) + w, (int)ld};
     const Col<double> lk2{const_cast<double *>(g.like_terms2) + w, (int)ld};
+    const Col<double> ET = drow(g.dd, 3 * np + 4 + c.max_blk);   // terms at CE
+    auto keep_end_terms = [&]() {
+        for (int l = 0; l < c.n_like; l++) ET[l] = lk1[l];
+    };
 
     auto scatter = [&]() {            // DataParams of both trial points
         for (int l = 0; l < c.n_like; l++)
@@ -589,6 +612,7 @@ __global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *h
                 mult += 1.0;
             } else {
                 for (int i = 0; i < np; i++) CE[i] = T[i];
+                keep_end_terms();
                 ss = csl;
                 se = cel;
                 next_delta();
@@ -617,6 +641,7 @@ __global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *h
                 }
                 cel = el;
                 csl = sl;
+                keep_end_terms();
             }
             ss = ss + csl;
             se = se + cel;
@@ -629,6 +654,7 @@ __global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *h
                     mult = 1.0;
                     for (int i = 0; i < np; i++) k.P[i] = CE[i];
                     cur = cel;
+                    for (int l = 0; l < c.n_like; l++) c.cur_terms[(size_t)l * ld + w] = ET[l];
                     dst = 4;
                 } else {
                     mult += 1.0;
@@ -645,6 +671,8 @@ __global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *h
                 for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = k.P[t.params_used[i]];
                 hist_row[(size_t)c.n_used * c.W + w] = cur;
             }
+            if (hist_terms)
+                for (int l = 0; l < c.n_like; l++) hist_terms[(size_t)l * c.W + w] = c.cur_terms[(size_t)l * ld + w];
         }
     }
     c.sd[(size_t)R.C * ld + w] = k.r.c;
@@ -676,6 +704,7 @@ __global__ void start_kernel(DevCfg c)
     Col<double> q{c.sd + (size_t)c.rows.T * W + w, c.ld};
     Col<const double> lk{c.like_terms + w, c.ld};
     c.sd[(size_t)c.rows.L * W + w] = target_like(c, t, q, lk);
+    for (int l = 0; l < c.n_like; l++) c.cur_terms[(size_t)l * W + w] = lk[l];
     for (int i = 0; i < c.np; i++) c.sd[(size_t)(c.rows.P + i) * W + w] = q[i];
     c.sd[(size_t)c.rows.M * W + w] = 0.0;
     c.si[(size_t)c.rows.NACC * W + w] = 0;
@@ -1037,6 +1066,18 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, int nuis_index0, const double
     std::swap(nt.bytes, s->like_terms.bytes);
     s->dc.n_like = (int)s->likes.size();
     s->dc.like_terms = s->like_terms.as<double>();
+    {   // current-point terms: one more row, the existing ones kept
+        DevBuf ct((size_t)s->likes.size() * s->dc.ld * 8);
+        HIP_CHECK(hipMemset(ct.p, 0, ct.bytes));
+        if (li > 0) HIP_CHECK(hipMemcpy(ct.p, s->cur_terms.p, (size_t)li * s->dc.ld * 8, hipMemcpyDeviceToDevice));
+        std::swap(ct.p, s->cur_terms.p);
+        std::swap(ct.bytes, s->cur_terms.bytes);
+        s->dc.cur_terms = s->cur_terms.as<double>();
+    }
+    if (s->hist_cap > 0) {   // the terms ring follows the number of likelihoods
+        s->hist_terms.alloc((size_t)s->hist_cap * s->likes.size() * s->W * 8);
+        HIP_CHECK(hipMemset(s->hist_terms.p, 0, s->hist_terms.bytes));
+    }
     s->nuis_bufs[li].alloc((size_t)std::max(nn, 1) * s->W * 8);
     s->dc.like_nuis[li] = s->nuis_bufs[li].as<double>();
     s->dc.like_nuis0[li] = nuis_index0 - 1;
@@ -1089,18 +1130,34 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
         }
 }
 
-static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, double *row, hipStream_t stream, int g0,
-                      int g1) {
+// the history ring slots of the next recorded step (none when history is off)
+struct HistRow {
+    double *p = nullptr;   // [n_used + 1][W]: used parameters, CurLike
+    double *t = nullptr;   // [n_like][W]: per-likelihood terms
+};
+
+static HistRow next_hist(cmbs *s) {
+    HistRow r;
+    if (s->hist_cap == 0) return r;
+    const size_t slot = (size_t)(s->hist_count % s->hist_cap);
+    r.p = s->hist.as<double>() + slot * (s->n_used + 1) * s->W;
+    if (!s->likes.empty() && s->hist_terms.p) r.t = s->hist_terms.as<double>() + slot * s->likes.size() * s->W;
+    s->hist_count++;
+    return r;
+}
+
+static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const HistRow &row, hipStream_t stream,
+                      int g0, int g1) {
     const dim3 g((g1 - g0 + NB - 1) / NB), b(NB * MH_WAVES);
     const int blk0 = g0 / NB;
     const size_t lds = s->mh_lds;
     timed_launch("mh_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
         if (accept && propose)
-            hipExtLaunchKernelGGL(mh_kernel<true, true>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row, blk0);
+            hipExtLaunchKernelGGL(mh_kernel<true, true>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row.p, row.t, blk0);
         else if (accept)
-            hipExtLaunchKernelGGL(mh_kernel<true, false>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row, blk0);
+            hipExtLaunchKernelGGL(mh_kernel<true, false>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row.p, row.t, blk0);
         else
-            hipExtLaunchKernelGGL(mh_kernel<false, true>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row, blk0);
+            hipExtLaunchKernelGGL(mh_kernel<false, true>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row.p, row.t, blk0);
     });
     HIP_CHECK(hipGetLastError());
 }
@@ -1125,22 +1182,16 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (!fast_only && s->slow_n > 0 && !s->likes.empty())
         fail(CMBL_ERR_ARG, "slow proposals need the theory at the trial point: use cmbs_step_theory");
     if (n_steps <= 0) return;
-    auto next_row = [&]() -> double * {
-        if (s->hist_cap == 0) return nullptr;
-        double *row = s->hist.as<double>() + (size_t)(s->hist_count % s->hist_cap) * (s->n_used + 1) * s->W;
-        s->hist_count++;
-        return row;
-    };
     // propose(1) | likes | accept(1)+propose(2) | likes | ... | likes | accept(n)
     const int G = s->n_groups;
     if (G == 1) {
-        launch_mh(s, false, true, fast_only, nullptr, stream, 0, s->W);
+        launch_mh(s, false, true, fast_only, HistRow{}, stream, 0, s->W);
         eval_likes(s, stream, false, 0, s->W, s->ws.p);
         for (int k = 1; k < n_steps; k++) {
-            launch_mh(s, true, true, fast_only, next_row(), stream, 0, s->W);
+            launch_mh(s, true, true, fast_only, next_hist(s), stream, 0, s->W);
             eval_likes(s, stream, false, 0, s->W, s->ws.p);
         }
-        launch_mh(s, true, false, fast_only, next_row(), stream, 0, s->W);
+        launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W);
         return;
     }
     // groups are independent chains: fork from the caller's stream, issue the
@@ -1148,7 +1199,7 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     HIP_CHECK(hipEventRecord(s->events[MAXGROUPS], stream));
     for (int g = 0; g < G; g++) HIP_CHECK(hipStreamWaitEvent(s->streams[g], s->events[MAXGROUPS], 0));
     for (int k = 0; k <= n_steps; k++) {
-        double *row = k > 0 ? next_row() : nullptr;
+        const HistRow row = k > 0 ? next_hist(s) : HistRow{};
         for (int g = 0; g < G; g++) {
             const int g0 = s->grp0[g], g1 = s->grp0[g + 1];
             launch_mh(s, k > 0, k < n_steps, fast_only, row, s->streams[g], g0, g1);
@@ -1205,7 +1256,7 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
     const size_t ld = s->dc.ld;
     const int np = s->np;
     if (!s->drag_dd.p) {
-        s->drag_dd.alloc((size_t)(3 * np + 4 + s->dc.max_blk) * ld * 8);
+        s->drag_dd.alloc((size_t)(3 * np + 4 + s->dc.max_blk + std::max<size_t>(1, s->likes.size())) * ld * 8);
         s->drag_di.alloc((size_t)(1 + s->all_n) * ld * 4);
         HIP_CHECK(hipMemset(s->drag_dd.p, 0, s->drag_dd.bytes));
         HIP_CHECK(hipMemset(s->drag_di.p, 0, s->drag_di.bytes));
@@ -1222,24 +1273,18 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
     int interp = (int)std::lround(dragging_steps * s->fast_n) + 1;   // MCMC.f90:386
     if (interp < 2) interp = 2;
     g.interp = interp;
-    auto next_row = [&]() -> double * {
-        if (s->hist_cap == 0) return nullptr;
-        double *row = s->hist.as<double>() + (size_t)(s->hist_count % s->hist_cap) * (s->n_used + 1) * s->W;
-        s->hist_count++;
-        return row;
-    };
     const dim3 grid((s->W + 63) / 64), blk(64);
     for (int step = 0; step < n_steps; step++) {
         s->num_drag++;
         if (s->num_drag % s->dc.oversample_fast != 0) {   // FastParameterSample (:357-361)
-            launch_mh(s, false, true, 1, nullptr, stream, 0, s->W);
+            launch_mh(s, false, true, 1, HistRow{}, stream, 0, s->W);
             eval_likes(s, stream, false, 0, s->W, s->ws.p);
-            launch_mh(s, true, false, 1, next_row(), stream, 0, s->W);
+            launch_mh(s, true, false, 1, next_hist(s), stream, 0, s->W);
             continue;
         }
         g.istep = 0;
         timed_launch("drag_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(drag_kernel<0>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, (double *)nullptr);
+            hipExtLaunchKernelGGL(drag_kernel<0>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, (double *)nullptr, (double *)nullptr);
         });
         HIP_CHECK(hipGetLastError());
         if (nl > 0) {
@@ -1248,7 +1293,7 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
             eval_likes_drag(s, 1, stream);
         }
         timed_launch("drag_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(drag_kernel<1>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, (double *)nullptr);
+            hipExtLaunchKernelGGL(drag_kernel<1>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, (double *)nullptr, (double *)nullptr);
         });
         HIP_CHECK(hipGetLastError());
         for (int is = 1; is <= interp - 1; is++) {
@@ -1257,9 +1302,9 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
                 eval_likes_drag(s, 2, stream);
             }
             g.istep = is;
-            double *row = is == interp - 1 ? next_row() : nullptr;
+            const HistRow row = is == interp - 1 ? next_hist(s) : HistRow{};
             timed_launch("drag_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                hipExtLaunchKernelGGL(drag_kernel<2>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, row);
+                hipExtLaunchKernelGGL(drag_kernel<2>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, row.p, row.t);
             });
             HIP_CHECK(hipGetLastError());
         }
@@ -1305,25 +1350,19 @@ void sampler_step_theory(cmbs *s, int n_steps, cmbs_theory_fn fn, void *user, hi
         if (!s->end_theory[i].dl) fail(CMBL_ERR_ARG, "likelihood %zu has no trial-theory buffer", i);
         if (s->likes[i].ld_walker == 0) fail(CMBL_ERR_ARG, "slow steps need per-walker theory rows");
     }
-    auto next_row = [&]() -> double * {
-        if (s->hist_cap == 0) return nullptr;
-        double *row = s->hist.as<double>() + (size_t)(s->hist_count % s->hist_cap) * (s->n_used + 1) * s->W;
-        s->hist_count++;
-        return row;
-    };
     const double *Ptrial = s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld;
     auto trial_likes = [&]() {
         if (fn(user, s->W, Ptrial, (long long)s->dc.ld, stream) != 0) fail(CMBL_ERR_ARG, "theory function failed");
         eval_likes_drag(s, 1, stream);
     };
-    launch_mh(s, false, true, 0, nullptr, stream, 0, s->W);
+    launch_mh(s, false, true, 0, HistRow{}, stream, 0, s->W);
     trial_likes();
     for (int k = 1; k < n_steps; k++) {
-        launch_mh(s, true, true, 0, next_row(), stream, 0, s->W);
+        launch_mh(s, true, true, 0, next_hist(s), stream, 0, s->W);
         swap_accepted_theory(s, stream);
         trial_likes();
     }
-    launch_mh(s, true, false, 0, next_row(), stream, 0, s->W);
+    launch_mh(s, true, false, 0, next_hist(s), stream, 0, s->W);
     swap_accepted_theory(s, stream);
 }
 
@@ -1348,6 +1387,10 @@ void sampler_enable_history(cmbs *s, int capacity) {
     s->hist.alloc((size_t)capacity * (s->n_used + 1) * s->W * 8);   // per step: P(params_used) rows, CurLike row
     s->hist_cap = capacity;
     s->hist_count = 0;
+    if (!s->likes.empty()) {   // per step: each likelihood's -lnL at the current point
+        s->hist_terms.alloc((size_t)capacity * s->likes.size() * s->W * 8);
+        HIP_CHECK(hipMemset(s->hist_terms.p, 0, s->hist_terms.bytes));
+    }
 }
 
 void sampler_history_stats(cmbs *s, int first, int last, double *means, double *covs, hipStream_t stream) {
@@ -1388,7 +1431,22 @@ void sampler_history_host(cmbs *s, int first, int count, double *out) {
 // written by sampler_history_host go back to their ring slots, and the ring
 // continues at first + count (the samples the convergence test windows over,
 // TMpiChainCollector_ReadState's Samples%LoadState, SampleCollector.f90:167)
-void sampler_history_restore(cmbs *s, int first, int count, const double *in) {
+void sampler_history_terms_host(cmbs *s, int first, int count, double *out) {
+    if (s->hist_cap == 0) fail(CMBL_ERR_ARG, "history not enabled");
+    const int oldest = std::max(0, s->hist_count - s->hist_cap);
+    if (first < oldest || first + count > s->hist_count)
+        fail(CMBL_ERR_ARG, "history rows [%d, %d) not kept (rows %d..%d)", first, first + count, oldest, s->hist_count - 1);
+    const size_t blk = s->likes.size() * (size_t)s->W;
+    if (blk == 0) return;
+    HIP_CHECK(hipDeviceSynchronize());
+    for (int k = 0; k < count; k++) {
+        const int slot = (first + k) % s->hist_cap;
+        HIP_CHECK(hipMemcpy(out + (size_t)k * blk, s->hist_terms.as<double>() + (size_t)slot * blk, blk * 8,
+                            hipMemcpyDeviceToHost));
+    }
+}
+
+void sampler_history_restore(cmbs *s, int first, int count, const double *in, const double *terms) {
     if (s->hist_cap == 0) fail(CMBL_ERR_ARG, "history not enabled");
     if (first < 0 || count < 0 || count > s->hist_cap)
         fail(CMBL_ERR_ARG, "history rows [%d, %d) do not fit the ring (capacity %d)", first, first + count,
@@ -1400,6 +1458,13 @@ void sampler_history_restore(cmbs *s, int first, int count, const double *in) {
         HIP_CHECK(hipMemcpy(s->hist.as<double>() + (size_t)slot * blk, in + (size_t)k * blk, blk * 8,
                             hipMemcpyHostToDevice));
     }
+    const size_t tblk = s->likes.size() * (size_t)s->W;
+    if (terms && tblk)
+        for (int k = 0; k < count; k++) {
+            const int slot = (first + k) % s->hist_cap;
+            HIP_CHECK(hipMemcpy(s->hist_terms.as<double>() + (size_t)slot * tblk, terms + (size_t)k * tblk,
+                                tblk * 8, hipMemcpyHostToDevice));
+        }
     s->hist_count = first + count;
 }
 
@@ -1425,26 +1490,27 @@ void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, 
 // proposal matrix (propose.f90:308-325) and restarts from the last chain row
 // with a fresh RNG (GeneralSetup.f90:123-131); this image holds the complete
 // device state instead -- point, CurLike, multiplicity, accept count, RANMAR
-// table and Gaussian1 cache, cyclic-index and rotation state -- so a resumed
-// run continues each chain exactly.  Layout: StateHeader, double rows
-// [ND][W], int rows [NI][W].  The proposal covariance is the caller's part
+// table and Gaussian1 cache, cyclic-index and rotation state, each
+// likelihood's term at the point -- so a resumed run continues each chain
+// exactly.  Layout: StateHeader, double rows [ND][W], int rows [NI][W],
+// current terms [n_like][W].  The proposal covariance is the caller's part
 // (cmbs_set_covariance before cmbs_load_state).
 struct StateHeader {
     unsigned magic, version;
-    int W, np, n_used, nblocks, all_n, slow_n, fast_n, R_total, ND, NI;
+    int W, np, n_used, nblocks, all_n, slow_n, fast_n, R_total, ND, NI, n_like, pad;
     long long num_drag;
 };
 static constexpr unsigned STATE_MAGIC = 0x53424d43u;   // "CMBS"
 
 size_t sampler_state_bytes(const cmbs *s) {
     const Rows &R = s->dc.rows;
-    return sizeof(StateHeader) + (size_t)R.ND * s->W * 8 + (size_t)R.NI * s->W * 4;
+    return sizeof(StateHeader) + (size_t)(R.ND + s->likes.size()) * s->W * 8 + (size_t)R.NI * s->W * 4;
 }
 
 static StateHeader state_header(const cmbs *s) {
     const Rows &R = s->dc.rows;
     return StateHeader{STATE_MAGIC, 1u, s->W, s->np, s->n_used, s->nblocks, s->all_n, s->slow_n, s->fast_n,
-                       s->R_total, R.ND, R.NI, s->num_drag};
+                       s->R_total, R.ND, R.NI, (int)s->likes.size(), 0, s->num_drag};
 }
 
 void sampler_save_state(cmbs *s, void *buf, size_t bytes) {
@@ -1461,6 +1527,9 @@ void sampler_save_state(cmbs *s, void *buf, size_t bytes) {
     HIP_CHECK(hipMemcpy2D(p, W * 8, s->dc.sd, ld * 8, W * 8, R.ND, hipMemcpyDeviceToHost));
     p += (size_t)R.ND * W * 8;
     HIP_CHECK(hipMemcpy2D(p, W * 4, s->dc.si, ld * 4, W * 4, R.NI, hipMemcpyDeviceToHost));
+    p += (size_t)R.NI * W * 4;
+    if (!s->likes.empty())
+        HIP_CHECK(hipMemcpy2D(p, W * 8, s->dc.cur_terms, ld * 8, W * 8, s->likes.size(), hipMemcpyDeviceToHost));
 }
 
 void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
@@ -1470,9 +1539,11 @@ void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
     if (h.magic != STATE_MAGIC || h.version != 1u) fail(CMBL_ERR_FORMAT, "not a cmbs state image");
     const StateHeader m = state_header(s);
     if (h.W != m.W || h.np != m.np || h.n_used != m.n_used || h.nblocks != m.nblocks || h.all_n != m.all_n ||
-        h.slow_n != m.slow_n || h.fast_n != m.fast_n || h.R_total != m.R_total || h.ND != m.ND || h.NI != m.NI)
-        fail(CMBL_ERR_ARG, "state image is for a different sampler (W %d np %d blocks %d; this one W %d np %d blocks %d)",
-             h.W, h.np, h.nblocks, m.W, m.np, m.nblocks);
+        h.slow_n != m.slow_n || h.fast_n != m.fast_n || h.R_total != m.R_total || h.ND != m.ND || h.NI != m.NI ||
+        h.n_like != m.n_like)
+        fail(CMBL_ERR_ARG,
+             "state image is for a different sampler (W %d np %d blocks %d likelihoods %d; this one W %d np %d "
+             "blocks %d likelihoods %d)", h.W, h.np, h.nblocks, h.n_like, m.W, m.np, m.nblocks, m.n_like);
     if (bytes < sampler_state_bytes(s)) fail(CMBL_ERR_FORMAT, "state image truncated");
     const Rows &R = s->dc.rows;
     const size_t ld = s->dc.ld, W = s->W;
@@ -1481,6 +1552,9 @@ void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
     HIP_CHECK(hipMemcpy2D(s->dc.sd, ld * 8, p, W * 8, W * 8, R.ND, hipMemcpyHostToDevice));
     p += (size_t)R.ND * W * 8;
     HIP_CHECK(hipMemcpy2D(s->dc.si, ld * 4, p, W * 4, W * 4, R.NI, hipMemcpyHostToDevice));
+    p += (size_t)R.NI * W * 4;
+    if (!s->likes.empty())
+        HIP_CHECK(hipMemcpy2D(s->dc.cur_terms, ld * 8, p, W * 8, W * 8, s->likes.size(), hipMemcpyHostToDevice));
     s->num_drag = h.num_drag;
     s->started = true;
 }

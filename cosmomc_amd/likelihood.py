@@ -41,6 +41,15 @@ class DataLikelihood:
         self.nuisance_indices: list[int] = []   # 1-based into P, filled by LikelihoodList
         self.dependent_params: set[int] = set()
         self.cl_lmax = [[0] * 4 for _ in range(4)]
+        self.version = ""
+
+    def get_tag(self) -> str:
+        """TDataLikelihood_GetTag (GeneralTypes.f90:533-543): the tag, else the name."""
+        return self.tag or self.name.strip()
+
+    def description(self) -> tuple:
+        """(tag, type, name, version): a root.likelihoods line / ChainWriter likelihoods entry."""
+        return (self.get_tag(), self.LikelihoodType, self.name, self.version)
 
     @property
     def n_nuis(self) -> int:

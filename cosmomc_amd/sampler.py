@@ -155,6 +155,14 @@ class BatchedMCMC:
         self._check(N.lib().cmbs_history_host(self._h, first, count, out.ctypes.data))
         return out
 
+    def history_terms(self, first: int, count: int):
+        """Each likelihood's -lnL at history rows [first, first+count) on the
+        host: [count, n_likelihoods, W] (add_likelihood order)."""
+        out = np.empty((count, len(self._likes), self.W))
+        if self._likes:
+            self._check(N.lib().cmbs_history_terms_host(self._h, first, count, out.ctypes.data))
+        return out
+
     def history_stats(self, first: int, last: int):
         """Per-walker means [W, n_used] and covariances [W, n_used, n_used] (cuda tensors)."""
         import torch
@@ -201,10 +209,13 @@ class BatchedMCMC:
         buf = C.create_string_buffer(bytes(image), len(image))
         self._check(N.lib().cmbs_load_state(self._h, buf, len(image)))
 
-    def history_restore(self, first: int, rows):
-        """Put history rows [first, first + len(rows)) back (layout of history_host)."""
+    def history_restore(self, first: int, rows, terms=None):
+        """Put history rows [first, first + len(rows)) back (layouts of
+        history_host / history_terms)."""
         r = np.ascontiguousarray(rows, dtype=np.float64)
-        self._check(N.lib().cmbs_history_restore(self._h, first, r.shape[0], r.ctypes.data))
+        t = None if terms is None else np.ascontiguousarray(terms, dtype=np.float64)
+        self._check(N.lib().cmbs_history_restore(self._h, first, r.shape[0], r.ctypes.data,
+                                                 None if t is None else t.ctypes.data))
 
     def close(self):
         if getattr(self, "_h", None):

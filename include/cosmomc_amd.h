@@ -245,11 +245,18 @@ size_t cmbs_state_bytes(const cmbs_t *s);
 int  cmbs_save_state(cmbs_t *s, void *host_buf, size_t bytes);
 int  cmbs_load_state(cmbs_t *s, const void *host_buf, size_t bytes);
 
-/* Put history rows [first, first + count) back (HOST array laid out as
- * cmbs_history_host writes it; count <= capacity) and continue the ring at
- * first + count: the samples the convergence exchange windows over survive a
- * resume (Samples%LoadState, SampleCollector.f90:167). */
-int  cmbs_history_restore(cmbs_t *s, int first, int count, const double *rows);
+/* Each likelihood's -lnL at the recorded points, history rows [first,
+ * first + count), to HOST memory: out[count][n_likelihoods][W] in
+ * cmbs_add_likelihood order (TCalculationAtParamPoint%Likelihoods: the
+ * chi2_<tag> = 2 x term derived columns of a chain row, GeneralTypes.f90:767-776). */
+int  cmbs_history_terms_host(cmbs_t *s, int first, int count, double *out);
+
+/* Put history rows [first, first + count) back (HOST arrays laid out as
+ * cmbs_history_host / cmbs_history_terms_host write them, terms may be NULL;
+ * count <= capacity) and continue the ring at first + count: the samples the
+ * convergence exchange windows over survive a resume (Samples%LoadState,
+ * SampleCollector.f90:167). */
+int  cmbs_history_restore(cmbs_t *s, int first, int count, const double *rows, const double *terms);
 
 #ifdef __cplusplus
 }

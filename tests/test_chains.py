@@ -1,5 +1,6 @@
 """Chain-file writer (IO_OutputChainRow IO.f90:85-93, '(*(E17.7))' FileUtils.f90:75)."""
 import numpy as np
+import pytest
 
 from cosmomc_amd.chains import ChainWriter, fortran_e
 
@@ -34,3 +35,32 @@ def test_run_length_rows(tmp_path):
     assert c1.shape == (6, 4) and np.all(c1[:, 0] == 1)
     assert (tmp_path / "ch.paramnames").read_text().split("\n")[0] == "a\ta"
     assert (tmp_path / "ch.ranges").exists()
+
+
+def test_chi2_columns_and_likelihoods_file(tmp_path):
+    """chi2_<tag> = 2 x term, chi2_prior = 2 x (like - sum terms), chi2_CMB for
+    two CMB likelihoods (GeneralTypes.f90:671-776), derived names starred in
+    .paramnames, 0..N ranges (ObjectParamNames.f90:480-508), .likelihoods lines
+    (GeneralTypes.f90:792-812)."""
+    root = str(tmp_path / "c")
+    cw = ChainWriter(root, ["a"], ranges=[(0, 1)],
+                     likelihoods=[("plik", "CMB", "plik_lite", "2018"), ("lens_x", "CMB", "lensing", "")])
+    rows = np.zeros((3, 2, 1))
+    rows[:, 0, 0] = [1.0, 1.0, 2.0]
+    rows[:, 1, 0] = [10.0, 10.0, 11.0]
+    terms = np.zeros((3, 2, 1))
+    terms[:, 0, 0] = [4.0, 4.0, 5.0]
+    terms[:, 1, 0] = [3.0, 3.0, 3.0]
+    with pytest.raises(ValueError):
+        cw.add_rows(rows)
+    cw.add_rows(rows, terms)
+    cw.close()
+    c = np.loadtxt(root + "_1.txt", ndmin=2)
+    np.testing.assert_allclose(c, [[2, 10, 1, 8, 6, 6, 14], [1, 11, 2, 10, 6, 6, 16]])
+    pn = open(root + ".paramnames").read().splitlines()
+    assert pn[1:] == ["chi2_plik*\t\\chi^2_{\\rm plik}", "chi2_lens_x*\t\\chi^2_{\\rm lens\\_x}",
+                      "chi2_prior*\t\\chi^2_{\\rm prior}", "chi2_CMB*\t\\chi^2_{\\rm CMB}"]
+    rg = open(root + ".ranges").read().splitlines()
+    assert rg[1] == "chi2_plik".ljust(22) + "    0.0000000E+00" + "    N".ljust(17)
+    assert open(root + ".likelihoods").read().splitlines() == ["1\tCMB\tplik\tplik_lite\t2018",
+                                                              "1\tCMB\tlens_x\tlensing\t"]

@@ -38,7 +38,7 @@ class FakeSampler:
     def history_host(self, first, count):
         return self.hist[first:first + count]
 
-    def history_restore(self, first, rows):
+    def history_restore(self, first, rows, terms=None):
         self.restored = (first, np.array(rows))
 
 

@@ -94,7 +94,7 @@ def test_resume_plik_chain_files_and_history(tmp_path):
     ref = sampler()
     ref.set_covariance(cov)
     ref.set_start(np.tile(P0, (W, 1)))
-    cw = ChainWriter(str(tmp_path / "ref"), ["calPlanck"])
+    cw = ChainWriter(str(tmp_path / "ref"), ["calPlanck"], likelihoods=[like.description()])
     for _ in range(3):
         ref.step(30, fast_only=True)
         cw.append(ref)
@@ -105,7 +105,7 @@ def test_resume_plik_chain_files_and_history(tmp_path):
     a.set_start(np.tile(P0, (W, 1)))
     ex = ConvergenceExchange(1)
     ex.flukecheck = True
-    cwa = ChainWriter(str(tmp_path / "run"), ["calPlanck"])
+    cwa = ChainWriter(str(tmp_path / "run"), ["calPlanck"], likelihoods=[like.description()])
     for _ in range(2):
         a.step(30, fast_only=True)
         cwa.append(a)
@@ -116,7 +116,7 @@ def test_resume_plik_chain_files_and_history(tmp_path):
 
     b = sampler()
     ex2 = ConvergenceExchange(1)
-    cwb = ChainWriter(str(tmp_path / "run"), ["calPlanck"])
+    cwb = ChainWriter(str(tmp_path / "run"), ["calPlanck"], likelihoods=[like.description()])
     read_checkpoint(str(tmp_path / "run"), b, chains=cwb, exchange=ex2)
     assert ex2.flukecheck
     assert b.history_count() == 60

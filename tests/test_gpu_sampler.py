@@ -271,11 +271,13 @@ def test_dragging_with_plik_theory_callback(tmp_path):
     s.add_likelihood(like, theory)
     s.set_drag_theory(0, end)
     s.set_start(np.tile([1.0, 1.0], (W, 1)))
+    s.enable_history(64)
 
     def theory_fn(P_end):
         end.copy_(base.unsqueeze(0) * P_end[0].reshape(-1, 1, 1))
     s.step_drag(40, theory_fn=theory_fn)
     P, lk, mult, nacc = s.state()
+    terms = s.history_terms(s.history_count() - 1, 1)[0, 0]     # plik -lnL at the current points
     assert np.any(np.abs(P[:, 0] - 1.0) > 1e-6), "no drag was accepted"
     th = theory.cpu().numpy()
     b = base.cpu().numpy()
@@ -284,6 +286,46 @@ def test_dragging_with_plik_theory_callback(tmp_path):
         np.testing.assert_allclose(th[w], P[w, 0] * b, rtol=1e-15, atol=0)
         ref = orc.loglike(th[w], P[w, 1]) + 0.5 * ((P[w, 1] - 1.0) / 0.0025) ** 2
         assert lk[w] == pytest.approx(ref, rel=1e-9)
+        assert terms[w] == pytest.approx(orc.loglike(th[w], P[w, 1]), rel=1e-9)
+
+
+def test_history_terms_and_chi2_chain_files(tmp_path):
+    """Per-likelihood terms of the recorded points (cmbs_history_terms_host)
+    equal the oracle's plik_lite -lnL at every recorded point, and the chain
+    files' chi2_plik / chi2_prior columns follow from them."""
+    from cosmomc_amd.chains import ChainWriter
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    data = syn.make_plik_lite(12345)
+    like = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    like.nuisance_indices = [2]
+    W, steps = 64, 40
+    th = syn.walker_theory(W, seed=3, n_fields=3)
+    dl = torch.tensor(th, device="cuda")
+    s = BatchedMCMC(W, 3, [2], [[1]], 0, [0.0222, 0.9, 3.05], [0.0222, 1.1, 3.05], [0.0, 1.0, 0.0],
+                    [0.0, 0.0025, 0.0], seed_ij=55, seed_kl=66)
+    s.set_covariance(np.array([[0.002 ** 2]]))
+    s.add_likelihood(like, dl)
+    s.enable_history(steps)
+    s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
+    cw = ChainWriter(str(tmp_path / "run"), ["calPlanck"], likelihoods=[like.description()])
+    s.step(steps, fast_only=True)
+    cw.append(s)
+    cw.close()
+    hist = s.history_host(0, steps)
+    terms = s.history_terms(0, steps)
+    orc = po.PlikLite(data)
+    for w in (0, 17, 63):
+        for k in (0, 11, steps - 1):
+            cal = hist[k, 0, w]
+            assert terms[k, 0, w] == pytest.approx(orc.loglike(th[w], cal), rel=1e-9)
+            assert hist[k, 1, w] == pytest.approx(terms[k, 0, w] + 0.5 * ((cal - 1.0) / 0.0025) ** 2, rel=1e-12)
+        c = np.loadtxt(tmp_path / f"run_{w + 1}.txt", ndmin=2)
+        assert c[:, 0].sum() == steps, (w, c[:, :3], hist[:, 0, w])
+        # chi2_prior; the file holds calPlanck to 7 digits (1e-6), so compare to 1e-3
+        np.testing.assert_allclose(c[:, 4], ((c[:, 2] - 1.0) / 0.0025) ** 2, rtol=0, atol=1e-3)
+        np.testing.assert_allclose(c[:, 3] / 2 + c[:, 4] / 2, c[:, 1], rtol=1e-6)                 # chi2s add up
+    assert open(tmp_path / "run.likelihoods").read().split("\t")[:3] == ["1", "CMB", "PLIK_LITE"]
 
 
 @pytest.mark.parametrize("oversample", [1, 3])
