@@ -19,7 +19,9 @@ per-step collective ("weak" scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 1024] [--no-lensing]
 
 The JSON line also carries, outside the headline value: "convergence" (R-1 vs
-wall-clock for the headline workload) and "config5_bk15_plik" (BASELINE
+wall-clock for the headline workload), "config4_fast21" (BASELINE configs[3]
+as a sampler-throughput workload: 21 fast parameters, 512 walkers per GPU;
+full plik needs the absent clik) and "config5_bk15_plik" (BASELINE
 configs[4]: BK15 + plik_lite jointly, fast-step throughput and R-1 vs
 wall-clock with the cross-GPU exchange).
 """
@@ -62,6 +64,8 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse ranks")
     p.add_argument("--converge-seconds", type=float, default=20.0,
                    help="R-1 vs wall-clock run after the throughput timing (0 = skip)")
+    p.add_argument("--config4-seconds", type=float, default=30.0,
+                   help="21-fast-parameter sampler workload (BASELINE configs[3]) throughput and R-1 run (< 0 = skip)")
     p.add_argument("--config5-seconds", type=float, default=60.0,
                    help="BK15 + plik_lite (BASELINE configs[4]) throughput and R-1 run (< 0 = skip)")
     return p.parse_args()
@@ -183,6 +187,112 @@ def convergence_run(W, rank, world, tmpdir, seconds, lensing=True):
             "converged_wall_s": done_at, "trace_wall_s_steps_R": trace}
 
 
+def kernel_profile(smp, steps):
+    """Average device time (us) per launch of every library kernel over `steps`
+    more fast steps (HIP events on the launch stream)."""
+    import torch
+    from cosmomc_amd import _native as N
+    names = ("plik_bin_delta", "plik_quadform_ksplit", "mh_kernel", "cmbl_bk_prologue", "cmbl_window_kernel",
+             "cmbl_reduce_kernel", "cmbl_hl_kernel", "cmbl_quadform", "cmbl_gauss_small_kernel")
+    N.profile_reset()
+    N.profile_enable(True)
+    smp.step(steps, fast_only=True)
+    torch.cuda.synchronize()
+    N.profile_enable(False)
+    out = {}
+    for k in names:
+        ms, cnt = N.profile_read(k)
+        if cnt:
+            out[k] = round(ms / cnt * 1e3, 2)
+    return out
+
+
+def config4_run(W, rank, world, tmpdir, seconds, steps=200):
+    """BASELINE configs[3] as a sampler-throughput workload:
+    full plik's 21 fast foreground/calibration nuisances need clik, which is
+    absent, so the likelihood is plik_lite TTTEEE (calPlanck) plus a correlated
+    20-dimensional Gaussian over the other fast parameters (test_likelihood
+    semantics, calclike.f90:180-199); one fast block of 21 parameters (random
+    21-d rotations every 21 steps per walker), 512 walkers per GPU (4096 over 8),
+    one shared cached slow point.  Reports fast-step throughput and, when
+    seconds > 0, R-1 vs wall-clock with the exchange every 40 x 21 samples."""
+    import torch
+    from cosmomc_amd import synthetic as syn
+    from cosmomc_amd.converge import CollectorSettings, ConvergenceExchange, reference_window
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    n = 21
+    plik = NativeCMBLikelihood("PLIK_LITE", syn.make_plik_lite(12345).write(os.path.join(tmpdir, "c4p")))
+    plik.nuisance_indices = [1]
+    rng = np.random.default_rng(2121)                 # synthetic nuisance posterior (same on every rank)
+    width = np.concatenate([[0.0025], rng.uniform(0.05, 2.0, n - 1)])
+    A = rng.standard_normal((n - 1, n - 1))
+    corr = A @ A.T / (n - 1) + np.eye(n - 1)
+    d = np.sqrt(np.diag(corr))
+    corr = corr / d[:, None] / d[None, :]
+    cov = np.zeros((n, n))
+    cov[0, 0] = 1.0                                   # calPlanck: left to plik_lite and its prior
+    cov[1:, 1:] = corr * np.outer(width[1:], width[1:])
+    P0 = np.concatenate([[1.0], rng.uniform(-1.0, 1.0, n - 1)])
+    pmin, pmax = P0 - 20 * width, P0 + 20 * width
+    pmin[0], pmax[0] = 0.9, 1.1
+    pm, ps = np.zeros(n), np.zeros(n)
+    pm[0], ps[0] = 1.0, 0.0025
+    used = list(range(1, n + 1))
+    smp = BatchedMCMC(W, n, used, [used], 0, pmin, pmax, pm, ps, propose_scale=2.4, seed_ij=4004 + rank,
+                      seed_kl=9373, first_walker=rank * W)
+    smp.set_covariance(np.diag(width ** 2))
+    smp.set_test_gaussian(cov, P0)
+    th = torch.tensor(syn.walker_theory(1, n_fields=3, ld_field=2512), device="cuda")
+    smp.add_likelihood(plik, th.expand(W, th.shape[1], th.shape[2]))
+    g = syn.gaussians(123 + rank, W * n).reshape(W, n)
+    smp.set_start(np.clip(P0 + 2 * width * g, pmin + 1e-9, pmax - 1e-9))
+    smp.step(5, fast_only=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    smp.step(steps, fast_only=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    out = {"workload": "plik_lite_TTTEEE + correlated 20-d Gaussian nuisance posterior (full plik's 21 fast "
+                       "parameters as a sampler-throughput stand-in: clik absent), one 21-parameter fast block, "
+                       "one shared slow point",
+           "walkers_total": W * world, "evals_per_s": W * world * steps / dt, "ms_per_step": dt / steps * 1e3,
+           "avg_kernel_us": kernel_profile(smp, 50)}
+    if seconds > 0:
+        steps_block = 40 * n
+        cap = 60 * steps_block
+        smp.enable_history(cap)
+        ex = ConvergenceExchange(n, CollectorSettings(MPI_R_Stop=0.01, MPI_Min_Sample_Update=55,
+                                                      covariance_is_diagonal=True))
+        trace, t0, done_at = [], time.perf_counter(), None
+        while smp.history_count() + steps_block <= cap:
+            smp.step(steps_block, fast_only=True)
+            r = ex.update_cov_and_check_converge(smp, *reference_window(smp.history_count()))
+            el = time.perf_counter() - t0
+            trace.append([round(el, 3), smp.history_count(), r.R])
+            if r.update_proposal:
+                smp.set_covariance(r.propose_cov)
+            if r.converged:
+                done_at = el
+                break
+            stop = el > seconds
+            if world > 1:
+                import torch.distributed as dist
+                flag = torch.tensor([1.0 if stop else 0.0], dtype=torch.float64, device="cuda")
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                stop = flag.item() > 0
+            if stop:
+                break
+        out.update({"target_r_minus_1": 0.01, "exchange_every_steps": steps_block, "converged_wall_s": done_at,
+                    "trace_wall_s_steps_R": trace})
+    return out
+
+
 BK15_DATASET = "BK15/BK15_dust.dataset"
 BK15_MAPS = "BK15_95_B BK15_150_B BK15_220_B W023_B P030_B W033_B P044_B P070_B P100_B P143_B P217_B P353_B"
 
@@ -246,7 +356,8 @@ def config5_run(W, rank, world, tmpdir, seconds, steps=100):
         dt = float(t.item())
     out = {"workload": "BK15 (12 B maps x 9 bins, HL, synthetic covariance) + plik_lite_TTTEEE joint, "
                        "8 fast parameters (calPlanck + 7 BK15 foreground), one shared slow point",
-           "walkers_total": W * world, "evals_per_s": W * world * steps / dt, "ms_per_step": dt / steps * 1e3}
+           "walkers_total": W * world, "evals_per_s": W * world * steps / dt, "ms_per_step": dt / steps * 1e3,
+           "avg_kernel_us": kernel_profile(smp, 20)}
     if seconds > 0:
         steps_block = 40 * len(used)                   # MPI_Sample_update_freq (SampleCollector.f90:399-403)
         cap = 100 * steps_block
@@ -430,6 +541,9 @@ def main():
         conv = None
         if args.converge_seconds > 0:
             conv = convergence_run(W, rank, world, td, args.converge_seconds, lensing=not args.no_lensing)
+        c4 = None
+        if args.config4_seconds >= 0:
+            c4 = config4_run(512, rank, world, td, args.config4_seconds)
         c5 = None
         if args.config5_seconds >= 0:
             c5 = config5_run(W, rank, world, td, args.config5_seconds)
@@ -471,6 +585,8 @@ def main():
         }
         if conv is not None:
             out["convergence"] = conv
+        if c4 is not None:
+            out["config4_fast21"] = c4
         if c5 is not None:
             out["config5_bk15_plik"] = c5
         if world == 1 and not args.no_cpu_baseline:

@@ -718,29 +718,81 @@ __global__ void gather_nuis(const double *trial, int W, int ld, int nuis0, int n
     for (int k = 0; k < n_nuis; k++) out[(size_t)w * n_nuis + k] = trial[(size_t)(nuis0 + k) * ld + w];
 }
 
-__global__ void hist_stats_kernel(const double *hist, int cap, int W, int n, int first, int last,
-                                  double *means, double *covs)
-{   // per-chain mean/cov over rows first..last (SampleCollector.f90:235-246)
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= W) return;
-    const int cnt = last - first + 1;
-    double *m = means + (size_t)w * n;
-    for (int i = 0; i < n; i++) m[i] = 0.0;
-    for (int tt = first; tt <= last; tt++) {
-        const double *row = hist + (size_t)(tt % cap) * (n + 1) * W;
-        for (int i = 0; i < n; i++) m[i] += row[(size_t)i * W + w];
-    }
-    for (int i = 0; i < n; i++) m[i] /= cnt;
-    double *C = covs + (size_t)w * n * n;
-    for (int i = 0; i < n * n; i++) C[i] = 0.0;
-    for (int tt = first; tt <= last; tt++) {
-        const double *row = hist + (size_t)(tt % cap) * (n + 1) * W;
+// Per-chain mean and covariance over history rows first..last
+// (SampleCollector.f90:235-246), two passes like the reference (mean, then
+// the centred products).  A block owns 64 walkers (lane = walker, coalesced
+// rows) and HS_PH row phases (wave p takes rows first+p, first+p+HS_PH, ...);
+// the phase partials are combined in fixed order, so results are
+// deterministic.  The covariance pass runs one block per (walker tile,
+// parameter i) with the n products of row i in registers (NC = n rounded up).
+static constexpr int HS_PH = 4;
+
+template <int NC>
+__global__ __launch_bounds__(64 * HS_PH) void hist_mean_kernel(const double *hist, int cap, int W, int n, int first,
+                                                              int last, double *means)
+{
+    __shared__ double part[HS_PH][NC][64];
+    const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const int w = blockIdx.x * 64 + lane;
+    double acc[NC];
+#pragma unroll
+    for (int j = 0; j < NC; j++) acc[j] = 0.0;
+    if (w < W)
+        for (int tt = first + ph; tt <= last; tt += HS_PH) {
+            const double *row = hist + (size_t)(tt % cap) * (n + 1) * W + w;
+#pragma unroll
+            for (int j = 0; j < NC; j++)
+                if (j < n) acc[j] += row[(size_t)j * W];
+        }
+#pragma unroll
+    for (int j = 0; j < NC; j++) part[ph][j][lane] = acc[j];
+    __syncthreads();
+    if (ph == 0 && w < W) {
+        const double cnt = last - first + 1;
         for (int j = 0; j < n; j++) {
-            const double dj = row[(size_t)j * W + w] - m[j];
-            for (int i = 0; i < n; i++) C[i * n + j] += (row[(size_t)i * W + w] - m[i]) * dj;
+            double v = part[0][j][lane];
+            for (int p = 1; p < HS_PH; p++) v += part[p][j][lane];
+            means[(size_t)w * n + j] = v / cnt;
         }
     }
-    for (int i = 0; i < n * n; i++) C[i] /= cnt;
+}
+
+template <int NC>
+__global__ __launch_bounds__(64 * HS_PH) void hist_cov_kernel(const double *hist, int cap, int W, int n, int first,
+                                                             int last, const double *means, double *covs)
+{
+    __shared__ double part[HS_PH][NC][64];
+    const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const int w = blockIdx.x * 64 + lane, i = blockIdx.y;
+    double acc[NC], m[NC];
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+        acc[j] = 0.0;
+        m[j] = (w < W && j < n) ? means[(size_t)w * n + j] : 0.0;
+    }
+    double mi = 0.0;
+#pragma unroll
+    for (int j = 0; j < NC; j++)
+        if (j == i) mi = m[j];
+    if (w < W)
+        for (int tt = first + ph; tt <= last; tt += HS_PH) {
+            const double *row = hist + (size_t)(tt % cap) * (n + 1) * W + w;
+            const double di = row[(size_t)i * W] - mi;
+#pragma unroll
+            for (int j = 0; j < NC; j++)
+                if (j < n) acc[j] += (row[(size_t)j * W] - m[j]) * di;
+        }
+#pragma unroll
+    for (int j = 0; j < NC; j++) part[ph][j][lane] = acc[j];
+    __syncthreads();
+    if (ph == 0 && w < W) {
+        const double cnt = last - first + 1;
+        for (int j = 0; j < n; j++) {
+            double v = part[0][j][lane];
+            for (int p = 1; p < HS_PH; p++) v += part[p][j][lane];
+            covs[(size_t)w * n * n + (size_t)i * n + j] = v / cnt;
+        }
+    }
 }
 
 // Per-GPU partial sums of the chain moments for the convergence exchange
@@ -1398,9 +1450,19 @@ void sampler_history_stats(cmbs *s, int first, int last, double *means, double *
     if (first < 0 || last < first || last >= s->hist_count || s->hist_count - first > s->hist_cap)
         fail(CMBL_ERR_ARG, "history rows [%d, %d] not available (count %d, capacity %d)", first, last,
              s->hist_count, s->hist_cap);
-    hipLaunchKernelGGL(hist_stats_kernel, dim3((s->W + 127) / 128), dim3(128), 0, stream, s->hist.as<double>(),
-                       s->hist_cap, s->W, s->n_used, first, last, means, covs);
-    HIP_CHECK(hipGetLastError());
+    const int n = s->n_used;
+    const dim3 gm((s->W + 63) / 64), gc((s->W + 63) / 64, n), blk(64 * HS_PH);
+    const double *h = s->hist.as<double>();
+    auto run = [&](auto kmean, auto kcov) {
+        hipLaunchKernelGGL(kmean, gm, blk, 0, stream, h, s->hist_cap, s->W, n, first, last, means);
+        HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(kcov, gc, blk, 0, stream, h, s->hist_cap, s->W, n, first, last, means, covs);
+        HIP_CHECK(hipGetLastError());
+    };
+    if (n <= 8) run(hist_mean_kernel<8>, hist_cov_kernel<8>);
+    else if (n <= 16) run(hist_mean_kernel<16>, hist_cov_kernel<16>);
+    else if (n <= 32) run(hist_mean_kernel<32>, hist_cov_kernel<32>);
+    else run(hist_mean_kernel<64>, hist_cov_kernel<64>);
 }
 
 void sampler_chain_moments(cmbs *s, int first, int last, const double *gmean, double *out, hipStream_t stream) {
@@ -1427,10 +1489,6 @@ void sampler_history_host(cmbs *s, int first, int count, double *out) {
     }
 }
 
-// checkpoint resume of the history ring: rows [first, first + count) as
-// written by sampler_history_host go back to their ring slots, and the ring
-// continues at first + count (the samples the convergence test windows over,
-// TMpiChainCollector_ReadState's Samples%LoadState, SampleCollector.f90:167)
 void sampler_history_terms_host(cmbs *s, int first, int count, double *out) {
     if (s->hist_cap == 0) fail(CMBL_ERR_ARG, "history not enabled");
     const int oldest = std::max(0, s->hist_count - s->hist_cap);
@@ -1446,6 +1504,10 @@ void sampler_history_terms_host(cmbs *s, int first, int count, double *out) {
     }
 }
 
+// checkpoint resume of the history ring: rows [first, first + count) as
+// written by sampler_history_host go back to their ring slots, and the ring
+// continues at first + count (the samples the convergence test windows over,
+// TMpiChainCollector_ReadState's Samples%LoadState, SampleCollector.f90:167)
 void sampler_history_restore(cmbs *s, int first, int count, const double *in, const double *terms) {
     if (s->hist_cap == 0) fail(CMBL_ERR_ARG, "history not enabled");
     if (first < 0 || count < 0 || count > s->hist_cap)
