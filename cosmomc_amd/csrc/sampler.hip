@@ -228,12 +228,14 @@ __device__ void block_proposal(const DevCfg &c, const Tabs &t, Walker &k, int bi
     }
     const double scale = rf * c.propose_scale;
     // vec(q) = R(q, loopix) * (r * wid);  P(changed) += mapping_matrix . vec
+    // (the column of R is read once: R may live in HBM when it is too big to stage)
     const int nc = t.blk_nchanged[b];
     const double *M = t.mapping + t.blk_map_off[b];
     const int *chg = t.changed + t.blk_changed_off[b];
+    for (int q = 0; q < n; q++) k.vec[q] = k.R[off + q * n + (lp - 1)] * scale;
     for (int j = 0; j < nc; j++) {
         double s = 0.0;
-        for (int q = 0; q < n; q++) s += M[j * n + q] * (k.R[off + q * n + (lp - 1)] * scale);
+        for (int q = 0; q < n; q++) s += M[j * n + q] * k.vec[q];
         k.trial[chg[j]] += s;
     }
 }
