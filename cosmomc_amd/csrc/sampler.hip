@@ -154,6 +154,8 @@ struct Walker {
     Col<double> R, P, trial, vec;
     Col<int> cyc, cyclp, blklp, itmp;
     int fast_ix;
+    int defer = 0;    // leave the mapping product to the caller (block index in pend_b, vec filled)
+    int pend_b = -1;
 };
 
 __device__ int cyc_next(Walker &k, int which, int n, int base)
@@ -233,6 +235,10 @@ __device__ void block_proposal(const DevCfg &c, const Tabs &t, Walker &k, int bi
     const double *M = t.mapping + t.blk_map_off[b];
     const int *chg = t.changed + t.blk_changed_off[b];
     for (int q = 0; q < n; q++) k.vec[q] = k.R[off + q * n + (lp - 1)] * scale;
+    if (k.defer) {
+        k.pend_b = b;
+        return;
+    }
     for (int j = 0; j < nc; j++) {
         double s = 0.0;
         for (int q = 0; q < n; q++) s += M[j * n + q] * k.vec[q];
@@ -267,8 +273,21 @@ __device__ void proposal(const DevCfg &c, const Tabs &t, Walker &k)
 
 // GetLogLike calclike.f90:136-151 with AddLikeTemp :82-94; likes[l] are the
 // data-likelihood terms at q (LogLikeWithTheorySet :374-387)
+// test_row(i): row i of covinv . (q - center) (TestLikelihoodFunction's inner sum)
+template <class Q>
+__device__ inline double test_row(const DevCfg &c, const Tabs &t, const Q &q, int i)
+{
+    const int n = c.n_used;
+    double s = 0.0;
+    for (int j = 0; j < n; j++) s += t.covinv[i * n + j] * (q[t.params_used[j]] - t.center[t.params_used[j]]);
+    return s;
+}
+
+// trows (stride NB), when given, holds test_row(i) for every i, computed by
+// the other waves of mh_kernel: the same sums in the same order
 template <class Q, class L>
-__device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const L &likes)
+__device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const L &likes,
+                              const double *trows = nullptr)
 {
     for (int i = 0; i < c.np; i++)
         if (q[i] > t.pmax[i] || q[i] < t.pmin[i]) return LOGZERO;   // GetLogLikeBounds :97-109
@@ -277,9 +296,7 @@ __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const 
         const int n = c.n_used;
         double d = 0.0;
         for (int i = 0; i < n; i++) {
-            double s = 0.0;
-            for (int j = 0; j < n; j++)
-                s += t.covinv[i * n + j] * (q[t.params_used[j]] - t.center[t.params_used[j]]);
+            const double s = trows ? trows[(size_t)i * NB] : test_row(c, t, q, i);
             d += (q[t.params_used[i]] - t.center[t.params_used[i]]) * s;
         }
         main = d / 2.0;
@@ -378,7 +395,8 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     double *sd = lds;                                            // [nd_st][NB]
     double *lk = sd + (size_t)nd_st * NB;                        // [nlk][NB]
     double *vc = lk + (size_t)nlk * NB;                          // [max_blk][NB]
-    double *td = vc + (size_t)c.max_blk * NB;                    // [n_dbl rounded to 32]
+    double *tq = vc + (size_t)c.max_blk * NB;                    // [n_used][NB] test-Gaussian row sums
+    double *td = tq + (size_t)c.n_used * NB;                     // [n_dbl rounded to 32]
     int *si = reinterpret_cast<int *>(td + ((c.tl.n_dbl + 31) & ~31));   // [NI][NB]
     int *it = si + (size_t)R.NI * NB;                            // [all_n][NB]
     int *ti = it + (size_t)c.all_n * NB;                         // [n_int rounded to 64]
@@ -411,6 +429,19 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     STAMP(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // the test-Gaussian rows of covinv . (trial - center) are spread over the
+    // waves (each row summed by one thread, in order) instead of run serially
+    // by the chain wave
+    const bool par_test = ACCEPT && c.test_like && c.n_used >= 4;
+    const bool par_map = PROPOSE && c.max_blk >= 4;
+    if (par_test) {
+        if (act) {
+            const Tabs t0 = make_tabs(c, ti, td);
+            const Col<double> q{sd + (size_t)SROW(R.T) * NB + lane, NB};
+            for (int i = wave; i < c.n_used; i += MH_WAVES) tq[(size_t)i * NB + lane] = test_row(c, t0, q, i);
+        }
+        __syncthreads();
+    }
     STAMP(2);
     if (wave == 0 && act) {
 
@@ -436,7 +467,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     int &nacc = si[(size_t)R.NACC * NB + lane];
 
     if (ACCEPT) {
-        const double like = target_like(c, t, k.trial, Col<double>{lk + lane, NB});
+        const double like = target_like(c, t, k.trial, Col<double>{lk + lane, NB}, par_test ? tq + lane : nullptr);
         bool acc = false;
         if (like != LOGZERO) {
             acc = cur > like;
@@ -470,11 +501,14 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     STAMP(3);
     if (PROPOSE) {
         for (int i = 0; i < c.np; i++) k.trial[i] = k.P[i];          // Trial = CurParams
+        k.defer = par_map;
         if (fast_only) proposal_fast(c, t, k);
         else proposal(c, t, k);
-        for (int l = 0; l < c.n_like; l++)
-            for (int q = 0; q < c.like_nn[l]; q++)
-                c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = k.trial[c.like_nuis0[l] + q];
+        if (par_map) tq[lane] = (double)k.pend_b;                    // the block, for the mapping waves
+        else
+            for (int l = 0; l < c.n_like; l++)
+                for (int q = 0; q < c.like_nn[l]; q++)
+                    c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = k.trial[c.like_nuis0[l] + q];
     }
     STAMP(4);
     sd[(size_t)R.C * NB + lane] = k.r.c;
@@ -483,6 +517,30 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     si[(size_t)R.J97 * NB + lane] = k.r.j97;
     si[(size_t)R.ISET * NB + lane] = k.r.iset;
     si[(size_t)R.FASTIX * NB + lane] = k.fast_ix;
+    }
+    if (par_map) {   // UpdateParams' mapping product, rows spread over the waves (one thread per row, same order)
+        __syncthreads();
+        if (act) {
+            const Tabs t = make_tabs(c, ti, td);
+            const int b = (int)tq[lane];
+            const int n = t.blk_n[b], nc = t.blk_nchanged[b];
+            const double *M = t.mapping + t.blk_map_off[b];
+            const int *chg = t.changed + t.blk_changed_off[b];
+            double *trial = sd + (size_t)SROW(R.T) * NB + lane;
+            const double *vec = vc + lane;
+            for (int j = wave; j < nc; j += MH_WAVES) {
+                double s = 0.0;
+                for (int q = 0; q < n; q++) s += M[j * n + q] * vec[(size_t)q * NB];
+                trial[(size_t)chg[j] * NB] += s;
+            }
+        }
+        __syncthreads();
+        if (wave == 0 && act) {
+            const double *trial = sd + (size_t)SROW(R.T) * NB + lane;
+            for (int l = 0; l < c.n_like; l++)
+                for (int q = 0; q < c.like_nn[l]; q++)
+                    c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = trial[(size_t)(c.like_nuis0[l] + q) * NB];
+        }
     }
     __syncthreads();
     if (!act) return;
@@ -848,7 +906,7 @@ __global__ __launch_bounds__(256) void chain_moments_kernel(const double *means,
 static size_t mh_lds_bytes(const cmbs *s, int stage_R) {
     const DevCfg &d = s->dc;
     const int nd_st = stage_R ? d.rows.ND : d.rows.ND - d.rows.RR;
-    return (size_t)(nd_st + MAXLIKE + d.max_blk) * NB * 8 + (size_t)((d.tl.n_dbl + 31) & ~31) * 8 +
+    return (size_t)(nd_st + MAXLIKE + d.max_blk + d.n_used) * NB * 8 + (size_t)((d.tl.n_dbl + 31) & ~31) * 8 +
            (size_t)(d.rows.NI + d.all_n) * NB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 + 64;
 }
 
