@@ -51,6 +51,7 @@ struct DevCfg {
     double *sd;             // [ND][ld]
     int *si;                // [NI][ld]
     int stage_R;            // R rows staged in LDS (else read in place, stride W)
+    int tq_rows;            // LDS scratch rows for the multi-wave test-Gaussian / mapping products
     int n_like;
     const double *like_terms;       // [n_like (even)][ld] -lnL of each likelihood at the trial point
     double *cur_terms;              // [n_like][ld] -lnL of each likelihood at the current point

@@ -395,8 +395,8 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     double *sd = lds;                                            // [nd_st][NB]
     double *lk = sd + (size_t)nd_st * NB;                        // [nlk][NB]
     double *vc = lk + (size_t)nlk * NB;                          // [max_blk][NB]
-    double *tq = vc + (size_t)c.max_blk * NB;                    // [n_used][NB] test-Gaussian row sums
-    double *td = tq + (size_t)c.n_used * NB;                     // [n_dbl rounded to 32]
+    double *tq = vc + (size_t)c.max_blk * NB;                    // [tq_rows][NB] test-Gaussian row sums / block
+    double *td = tq + (size_t)c.tq_rows * NB;                    // [n_dbl rounded to 32]
     int *si = reinterpret_cast<int *>(td + ((c.tl.n_dbl + 31) & ~31));   // [NI][NB]
     int *it = si + (size_t)R.NI * NB;                            // [all_n][NB]
     int *ti = it + (size_t)c.all_n * NB;                         // [n_int rounded to 64]
@@ -432,8 +432,8 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     // the test-Gaussian rows of covinv . (trial - center) are spread over the
     // waves (each row summed by one thread, in order) instead of run serially
     // by the chain wave
-    const bool par_test = ACCEPT && c.test_like && c.n_used >= 4;
-    const bool par_map = PROPOSE && c.max_blk >= 4;
+    const bool par_test = ACCEPT && c.test_like && c.n_used >= 4 && c.tq_rows >= c.n_used;
+    const bool par_map = PROPOSE && c.max_blk >= 4 && c.tq_rows >= 1;
     if (par_test) {
         if (act) {
             const Tabs t0 = make_tabs(c, ti, td);
@@ -906,11 +906,15 @@ __global__ __launch_bounds__(256) void chain_moments_kernel(const double *means,
 static size_t mh_lds_bytes(const cmbs *s, int stage_R) {
     const DevCfg &d = s->dc;
     const int nd_st = stage_R ? d.rows.ND : d.rows.ND - d.rows.RR;
-    return (size_t)(nd_st + MAXLIKE + d.max_blk + d.n_used) * NB * 8 + (size_t)((d.tl.n_dbl + 31) & ~31) * 8 +
+    return (size_t)(nd_st + MAXLIKE + d.max_blk + d.tq_rows) * NB * 8 + (size_t)((d.tl.n_dbl + 31) & ~31) * 8 +
            (size_t)(d.rows.NI + d.all_n) * NB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 + 64;
 }
 
 static void set_mh_lds(cmbs *s) {
+    // scratch for the multi-wave products: a row per test-Gaussian row, or one
+    // row (the proposal's block) for the mapping; dropped if the image is too big
+    s->dc.tq_rows = s->dc.test_like ? s->n_used : 1;
+    if (mh_lds_bytes(s, s->dc.stage_R) > 160 * 1024) s->dc.tq_rows = 0;
     s->mh_lds = mh_lds_bytes(s, s->dc.stage_R);
     if (s->mh_lds > 160 * 1024) fail(CMBL_ERR_ARG, "sampler state too large for LDS (%zu bytes)", s->mh_lds);
     const int lds = (int)s->mh_lds;
@@ -1157,8 +1161,8 @@ void sampler_set_test_gaussian(cmbs *s, const double *cov, const double *center)
     tl.center = (int)vd.size();
     vd.insert(vd.end(), center, center + s->np);
     tl.n_dbl = (int)vd.size();
-    set_mh_lds(s);
     s->dc.test_like = 1;
+    set_mh_lds(s);
     upload_tables(s);
 }
 

@@ -151,6 +151,36 @@ def test_history_stats():
     np.testing.assert_allclose(c.cpu().numpy(), cov, rtol=1e-10, atol=1e-13)
 
 
+@pytest.mark.parametrize("n", [5, 12, 21, 40])
+def test_history_stats_wide(n):
+    """hist_mean_kernel / hist_cov_kernel at every register width (8, 16, 32,
+    64 parameters), over a wrapped ring and a walker count that is not a
+    multiple of 64, against numpy on history_host's rows."""
+    from cosmomc_amd.sampler import BatchedMCMC
+    W, cap, steps = 100, 48, 70
+    used = list(range(1, n + 1))
+    rng = np.random.default_rng(n)
+    A = rng.standard_normal((n, n))
+    cov = A @ A.T / n + np.eye(n)
+    s = BatchedMCMC(W, n, used, [used[:n // 2], used[n // 2:]], 1, -50 * np.ones(n), 50 * np.ones(n),
+                    seed_ij=11, seed_kl=12)
+    s.set_covariance(np.eye(n) * 0.3)
+    if n <= 32:      # a 40-d test Gaussian's tables do not fit the LDS image: flat target in the box
+        s.set_test_gaussian(cov, np.zeros(n))
+    s.set_start(rng.standard_normal((W, n)))
+    s.enable_history(cap)
+    s.step(steps)
+    first, last = steps - 40, steps - 1
+    rows = s.history_host(first, last - first + 1)          # [T, n + 1, W]
+    x = np.transpose(rows[:, :n, :], (0, 2, 1))             # [T, W, n]
+    mu = x.mean(axis=0)
+    d = x - mu
+    ref = np.einsum("twi,twj->wij", d, d) / x.shape[0]
+    m, c = s.history_stats(first, last)
+    np.testing.assert_allclose(m.cpu().numpy(), mu, rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(c.cpu().numpy(), ref, rtol=1e-9, atol=1e-12)
+
+
 @pytest.mark.parametrize("groups", [2, 3, 8])
 def test_walker_groups_same_chains(tmp_path, groups):
     """cmbs_set_groups only changes how the step is scheduled: every walker's
