@@ -1001,6 +1001,19 @@ __global__ __launch_bounds__(64) void cmbl_hl_kernel(HLDev h, const double *__re
 // row (one LDS exchange); the column rotation is dispatched per round to a
 // compile-time instance, so every register index is static.  The matrix
 // products go through per-group LDS row buffers.
+#ifdef CMAMD_STAMPS
+// phase timestamps (s_memtime) of the first Jacobi rounds of block 0, lane 0
+// (instrumented build only; tools/hl_stamps.py)
+__device__ unsigned long long g_hl_stamps[32][6];
+#define HSTAMP(k)                                                                                      \
+    do {                                                                                               \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                   \
+        if (blockIdx.x == 0 && lane == 0 && nst < 32) g_hl_stamps[nst][k] = t_;                      \
+    } while (0)
+#else
+#define HSTAMP(k) ((void)0)
+#endif
+
 template <int M>
 struct HLRowsLds {
     double rows[4][2][16][M + 1];   // two row buffers per problem (odd stride: fewer bank conflicts)
@@ -1081,6 +1094,10 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
         if (!__any(big)) break;        // wave-uniform: converged groups keep rotating by ~0
 #pragma unroll 1
         for (int rr = 0; rr < M - 1; rr++) {
+#ifdef CMAMD_STAMPS
+            const int nst = sweep * (M - 1) + rr;
+#endif
+            HSTAMP(0);
             // (1) this row's pair and rotation (the lower row's a_pq for both lanes)
             double c = 1.0, s = 0.0;
             int p = r;
@@ -1090,6 +1107,7 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
                 S.rows[grp][0][r][0] = hl_pick<M>(A, p);
             }
             __syncthreads();
+            HSTAMP(1);
             if (r < M) {
                 const int lo = r < p ? r : p, hi = r < p ? p : r;
                 const double apq = S.rows[grp][0][lo][0], app = S.dg[grp][lo], aqq = S.dg[grp][hi];
@@ -1106,6 +1124,7 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
                 S.cs[grp][r][1] = s;
             }
             __syncthreads();
+            HSTAMP(2);
             // (2) B = A J, V = V J on this lane's row; (3) A' = J^T B: row r = c B_r + s B_p
             if (r < M) {
                 hl_colrot_round<M>(rr, A, V, S.cs[grp]);
@@ -1113,6 +1132,7 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
                 for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = A[k];
             }
             __syncthreads();
+            HSTAMP(3);
             if (r < M) {
                 const double *Bp = S.rows[grp][0][p];
                 // the rotated-away a_rp is exactly 0 (standard Jacobi; computing it leaves
@@ -1121,6 +1141,7 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
                 for (int k = 0; k < M; k++) A[k] = (k == p) ? 0.0 : c * A[k] + s * Bp[k];
             }
             __syncthreads();
+            HSTAMP(4);
         }
     }
 }
@@ -2193,3 +2214,9 @@ std::unique_ptr<Like> make_cmblikes(const Ini &ini, const std::string &tag) {
 }
 
 }  // namespace cmamd
+
+#ifdef CMAMD_STAMPS
+extern "C" int cmamd_debug_hl_stamps(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_hl_stamps), sizeof(cmamd::g_hl_stamps)) == hipSuccess ? 0 : -5;
+}
+#endif
