@@ -1016,9 +1016,11 @@ __device__ unsigned long long g_hl_stamps[32][6];
 
 template <int M>
 struct HLRowsLds {
-    double rows[4][2][16][M + 1];   // two row buffers per problem (odd stride: fewer bank conflicts)
-    double cs[4][16][2];            // (c, s) of each column in the current round
-    double dg[4][16];               // a diagonal / g(x) broadcast
+    static constexpr int G = 64 / M;   // problems per wave: M lanes each, packed (5 for M = 12)
+    double rows[G][2][M][M + 1];    // two row buffers per problem (odd stride: fewer bank conflicts)
+    double cs[G][M][2];             // (c, s) of each column in the current round
+    double dg[G][M];                // a diagonal / g(x) broadcast
+    double ap[G][M];                // a_{r p(r)} of the coming round (written one phase ahead)
 };
 
 template <int M>
@@ -1075,14 +1077,19 @@ template <int M>
 __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, int grp, int r, int lane,
                                int max_sweeps)
 {
+    const bool on = grp < HLRowsLds<M>::G;        // lanes past G*M idle
 #pragma unroll
     for (int k = 0; k < M; k++) V[k] = (k == r) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < max_sweeps; sweep++) {
-        // convergence (as cmbl_hl_kernel): every off-diagonal |a_rk| <= 1e-18 sqrt(|a_rr a_kk|) or 0
-        if (r < M) S.dg[grp][r] = hl_pick<M>(A, r);
+        // convergence (as cmbl_hl_kernel): every off-diagonal |a_rk| <= 1e-18 sqrt(|a_rr a_kk|) or 0;
+        // the diagonal and a_{r p} written here also serve round 0
+        if (on) {
+            S.dg[grp][r] = hl_pick<M>(A, r);
+            S.ap[grp][r] = hl_pick<M>(A, hl_partner<M>(0, r));
+        }
         __syncthreads();
         bool big = false;
-        if (r < M) {
+        if (on) {
             const double arr = S.dg[grp][r];
 #pragma unroll
             for (int k = 0; k < M; k++) {
@@ -1098,19 +1105,15 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
             const int nst = sweep * (M - 1) + rr;
 #endif
             HSTAMP(0);
-            // (1) this row's pair and rotation (the lower row's a_pq for both lanes)
+            // (1) this row's pair and rotation (the lower row's a_pq for both lanes); the
+            // diagonal and a_{r p} were exchanged at the end of the previous round
             double c = 1.0, s = 0.0;
             int p = r;
-            if (r < M) {
-                p = hl_partner<M>(rr, r);
-                S.dg[grp][r] = hl_pick<M>(A, r);
-                S.rows[grp][0][r][0] = hl_pick<M>(A, p);
-            }
-            __syncthreads();
+            if (on) p = hl_partner<M>(rr, r);
             HSTAMP(1);
-            if (r < M) {
+            if (on) {
                 const int lo = r < p ? r : p, hi = r < p ? p : r;
-                const double apq = S.rows[grp][0][lo][0], app = S.dg[grp][lo], aqq = S.dg[grp][hi];
+                const double apq = S.ap[grp][lo], app = S.dg[grp][lo], aqq = S.dg[grp][hi];
                 double cc = 1.0, ss = 0.0;
                 if (apq != 0.0 && fabs(apq) > 1e-300) {
                     const double theta = (aqq - app) / (2.0 * apq);
@@ -1126,19 +1129,23 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
             __syncthreads();
             HSTAMP(2);
             // (2) B = A J, V = V J on this lane's row; (3) A' = J^T B: row r = c B_r + s B_p
-            if (r < M) {
+            if (on) {
                 hl_colrot_round<M>(rr, A, V, S.cs[grp]);
 #pragma unroll
                 for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = A[k];
             }
             __syncthreads();
             HSTAMP(3);
-            if (r < M) {
+            if (on) {
                 const double *Bp = S.rows[grp][0][p];
                 // the rotated-away a_rp is exactly 0 (standard Jacobi; computing it leaves
                 // O(eps) noise that the convergence test would keep rotating)
 #pragma unroll
                 for (int k = 0; k < M; k++) A[k] = (k == p) ? 0.0 : c * A[k] + s * Bp[k];
+                if (rr + 1 < M - 1) {       // the next round's exchange, one barrier early
+                    S.dg[grp][r] = hl_pick<M>(A, r);
+                    S.ap[grp][r] = hl_pick<M>(A, hl_partner<M>(rr + 1, r));
+                }
             }
             __syncthreads();
             HSTAMP(4);
@@ -1151,13 +1158,15 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
                                                          double *__restrict__ xrows, int W, int max_sweeps)
 {
     __shared__ HLRowsLds<M> S;
-    const int lane = threadIdx.x, grp = lane >> 4, r = lane & 15;
-    const int prob = blockIdx.x * 4 + grp;
+    constexpr int G = HLRowsLds<M>::G;
+    const int lane = threadIdx.x, grp = lane / M, r = lane % M;
+    const bool on = grp < G;                      // lanes past G*M idle
+    const int prob = blockIdx.x * G + grp;
     const int nprob = W * h.nb;
-    const bool live = prob < nprob;
+    const bool live = on && prob < nprob;
     const int w = live ? prob / h.nb : 0, b = live ? prob % h.nb : 0;
     const int n = h.n;
-    const bool row_ok = r < n;
+    const bool row_ok = on && r < n;
     auto U_row = [&](int k, int j) { return S.rows[grp][0][k][j]; };
     // C row r from its lower-triangle elements (ElementsToMatrix :950-965), zero padded to M
     double A[M], V[M];
@@ -1173,8 +1182,8 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
     }
     // (1) C = U diag U^T
     hl_jacobi_rows<M>(A, V, S, grp, r, lane, max_sweeps);
-    const double dgr = hl_pick<M>(A, r < M ? r : 0);
-    if (r < M) {
+    const double dgr = hl_pick<M>(A, r);
+    if (on) {
         S.dg[grp][r] = dgr;
 #pragma unroll
         for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = V[k];     // U rows
@@ -1190,7 +1199,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
             for (int k = 0; k < n; k++) s += ch[r * n + k] * U_row(k, j);
         T[j] = s;
     }
-    if (r < M)
+    if (on)
 #pragma unroll
         for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = T[k];
     __syncthreads();
@@ -1208,7 +1217,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
     }
     __syncthreads();
     // (3) Rot = U R U^T (:891): T2 = R U^T (rows through LDS), A = U T2
-    if (r < M)
+    if (on)
 #pragma unroll
         for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = R[k];
     __syncthreads();
@@ -1222,7 +1231,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
         T[j] = s;
     }
     __syncthreads();
-    if (r < M)
+    if (on)
 #pragma unroll
         for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = T[k];
     __syncthreads();
@@ -1236,7 +1245,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
     __syncthreads();
     // (4) Rot = V diag V^T; g(x) = sign(x - 1) sqrt(2 max(0, x - ln x - 1))  (:892-894)
     hl_jacobi_rows<M>(A, V, S, grp, r, lane, max_sweeps);
-    if (r < M) {
+    if (on) {
         const double x = hl_pick<M>(A, r);
         const double g = sqrt(2 * fmax(0.0, x - log(x) - 1));
         S.dg[grp][r] = (x - 1 >= 0) ? g : -g;
@@ -1254,7 +1263,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
         T[j] = s;
     }
     __syncthreads();
-    if (r < M)
+    if (on)
 #pragma unroll
         for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = T[k];
     __syncthreads();
@@ -1268,14 +1277,14 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
         A[j] = s;
     }
     __syncthreads();
-    if (r < M)
+    if (on)
 #pragma unroll
         for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = A[k];
     __syncthreads();
     // vecp = lower-triangle elements (MatrixToElements :917-931); bigX entries of this bin
     if (live) {
         double *x = xrows + (long long)w * h.Np + (long long)b * h.ncl_used;
-        for (int u = r; u < h.ncl_used; u += 16) {
+        for (int u = r; u < h.ncl_used; u += M) {
             const int k = h.cl_use[u];
             int i = 0;
             while ((i + 1) * (i + 2) / 2 <= k) i++;
@@ -2185,11 +2194,12 @@ struct CMBLikes final : Like {
                 static const bool lds_hl = std::getenv("CMAMD_HL_LDS") != nullptr;   // A/B measurement switch
                 if (!lds_hl) {
                     static const int sweeps = std::getenv("CMAMD_HL_SWEEPS") ? atoi(std::getenv("CMAMD_HL_SWEEPS")) : 40;
-                    const dim3 g((W * nb + 3) / 4), bl(64);
+                    const dim3 bl(64);
                     switch (hl.m) {
 #define CMBL_HLR(MM)                                                                                              \
     case MM:                                                                                                      \
-        hipExtLaunchKernelGGL(cmbl_hl_rows_kernel<MM>, g, bl, 0, stream, e0, e1, 0, hl, (const double *)cmat,      \
+        hipExtLaunchKernelGGL(cmbl_hl_rows_kernel<MM>, dim3((W * nb + 64 / MM - 1) / (64 / MM)), bl, 0, stream,    \
+                              e0, e1, 0, hl, (const double *)cmat,                                                \
                               qf.x_rows(qws), W, sweeps);                                                         \
         break;
                         CMBL_HLR(2) CMBL_HLR(4) CMBL_HLR(6) CMBL_HLR(8) CMBL_HLR(10) CMBL_HLR(12) CMBL_HLR(14)
