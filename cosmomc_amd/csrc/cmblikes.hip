@@ -1094,7 +1094,7 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
 #pragma unroll
             for (int k = 0; k < M; k++) {
                 const double a = A[k];
-                if (k != r && a != 0.0 && fabs(a) > 1e-18 * sqrt(fabs(arr * S.dg[grp][k]))) big = true;
+                if (k != r && a != 0.0 && a * a > 1e-36 * fabs(arr * S.dg[grp][k])) big = true;   // squared: no sqrt
             }
         }
         __syncthreads();
@@ -1116,9 +1116,12 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
                 const double apq = S.ap[grp][lo], app = S.dg[grp][lo], aqq = S.dg[grp][hi];
                 double cc = 1.0, ss = 0.0;
                 if (apq != 0.0 && fabs(apq) > 1e-300) {
-                    const double theta = (aqq - app) / (2.0 * apq);
-                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                    cc = 1.0 / sqrt(t * t + 1.0);
+                    // t = sign(theta) / (|theta| + sqrt(theta^2 + 1)), theta = d / e, written with
+                    // one division; c = rsqrt(t^2 + 1).  The round's dependent chain of f64
+                    // divides and square roots is what a round waits on.
+                    const double d = aqq - app, e = 2.0 * apq;
+                    const double t = ((d >= 0) == (e >= 0) ? fabs(e) : -fabs(e)) / (fabs(d) + sqrt(d * d + e * e));
+                    cc = rsqrt(t * t + 1.0);
                     ss = t * cc;
                 }
                 c = cc;
