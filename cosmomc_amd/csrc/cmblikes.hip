@@ -1120,7 +1120,11 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
                     // one division; c = rsqrt(t^2 + 1).  The round's dependent chain of f64
                     // divides and square roots is what a round waits on.
                     const double d = aqq - app, e = 2.0 * apq;
-                    const double t = ((d >= 0) == (e >= 0) ? fabs(e) : -fabs(e)) / (fabs(d) + sqrt(d * d + e * e));
+                    const double den = fabs(d) + sqrt(d * d + e * e);
+                    double q = __builtin_amdgcn_rcp(den);           // reciprocal + two Newton steps
+                    q = fma(q, fma(-den, q, 1.0), q);
+                    q = fma(q, fma(-den, q, 1.0), q);
+                    const double t = ((d >= 0) == (e >= 0) ? fabs(e) : -fabs(e)) * q;
                     cc = rsqrt(t * t + 1.0);
                     ss = t * cc;
                 }
