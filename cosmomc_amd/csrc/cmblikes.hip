@@ -1017,10 +1017,10 @@ __device__ unsigned long long g_hl_stamps[32][6];
 template <int M>
 struct HLRowsLds {
     static constexpr int G = 64 / M;   // problems per wave: M lanes each, packed (5 for M = 12)
-    double rows[G][2][M][M + 1];    // two row buffers per problem (odd stride: fewer bank conflicts)
+    double rows[G][2][M][M + 1];    // two row buffers per problem (odd stride: fewer bank conflicts);
+                                    // in the Jacobi, buffer 1 holds each row as of the round start
     double cs[G][M][2];             // (c, s) of each column in the current round
     double dg[G][M];                // a diagonal / g(x) broadcast
-    double ap[G][M];                // a_{r p(r)} of the coming round (written one phase ahead)
 };
 
 template <int M>
@@ -1084,17 +1084,17 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
         // convergence (as cmbl_hl_kernel): every off-diagonal |a_rk| <= 1e-18 sqrt(|a_rr a_kk|) or 0;
         // the diagonal and a_{r p} written here also serve round 0
         if (on) {
-            S.dg[grp][r] = hl_pick<M>(A, r);
-            S.ap[grp][r] = hl_pick<M>(A, hl_partner<M>(0, r));
+#pragma unroll
+            for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = A[k];   // the whole row: no runtime-index picks
         }
         __syncthreads();
         bool big = false;
         if (on) {
-            const double arr = S.dg[grp][r];
+            const double arr = S.rows[grp][1][r][r];
 #pragma unroll
             for (int k = 0; k < M; k++) {
                 const double a = A[k];
-                if (k != r && a != 0.0 && a * a > 1e-36 * fabs(arr * S.dg[grp][k])) big = true;   // squared: no sqrt
+                if (k != r && a != 0.0 && a * a > 1e-36 * fabs(arr * S.rows[grp][1][k][k])) big = true;   // squared: no sqrt
             }
         }
         __syncthreads();
@@ -1113,7 +1113,7 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
             HSTAMP(1);
             if (on) {
                 const int lo = r < p ? r : p, hi = r < p ? p : r;
-                const double apq = S.ap[grp][lo], app = S.dg[grp][lo], aqq = S.dg[grp][hi];
+                const double apq = S.rows[grp][1][lo][hi], app = S.rows[grp][1][lo][lo], aqq = S.rows[grp][1][hi][hi];
                 double cc = 1.0, ss = 0.0;
                 if (apq != 0.0 && fabs(apq) > 1e-300) {
                     // t = sign(theta) / (|theta| + sqrt(theta^2 + 1)), theta = d / e, written with
@@ -1149,10 +1149,9 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
                 // O(eps) noise that the convergence test would keep rotating)
 #pragma unroll
                 for (int k = 0; k < M; k++) A[k] = (k == p) ? 0.0 : c * A[k] + s * Bp[k];
-                if (rr + 1 < M - 1) {       // the next round's exchange, one barrier early
-                    S.dg[grp][r] = hl_pick<M>(A, r);
-                    S.ap[grp][r] = hl_pick<M>(A, hl_partner<M>(rr + 1, r));
-                }
+                if (rr + 1 < M - 1)         // the next round's exchange, one barrier early
+#pragma unroll
+                    for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = A[k];
             }
             __syncthreads();
             HSTAMP(4);
