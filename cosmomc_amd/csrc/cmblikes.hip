@@ -141,6 +141,10 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
     const double alphasync = P[5], betasync = P[6], dustsync_corr = P[7];
     const double G = ghz_kelvin();
     double *cw = coef + (long long)w * 3 * c.nreq;
+    // pivot-frequency SEDs: the same for every map of this walker, so computed once
+    const double nu0d = c.fpivot_dust, nu0s = c.fpivot_sync;
+    const double gb0 = pow(nu0d, 3 + betadust) / (exp(G * nu0d / Tdust) - 1);
+    const double pl0 = pow(nu0s, 2 + betasync);
     for (int i = wave; i < c.nreq; i += 4) {
         const BKMap m = c.bkmaps[i];
         double gb = 0.0, pl = 0.0;
@@ -157,9 +161,6 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
             if (m.bc == 1) bc = P[12] + P[13] + 1.;
             else if (m.bc == 2) bc = P[12] + P[14] + 1.;
             else if (m.bc == 3) bc = P[12] + P[15] + 1.;
-            const double nu0d = c.fpivot_dust, nu0s = c.fpivot_sync;
-            const double gb0 = pow(nu0d, 3 + betadust) / (exp(G * nu0d / Tdust) - 1);
-            const double pl0 = pow(nu0s, 2 + betasync);
             double th_err = 1.0, gb_err = 1.0, pl_err = 1.0;
             if (bc != 1.) {                                   // DustScaling :130-141, SyncScaling :169-178
                 const double e1 = exp(G * m.nu_bar / BK_TCMB) - 1, e2 = exp(G * m.nu_bar * bc / BK_TCMB) - 1;
