@@ -98,3 +98,27 @@ def test_cmblikes_many_walkers_sampled(cmbl_golden, refdata):
     o = co.CMBLikesOracle(os.path.join(refdata, c["dataset"]), c["overrides"], c["tag"])
     for w in (0, 333, 1023):
         assert got[w] == pytest.approx(o.loglike(th[w], nu[w]), rel=1e-9)
+
+
+BK15_NAMES = ("BK15_95_E BK15_95_B BK15_150_E BK15_150_B BK15_220_E BK15_220_B W023_E W023_B P030_E P030_B "
+              "W033_E W033_B P044_E P044_B P070_E P070_B P100_E P100_B P143_E P143_B P217_E P217_B "
+              "P353_E P353_B").split()
+
+
+@pytest.mark.parametrize("nmaps", [1, 2, 5, 7, 9, 13, 16])
+def test_hl_every_kernel_width(cmbl_golden, refdata, nmaps):
+    """The HL kernel at every packed width (M = 2, 6, 8, 10, 14, 16 lanes per
+    matrix; 12 is the BK15 golden case): BK15 map subsets, E and B mixed,
+    against the numpy oracle."""
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    c = cmbl_golden["cases"]["bk15_B_12maps"]
+    ov = {"maps_use": " ".join(BK15_NAMES[:nmaps]), "use_min": "1", "use_max": "9"}
+    like = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), ov)
+    o = co.CMBLikesOracle(os.path.join(refdata, c["dataset"]), ov, c["tag"])
+    W = 7
+    th = syn.walker_theory(W, seed=500 + nmaps, lmax=c["lmax"])
+    base = np.array(c["nuis"])
+    nu = base[np.arange(W) % len(base)]
+    got = like.loglike_batch(torch.tensor(th, device="cuda"), torch.tensor(nu, device="cuda")).cpu().numpy()
+    ref = np.array([o.loglike(th[w], nu[w]) for w in range(W)])
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-8)
