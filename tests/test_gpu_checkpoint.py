@@ -128,3 +128,41 @@ def test_resume_plik_chain_files_and_history(tmp_path):
         assert (tmp_path / f"run_{w + 1}.txt").read_bytes() == (tmp_path / f"ref_{w + 1}.txt").read_bytes()
     for x, y in zip(ref.history_stats(45, 89), b.history_stats(45, 89)):
         assert torch.equal(x, y)
+
+
+def test_resume_two_likelihoods(cmbl_golden, refdata, tmp_path):
+    """plik_lite + Planck 2018 lensing sharing calPlanck: the image carries
+    both likelihoods' current terms, and the resumed run (chains and history
+    terms) matches the uninterrupted one."""
+    import os
+    from cosmomc_amd.checkpoint import read_checkpoint, write_checkpoint
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    lc = cmbl_golden["cases"]["lensing_consext8"]
+    plik = NativeCMBLikelihood("PLIK_LITE", syn.make_plik_lite(12345).write(str(tmp_path)))
+    lens = NativeCMBLikelihood(lc["tag"], os.path.join(refdata, lc["dataset"]), lc["overrides"])
+    plik.nuisance_indices = lens.nuisance_indices = [2]
+    W = 64
+    dl = torch.tensor(syn.walker_theory(W, seed=5, n_fields=10, ld_field=2512), device="cuda")
+    cov = np.array([[0.002 ** 2]])
+
+    def sampler():
+        s = BatchedMCMC(W, 3, [2], [[1]], 0, [0.0222, 0.9, 3.05], [0.0222, 1.1, 3.05], [0.0, 1.0, 0.0],
+                        [0.0, 0.0025, 0.0], seed_ij=77, seed_kl=88)
+        s.add_likelihood(plik, dl)
+        s.add_likelihood(lens, dl)
+        s.enable_history(40)
+        return s
+
+    a = sampler()
+    a.set_covariance(cov)
+    a.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
+    a.step(15, fast_only=True)
+    write_checkpoint(str(tmp_path / "two"), a, cov)
+    a.step(15, fast_only=True)
+    b = sampler()
+    read_checkpoint(str(tmp_path / "two"), b)
+    b.step(15, fast_only=True)
+    _same_state(a, b)
+    np.testing.assert_array_equal(a.history_terms(25, 5), b.history_terms(25, 5))
+    assert a.history_terms(29, 1).shape == (1, 2, W)
