@@ -37,7 +37,10 @@ class CmbsConfig(C.Structure):
                 ("propose_scale", C.c_double), ("temperature", C.c_double),
                 ("pmin", C.POINTER(C.c_double)), ("pmax", C.POINTER(C.c_double)),
                 ("prior_mean", C.POINTER(C.c_double)), ("prior_std", C.POINTER(C.c_double)),
-                ("seed_ij", C.c_int), ("seed_kl", C.c_int), ("first_walker", C.c_int)]
+                ("seed_ij", C.c_int), ("seed_kl", C.c_int), ("first_walker", C.c_int),
+                ("include_fixed_parameter_priors", C.c_int), ("n_lincomb", C.c_int),
+                ("lincomb_weights", C.POINTER(C.c_double)), ("lincomb_mean", C.POINTER(C.c_double)),
+                ("lincomb_std", C.POINTER(C.c_double))]
 
 
 _lib = None

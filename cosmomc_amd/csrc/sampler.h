@@ -26,8 +26,9 @@ struct Rows {
     int I97 = 0, J97 = 1, ISET = 2, FASTIX = 3, NACC = 4;
     int CYCLP = 5;      // 3 rows: All, Slow, Fast CyclicIndexRandomizer%loopix
     int BLKLP = 8;      // nblocks rows: RandDirectionProposer%loopix
-    int CYC;            // all_n + slow_n + fast_n rows: the three index permutations
     int ACCF;           // 1 if the last accept of this walker moved it (theory swap for slow steps)
+    int CYC;            // multiple of 4; all_n + slow_n + fast_n rows: the three index permutations
+                        //   (last, so an LDS image without them is the prefix [0, CYC))
     int NI;             // multiple of 4: rows are moved four at a time
 };
 
@@ -36,14 +37,14 @@ struct TabLayout {
     // int table offsets (ints)
     int blk_n, blk_nchanged, blk_changed_off, blk_map_off, blk_R_off, changed, pfi, params_used, n_int;
     // double table offsets (doubles)
-    int mapping, pmin, pmax, pmean, pstd, covinv, center, n_dbl;
+    int mapping, pmin, pmax, pmean, pstd, lin_w, lin_m, lin_s, covinv, center, n_dbl;
 };
 
 struct DevCfg {
     int W, np, n_used, nblocks, slow_n, fast_n, all_n, oversample_fast, max_blk, R_total;
     int ld;                 // row stride of sd / si / like_terms: W rounded up to 64
     double propose_scale, temperature;
-    int has_priors, test_like;
+    int has_priors, test_like, n_lin;
     Rows rows;
     TabLayout tl;
     const int *tab_i;       // [tl.n_int] (allocation padded to a multiple of 64 words)
@@ -51,6 +52,9 @@ struct DevCfg {
     double *sd;             // [ND][ld]
     int *si;                // [NI][ld]
     int stage_R;            // R rows staged in LDS (else read in place, stride W)
+    int stage_cyc;          // CYC rows + RandIndices scratch in LDS (else in place / itmp_g)
+    int stage_cov;          // test-Gaussian covinv + center tables in LDS (else read from tab_d)
+    int *itmp_g;            // [all_n][ld] RandIndices scratch when !stage_cyc
     int tq_rows;            // LDS scratch rows for the multi-wave test-Gaussian / mapping products
     int n_like;
     const double *like_terms;       // [n_like (even)][ld] -lnL of each likelihood at the trial point
@@ -74,7 +78,7 @@ struct cmbs {
     int W = 0, np = 0, n_used = 0;
     std::vector<int> params_used;
     std::string last_error;
-    cmamd::DevBuf tab_i, tab_d, sd, si, like_terms, cur_terms, ws, hist, hist_terms, mom;
+    cmamd::DevBuf tab_i, tab_d, sd, si, like_terms, cur_terms, ws, hist, hist_terms, mom, itmp_g;
     cmamd::DevBuf nuis_bufs[cmamd::MAXLIKE];
     std::vector<int> h_tab_i;
     std::vector<double> h_tab_d;

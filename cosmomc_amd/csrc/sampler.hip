@@ -138,15 +138,19 @@ __global__ void rng_init_kernel(DevCfg c, const int *ij, const int *kl)
 
 struct Tabs {   // shared tables (LDS copies)
     const int *blk_n, *blk_nchanged, *blk_changed_off, *blk_map_off, *blk_R_off, *changed, *pfi, *params_used;
-    const double *mapping, *pmin, *pmax, *pmean, *pstd, *covinv, *center;
+    const double *mapping, *pmin, *pmax, *pmean, *pstd, *lin_w, *lin_m, *lin_s, *covinv, *center;
 };
 
-__device__ Tabs make_tabs(const DevCfg &c, const int *ti, const double *td)
+// td_cov: where the test-Gaussian tables (covinv, center: the tail of the
+// double table) live -- the LDS copy, or tab_d itself when not staged
+__device__ Tabs make_tabs(const DevCfg &c, const int *ti, const double *td, const double *td_cov = nullptr)
 {
     const TabLayout &l = c.tl;
+    if (!td_cov) td_cov = td;
     return Tabs{ti + l.blk_n, ti + l.blk_nchanged, ti + l.blk_changed_off, ti + l.blk_map_off, ti + l.blk_R_off,
                 ti + l.changed, ti + l.pfi, ti + l.params_used, td + l.mapping, td + l.pmin, td + l.pmax,
-                td + l.pmean, td + l.pstd, td + l.covinv, td + l.center};
+                td + l.pmean, td + l.pstd, td + l.lin_w, td + l.lin_m, td + l.lin_s, td_cov + l.covinv,
+                td_cov + l.center};
 }
 
 struct Walker {
@@ -309,9 +313,17 @@ __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const 
     double like = main / c.temperature;
     if (c.has_priors) {                                              // GetLogPriors :111-134
         double pri = 0.0;
-        for (int i = 0; i < c.np; i++)
+        for (int i = 0; i < c.np; i++)       // std already 0 where the varying/include_fixed gate (:119) is off
             if (t.pstd[i] != 0.0) {
                 const double z = (q[i] - t.pmean[i]) / t.pstd[i];
+                pri += z * z;
+            }
+        for (int k = 0; k < c.n_lin; k++)    // linear combinations :125-131
+            if (t.lin_s[k] != 0.0) {
+                const double *wk = t.lin_w + (size_t)k * c.np;
+                double s = 0.0;
+                for (int i = 0; i < c.np; i++) s += wk[i] * q[i];
+                const double z = (s - t.lin_m[k]) / t.lin_s[k];
                 pri += z * z;
             }
         like = like + (pri / 2.0) / c.temperature;
@@ -392,14 +404,16 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     const int nlk = (c.n_like + 1) & ~1;
     // LDS carve: state doubles | like terms | vec scratch | tables(d) | state ints | itmp | tables(i)
     const int nd_st = c.stage_R ? R.ND : R.ND - R.RR;           // staged double rows
+    const int ni_st = c.stage_cyc ? R.NI : R.CYC;                // staged int rows
+    const int ntd = c.stage_cov ? c.tl.n_dbl : c.tl.covinv;      // staged double-table words
     double *sd = lds;                                            // [nd_st][NB]
     double *lk = sd + (size_t)nd_st * NB;                        // [nlk][NB]
     double *vc = lk + (size_t)nlk * NB;                          // [max_blk][NB]
     double *tq = vc + (size_t)c.max_blk * NB;                    // [tq_rows][NB] test-Gaussian row sums / block
-    double *td = tq + (size_t)c.tq_rows * NB;                    // [n_dbl rounded to 32]
-    int *si = reinterpret_cast<int *>(td + ((c.tl.n_dbl + 31) & ~31));   // [NI][NB]
-    int *it = si + (size_t)R.NI * NB;                            // [all_n][NB]
-    int *ti = it + (size_t)c.all_n * NB;                         // [n_int rounded to 64]
+    double *td = tq + (size_t)c.tq_rows * NB;                    // [ntd rounded to 32]
+    int *si = reinterpret_cast<int *>(td + ((ntd + 31) & ~31));  // [ni_st][NB]
+    int *it = si + (size_t)ni_st * NB;                           // [all_n][NB] when stage_cyc
+    int *ti = it + (size_t)(c.stage_cyc ? c.all_n : 0) * NB;     // [n_int rounded to 64]
     const bool skipR = !c.stage_R;
     // staged double row index of global row r (rotation rows dropped when not staged)
 #define SROW(r) ((skipR && (r) >= R.R) ? (r) - R.RR : (r))
@@ -416,8 +430,8 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
         dma_rows_f64(sd, 0, c.sd, 0, R.ND, W, wb, lane, wave, MH_WAVES);
     }
     dma_rows_f64(lk, 0, c.like_terms, 0, nlk, W, wb, lane, wave, MH_WAVES);
-    dma_rows_i32(si, c.si, R.NI, W, wb, lane, wave, MH_WAVES);
-    dma_words(td, c.tab_d, 2 * c.tl.n_dbl, lane, wave, MH_WAVES);
+    dma_rows_i32(si, c.si, ni_st, W, wb, lane, wave, MH_WAVES);
+    dma_words(td, c.tab_d, 2 * ntd, lane, wave, MH_WAVES);
     dma_words(ti, c.tab_i, c.tl.n_int, lane, wave, MH_WAVES);
     // per-likelihood terms of the current point, for the history (rejected walkers keep theirs)
     double ct[MAXLIKE];
@@ -436,7 +450,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     const bool par_map = PROPOSE && c.max_blk >= 4 && c.tq_rows >= 1;
     if (par_test) {
         if (act) {
-            const Tabs t0 = make_tabs(c, ti, td);
+            const Tabs t0 = make_tabs(c, ti, td, c.stage_cov ? td : c.tab_d);
             const Col<double> q{sd + (size_t)SROW(R.T) * NB + lane, NB};
             for (int i = wave; i < c.n_used; i += MH_WAVES) tq[(size_t)i * NB + lane] = test_row(c, t0, q, i);
         }
@@ -445,7 +459,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     STAMP(2);
     if (wave == 0 && act) {
 
-    const Tabs t = make_tabs(c, ti, td);
+    const Tabs t = make_tabs(c, ti, td, c.stage_cov ? td : c.tab_d);
     Walker k;
     k.r.u = Col<double>{sd + (size_t)R.U * NB + lane, NB};
     k.r.c = sd[(size_t)R.C * NB + lane];
@@ -457,10 +471,10 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     k.P = Col<double>{sd + (size_t)SROW(R.P) * NB + lane, NB};
     k.trial = Col<double>{sd + (size_t)SROW(R.T) * NB + lane, NB};
     k.vec = Col<double>{vc + lane, NB};
-    k.cyc = Col<int>{si + (size_t)R.CYC * NB + lane, NB};
+    k.cyc = c.stage_cyc ? Col<int>{si + (size_t)R.CYC * NB + lane, NB} : Col<int>{c.si + (size_t)R.CYC * W + w, c.ld};
     k.cyclp = Col<int>{si + (size_t)R.CYCLP * NB + lane, NB};
     k.blklp = Col<int>{si + (size_t)R.BLKLP * NB + lane, NB};
-    k.itmp = Col<int>{it + lane, NB};
+    k.itmp = c.stage_cyc ? Col<int>{it + lane, NB} : Col<int>{c.itmp_g + w, c.ld};
     k.fast_ix = si[(size_t)R.FASTIX * NB + lane];
     double &cur = sd[(size_t)SROW(R.L) * NB + lane];
     double &mult = sd[(size_t)SROW(R.M) * NB + lane];
@@ -521,7 +535,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     if (par_map) {   // UpdateParams' mapping product, rows spread over the waves (one thread per row, same order)
         __syncthreads();
         if (act) {
-            const Tabs t = make_tabs(c, ti, td);
+            const Tabs t = make_tabs(c, ti, td, c.stage_cov ? td : c.tab_d);
             const int b = (int)tq[lane];
             const int n = t.blk_n[b], nc = t.blk_nchanged[b];
             const double *M = t.mapping + t.blk_map_off[b];
@@ -550,7 +564,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     } else {
         stage_out(c.sd, sd, 0, 0, R.ND, W, w, lane, wave, MH_WAVES);
     }
-    stage_out(c.si, si, 0, 0, R.NI, W, w, lane, wave, MH_WAVES);
+    stage_out(c.si, si, 0, 0, ni_st, W, w, lane, wave, MH_WAVES);
     STAMP(5);
 #ifdef CMAMD_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -903,20 +917,34 @@ __global__ __launch_bounds__(256) void chain_moments_kernel(const double *means,
 
 // ------------------------------------------------------------ host side
 
-static size_t mh_lds_bytes(const cmbs *s, int stage_R) {
+static size_t mh_lds_bytes(const cmbs *s) {
     const DevCfg &d = s->dc;
-    const int nd_st = stage_R ? d.rows.ND : d.rows.ND - d.rows.RR;
-    return (size_t)(nd_st + MAXLIKE + d.max_blk + d.tq_rows) * NB * 8 + (size_t)((d.tl.n_dbl + 31) & ~31) * 8 +
-           (size_t)(d.rows.NI + d.all_n) * NB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 + 64;
+    const int nd_st = d.stage_R ? d.rows.ND : d.rows.ND - d.rows.RR;
+    const int ni_st = d.stage_cyc ? d.rows.NI : d.rows.CYC;
+    const int ntd = d.stage_cov ? d.tl.n_dbl : d.tl.covinv;
+    return (size_t)(nd_st + MAXLIKE + d.max_blk + d.tq_rows) * NB * 8 + (size_t)((ntd + 31) & ~31) * 8 +
+           (size_t)(ni_st + (d.stage_cyc ? d.all_n : 0)) * NB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 + 64;
 }
 
 static void set_mh_lds(cmbs *s) {
-    // scratch for the multi-wave products: a row per test-Gaussian row, or one
-    // row (the proposal's block) for the mapping; dropped if the image is too big
-    s->dc.tq_rows = s->dc.test_like ? s->n_used : 1;
-    if (mh_lds_bytes(s, s->dc.stage_R) > 160 * 1024) s->dc.tq_rows = 0;
-    s->mh_lds = mh_lds_bytes(s, s->dc.stage_R);
-    if (s->mh_lds > 160 * 1024) fail(CMBL_ERR_ARG, "sampler state too large for LDS (%zu bytes)", s->mh_lds);
+    // The mh_kernel LDS image: everything staged when it fits the 160 KB of a
+    // CU; otherwise, in this order, the rotation rows, the cyclic-index
+    // permutations (+ RandIndices scratch), the test-Gaussian tables and the
+    // multi-wave scratch rows stay in HBM and are read in place.
+    DevCfg &d = s->dc;
+    const size_t cap = 160 * 1024;
+    d.stage_R = d.stage_cyc = d.stage_cov = 1;
+    d.tq_rows = d.test_like ? s->n_used : 1;   // a row per test-Gaussian row, or one (the proposal's block)
+    if (mh_lds_bytes(s) > cap) d.stage_R = 0;
+    if (mh_lds_bytes(s) > cap) d.stage_cyc = 0;
+    if (mh_lds_bytes(s) > cap) d.stage_cov = 0;
+    if (mh_lds_bytes(s) > cap) d.tq_rows = 0;
+    s->mh_lds = mh_lds_bytes(s);
+    if (s->mh_lds > cap) fail(CMBL_ERR_ARG, "sampler state too large for LDS (%zu bytes)", s->mh_lds);
+    if (!d.stage_cyc && !s->itmp_g.p) {
+        s->itmp_g.alloc((size_t)std::max(1, s->all_n) * d.ld * 4);
+        d.itmp_g = s->itmp_g.as<int>();
+    }
     const int lds = (int)s->mh_lds;
     HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -1037,9 +1065,13 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     put_d(tl.pmin, cfg->pmin, np);
     put_d(tl.pmax, cfg->pmax, np);
     std::vector<double> pm(np, 0.0), ps(np, 0.0);
+    std::vector<char> varying(np, 0);
+    for (int p : s->params_used) varying[p - 1] = 1;
     bool has_pri = false;
     if (cfg->prior_mean && cfg->prior_std) {
         for (int i = 0; i < np; i++) {
+            // GetLogPriors gate, calclike.f90:119 (TBaseParameters_ReadPriors :175 reads no prior otherwise)
+            if (!varying[i] && !cfg->include_fixed_parameter_priors) continue;
             pm[i] = cfg->prior_mean[i];
             ps[i] = cfg->prior_std[i];
             has_pri |= ps[i] != 0.0;
@@ -1047,6 +1079,14 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     }
     put_d(tl.pmean, pm.data(), np);
     put_d(tl.pstd, ps.data(), np);
+    const int nlin = cfg->n_lincomb > 0 ? cfg->n_lincomb : 0;
+    if (nlin && (!cfg->lincomb_weights || !cfg->lincomb_mean || !cfg->lincomb_std))
+        fail(CMBL_ERR_ARG, "n_lincomb > 0 needs lincomb_weights, lincomb_mean and lincomb_std");
+    put_d(tl.lin_w, cfg->lincomb_weights, nlin * np);
+    put_d(tl.lin_m, cfg->lincomb_mean, nlin);
+    put_d(tl.lin_s, cfg->lincomb_std, nlin);
+    for (int k = 0; k < nlin; k++) has_pri |= cfg->lincomb_std[k] != 0.0;
+    d.n_lin = nlin;
     tl.covinv = tl.center = (int)vd.size();   // set by cmbs_set_test_gaussian
     tl.n_dbl = (int)vd.size();
     d.has_priors = has_pri;
@@ -1061,9 +1101,9 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     R.L = R.T + np;
     R.M = R.L + 1;
     R.ND = (R.M + 2) & ~1;
-    R.CYC = R.BLKLP + nb;
-    R.ACCF = R.CYC + s->all_n + s->slow_n + s->fast_n;
-    R.NI = (R.ACCF + 1 + 3) & ~3;
+    R.ACCF = R.BLKLP + nb;
+    R.CYC = (R.ACCF + 1 + 3) & ~3;
+    R.NI = (R.CYC + s->all_n + s->slow_n + s->fast_n + 3) & ~3;
     d.ld = (W + NB - 1) / NB * NB;
     s->sd.alloc((size_t)R.ND * d.ld * 8);
     s->si.alloc((size_t)R.NI * d.ld * 4);
@@ -1072,9 +1112,6 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     d.sd = s->sd.as<double>();
     d.si = s->si.as<int>();
 
-    // LDS budget: stage the rotation matrices too when everything fits
-    d.stage_R = 1;
-    if (mh_lds_bytes(s, 1) > 144 * 1024) d.stage_R = 0;
     set_mh_lds(s);
 
     // seeds
@@ -1635,7 +1672,7 @@ size_t sampler_state_bytes(const cmbs *s) {
 
 static StateHeader state_header(const cmbs *s) {
     const Rows &R = s->dc.rows;
-    return StateHeader{STATE_MAGIC, 1u, s->W, s->np, s->n_used, s->nblocks, s->all_n, s->slow_n, s->fast_n,
+    return StateHeader{STATE_MAGIC, 2u, s->W, s->np, s->n_used, s->nblocks, s->all_n, s->slow_n, s->fast_n,
                        s->R_total, R.ND, R.NI, (int)s->likes.size(), 0, s->num_drag};
 }
 
@@ -1662,7 +1699,7 @@ void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
     if (bytes < sizeof(StateHeader)) fail(CMBL_ERR_ARG, "state image too short");
     StateHeader h;
     std::memcpy(&h, buf, sizeof h);
-    if (h.magic != STATE_MAGIC || h.version != 1u) fail(CMBL_ERR_FORMAT, "not a cmbs state image");
+    if (h.magic != STATE_MAGIC || h.version != 2u) fail(CMBL_ERR_FORMAT, "not a cmbs state image");
     const StateHeader m = state_header(s);
     if (h.W != m.W || h.np != m.np || h.n_used != m.n_used || h.nblocks != m.nblocks || h.all_n != m.all_n ||
         h.slow_n != m.slow_n || h.fast_n != m.fast_n || h.R_total != m.R_total || h.ND != m.ND || h.NI != m.NI ||

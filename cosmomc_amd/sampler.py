@@ -35,7 +35,10 @@ class BatchedMCMC:
     def __init__(self, n_walkers: int, num_params: int, params_used, blocks, slow_block_max: int,
                  pmin, pmax, prior_mean=None, prior_std=None, oversample_fast: int = 1,
                  propose_scale: float = 2.4, temperature: float = 1.0, seed_ij: int = 1802,
-                 seed_kl: int = 9373, first_walker: int = 0):
+                 seed_kl: int = 9373, first_walker: int = 0, include_fixed_parameter_priors: bool = False,
+                 linear_combinations=None):
+        """linear_combinations: [(weights[num_params], mean, std), ...] priors on
+        dot(weights, P) (BaseParams%LinearCombinations, BaseParameters.f90:184-201)."""
         self.W, self.np = n_walkers, num_params
         self.params_used = list(params_used)
         self._keep = []
@@ -54,6 +57,14 @@ class BatchedMCMC:
         a, cfg.prior_mean = _da(pm); self._keep.append(a)
         a, cfg.prior_std = _da(ps); self._keep.append(a)
         cfg.seed_ij, cfg.seed_kl, cfg.first_walker = seed_ij, seed_kl, first_walker
+        cfg.include_fixed_parameter_priors = int(bool(include_fixed_parameter_priors))
+        lin = list(linear_combinations or [])
+        cfg.n_lincomb = len(lin)
+        if lin:
+            a, cfg.lincomb_weights = _da(np.array([np.asarray(l[0], dtype=np.float64) for l in lin]))
+            self._keep.append(a)
+            a, cfg.lincomb_mean = _da([float(l[1]) for l in lin]); self._keep.append(a)
+            a, cfg.lincomb_std = _da([float(l[2]) for l in lin]); self._keep.append(a)
         h = C.c_void_p()
         err = C.create_string_buffer(1024)
         rc = N.lib().cmbs_create(C.byref(cfg), C.byref(h), err, 1024)

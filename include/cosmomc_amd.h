@@ -129,6 +129,14 @@ typedef struct {
     int seed_ij, seed_kl;      /* RANMAR seeds of walker 0; walker w uses
                                   cmbs_walker_seed() (documented in DESIGN.md) */
     int first_walker;          /* global index of walker 0 (for sharding) */
+    /* GetLogPriors (calclike.f90:111-134): a Gaussian prior on parameter i counts
+     * when i is varying (in params_used) or include_fixed_parameter_priors is set
+     * (BaseParameters.f90:170-181); linear-combination priors
+     * ((dot(weights, P) - mean)/std)^2 over all num_params (:184-201), std 0 = none */
+    int include_fixed_parameter_priors;
+    int n_lincomb;
+    const double *lincomb_weights;              /* n_lincomb x num_params, row-major */
+    const double *lincomb_mean, *lincomb_std;   /* n_lincomb */
 } cmbs_config_t;
 
 /* walker w's RANMAR seeds (ij in 0..31328, kl in 0..30081) */

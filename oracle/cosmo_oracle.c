@@ -580,10 +580,18 @@ double orc_target_loglike(const orc_target_t *t, const double *P)
     double pri = 0.0;                                  /* GetLogPriors :111-134 */
     if (t->prior_std)
         for (int i = 0; i < t->num_params; i++)
-            if (t->prior_std[i] != 0.0) {
+            if ((!t->varying || t->varying[i] || t->include_fixed_parameter_priors) && t->prior_std[i] != 0.0) {
                 double z = (P[i] - t->prior_mean[i]) / t->prior_std[i];
                 pri += z * z;
             }
+    for (int k = 0; k < t->n_lincomb; k++)             /* :125-131 */
+        if (t->lincomb_std[k] != 0.0) {
+            const double *w = t->lincomb_weights + (size_t)k * t->num_params;
+            double d = 0.0;
+            for (int i = 0; i < t->num_params; i++) d += w[i] * P[i];
+            double z = (d - t->lincomb_mean[k]) / t->lincomb_std[k];
+            pri += z * z;
+        }
     pri = pri / 2.0;
     add_like_temp(&like, pri, t->temperature);
     return like;

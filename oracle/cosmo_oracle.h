@@ -88,6 +88,14 @@ typedef struct {
     /* slow-theory test model: theory = P(plik_scale_index) x plik_dl (0: off),
      * standing in for CAMB's recomputation at the trial point */
     int plik_scale_index;               /* 1-based */
+    /* GetLogPriors gate (calclike.f90:119): a Gaussian prior on parameter i
+     * counts when varying[i] (NULL: every parameter varies) or
+     * include_fixed_parameter_priors; linear-combination priors :125-131 */
+    int include_fixed_parameter_priors;
+    const int *varying;                 /* num_params flags or NULL */
+    int n_lincomb;
+    const double *lincomb_weights;      /* n_lincomb x num_params */
+    const double *lincomb_mean, *lincomb_std;
 } orc_target_t;
 
 double orc_target_loglike(const orc_target_t *t, const double *P); /* GetLogLike :136-151 */

@@ -1,10 +1,13 @@
 """ORACLE TEST INFRASTRUCTURE -- generates tests/golden/*.json from the compiled
 reference (oracle/_ref, built by `make -C oracle ref` from /root/reference).
 
-Runs only in the development container (the reference never travels to the
-GPU box).  Each fixture records the seeds that regenerate its inputs through
-cosmomc_amd.synthetic, plus the reference outputs; the committed fixtures are
-small, the inputs are rebuilt on both sides.
+Runs only in the development container: it needs /root/reference to build
+oracle/_ref.  The built oracle/_ref binaries do travel to the GPU box (they are
+git-ignored, not gpurun-ignored), where bench.py's cpu_baseline leg times
+plik_bench; nothing on the box regenerates fixtures.  Each fixture records the
+seeds that regenerate its inputs through cosmomc_amd.synthetic, plus the
+reference outputs; the committed fixtures are small, the inputs are rebuilt on
+both sides.
 
     python oracle/gen_golden.py            # all fixtures
 """
@@ -95,25 +98,50 @@ def _fmt(a):
     return " ".join(f"{x:.17e}" for x in np.ravel(a))
 
 
-# chain configurations: (name, n, blocks, slow_block_max, oversample_fast, propose_scale, fast_only, steps)
+# chain configurations: (name, n_used, blocks, slow_block_max, oversample_fast, propose_scale, fast_only, steps,
+#                        extra) with extra = {"fixed": k fixed parameters appended after the used ones,
+#                        "include_fixed": include_fixed_parameter_priors, "lincomb": number of
+#                        linear-combination priors (BaseParameters.f90:184-201)}
 CHAIN_CASES = [
     # config 1: 6-D Gaussian, test_likelihood, one (slow) block, no fast/slow split
-    ("gauss6_single_block", 6, [[1, 2, 3, 4, 5, 6]], 1, 1, 2.4, 0, 400),
+    ("gauss6_single_block", 6, [[1, 2, 3, 4, 5, 6]], 1, 1, 2.4, 0, 400, {}),
     # slow 2 + fast 3 + fast 1, oversample_fast 2, full GetProposal cycle
-    ("gauss6_blocked", 6, [[1, 2], [3, 4, 5], [6]], 1, 2, 2.4, 0, 400),
+    ("gauss6_blocked", 6, [[1, 2], [3, 4, 5], [6]], 1, 2, 2.4, 0, 400, {}),
     # fast-only steps (FastParameterSample path) with propose_scale 1.9 (batch3/common.ini)
-    ("gauss6_fast_only", 6, [[1, 2], [3, 4, 5], [6]], 1, 1, 1.9, 1, 400),
+    ("gauss6_fast_only", 6, [[1, 2], [3, 4, 5], [6]], 1, 1, 1.9, 1, 400, {}),
     # 1-D block of calPlanck-like width (sign flip RotMatrix branch, n=1)
-    ("gauss3_n1_blocks", 3, [[1], [2], [3]], 1, 3, 2.4, 0, 300),
+    ("gauss3_n1_blocks", 3, [[1], [2], [3]], 1, 3, 2.4, 0, 300, {}),
     # fast dragging (TFastDraggingSampler, fast_only = 2): slow 2 + fast 3 + fast 1, drag every 2nd step
-    ("gauss6_drag", 6, [[1, 2], [3, 4, 5], [6]], 1, 2, 2.4, 2, 240),
+    ("gauss6_drag", 6, [[1, 2], [3, 4, 5], [6]], 1, 2, 2.4, 2, 240, {}),
     # dragging every step (oversample_fast 1), one fast parameter (interp_steps 4)
-    ("gauss4_drag_every_step", 4, [[1, 2, 3], [4]], 1, 1, 2.0, 2, 200),
+    ("gauss4_drag_every_step", 4, [[1, 2, 3], [4]], 1, 1, 2.0, 2, 200, {}),
+    # BASELINE configs[3] shape: 6 slow + one 21-parameter fast block (full plik's foreground
+    # nuisance set), fast-only steps; rotations of 21x21 regenerated every 21 draws
+    ("gauss27_fast21_fast_only", 27, [list(range(1, 7)), list(range(7, 28))], 1, 1, 1.9, 1, 320,
+     {"lincomb": 1, "fixed": 1}),
+    # same parameters, full GetProposal cycle with oversample_fast 3
+    ("gauss27_fast21_os3", 27, [list(range(1, 7)), list(range(7, 28))], 1, 3, 2.4, 0, 320,
+     {"lincomb": 1}),
+    # the 21 fast parameters split 12 + 9 (block_fast_likelihood_params: two likelihoods),
+    # a linear-combination prior (batch2/plik_dx11dr2_HM_v18_TT.ini:16-17 SZComb) and fixed
+    # parameters whose priors count (include_fixed_parameter_priors = T)
+    ("gauss27_fast12_9_lincomb", 27, [list(range(1, 7)), list(range(7, 19)), list(range(19, 28))], 1, 3, 2.4, 0,
+     320, {"lincomb": 2, "fixed": 2, "include_fixed": 1}),
+    # 40 used parameters: slow 6 + semi-slow 4 + fast 21 + fast 9, oversample_fast 3,
+    # fixed-parameter priors present but not counted (include_fixed_parameter_priors = F)
+    ("gauss40_slow_fast", 40, [list(range(1, 7)), list(range(7, 11)), list(range(11, 32)), list(range(32, 41))],
+     2, 3, 2.4, 0, 300, {"lincomb": 1, "fixed": 2}),
+    # dragging with a 21-parameter fast block (interp_steps = 64)
+    ("gauss27_fast21_drag", 27, [list(range(1, 7)), list(range(7, 28))], 1, 2, 2.4, 2, 40, {"lincomb": 1}),
 ]
 
 
-def chain_problem(n: int, seed: int):
-    """SPD covariance, centre, bounds, priors for a test Gaussian chain."""
+def chain_problem(n: int, seed: int, extra=None):
+    """SPD covariance, centre, bounds, priors for a test Gaussian chain over n
+    used parameters, plus extra["fixed"] fixed parameters (appended, bounds
+    pinned at their value, each with a Gaussian prior) and extra["lincomb"]
+    linear-combination priors over all parameters."""
+    extra = extra or {}
     g = syn.gaussians(seed, n * n + 3 * n)
     A = g[:n * n].reshape(n, n)
     sig = 0.5 + np.abs(g[n * n:n * n + n])
@@ -129,7 +157,27 @@ def chain_problem(n: int, seed: int):
     pmean[-1] = center[-1] + 0.2 * sig[-1]
     pstd[-1] = 2.0 * sig[-1]
     P0 = center + 0.5 * sig * g[n * n + 2 * n:n * n + 3 * n]
-    return cov, center, pmin, pmax, pmean, pstd, P0
+    nf = extra.get("fixed", 0)
+    if nf:
+        fv = 0.3 + 0.1 * np.arange(nf)
+        center = np.concatenate([center, fv])
+        pmin = np.concatenate([pmin, fv])
+        pmax = np.concatenate([pmax, fv])
+        pmean = np.concatenate([pmean, fv + 0.05])
+        pstd = np.concatenate([pstd, 0.1 * np.ones(nf)])
+        P0 = np.concatenate([P0, fv])
+    lin = []
+    gl = syn.gaussians(seed + 99, 3 * max(1, extra.get("lincomb", 0)))
+    for k in range(extra.get("lincomb", 0)):
+        w = np.zeros(n + nf)
+        i, j = (2 * k) % n, (2 * k + 5) % n
+        w[i], w[j] = 1.0, 0.5 + 0.1 * gl[3 * k]            # e.g. SZComb = A_kSZ + 1.6 A_tSZ
+        if nf:
+            w[n] = 0.25                                       # fixed parameters enter dot_product(Comb, P)
+        mean = float(w @ np.concatenate([center[:n], center[n:]]) + 0.3 * gl[3 * k + 1])
+        std = float(1.5 + abs(gl[3 * k + 2]))
+        lin.append({"weights": w.tolist(), "mean": mean, "std": std})
+    return cov, center, pmin, pmax, pmean, pstd, P0, lin
 
 
 def gen_rng():
@@ -144,27 +192,34 @@ def gen_rng():
                 "ij": ij, "kl": kl, "ranmar": vals[:n], "gaussian1": vals[n:2 * n],
                 "randexp1": vals[2 * n:3 * n], "rand_indices": [int(v) for v in vals[3 * n:3 * n + nidx]],
                 "rotation": vals[3 * n + nidx:], "nidx": nidx, "nrot": nrot}
-        for ci, (name, n, blocks, sbm, ovs, scale, fast_only, steps) in enumerate(CHAIN_CASES):
-            cov, center, pmin, pmax, pmean, pstd, P0 = chain_problem(n, 777 + ci)
+        for ci, (name, n, blocks, sbm, ovs, scale, fast_only, steps, extra) in enumerate(CHAIN_CASES):
+            cov, center, pmin, pmax, pmean, pstd, P0, lin = chain_problem(n, 777 + ci, extra)
+            npar = len(center)
             ij, kl = 4321 + ci, 9373
             T = 1.0
-            cfg = [f"{ij} {kl} {n} {steps} {fast_only}",
+            incl = int(extra.get("include_fixed", 0))
+            used = list(range(1, n + 1))
+            cfg = [f"{ij} {kl} {npar} {n} {steps} {fast_only} {incl} {len(lin)}",
                    f"{len(blocks)} {sbm} {ovs} {scale!r} {T!r}",
+                   " ".join(str(u) for u in used),
                    " ".join(str(len(b)) for b in blocks)]
             cfg += [" ".join(str(x) for x in b) for b in blocks]
-            cfg += [_fmt(cov), _fmt(cov), _fmt(center), _fmt(pmin), _fmt(pmax), _fmt(pmean), _fmt(pstd), _fmt(P0)]
+            cfg += [_fmt(cov), _fmt(center), _fmt(pmin), _fmt(pmax), _fmt(pmean), _fmt(pstd), _fmt(P0)]
+            for lc in lin:
+                cfg += [_fmt(lc["weights"]), f"{lc['mean']!r} {lc['std']!r}"]
             lines = [x for x in run_rng("chain", "\n".join(cfg) + "\n", td) if x.strip()]
             like0 = float(lines[0])
             rows = np.array([[float(v) for v in l.split()] for l in lines[1:]])
             out["chains"][name] = {
-                "ij": ij, "kl": kl, "n": n, "blocks": blocks, "slow_block_max": sbm,
-                "oversample_fast": ovs, "propose_scale": scale, "fast_only": fast_only,
-                "temperature": T, "steps": steps, "problem_seed": 777 + ci,
+                "ij": ij, "kl": kl, "n": n, "num_params": npar, "params_used": used, "blocks": blocks,
+                "slow_block_max": sbm, "oversample_fast": ovs, "propose_scale": scale, "fast_only": fast_only,
+                "temperature": T, "steps": steps, "problem_seed": 777 + ci, "include_fixed_parameter_priors": incl,
+                "linear_combinations": lin,
                 "cov": cov.tolist(), "center": center.tolist(), "pmin": pmin.tolist(), "pmax": pmax.tolist(),
                 "prior_mean": pmean.tolist(), "prior_std": pstd.tolist(), "P0": P0.tolist(),
                 "like0": like0, "accept": rows[:, 0].astype(int).tolist(), "trial_like": rows[:, 1].tolist(),
                 "cur_like": rows[:, 2].tolist(), "P": rows[:, 3:].tolist()}
-            print(f"chain {name:22s} accept rate {rows[:, 0].mean():.3f}  final -lnL {rows[-1, 2]:.6f}")
+            print(f"chain {name:26s} accept rate {rows[:, 0].mean():.3f}  final -lnL {rows[-1, 2]:.6f}")
     with open(os.path.join(GOLDEN, "rng_sampler_ref.json"), "w") as f:
         json.dump(out, f, indent=0)
 

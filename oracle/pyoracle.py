@@ -35,7 +35,9 @@ class Target(C.Structure):
                 ("test_like", C.c_int), ("n_used", C.c_int), ("params_used", C.c_void_p),
                 ("test_covinv", C.c_void_p), ("center", C.c_void_p), ("plik", C.c_void_p),
                 ("plik_nuis_index", C.c_int), ("plik_dl", C.c_void_p), ("plik_ld_field", C.c_long),
-                ("plik_scale_index", C.c_int)]
+                ("plik_scale_index", C.c_int), ("include_fixed_parameter_priors", C.c_int),
+                ("varying", C.c_void_p), ("n_lincomb", C.c_int), ("lincomb_weights", C.c_void_p),
+                ("lincomb_mean", C.c_void_p), ("lincomb_std", C.c_void_p)]
 
 
 def lib():

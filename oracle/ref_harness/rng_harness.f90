@@ -12,12 +12,16 @@
 !                   MCMC.f90:338-452, restated inline on the reference's
 !                   BlockedProposer GetProposalSlow / GetProposalFastDelta)
 !                   BlockedProposer + Metropolis chain on the test_likelihood
-!                   Gaussian (calclike.f90:180-199) with hard bounds
-!                   (calclike.f90:97-109) and Gaussian priors (:111-134).
-!                   The three-line MetropolisAccept of MCMC.f90:119-131 and the
-!                   GetLogLike sum (calclike.f90:136-151) are restated inline
-!                   (their modules drag in every likelihood); the RNG,
-!                   proposer, Cholesky and inverse are the reference's own code.
+!                   Gaussian.  Every -lnL is the reference's own
+!                   TLikeCalculator%GetLogLike (calclike.f90:136-151: hard
+!                   bounds :97-109, TestLikelihoodFunction :180-199, Gaussian
+!                   and linear-combination priors with the
+!                   include_fixed_parameter_priors gate :111-134, temperature
+!                   :82-94) on BaseParams set from the config; num_params may
+!                   exceed num_params_used (fixed parameters).  Only the
+!                   three-line MetropolisAccept of MCMC.f90:119-131 is restated
+!                   inline; the RNG, proposer, Cholesky and inverse are the
+!                   reference's own code.
 !
 ! usage: rng_harness kat|stream|chain|gr <config.txt> <out.txt>
 program rng_harness
@@ -27,6 +31,8 @@ program rng_harness
     use MatrixUtils
     use propose
     use Samples, only: GelmanRubinEvalues
+    use BaseParameters
+    use CalcLike
     implicit none
     character(LEN=1024) :: mode, cfg, outf
     integer :: u_in, u_out, i, j, k, n, nsteps, nblocks, slow_block_max, oversample, ij, kl, nrot
@@ -43,6 +49,9 @@ program rng_harness
     real(mcp), allocatable :: cend(:), cstart(:), tend(:), tstart(:), delta(:)
     real(mcp) :: cendlike, cstartlike, elike, slike, sum_s, sum_e, frac, cintlike, intlike, mult
     integer :: num_drag, num_fast, interp, istep
+    integer :: n_used, incl_fixed, nlin
+    Type(TGenericLikeCalculator) :: Calc
+    Type(TCalculationAtParamPoint) :: Pt
 
     call get_command_argument(1, mode)
     call get_command_argument(2, cfg)
@@ -98,29 +107,49 @@ program rng_harness
         end do
     case ('chain')
         open(newunit=u_in, file=trim(cfg), status='old')
-        read(u_in, *) ij, kl, n, nsteps, fast_only
+        read(u_in, *) ij, kl, n, n_used, nsteps, fast_only, incl_fixed, nlin
         read(u_in, *) nblocks, slow_block_max, oversample, scale, temperature
+        num_params = n
+        num_params_used = n_used
+        allocate(params_used(n_used))
+        read(u_in, *) params_used
         allocate(bsize(nblocks), blocks(nblocks))
         read(u_in, *) bsize
         do i = 1, nblocks
             allocate(blocks(i)%P(bsize(i)))
             read(u_in, *) blocks(i)%P
         end do
-        allocate(cov(n,n), covinv(n,n), P(n), trial(n), center(n), pmin(n), pmax(n), pmean(n), pstd(n), X(n))
-        read(u_in, *) ((cov(i,j), j=1,n), i=1,n)
-        read(u_in, *) ((covinv(i,j), j=1,n), i=1,n)
+        allocate(cov(n_used,n_used), P(n), trial(n), center(n), pmin(n), pmax(n), pmean(n), pstd(n))
+        read(u_in, *) ((cov(i,j), j=1,n_used), i=1,n_used)
         read(u_in, *) center
         read(u_in, *) pmin
         read(u_in, *) pmax
         read(u_in, *) pmean
         read(u_in, *) pstd
         read(u_in, *) P
+        ! BaseParams as TBaseParameters_ReadParams / ReadPriors leave them (BaseParameters.f90:60-203)
+        allocate(BaseParams%PMin(n), BaseParams%PMax(n), BaseParams%center(n), BaseParams%varying(n))
+        allocate(BaseParams%GaussPriors%mean(n), BaseParams%GaussPriors%std(n))
+        BaseParams%PMin = pmin
+        BaseParams%PMax = pmax
+        BaseParams%center = center
+        BaseParams%varying = .false.
+        BaseParams%varying(params_used) = .true.
+        BaseParams%GaussPriors%mean = pmean
+        BaseParams%GaussPriors%std = pstd
+        BaseParams%include_fixed_parameter_priors = incl_fixed /= 0
+        allocate(BaseParams%LinearCombinations(nlin))
+        do k = 1, nlin
+            allocate(BaseParams%LinearCombinations(k)%Combination(n))
+            read(u_in, *) BaseParams%LinearCombinations(k)%Combination
+            read(u_in, *) BaseParams%LinearCombinations(k)%mean, BaseParams%LinearCombinations(k)%std
+        end do
         close(u_in)
-        num_params = n
-        num_params_used = n
-        allocate(params_used(n))
-        params_used = [(i, i=1,n)]
-        call Matrix_Inverse(covinv)          ! test_likelihood inverts its covariance
+        Calc%test_likelihood = .true.
+        Calc%Temperature = temperature
+        allocate(Calc%test_cov_matrix(n_used, n_used))
+        Calc%test_cov_matrix = cov       ! TestLikelihoodFunction inverts it (calclike.f90:187-195)
+        Pt%P = 0
         call initRandom(ij, kl)
         call Prop%Init(blocks, slow_block_max=slow_block_max, oversample_fast=oversample, &
             propose_scale=scale)
@@ -225,19 +254,9 @@ contains
 
     function target(Q) result(L)
         real(mcp), intent(in) :: Q(:)
-        real(mcp) :: L, main, pri
-        if (any(Q > pmax) .or. any(Q < pmin)) then
-            L = LogZero
-            return
-        end if
-        X = Q - center
-        main = dot_product(X, matmul(covinv, X))/2
-        L = main/temperature
-        pri = 0
-        do i = 1, n
-            if (pstd(i) /= 0) pri = pri + ((Q(i) - pmean(i))/pstd(i))**2
-        end do
-        L = L + (pri/2)/temperature
+        real(mcp) :: L
+        Pt%P(1:num_params) = Q(1:num_params)
+        L = Calc%GetLogLike(Pt)                 ! calclike.f90:136-151
     end function target
 
 end program rng_harness

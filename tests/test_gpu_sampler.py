@@ -18,15 +18,21 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 CHAINS = ["gauss6_single_block", "gauss6_blocked", "gauss6_fast_only", "gauss3_n1_blocks"]
+# BASELINE configs[3] shapes: 21-parameter fast blocks (rotations read in place from HBM when the
+# LDS image is full), a 12 + 9 split, 40 used parameters, fixed parameters and linear-combination priors
+WIDE_CHAINS = ["gauss27_fast21_fast_only", "gauss27_fast21_os3", "gauss27_fast12_9_lincomb", "gauss40_slow_fast"]
 
 
 def _make_sampler(ch, W):
     from cosmomc_amd.sampler import BatchedMCMC
     n = ch["n"]
-    s = BatchedMCMC(W, n, list(range(1, n + 1)), ch["blocks"], ch["slow_block_max"], ch["pmin"], ch["pmax"],
-                    ch["prior_mean"], ch["prior_std"], oversample_fast=ch["oversample_fast"],
+    npar = ch.get("num_params", n)
+    lin = [(lc["weights"], lc["mean"], lc["std"]) for lc in ch.get("linear_combinations", [])]
+    s = BatchedMCMC(W, npar, ch.get("params_used", list(range(1, n + 1))), ch["blocks"], ch["slow_block_max"],
+                    ch["pmin"], ch["pmax"], ch["prior_mean"], ch["prior_std"], oversample_fast=ch["oversample_fast"],
                     propose_scale=ch["propose_scale"], temperature=ch["temperature"], seed_ij=ch["ij"],
-                    seed_kl=ch["kl"])
+                    seed_kl=ch["kl"], include_fixed_parameter_priors=bool(ch.get("include_fixed_parameter_priors")),
+                    linear_combinations=lin)
     s.set_covariance(np.array(ch["cov"]))
     s.set_test_gaussian(np.array(ch["cov"]), np.array(ch["center"]))
     s.set_start(np.tile(np.array(ch["P0"]), (W, 1)))
@@ -50,7 +56,7 @@ def _oracle_chain(ch, ij, kl, steps):
     return np.array(Ps), np.array(likes)
 
 
-@pytest.mark.parametrize("name", CHAINS)
+@pytest.mark.parametrize("name", CHAINS + WIDE_CHAINS)
 def test_walker0_follows_reference_chain(rng_golden, name):
     ch = rng_golden["chains"][name]
     W = 8
@@ -77,6 +83,23 @@ def test_all_walkers_vs_oracle(rng_golden, name):
         ij, kl = walker_seed(ch["ij"], ch["kl"], w)
         Ps, likes = _oracle_chain(ch, ij, kl, steps)
         np.testing.assert_allclose(P[w], Ps[-1], rtol=1e-10, atol=1e-11)
+        assert like[w] == pytest.approx(likes[-1], rel=1e-9)
+
+
+@pytest.mark.parametrize("name", WIDE_CHAINS)
+def test_wide_chains_many_walkers_vs_oracle(rng_golden, name):
+    """W = 576 (nine 64-walker blocks): walkers 1, 63, 64 and W-1 follow the C
+    oracle's chains with their own seeds over every step of the golden run."""
+    from cosmomc_amd.sampler import walker_seed
+    ch = rng_golden["chains"][name]
+    W, steps = 576, ch["steps"]
+    s = _make_sampler(ch, W)
+    s.step(steps, fast_only=bool(ch["fast_only"]))
+    P, like, _, _ = s.state()
+    for w in (1, 63, 64, W - 1):
+        ij, kl = walker_seed(ch["ij"], ch["kl"], w)
+        Ps, likes = _oracle_chain(ch, ij, kl, steps)
+        np.testing.assert_allclose(P[w], Ps[-1], rtol=1e-10, atol=1e-11, err_msg=f"walker {w}")
         assert like[w] == pytest.approx(likes[-1], rel=1e-9)
 
 
@@ -249,7 +272,7 @@ def test_convergence_exchange_on_device():
     assert np.all(np.isfinite(s.state()[1]))
 
 
-@pytest.mark.parametrize("name", ["gauss6_drag", "gauss4_drag_every_step"])
+@pytest.mark.parametrize("name", ["gauss6_drag", "gauss4_drag_every_step", "gauss27_fast21_drag"])
 def test_walker0_follows_reference_dragging(rng_golden, name):
     """cmbs_step_drag: walker 0 (seeded as the reference chain) follows the
     reference TFastDraggingSampler chain step by step; every walker follows

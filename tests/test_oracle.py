@@ -52,23 +52,37 @@ def test_oracle_plik_lite_vs_reference(plik_golden, case):
 
 
 def _target(ch):
+    """orc_target_t of a golden chain: test Gaussian over params_used, bounds,
+    Gaussian priors (varying / include_fixed gate) and linear-combination priors."""
     n = ch["n"]
+    npar = ch.get("num_params", n)
+    used = np.array(ch.get("params_used", list(range(1, n + 1))), dtype=np.int32)
     keep = {k: np.ascontiguousarray(ch[k], dtype=np.float64) for k in
             ("pmin", "pmax", "prior_mean", "prior_std", "center")}
-    cov = np.array(ch["cov"])
-    keep["covinv"] = np.ascontiguousarray(np.linalg.inv(cov))
-    covinv = np.ascontiguousarray(cov.copy())
+    covinv = np.ascontiguousarray(np.array(ch["cov"], dtype=np.float64))
     assert po.lib().orc_matrix_inverse(covinv, n) == 0
     keep["covinv"] = covinv
-    keep["used"] = np.arange(1, n + 1, dtype=np.int32)
+    keep["used"] = used
+    vary = np.zeros(npar, dtype=np.int32)
+    vary[used - 1] = 1
+    keep["vary"] = vary
+    lin = ch.get("linear_combinations", [])
+    keep["lw"] = np.ascontiguousarray([lc["weights"] for lc in lin] or [[0.0]], dtype=np.float64)
+    keep["lm"] = np.ascontiguousarray([lc["mean"] for lc in lin] or [0.0], dtype=np.float64)
+    keep["ls"] = np.ascontiguousarray([lc["std"] for lc in lin] or [0.0], dtype=np.float64)
     t = po.Target()
-    t.num_params = n
+    t.num_params = npar
     t.pmin, t.pmax = keep["pmin"].ctypes.data, keep["pmax"].ctypes.data
     t.prior_mean, t.prior_std = keep["prior_mean"].ctypes.data, keep["prior_std"].ctypes.data
     t.temperature = ch["temperature"]
     t.test_like, t.n_used = 1, n
     t.params_used = keep["used"].ctypes.data
     t.test_covinv, t.center = keep["covinv"].ctypes.data, keep["center"].ctypes.data
+    t.include_fixed_parameter_priors = int(ch.get("include_fixed_parameter_priors", 0))
+    t.varying = keep["vary"].ctypes.data
+    t.n_lincomb = len(lin)
+    t.lincomb_weights, t.lincomb_mean, t.lincomb_std = (keep["lw"].ctypes.data, keep["lm"].ctypes.data,
+                                                        keep["ls"].ctypes.data)
     return t, keep
 
 
@@ -76,14 +90,19 @@ def make_oracle_proposer(ch):
     blocks = ch["blocks"]
     bn = np.array([len(b) for b in blocks], dtype=np.int32)
     bp = np.array([x for b in blocks for x in b], dtype=np.int32)
-    pu = np.arange(1, ch["n"] + 1, dtype=np.int32)
+    pu = np.array(ch.get("params_used", list(range(1, ch["n"] + 1))), dtype=np.int32)
     h = po.lib().orc_proposer_create(len(blocks), bn, bp, ch["slow_block_max"], ch["oversample_fast"],
                                      ch["propose_scale"], ch["n"], pu)
     po.lib().orc_proposer_set_covariance(h, np.ascontiguousarray(ch["cov"], dtype=np.float64))
     return h
 
 
-@pytest.mark.parametrize("name", ["gauss6_single_block", "gauss6_blocked", "gauss6_fast_only", "gauss3_n1_blocks"])
+MH_CHAINS = ["gauss6_single_block", "gauss6_blocked", "gauss6_fast_only", "gauss3_n1_blocks",
+             "gauss27_fast21_fast_only", "gauss27_fast21_os3", "gauss27_fast12_9_lincomb", "gauss40_slow_fast"]
+DRAG_CHAINS = ["gauss6_drag", "gauss4_drag_every_step", "gauss27_fast21_drag"]
+
+
+@pytest.mark.parametrize("name", MH_CHAINS)
 def test_oracle_chain_vs_reference(rng_golden, name):
     import ctypes as C
     ch = rng_golden["chains"][name]
@@ -111,7 +130,7 @@ def test_gelman_rubin_identity():
     assert po.lib().orc_gelman_rubin(cov, cov.copy(), n) == pytest.approx(1.0, rel=1e-12)
 
 
-@pytest.mark.parametrize("name", ["gauss6_drag", "gauss4_drag_every_step"])
+@pytest.mark.parametrize("name", DRAG_CHAINS)
 def test_oracle_dragging_vs_reference(rng_golden, name):
     """TFastDraggingSampler_GetNewSample (MCMC.f90:338-452) step by step."""
     import ctypes as C
