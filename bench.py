@@ -58,7 +58,7 @@ def parse():
     p.add_argument("--walkers", type=int, default=1024, help="walkers per GPU")
     p.add_argument("--groups", type=int, default=int(os.environ.get("CMBS_GROUPS", "1")),
                    help="walker groups stepped on concurrent streams (cmbs_set_groups)")
-    p.add_argument("--cpu-seconds", type=float, default=1.5, help="per-process CPU baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=2.0, help="per-round CPU baseline sample (5 rounds)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-lensing", action="store_true", help="plik_lite only (configs[2] minus lensing)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse ranks")
@@ -388,22 +388,49 @@ def config5_run(W, rank, world, tmpdir, seconds, steps=100):
     return out
 
 
-def cpu_baseline(seconds, lensing=True):
-    """The reference's own plik_lite LogLike (oracle/_ref/plik_bench, compiled
-    from /root/reference) on this host's cores, one single-threaded process per
-    core like CosmoMC's one-chain-per-MPI-rank; falls back to the C
-    restatement (oracle/liboracle.so, kind "port") when _ref is absent."""
-    from cosmomc_amd import synthetic as syn
+def host_cores():
+    """Cores this job may use: the affinity mask, capped by the cgroup CPU
+    quota (cpu.max) when one is set -- on the GPU box nproc shows the whole
+    machine while the job's share is a quota."""
     try:
-        ncores = len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except AttributeError:
-        ncores = os.cpu_count() or 1
-    P = max(1, min(16, ncores))
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds, lensing=True, repeats=5):
+    """The reference's own plik_lite (+ lensing) LogLike (oracle/_ref/plik_bench,
+    compiled from /root/reference with the reference's -O3 -ffast-math flags)
+    on this host's cores: one single-threaded process per core (CosmoMC's
+    one chain per MPI rank, OPENBLAS_NUM_THREADS=1), `repeats` timed rounds of
+    `seconds` each, median of the per-round totals.  Falls back to
+    the C restatement (oracle/liboracle.so, kind "port") when _ref is absent."""
+    from cosmomc_amd import synthetic as syn
+    P, n_aff, quota = host_cores()
     exe = os.path.join(ROOT, "oracle", "_ref", "plik_bench")
     data = syn.make_plik_lite(12345)
     Wc = 16
     th = syn.walker_theory(Wc, n_fields=3)
     cal = syn.walker_calibrations(Wc)
+    host = {"cpu_model": cpu_model(), "affinity_cores": n_aff, "cgroup_quota_cores": quota}
     with tempfile.TemporaryDirectory() as td:
         ds = data.write(td)
         if os.path.exists(exe):
@@ -418,18 +445,23 @@ def cpu_baseline(seconds, lensing=True):
             env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
             cmd = [exe, ini, os.path.join(td, "t.bin"), os.path.join(td, "n.bin"), str(Wc), "2508",
                    str(th.shape[1]), "1", str(seconds)]
-            procs = [subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env) for _ in range(P)]
-            rates = []
-            for pr in procs:
-                out, _ = pr.communicate(timeout=120)
-                n, t, _s = out.split()
-                rates.append(float(n) / float(t))
+            totals = []
+            for _ in range(repeats):
+                procs = [subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env) for _ in range(P)]
+                rates = []
+                for pr in procs:
+                    out, _ = pr.communicate(timeout=120)
+                    n, t, _s = out.split()
+                    rates.append(float(n) / float(t))
+                totals.append(float(sum(rates)))
             what = "TPlikLiteLikelihood_LogLike + CMBLikes_LogLike (lensing)" if lensing else \
                 "TPlikLiteLikelihood_LogLike"
-            return {"value": float(sum(rates)), "unit": "evals/s", "cores": P, "kind": "reference",
-                    "sample": f"reference {what} (amdflang -O2 + OpenBLAS 1 thread), "
-                              f"{P} concurrent single-thread processes x {seconds:g} s over {Wc} synthetic "
-                              f"walkers"}
+            return {"value": float(np.median(totals)), "unit": "evals/s", "cores": P, "kind": "reference",
+                    "repeats": [round(x, 1) for x in totals], "host": host,
+                    "flags": "amdflang -O3 -ffast-math -march=x86-64-v3 (reference source/Makefile:60 "
+                             "-O3 -ffast-math -march=native) + OpenBLAS 1 thread",
+                    "sample": f"reference {what}, {P} concurrent single-thread processes (one per core of "
+                              f"this job) x {seconds:g} s over {Wc} synthetic walkers, median of {repeats} rounds"}
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle as po
         orc = po.PlikLite(data)
@@ -438,7 +470,7 @@ def cpu_baseline(seconds, lensing=True):
             orc.loglike(th[n % Wc], cal[n % Wc])
             n += 1
         dt = time.perf_counter() - t0
-        return {"value": n / dt, "unit": "evals/s", "cores": 1, "kind": "port",
+        return {"value": n / dt, "unit": "evals/s", "cores": 1, "kind": "port", "host": host,
                 "sample": f"C restatement oracle/liboracle.so (plik_lite only), 1 thread, {seconds:g} s"}
 
 
