@@ -100,6 +100,7 @@ def lib():
         L.cmbs_set_trial_theory.argtypes = [vp, i, vp, ll, ll]
         L.cmbs_step_drag.argtypes = [vp, i, d, THEORY_FN, vp, vp]
         L.cmbs_step_theory.argtypes = [vp, i, THEORY_FN, vp, vp]
+        L.cmbs_refresh_theory.argtypes = [vp, THEORY_FN, vp, vp]
         L.cmbs_chain_moments.argtypes = [vp, i, i, vp, vp, vp]
         L.cmbs_enable_history.argtypes = [vp, i]
         L.cmbs_history_stats.argtypes = [vp, i, i, vp, vp, vp]

@@ -7,9 +7,23 @@ in Fortran ``'(*(E17.7))'`` (source/FileUtils.f90:75), one ``root_N.txt`` per
 chain, plus ``root.paramnames`` and ``root.ranges``.
 
 Here every walker is a chain: the sampler's history ring holds each walker's
-current point and -lnL after every step (``cmbs_history_host``); runs of
-identical consecutive points are the reference's weighted rows.  A run that is
-still open at the end of a block stays pending until it closes (or ``close``).
+current point and -lnL after every step (``cmbs_history_host``); a run of
+identical consecutive points is one stay, its length the multiplicity ``mult``
+that MoveDone passes on when the chain moves off it.  A run still open at the
+end of a block stays pending until the chain leaves the point; like the
+reference, the point a chain sits at when the run ends is never written.
+
+MoveDone / AddNewWeightedPoint semantics (MCMC.f90:166-190,
+SampleCollector.f90:82-111):
+  * ``burn_in`` (MCMC.f90:39, default 2, ini ``burn_in``): a stay is written
+    only if num_accept > burn_in when the chain leaves it -- the first
+    burn_in + 1 stays are dropped;
+  * ``thin`` (the thin_fac MoveDone passes: oversample_fast for
+    TMetropolisSampler_GetNewSample :290, 1 for FastParameterSample and the
+    dragging sampler :327, :440): acc += mult; when acc >= thin (or thin = 1)
+    the row is written with weight acc/thin and acc = mod(acc, thin);
+  * stays at logZero are not written; MaxLike / MaxLikeParams track the best
+    point a chain has moved off (:182-185).
 
 With ``likelihoods`` given, rows carry the reference's likelihood-derived
 columns (AddOutputLikelihoodParams / addLikelihoodDerivedParams,
@@ -24,6 +38,8 @@ import math
 import os
 
 import numpy as np
+
+LOGZERO = 1e30            # settings.f90:114
 
 
 def fortran_e(x: float, w: int = 17, d: int = 7) -> str:
@@ -51,9 +67,10 @@ class ChainWriter:
     ranges: list of (min, max) or None."""
 
     def __init__(self, root: str, names, labels=None, ranges=None, walkers=None, first_chain: int = 1,
-                 likelihoods=None):
+                 likelihoods=None, burn_in: int = 2, thin: int = 1):
         """likelihoods: one (tag, type, name, version) per sampler likelihood,
-        in add_likelihood order, to add the chi2_* columns."""
+        in add_likelihood order, to add the chi2_* columns.  burn_in / thin as
+        TChainSampler%burn_in and MoveDone's thin_fac (module docstring)."""
         self.root = root
         self.names = list(names)
         self.labels = list(labels) if labels is not None else list(names)
@@ -63,6 +80,10 @@ class ChainWriter:
         self.likelihoods = [tuple(x) for x in likelihoods] if likelihoods else []
         self.pending = {}                          # walker -> [point values (like, P..., chi2...), count]
         self.next_step = None
+        self.burn_in, self.thin = int(burn_in), max(1, int(thin))
+        self.num_accept = {}                       # walker -> stays left so far (MoveDone's num_accept)
+        self.acc = {}                              # walker -> AddNewWeightedPoint acc
+        self.max_like = {}                         # walker -> (MaxLike, point values)
         d = os.path.dirname(root)
         if d:
             os.makedirs(d, exist_ok=True)
@@ -113,8 +134,23 @@ class ChainWriter:
     def _file(self, w):
         return f"{self.root}_{w + self.first_chain}.txt"
 
-    def _emit(self, fh, point, count):
-        fh.write("".join(fortran_e(v) for v in [float(count), point[0], *point[1:]]) + "\n")
+    def _emit(self, fh, point, weight):
+        fh.write("".join(fortran_e(v) for v in [float(weight), point[0], *point[1:]]) + "\n")
+
+    def _move_done(self, fh, w, point, mult):
+        """The chain leaves ``point`` after ``mult`` steps there (MoveDone with accpt)."""
+        like = float(point[0])
+        nacc = self.num_accept.get(w, 0)
+        if like != LOGZERO and nacc > self.burn_in:               # MCMC.f90:177
+            acc = self.acc.get(w, 0.0) + mult                      # SampleCollector.f90:97-104
+            if acc >= self.thin or self.thin == 1:
+                self._emit(fh, point, acc / self.thin)
+                acc = math.fmod(acc, float(self.thin))
+            self.acc[w] = acc
+        self.num_accept[w] = nacc + 1
+        best = self.max_like.get(w)
+        if best is None or like < best[0]:                        # :182-185
+            self.max_like[w] = (like, point.copy())
 
     def add_rows(self, rows, terms=None):
         """rows: [steps, n_used + 1, W] history block (params_used..., CurLike);
@@ -136,7 +172,7 @@ class ChainWriter:
                         cur[1] += 1
                     else:
                         if cur is not None:
-                            self._emit(fh, cur[0], cur[1])
+                            self._move_done(fh, w, cur[0], cur[1])
                         cur = [p.copy(), 1]
                 self.pending[w] = cur
 
@@ -153,29 +189,43 @@ class ChainWriter:
             self.add_rows(sampler.history_host(first, count), terms)
         self.next_step = first + max(count, 0)
 
-    def checkpoint_state(self) -> dict:
+    def _walkers(self, W):
+        return list(range(W)) if self.walkers is None else list(self.walkers)
+
+    def checkpoint_state(self, W: int) -> dict:
         """What a resume needs: the open weighted rows, the next history step
-        and every chain file's length (rows written after the checkpoint are
-        cut off on resume, so the files continue as if never interrupted)."""
-        walkers = self.pending.keys()
+        and every chain file's length -- for every walker of the W-walker
+        sampler, written or not -- so rows written after the checkpoint are cut
+        off on resume and the files continue as if never interrupted."""
         return {"pending": {str(w): [np.asarray(c[0]).tolist(), int(c[1])]
                             for w, c in self.pending.items() if c is not None},
                 "next_step": self.next_step,
+                "num_accept": {str(w): n for w, n in self.num_accept.items()},
+                "acc": {str(w): a for w, a in self.acc.items()},
+                "max_like": {str(w): [b[0], np.asarray(b[1]).tolist()] for w, b in self.max_like.items()},
                 "sizes": {str(w): (os.path.getsize(self._file(w)) if os.path.exists(self._file(w)) else 0)
-                          for w in walkers}}
+                          for w in self._walkers(W)}}
 
-    def restore(self, state: dict):
-        for w, n in state.get("sizes", {}).items():
-            f = self._file(int(w))
+    def restore(self, state: dict, W: int):
+        sizes = state.get("sizes", {})
+        for w in self._walkers(W):
+            n = int(sizes.get(str(w), 0))
+            f = self._file(w)
             if os.path.exists(f) and os.path.getsize(f) > n:
                 with open(f, "r+b") as fh:
                     fh.truncate(n)
         self.pending = {int(w): [np.asarray(p, dtype=np.float64), c] for w, (p, c) in state["pending"].items()}
         self.next_step = state.get("next_step")
+        self.num_accept = {int(w): int(n) for w, n in state.get("num_accept", {}).items()}
+        self.acc = {int(w): float(a) for w, a in state.get("acc", {}).items()}
+        self.max_like = {int(w): (float(b[0]), np.asarray(b[1], dtype=np.float64))
+                         for w, b in state.get("max_like", {}).items()}
+
+    def max_like_params(self, w):
+        """(MaxLike, [like, P...]) of walker w: the best point it has moved off."""
+        return self.max_like.get(w)
 
     def close(self):
-        for w, cur in self.pending.items():
-            if cur is not None:
-                with open(self._file(w), "a") as fh:
-                    self._emit(fh, cur[0], cur[1])
+        """End of the run: the points the chains sit at are not written
+        (MoveDone writes a point only when the chain leaves it)."""
         self.pending = {}

@@ -41,7 +41,7 @@ def write_checkpoint(root: str, sampler, propose_cov, chains=None, exchange=None
             "propose_cov": np.asarray(propose_cov, dtype=np.float64).tolist(),
             "collector": collector or {},
             "flukecheck": bool(exchange.flukecheck) if exchange is not None else False,
-            "chains": chains.checkpoint_state() if chains is not None else None}
+            "chains": chains.checkpoint_state(sampler.W) if chains is not None else None}
     hist = b""
     if history and getattr(sampler, "_hist_cap", 0):
         count = sampler.history_count()
@@ -63,9 +63,12 @@ def write_checkpoint(root: str, sampler, propose_cov, chains=None, exchange=None
     return root + ".chk"
 
 
-def read_checkpoint(root: str, sampler, chains=None, exchange=None) -> dict:
+def read_checkpoint(root: str, sampler, chains=None, exchange=None, theory_fn=None) -> dict:
     """Resume ``sampler`` (same configuration and likelihoods as the run that
-    wrote the file) from ``root.chk``; returns the ``collector`` dict."""
+    wrote the file) from ``root.chk``; returns the ``collector`` dict.
+    theory_fn: when the run moved slow parameters (step_theory / step_drag),
+    the theory at the restored points is recomputed with it
+    (BatchedMCMC.refresh_theory); without it stepping fails loudly."""
     with open(root + ".chk", "rb") as f:
         data = f.read()
     if len(data) < 8:
@@ -97,10 +100,12 @@ def read_checkpoint(root: str, sampler, chains=None, exchange=None) -> dict:
             keep = min(h["count"], sampler._hist_cap)
             sampler.history_restore(h["first"] + h["count"] - keep, rows[h["count"] - keep:],
                                     None if terms is None else terms[h["count"] - keep:])
-        else:
-            sampler.history_restore(h["first"], rows.reshape(0, len(sampler.params_used) + 1, sampler.W))
+        else:                                   # checkpoint taken before the first recorded step
+            sampler.history_restore(h["first"], np.empty((0, len(sampler.params_used) + 1, sampler.W)))
     if chains is not None and meta.get("chains") is not None:
-        chains.restore(meta["chains"])
+        chains.restore(meta["chains"], sampler.W)
     if exchange is not None:
         exchange.flukecheck = meta["flukecheck"]
+    if theory_fn is not None:
+        sampler.refresh_theory(theory_fn)
     return meta["collector"]

@@ -265,6 +265,12 @@ int cmbs_step_theory(cmbs_t *s, int n_steps, cmbs_theory_fn theory_fn, void *use
                    [&] { cmamd::sampler_step_theory(s, n_steps, theory_fn, user, (hipStream_t)stream); });
 }
 
+int cmbs_refresh_theory(cmbs_t *s, cmbs_theory_fn theory_fn, void *user, void *stream) {
+    if (!s) return CMBL_ERR_ARG;
+    return guarded(&s->last_error,
+                   [&] { cmamd::sampler_refresh_theory(s, theory_fn, user, (hipStream_t)stream); });
+}
+
 int cmbs_set_groups(cmbs_t *s, int n_groups) {
     if (!s) return CMBL_ERR_ARG;
     return guarded(&s->last_error, [&] { cmamd::sampler_set_groups(s, n_groups); });

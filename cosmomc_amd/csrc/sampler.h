@@ -104,6 +104,10 @@ struct cmbs {
     struct EndTheory { double *dl = nullptr; long long ld_field = 0, ld_walker = 0; };
     EndTheory end_theory[cmamd::MAXLIKE];
     long long num_drag = 0;
+    // the sampler swapped accepted trial theories into the walkers' theory rows
+    // (cmbs_step_theory / cmbs_step_drag); after a resume those rows must be
+    // recomputed at the restored points (cmbs_refresh_theory) before stepping
+    bool theory_moved = false, theory_stale = false;
     // likelihoods of one step run concurrently: likelihood i > 0 on its own
     // stream (forked from / joined to the caller's) with its own workspace
     hipStream_t like_streams[cmamd::MAXLIKE] = {};
@@ -130,4 +134,5 @@ void sampler_history_host(cmbs *s, int first, int count, double *out);
 void sampler_set_trial_theory(cmbs *s, int like_index, double *dl_end, long long ld_field, long long ld_walker);
 void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_fn fn, void *user, hipStream_t stream);
 void sampler_step_theory(cmbs *s, int n_steps, cmbs_theory_fn fn, void *user, hipStream_t stream);
+void sampler_refresh_theory(cmbs *s, cmbs_theory_fn fn, void *user, hipStream_t stream);
 }

@@ -1329,8 +1329,15 @@ void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream) {
     s->started = true;
 }
 
+static void check_theory_fresh(const cmbs *s) {
+    if (s->theory_stale)
+        fail(CMBL_ERR_ARG, "resumed from a state image whose walkers moved their slow parameters: recompute the "
+                           "theory at the restored points with cmbs_refresh_theory before stepping");
+}
+
 void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (!s->started) fail(CMBL_ERR_ARG, "cmbs_set_start must be called before cmbs_step");
+    check_theory_fresh(s);
     if (fast_only && s->fast_n == 0) fail(CMBL_ERR_ARG, "no fast parameters");
     if (!fast_only && s->slow_n > 0 && !s->likes.empty())
         fail(CMBL_ERR_ARG, "slow proposals need the theory at the trial point: use cmbs_step_theory");
@@ -1397,6 +1404,7 @@ static void eval_likes_drag(cmbs *s, int set, hipStream_t stream) {
 void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_fn fn, void *user,
                        hipStream_t stream) {
     if (!s->started) fail(CMBL_ERR_ARG, "cmbs_set_start must be called before cmbs_step_drag");
+    check_theory_fresh(s);
     if (n_steps <= 0) return;
     if (s->fast_n == 0 || s->slow_n == 0) {   // MCMC.f90:351-354: plain Metropolis
         sampler_step(s, n_steps, 0, stream);
@@ -1461,6 +1469,7 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
             });
             HIP_CHECK(hipGetLastError());
         }
+        s->theory_moved = s->theory_moved || nl > 0;
         for (int i = 0; i < nl; i++) {               // accepted drags keep the end theory
             const auto &e = s->end_theory[i];
             const auto &l = s->likes[i];
@@ -1481,6 +1490,7 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
 // take the trial theory as their own
 static void swap_accepted_theory(cmbs *s, hipStream_t stream) {
     const int *flag = s->dc.si + (size_t)s->dc.rows.ACCF * s->dc.ld;
+    s->theory_moved = true;
     for (size_t i = 0; i < s->likes.size(); i++) {
         const auto &e = s->end_theory[i];
         const auto &l = s->likes[i];
@@ -1493,6 +1503,7 @@ static void swap_accepted_theory(cmbs *s, hipStream_t stream) {
 
 void sampler_step_theory(cmbs *s, int n_steps, cmbs_theory_fn fn, void *user, hipStream_t stream) {
     if (!s->started) fail(CMBL_ERR_ARG, "cmbs_set_start must be called before cmbs_step_theory");
+    check_theory_fresh(s);
     if (n_steps <= 0) return;
     if (s->likes.empty()) {
         sampler_step(s, n_steps, 0, stream);
@@ -1517,6 +1528,38 @@ void sampler_step_theory(cmbs *s, int n_steps, cmbs_theory_fn fn, void *user, hi
     }
     launch_mh(s, true, false, 0, next_hist(s), stream, 0, s->W);
     swap_accepted_theory(s, stream);
+}
+
+// After a resume: the theory at every walker's current point (rows P) from the
+// caller's theory function, copied into each likelihood's walker theory rows;
+// the restored CurLike / terms are then checked against the likelihoods
+// re-evaluated there (the reference recomputes theory at the restart point
+// too, GeneralSetup.f90:123-131).
+__global__ void copy_theory_rows(int W, const double *src, long long src_ld, double *dst, long long dst_ld, long long n)
+{
+    const int w = blockIdx.y;
+    if (w >= W) return;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        dst[(long long)w * dst_ld + i] = src[(long long)w * src_ld + i];
+}
+
+void sampler_refresh_theory(cmbs *s, cmbs_theory_fn fn, void *user, hipStream_t stream) {
+    if (!s->started) fail(CMBL_ERR_ARG, "no chain state: cmbs_set_start or cmbs_load_state first");
+    if (!fn) fail(CMBL_ERR_ARG, "cmbs_refresh_theory needs a theory function");
+    for (size_t i = 0; i < s->likes.size(); i++) {
+        if (!s->end_theory[i].dl) fail(CMBL_ERR_ARG, "likelihood %zu has no trial-theory buffer", i);
+        if (s->likes[i].ld_walker == 0) fail(CMBL_ERR_ARG, "per-walker theory rows needed (ld_walker > 0)");
+    }
+    const double *Pcur = s->dc.sd + (size_t)s->dc.rows.P * s->dc.ld;
+    if (fn(user, s->W, Pcur, (long long)s->dc.ld, stream) != 0) fail(CMBL_ERR_ARG, "theory function failed");
+    for (size_t i = 0; i < s->likes.size(); i++) {
+        const auto &e = s->end_theory[i];
+        const auto &l = s->likes[i];
+        hipLaunchKernelGGL(copy_theory_rows, dim3(16, s->W), dim3(256), 0, stream, s->W, e.dl, e.ld_walker,
+                           const_cast<double *>(l.dl), l.ld_walker, std::min(e.ld_walker, l.ld_walker));
+        HIP_CHECK(hipGetLastError());
+    }
+    s->theory_stale = false;
 }
 
 void sampler_set_groups(cmbs *s, int n_groups) {
@@ -1660,7 +1703,7 @@ void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, 
 // (cmbs_set_covariance before cmbs_load_state).
 struct StateHeader {
     unsigned magic, version;
-    int W, np, n_used, nblocks, all_n, slow_n, fast_n, R_total, ND, NI, n_like, pad;
+    int W, np, n_used, nblocks, all_n, slow_n, fast_n, R_total, ND, NI, n_like, theory_moved;
     long long num_drag;
 };
 static constexpr unsigned STATE_MAGIC = 0x53424d43u;   // "CMBS"
@@ -1673,7 +1716,7 @@ size_t sampler_state_bytes(const cmbs *s) {
 static StateHeader state_header(const cmbs *s) {
     const Rows &R = s->dc.rows;
     return StateHeader{STATE_MAGIC, 2u, s->W, s->np, s->n_used, s->nblocks, s->all_n, s->slow_n, s->fast_n,
-                       s->R_total, R.ND, R.NI, (int)s->likes.size(), 0, s->num_drag};
+                       s->R_total, R.ND, R.NI, (int)s->likes.size(), s->theory_moved ? 1 : 0, s->num_drag};
 }
 
 void sampler_save_state(cmbs *s, void *buf, size_t bytes) {
@@ -1719,6 +1762,8 @@ void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
     if (!s->likes.empty())
         HIP_CHECK(hipMemcpy2D(s->dc.cur_terms, ld * 8, p, W * 8, W * 8, s->likes.size(), hipMemcpyHostToDevice));
     s->num_drag = h.num_drag;
+    s->theory_moved = h.theory_moved != 0;
+    s->theory_stale = s->theory_moved && !s->likes.empty();
     s->started = true;
 }
 

@@ -148,6 +148,12 @@ class GPUEvaluator:
         self.theory_fn = theory_fn
         self.W = sampler.W
 
+    def prior_cut(self, P: np.ndarray) -> np.ndarray:
+        """True for rows outside the new run's hard bounds: CheckPriorCuts
+        (calclike.f90:320-331) = GetLogLikeBounds (:97-109); the cosmology
+        parameterization's NonBaseParameterPriors term is out of scope."""
+        return np.any((P > self.s.pmax[None, :]) | (P < self.s.pmin[None, :]), axis=1)
+
     def __call__(self, P: np.ndarray) -> np.ndarray:
         n = P.shape[0]
         out = np.empty(n)
@@ -162,6 +168,11 @@ class GPUEvaluator:
             _, like, _, _ = self.s.state()
             out[b0:b0 + m] = like[:m]
         return out
+
+
+def nint(x: float) -> int:
+    """Fortran NINT: round half away from zero (Python's round is half-to-even)."""
+    return int(math.copysign(math.floor(abs(x) + 0.5), x))
 
 
 class ImportanceSampler:
@@ -183,7 +194,7 @@ class ImportanceSampler:
         data = read_chain_rows(path)
         skip = self.s.redo_skip
         if skip < 1:                                   # a fraction of the lines (:146-148)
-            skip = round(data.shape[0] * skip)
+            skip = nint(data.shape[0] * skip)
         num = np.arange(1, data.shape[0] + 1)
         keep = ~((skip >= 1) & (num <= skip))          # num <= redo_skip: cycle (:245)
         data = data[keep]
@@ -196,7 +207,7 @@ class ImportanceSampler:
                 raise ValueError("redo_thin can only be used with chains with integer weights")
             acc, sel, newm = 0, [], []
             for k, m in enumerate(mult):
-                acc += int(round(m))
+                acc += nint(m)
                 if acc >= self.s.redo_thin:
                     newm.append(acc // self.s.redo_thin)
                     acc = acc % self.s.redo_thin
@@ -209,6 +220,12 @@ class ImportanceSampler:
         """Importance-sample the chain file ``in_path``; writes out_root.txt
         (GetDist rows, E17.7) when out_root is given."""
         mult0, like, P = self.read(in_path)
+        cut = getattr(self.evaluate, "prior_cut", None)
+        if self.s.redo_likelihoods and cut is not None:
+            # rows outside the new prior bounds are skipped before anything is
+            # counted (ImportanceSampling.f90:296-302)
+            keep = ~cut(P)
+            mult0, like, P = mult0[keep], like[keep], P[keep]
         truelike_all = self.evaluate(P) if self.s.redo_likelihoods else like.copy()
         offset = self.s.redo_likeoffset
         redo_loop = 1

@@ -41,6 +41,8 @@ class BatchedMCMC:
         dot(weights, P) (BaseParams%LinearCombinations, BaseParameters.f90:184-201)."""
         self.W, self.np = n_walkers, num_params
         self.params_used = list(params_used)
+        self.pmin = np.array(pmin, dtype=np.float64)
+        self.pmax = np.array(pmax, dtype=np.float64)
         self._keep = []
         cfg = N.CmbsConfig()
         cfg.n_walkers, cfg.num_params, cfg.n_used = n_walkers, num_params, len(self.params_used)
@@ -151,6 +153,15 @@ class BatchedMCMC:
             stream = N.current_stream_ptr()
         cb = self._theory_cb(theory_fn)
         self._check(N.lib().cmbs_step_drag(self._h, n_steps, dragging_steps, cb, None, stream))
+
+    def refresh_theory(self, theory_fn, stream=None):
+        """After load_state of a run that moved slow parameters: theory_fn(P
+        [num_params, W]) fills the trial-theory buffers at the current points,
+        which become the walkers' theory (cmbs_refresh_theory)."""
+        if stream is None:
+            stream = N.current_stream_ptr()
+        cb = self._theory_cb(theory_fn)
+        self._check(N.lib().cmbs_refresh_theory(self._h, cb, None, stream))
 
     def enable_history(self, capacity: int):
         self._check(N.lib().cmbs_enable_history(self._h, capacity))

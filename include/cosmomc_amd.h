@@ -200,6 +200,16 @@ int  cmbs_step_drag(cmbs_t *s, int n_steps, double dragging_steps, cmbs_theory_f
  * slow proposals when data likelihoods are registered. */
 int  cmbs_step_theory(cmbs_t *s, int n_steps, cmbs_theory_fn theory_fn, void *user, void *stream);
 
+/* After cmbs_load_state of an image whose walkers moved their slow parameters
+ * (cmbs_step_theory / cmbs_step_drag ran before the checkpoint), the walker
+ * theory rows given to cmbs_add_likelihood hold whatever the new process put
+ * there: every cmbs_step* call fails until this refreshes them.  theory_fn is
+ * called once with the current points P [num_params][ld] and fills every
+ * trial-theory buffer (cmbs_set_trial_theory), which is then copied into the
+ * walkers' theory rows.  The reference likewise recomputes the theory at the
+ * restart point (GeneralSetup.f90:123-131). */
+int  cmbs_refresh_theory(cmbs_t *s, cmbs_theory_fn theory_fn, void *user, void *stream);
+
 /* Execution tuning (no reference counterpart; results are unchanged): split the
  * walkers into n_groups 64-aligned slices, each stepped on an internal stream
  * forked from / joined to the caller's, so the Metropolis kernel of one slice

@@ -75,15 +75,16 @@ def test_chain_files_cut_back_to_checkpoint(tmp_path):
     rows = np.zeros((4, 2, 2))
     rows[:, 0, :] = np.array([[1.0, 5.0], [1.0, 5.0], [2.0, 6.0], [3.0, 6.0]])
     rows[:, 1, :] = 10.0
-    cw = ChainWriter(root, ["a"])
+    cw = ChainWriter(root, ["a"], burn_in=-1)
     cw.add_rows(rows)
-    st = cw.checkpoint_state()
+    st = cw.checkpoint_state(2)
     before = {w: open(f"{root}_{w + 1}.txt").read() for w in range(2)}
     cw.add_rows(rows + 1.0)                       # rows written after the checkpoint
-    cw2 = ChainWriter(root, ["a"])
-    cw2.restore(st)
+    cw2 = ChainWriter(root, ["a"], burn_in=-1)
+    cw2.restore(st, 2)
     assert {w: open(f"{root}_{w + 1}.txt").read() for w in range(2)} == before
     assert cw2.pending[0][1] == 1 and cw2.pending[1][1] == 2     # open runs carried over
+    cw2.add_rows(rows[:1] + 7.0)                  # both walkers move off their open points
     cw2.close()
     c1 = np.loadtxt(f"{root}_2.txt", ndmin=2)
     np.testing.assert_array_equal(c1[:, 0], [2, 2])

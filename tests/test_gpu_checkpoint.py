@@ -166,3 +166,88 @@ def test_resume_two_likelihoods(cmbl_golden, refdata, tmp_path):
     _same_state(a, b)
     np.testing.assert_array_equal(a.history_terms(25, 5), b.history_terms(25, 5))
     assert a.history_terms(29, 1).shape == (1, 2, W)
+
+
+def test_checkpoint_before_first_step(rng_golden, tmp_path):
+    """A checkpoint written right after set_start (empty history, no chain
+    rows yet) resumes: the history ring, chain files and chains continue as in
+    the uninterrupted run; rows a crashed run wrote after the checkpoint are cut."""
+    from cosmomc_amd.chains import ChainWriter
+    from cosmomc_amd.checkpoint import read_checkpoint, write_checkpoint
+    ch = rng_golden["chains"]["gauss6_blocked"]
+    W = 64
+
+    def sampler():
+        s = _gauss_sampler(ch, W)
+        s.enable_history(64)
+        return s
+    ref = sampler()
+    ref.set_covariance(np.array(ch["cov"]))
+    ref.set_start(np.tile(np.array(ch["P0"]), (W, 1)))
+    cw = ChainWriter(str(tmp_path / "ref"), [f"p{i}" for i in range(6)])
+    ref.step(30)
+    cw.append(ref)
+    cw.close()
+    a = sampler()
+    a.set_covariance(np.array(ch["cov"]))
+    a.set_start(np.tile(np.array(ch["P0"]), (W, 1)))
+    cwa = ChainWriter(str(tmp_path / "run"), [f"p{i}" for i in range(6)])
+    root = str(tmp_path / "run")
+    write_checkpoint(root, a, np.array(ch["cov"]), chains=cwa)
+    a.step(20)
+    cwa.append(a)                                     # the crashed run's rows
+    b = sampler()
+    cwb = ChainWriter(str(tmp_path / "run"), [f"p{i}" for i in range(6)])
+    read_checkpoint(root, b, chains=cwb)
+    assert b.history_count() == 0
+    b.step(30)
+    cwb.append(b)
+    cwb.close()
+    _same_state(ref, b)
+    for w in range(W):
+        assert (tmp_path / f"run_{w + 1}.txt").read_bytes() == (tmp_path / f"ref_{w + 1}.txt").read_bytes()
+
+
+def test_resume_slow_steps_refreshes_theory(tmp_path):
+    """Full GetNewSample steps with theory recomputed at trial points (slow
+    amplitude A, theory = A x base): after a resume in a fresh sampler whose
+    theory rows hold the base theory, stepping fails until refresh_theory has
+    recomputed the theory at the restored points; then every chain continues
+    exactly as in the uninterrupted run."""
+    from cosmomc_amd._native import NativeError
+    from cosmomc_amd.checkpoint import read_checkpoint, write_checkpoint
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    data = syn.make_plik_lite(12345)
+    like = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    like.nuisance_indices = [2]
+    W = 64
+    base = torch.tensor(syn.base_theory(2508)[:3], device="cuda")
+    cov = np.diag([0.002 ** 2, 0.0025 ** 2])
+
+    def sampler():
+        s = BatchedMCMC(W, 2, [1, 2], [[1], [2]], 1, [0.9, 0.9], [1.1, 1.1], [0.0, 1.0], [0.0, 0.0025],
+                        oversample_fast=2, seed_ij=81, seed_kl=82)
+        theory = base.unsqueeze(0).repeat(W, 1, 1).contiguous()
+        trial = torch.empty_like(theory)
+        s.add_likelihood(like, theory)
+        s.set_trial_theory(0, trial)
+        s.set_covariance(cov)
+
+        def theory_fn(P):
+            trial.copy_(base.unsqueeze(0) * P[0].reshape(-1, 1, 1))
+        return s, theory, theory_fn
+    a, th_a, fn_a = sampler()
+    a.set_start(np.tile([1.0, 1.0], (W, 1)))
+    a.step_theory(20, theory_fn=fn_a)
+    root = str(tmp_path / "slow")
+    write_checkpoint(root, a, cov)
+    a.step_theory(20, theory_fn=fn_a)
+    b, th_b, fn_b = sampler()
+    read_checkpoint(root, b)
+    with pytest.raises(NativeError, match="refresh"):
+        b.step_theory(1, theory_fn=fn_b)
+    b.refresh_theory(fn_b)
+    b.step_theory(20, theory_fn=fn_b)
+    _same_state(a, b)
+    assert torch.equal(th_a, th_b)

@@ -71,3 +71,5 @@ def test_importance_plik_theory_batches(tmp_path, temperature):
     np.testing.assert_allclose(got_t, tl[keep], rtol=1e-9)
     np.testing.assert_allclose(got_m, (chain[:, 0] * w)[keep], rtol=1e-8)
     assert r.mult_ratio == pytest.approx(w.sum(), rel=1e-8)
+    assert r.num_used == n - 1                        # the out-of-bounds row is skipped (CheckPriorCuts)
+    assert r.weight_min == pytest.approx(w[keep].min(), rel=1e-8)

@@ -361,9 +361,10 @@ def test_history_terms_and_chi2_chain_files(tmp_path):
     s.add_likelihood(like, dl)
     s.enable_history(steps)
     s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
-    cw = ChainWriter(str(tmp_path / "run"), ["calPlanck"], likelihoods=[like.description()])
+    cw = ChainWriter(str(tmp_path / "run"), ["calPlanck"], likelihoods=[like.description()], burn_in=-1)
     s.step(steps, fast_only=True)
     cw.append(s)
+    open_runs = {w: c[1] for w, c in cw.pending.items()}
     cw.close()
     hist = s.history_host(0, steps)
     terms = s.history_terms(0, steps)
@@ -374,7 +375,7 @@ def test_history_terms_and_chi2_chain_files(tmp_path):
             assert terms[k, 0, w] == pytest.approx(orc.loglike(th[w], cal), rel=1e-9)
             assert hist[k, 1, w] == pytest.approx(terms[k, 0, w] + 0.5 * ((cal - 1.0) / 0.0025) ** 2, rel=1e-12)
         c = np.loadtxt(tmp_path / f"run_{w + 1}.txt", ndmin=2)
-        assert c[:, 0].sum() == steps, (w, c[:, :3], hist[:, 0, w])
+        assert c[:, 0].sum() + open_runs[w] == steps, (w, c[:, :3], hist[:, 0, w])
         # chi2_prior; the file holds calPlanck to 7 digits (1e-6), so compare to 1e-3
         np.testing.assert_allclose(c[:, 4], ((c[:, 2] - 1.0) / 0.0025) ** 2, rtol=0, atol=1e-3)
         np.testing.assert_allclose(c[:, 3] / 2 + c[:, 4] / 2, c[:, 1], rtol=1e-6)                 # chi2s add up
@@ -452,15 +453,17 @@ def test_chain_files_from_history(tmp_path):
     s.set_test_gaussian(np.array([[1.0, 0.3], [0.3, 2.0]]), np.zeros(2))
     s.set_start(np.zeros((W, n)))
     s.enable_history(40)
-    cw = ChainWriter(str(tmp_path / "run"), ["x", "y"])
+    cw = ChainWriter(str(tmp_path / "run"), ["x", "y"], burn_in=-1)
     for _ in range(3):
         s.step(30)
         cw.append(s)
+    P, like, mult, _ = s.state()
+    open_runs = {w: c for w, c in cw.pending.items()}
     cw.close()
-    P, like, _, _ = s.state()
     for w in range(W):
         c = np.loadtxt(tmp_path / f"run_{w + 1}.txt", ndmin=2)
-        assert c[:, 0].sum() == T
+        assert c[:, 0].sum() + open_runs[w][1] == T
+        assert open_runs[w][1] == mult[w]                      # the open stay is the sampler's multiplicity
         assert np.all(np.any(np.diff(c[:, 2:], axis=0) != 0, axis=1))
-        np.testing.assert_allclose(c[-1, 2:], P[w], rtol=1e-6)
-        assert c[-1, 1] == pytest.approx(like[w], rel=1e-6)
+        np.testing.assert_allclose(open_runs[w][0][1:], P[w], rtol=1e-15)
+        assert open_runs[w][0][0] == pytest.approx(like[w], rel=1e-15)

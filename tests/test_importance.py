@@ -31,9 +31,52 @@ def _eval(P):       # new target: shifted Gaussian in the two used parameters, b
     return t
 
 
+class _BoundedEval:
+    """_eval with the new run's hard bounds exposed as prior_cut (GPUEvaluator does the same)."""
+
+    def __call__(self, P):
+        return _eval(P)
+
+    def prior_cut(self, P):
+        return np.any(np.abs(P[:, :2]) > 3, axis=1)
+
+
+def test_prior_cut_rows_skipped_before_counting(tmp_path):
+    """A row outside the new prior bounds is skipped before anything is
+    counted (CheckPriorCuts, ImportanceSampling.f90:296-302): it adds nothing
+    to num_used, mult_ratio or weight_min."""
+    rows = _chain()
+    rows[5, 2] = 3.5
+    _write_chain(tmp_path / "in.txt", rows)
+    st = ImportanceSettings(redo_likelihoods=True, redo_skip=0, redo_auto_likescale=False)
+    r = ImportanceSampler(st, [1, 2], np.zeros(3), _BoundedEval()).run(str(tmp_path / "in.txt"))
+    chain = read_chain_rows(str(tmp_path / "in.txt"))
+    inside = ~np.any(np.abs(chain[:, 2:4]) > 3, axis=1)
+    assert not inside[5]
+    chain = chain[inside]
+    tl = _eval(np.column_stack([chain[:, 2:], np.zeros(len(chain))]))
+    w = np.exp(chain[:, 1] - tl)
+    assert r.num_used == inside.sum()
+    assert r.mult_ratio == pytest.approx(w.sum())
+    assert r.weight_min == pytest.approx(w.min()) and r.weight_min > 0
+    assert len(r.rows) == inside.sum()
+
+
+def test_nint_rounds_half_away_from_zero(tmp_path):
+    """redo_skip fraction x lines = 2.5 -> NINT 3 (ImportanceSampling.f90:147-148),
+    where Python's round would give 2."""
+    from cosmomc_amd.importance import nint
+    assert nint(2.5) == 3 and nint(3.5) == 4 and nint(-2.5) == -3 and nint(2.4999) == 2
+    rows = _chain(10)
+    _write_chain(tmp_path / "in.txt", rows)
+    st = ImportanceSettings(redo_likelihoods=False, redo_skip=0.25)
+    mult, like, P = ImportanceSampler(st, [1, 2], np.zeros(2), _eval).read(str(tmp_path / "in.txt"))
+    assert mult.size == 10 - 3
+
+
 def test_weights_and_rows(tmp_path):
     rows = _chain()
-    rows[5, 2] = 3.5                      # outside the new bounds -> weight 0, row dropped
+    rows[5, 2] = 3.5                      # an evaluator without prior_cut: weight 0, row dropped
     _write_chain(tmp_path / "in.txt", rows)
     st = ImportanceSettings(redo_likelihoods=True, redo_skip=0, redo_auto_likescale=False)
     r = ImportanceSampler(st, [1, 2], np.zeros(3), _eval).run(str(tmp_path / "in.txt"), str(tmp_path / "post"))
