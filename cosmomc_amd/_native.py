@@ -85,6 +85,8 @@ def lib():
         L.cmbl_loglike_batch.argtypes = [vp, i, vp, ll, ll, vp, ll, vp, vp, vp]
         L.cmbl_loglike_batch_host.argtypes = [vp, i, vp, ll, ll, vp, ll, vp]
         L.cmbl_clik_compute_batch.argtypes = [vp, i, vp, vp, ll, vp, vp, vp]
+        L.cmbl_clik_workspace_size.argtypes = [vp, i]
+        L.cmbl_clik_workspace_size.restype = sz
         L.cmbs_walker_seed.argtypes = [i, i, i, C.POINTER(i), C.POINTER(i)]
         L.cmbs_create.argtypes = [C.POINTER(CmbsConfig), C.POINTER(vp), C.c_char_p, sz]
         L.cmbs_destroy.argtypes = [vp]
@@ -92,7 +94,7 @@ def lib():
         L.cmbs_last_error.restype = C.c_char_p
         L.cmbs_set_covariance.argtypes = [vp, vp]
         L.cmbs_set_test_gaussian.argtypes = [vp, vp, vp]
-        L.cmbs_add_likelihood.argtypes = [vp, vp, i, vp, ll, ll]
+        L.cmbs_add_likelihood.argtypes = [vp, vp, vp, vp, ll, ll]
         L.cmbs_set_start.argtypes = [vp, vp, vp]
         L.cmbs_step.argtypes = [vp, i, i, vp]
         L.cmbs_set_groups.argtypes = [vp, i]

@@ -1,5 +1,6 @@
 // C ABI of libcosmomc_amd.so (include/cosmomc_amd.h).  Every entry point
 // catches internal errors and turns them into codes + messages.
+#include <algorithm>
 #include <cstring>
 
 #include "sampler.h"
@@ -8,7 +9,7 @@ namespace cmamd {
 void sampler_create(cmbs *s, const cmbs_config_t *cfg);
 void sampler_set_covariance(cmbs *s, const double *cov);
 void sampler_set_test_gaussian(cmbs *s, const double *cov, const double *center);
-void sampler_add_likelihood(cmbs *s, cmbl_t *like, int nuis_index0, const double *dl, long long ld_field,
+void sampler_add_likelihood(cmbs *s, cmbl_t *like, const int *nuisance_indices, const double *dl, long long ld_field,
                             long long ld_walker);
 void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream);
 void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream);
@@ -20,6 +21,7 @@ void sampler_history_restore(cmbs *s, int first, int count, const double *in, co
 void sampler_history_terms_host(cmbs *s, int first, int count, double *out);
 void sampler_save_state(cmbs *s, void *buf, size_t bytes);
 void sampler_load_state(cmbs *s, const void *buf, size_t bytes);
+void launch_negate(const double *in, double *out, int W, hipStream_t stream);
 void launch_clik_to_dl(const double *clp, long long ld, const int *lm, double *dl, long long ld_field,
                        long long ld_walker, int lmax_out, int W, hipStream_t stream);
 }  // namespace cmamd
@@ -132,19 +134,80 @@ int cmbl_loglike_batch(cmbl_t *h, int W, const double *dl, long long ld_field, l
     });
 }
 
+// Doubles of one walker's theory the likelihood reads: fields in
+// cmbl_loglike_batch order (TT, TE, EE, TB, EB, BB, PT, PE, PB, PP), each
+// l = 0..cl_lmax of its pair; the last used field ends at its lmax.
+static long long theory_extent(const cmamd::Like &L, long long ld_field) {
+    static const int fi[10] = {1, 2, 2, 3, 3, 3, 4, 4, 4, 4}, fj[10] = {1, 1, 2, 1, 2, 3, 1, 2, 3, 4};
+    long long ext = 0;
+    for (int f = 0; f < 10; f++) {
+        const int lm = L.cl_lmax[(fi[f] - 1) * 4 + (fj[f] - 1)];
+        if (lm > 0) ext = std::max(ext, f * ld_field + lm + 1);
+    }
+    return ext;
+}
+
 int cmbl_loglike_batch_host(cmbl_t *h, int W, const double *dl, long long ld_field, long long ld_walker,
                             const double *nuis, long long ld_nuis, double *out) {
     if (!h || !h->like) return CMBL_ERR_ARG;
     return guarded(&h->like->last_error, [&] {
         if (W <= 0) return;
-        const size_t nd = (size_t)ld_walker * W, nn = (size_t)(ld_nuis > 0 ? ld_nuis : 1) * W;
-        cmamd::DevBuf d_dl(nd * 8), d_n(nn * 8), d_out((size_t)W * 8), ws(h->like->workspace_size(W));
-        d_dl.upload(dl, nd * 8);
-        if (nuis) d_n.upload(nuis, nn * 8);
-        h->like->loglike_batch(W, d_dl.as<double>(), ld_field, ld_walker, nuis ? d_n.as<double>() : nullptr,
-                               ld_nuis, d_out.as<double>(), ws.p, 0);
-        HIP_CHECK(hipMemcpy(out, d_out.p, (size_t)W * 8, hipMemcpyDeviceToHost));
+        if (!dl || !out) cmamd::fail(CMBL_ERR_ARG, "cmbl_loglike_batch_host: bad arguments");
+        std::lock_guard<std::mutex> lock(h->host_mu);
+        const auto &L = *h->like;
+        const size_t nd = (size_t)((W - 1) * ld_walker + theory_extent(L, ld_field));
+        const size_t nn = nuis ? (size_t)((W - 1) * ld_nuis + L.n_nuis) : 0;
+        if (!h->host_stream) HIP_CHECK(hipStreamCreateWithFlags(&h->host_stream, hipStreamNonBlocking));
+        const size_t pin_need = (nd + nn + (size_t)W) * 8;
+        if (pin_need > h->pin_bytes) {
+            if (h->pin) HIP_CHECK(hipHostFree(h->pin));
+            h->pin = nullptr;
+            HIP_CHECK(hipHostMalloc(&h->pin, pin_need, hipHostMallocDefault));
+            h->pin_bytes = pin_need;
+        }
+        h->h_dl.grow(nd * 8);
+        h->h_nuis.grow(std::max<size_t>(nn, 1) * 8);
+        h->h_out.grow((size_t)W * 8);
+        h->h_ws.grow(L.workspace_size(W));
+        double *pdl = static_cast<double *>(h->pin), *pn = pdl + nd, *pout = pn + nn;
+        std::memcpy(pdl, dl, nd * 8);                          // pinned staging: one DMA each way
+        if (nn) std::memcpy(pn, nuis, nn * 8);
+        hipStream_t st = h->host_stream;
+        HIP_CHECK(hipMemcpyAsync(h->h_dl.p, pdl, nd * 8, hipMemcpyHostToDevice, st));
+        if (nn) HIP_CHECK(hipMemcpyAsync(h->h_nuis.p, pn, nn * 8, hipMemcpyHostToDevice, st));
+        h->like->loglike_batch(W, h->h_dl.as<double>(), ld_field, ld_walker, nn ? h->h_nuis.as<double>() : nullptr,
+                               ld_nuis, h->h_out.as<double>(), h->h_ws.p, st);
+        HIP_CHECK(hipMemcpyAsync(pout, h->h_out.p, (size_t)W * 8, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        std::memcpy(out, pout, (size_t)W * 8);
     });
+}
+
+// clik layout -> D_l rows + the native likelihood's scratch, carved from one workspace
+struct ClikWs {
+    int lm[6];
+    long long ncl, ldf, ldw;
+    int lmax_out;
+    size_t bytes;
+};
+
+static ClikWs clik_ws_layout(const cmamd::Like &L, int W, const int *clik_lmax) {
+    ClikWs c{};
+    c.ncl = 0;
+    for (int i = 0; i < 6; i++) {
+        c.lm[i] = clik_lmax ? clik_lmax[i] : 0;
+        c.ncl += c.lm[i] + 1;                // lmax = -1 -> absent (0 entries)
+    }
+    // D_l rows long enough for every spectrum the native likelihood reads
+    c.lmax_out = std::max(L.cl_lmax[0], std::max(L.cl_lmax[4], L.cl_lmax[5]));
+    c.ldf = c.lmax_out + 1;
+    c.ldw = 3 * c.ldf;
+    c.bytes = (size_t)c.ldw * W * 8 + (size_t)W * 8 + L.workspace_size(W);
+    return c;
+}
+
+size_t cmbl_clik_workspace_size(const cmbl_t *h, int W) {
+    return h && h->like && W > 0 ? clik_ws_layout(*h->like, W, nullptr).bytes : 0;
 }
 
 int cmbl_clik_compute_batch(cmbl_t *h, int W, const int *clik_lmax, const double *cl_and_pars, long long ld,
@@ -153,30 +216,20 @@ int cmbl_clik_compute_batch(cmbl_t *h, int W, const int *clik_lmax, const double
     return guarded(&h->like->last_error, [&] {
         if (h->like->tag != "PLIK_LITE") cmamd::fail(CMBL_ERR_UNSUPPORTED, "clik entry only routes to PLIK_LITE");
         if (W <= 0) return;
-        int lm[6];
-        long long ncl = 0;
-        for (int i = 0; i < 6; i++) {
-            lm[i] = clik_lmax[i];
-            ncl += lm[i] + 1;                // lmax = -1 -> absent (0 entries)
+        if (!clik_lmax || !cl_and_pars || !lnlike) cmamd::fail(CMBL_ERR_ARG, "cmbl_clik_compute_batch: bad arguments");
+        const ClikWs c = clik_ws_layout(*h->like, W, clik_lmax);
+        if (!workspace) {
+            h->clik_ws.grow(c.bytes);
+            workspace = h->clik_ws.p;
         }
-        // D_l rows long enough for every spectrum the native likelihood reads
-        const int lmax_out = std::max(h->like->cl_lmax[0], std::max(h->like->cl_lmax[4], h->like->cl_lmax[5]));
-        const long long ldf = lmax_out + 1, ldw = 3 * ldf;
-        const size_t need = (size_t)ldw * W * 8 + (size_t)W * 8 + h->like->workspace_size(W);
-        (void)workspace;
-        cmamd::DevBuf tmp(need);
-        double *dl = tmp.as<double>();
-        double *mlnl = dl + (size_t)ldw * W;
+        double *dl = static_cast<double *>(workspace);
+        double *mlnl = dl + (size_t)c.ldw * W;
         void *lws = mlnl + W;
-        cmamd::launch_clik_to_dl(cl_and_pars, ld, lm, dl, ldf, ldw, lmax_out, W, (hipStream_t)stream);
+        cmamd::launch_clik_to_dl(cl_and_pars, ld, c.lm, dl, c.ldf, c.ldw, c.lmax_out, W, (hipStream_t)stream);
         // nuisance parameters follow the C_l blocks (cliklike.f90:157-163)
-        h->like->loglike_batch(W, dl, ldf, ldw, cl_and_pars + ncl, ld, mlnl, lws, (hipStream_t)stream);
-        // lnlike = -(-lnL): clik_compute returns +lnL (cliklike.f90:166)
-        std::vector<double> hv(W);
-        HIP_CHECK(hipMemcpyAsync(hv.data(), mlnl, (size_t)W * 8, hipMemcpyDeviceToHost, (hipStream_t)stream));
-        HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
-        for (auto &v : hv) v = -v;
-        HIP_CHECK(hipMemcpy(lnlike, hv.data(), (size_t)W * 8, hipMemcpyHostToDevice));
+        h->like->loglike_batch(W, dl, c.ldf, c.ldw, cl_and_pars + c.ncl, ld, mlnl, lws, (hipStream_t)stream);
+        // lnlike = -(-lnL): clik_compute returns +lnL (cliklike.f90:166), negated on device
+        cmamd::launch_negate(mlnl, lnlike, W, (hipStream_t)stream);
     });
 }
 
@@ -217,11 +270,12 @@ int cmbs_set_test_gaussian(cmbs_t *s, const double *cov, const double *center) {
     return guarded(&s->last_error, [&] { cmamd::sampler_set_test_gaussian(s, cov, center); });
 }
 
-int cmbs_add_likelihood(cmbs_t *s, cmbl_t *like, int nuis_index0, const double *dl, long long ld_field,
+int cmbs_add_likelihood(cmbs_t *s, cmbl_t *like, const int *nuisance_indices, const double *dl, long long ld_field,
                         long long ld_walker) {
     if (!s) return CMBL_ERR_ARG;
-    return guarded(&s->last_error,
-                   [&] { cmamd::sampler_add_likelihood(s, like, nuis_index0, dl, ld_field, ld_walker); });
+    return guarded(&s->last_error, [&] {
+        cmamd::sampler_add_likelihood(s, like, nuisance_indices, dl, ld_field, ld_walker);
+    });
 }
 
 int cmbs_set_start(cmbs_t *s, const double *P0, void *stream) {

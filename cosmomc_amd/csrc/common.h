@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -179,4 +180,18 @@ std::unique_ptr<Like> make_sptpol(const Ini &ini, const std::string &tag);   // 
 
 struct cmbl {
     std::unique_ptr<cmamd::Like> like;
+    // cmbl_loglike_batch_host: device buffers, pinned host staging and a stream
+    // kept across calls, so a W = 1 call per evaluation (the Fortran LogLike
+    // binding) allocates nothing; one host call at a time per handle
+    std::mutex host_mu;
+    cmamd::DevBuf h_dl, h_nuis, h_out, h_ws;
+    void *pin = nullptr;
+    size_t pin_bytes = 0;
+    hipStream_t host_stream = nullptr;
+    // cmbl_clik_compute_batch scratch when the caller passes no workspace
+    cmamd::DevBuf clik_ws;
+    ~cmbl() {
+        if (pin) (void)hipHostFree(pin);
+        if (host_stream) (void)hipStreamDestroy(host_stream);
+    }
 };

@@ -341,6 +341,17 @@ struct PlikLite final : Like {
 std::unique_ptr<Like> make_plik_lite(const Ini &ini) { return std::unique_ptr<Like>(new PlikLite(ini)); }
 
 // exported for the clik entry point (api.cpp)
+__global__ void negate_kernel(const double *in, double *out, int W)
+{
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < W) out[w] = -in[w];
+}
+
+void launch_negate(const double *in, double *out, int W, hipStream_t stream) {
+    hipLaunchKernelGGL(negate_kernel, dim3((W + 255) / 256), dim3(256), 0, stream, in, out, W);
+    HIP_CHECK(hipGetLastError());
+}
+
 void launch_clik_to_dl(const double *clp, long long ld, const int *lm, double *dl, long long ld_field,
                        long long ld_walker, int lmax_out, int W, hipStream_t stream) {
     hipLaunchKernelGGL(clik_to_dl, dim3((lmax_out + 256) / 256, W), dim3(256), 0, stream, clp, ld, lm[0], lm[1],

@@ -60,13 +60,14 @@ struct DevCfg {
     const double *like_terms;       // [n_like (even)][ld] -lnL of each likelihood at the trial point
     double *cur_terms;              // [n_like][ld] -lnL of each likelihood at the current point
                                     //   (TCalculationAtParamPoint%Likelihoods, for chi2_* output)
-    int like_nuis0[MAXLIKE], like_nn[MAXLIKE];
+    int like_nidx[MAXLIKE], like_nn[MAXLIKE];   // offset in tab_i of each likelihood's nuisance_indices
+                                                //   (0-based indices into P), and their count
     double *like_nuis[MAXLIKE];     // [W][like_nn] DataParams buffers written by mh_kernel
 };
 
 struct LikeSlot {
     cmbl_t *like;
-    int nuis0;   // 0-based
+    std::vector<int> nidx;   // nuisance_indices, 0-based
     const double *dl;
     long long ld_field, ld_walker;
 };

@@ -137,6 +137,7 @@ __global__ void rng_init_kernel(DevCfg c, const int *ij, const int *kl)
 // ------------------------------------------------------------ per-walker view
 
 struct Tabs {   // shared tables (LDS copies)
+    const int *ti;   // the whole int table (likelihood nuisance_indices at DevCfg::like_nidx offsets)
     const int *blk_n, *blk_nchanged, *blk_changed_off, *blk_map_off, *blk_R_off, *changed, *pfi, *params_used;
     const double *mapping, *pmin, *pmax, *pmean, *pstd, *lin_w, *lin_m, *lin_s, *covinv, *center;
 };
@@ -147,7 +148,7 @@ __device__ Tabs make_tabs(const DevCfg &c, const int *ti, const double *td, cons
 {
     const TabLayout &l = c.tl;
     if (!td_cov) td_cov = td;
-    return Tabs{ti + l.blk_n, ti + l.blk_nchanged, ti + l.blk_changed_off, ti + l.blk_map_off, ti + l.blk_R_off,
+    return Tabs{ti, ti + l.blk_n, ti + l.blk_nchanged, ti + l.blk_changed_off, ti + l.blk_map_off, ti + l.blk_R_off,
                 ti + l.changed, ti + l.pfi, ti + l.params_used, td + l.mapping, td + l.pmin, td + l.pmax,
                 td + l.pmean, td + l.pstd, td + l.lin_w, td + l.lin_m, td + l.lin_s, td_cov + l.covinv,
                 td_cov + l.center};
@@ -522,7 +523,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
         else
             for (int l = 0; l < c.n_like; l++)
                 for (int q = 0; q < c.like_nn[l]; q++)
-                    c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = k.trial[c.like_nuis0[l] + q];
+                    c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = k.trial[t.ti[c.like_nidx[l] + q]];
     }
     STAMP(4);
     sd[(size_t)R.C * NB + lane] = k.r.c;
@@ -553,7 +554,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
             const double *trial = sd + (size_t)SROW(R.T) * NB + lane;
             for (int l = 0; l < c.n_like; l++)
                 for (int q = 0; q < c.like_nn[l]; q++)
-                    c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = trial[(size_t)(c.like_nuis0[l] + q) * NB];
+                    c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = trial[(size_t)ti[c.like_nidx[l] + q] * NB];
         }
     }
     __syncthreads();
@@ -641,8 +642,8 @@ __global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *h
     auto scatter = [&]() {            // DataParams of both trial points
         for (int l = 0; l < c.n_like; l++)
             for (int q = 0; q < c.like_nn[l]; q++) {
-                c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = T[c.like_nuis0[l] + q];
-                g.like_nuis2[l][(size_t)w * c.like_nn[l] + q] = T2[c.like_nuis0[l] + q];
+                c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = T[t.ti[c.like_nidx[l] + q]];
+                g.like_nuis2[l][(size_t)w * c.like_nn[l] + q] = T2[t.ti[c.like_nidx[l] + q]];
             }
     };
     auto next_delta = [&]() {         // GetProposalFastDelta (propose.f90:291-298) on both ends
@@ -784,12 +785,13 @@ __global__ void start_kernel(DevCfg c)
     c.si[(size_t)c.rows.NACC * W + w] = 0;
 }
 
-// nuisance slice of every walker's trial point: out[w][k] = trial[nuis0 + k][w]
-__global__ void gather_nuis(const double *trial, int W, int ld, int nuis0, int n_nuis, double *out)
+// DataParams of every walker's trial point, P(nuisance_indices)
+// (GeneralTypes.f90:642-646, calclike.f90:380): out[w][k] = trial[nidx[k]][w]
+__global__ void gather_nuis(const double *trial, int W, int ld, const int *nidx, int n_nuis, double *out)
 {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
-    for (int k = 0; k < n_nuis; k++) out[(size_t)w * n_nuis + k] = trial[(size_t)(nuis0 + k) * ld + w];
+    for (int k = 0; k < n_nuis; k++) out[(size_t)w * n_nuis + k] = trial[(size_t)nidx[k] * ld + w];
 }
 
 // Per-chain mean and covariance over history rows first..last
@@ -1203,14 +1205,26 @@ void sampler_set_test_gaussian(cmbs *s, const double *cov, const double *center)
     upload_tables(s);
 }
 
-void sampler_add_likelihood(cmbs *s, cmbl_t *like, int nuis_index0, const double *dl, long long ld_field,
+void sampler_add_likelihood(cmbs *s, cmbl_t *like, const int *nuisance_indices, const double *dl, long long ld_field,
                             long long ld_walker) {
     if (!like) fail(CMBL_ERR_ARG, "null likelihood");
     const int nn = like->like->n_nuis;
-    if (nuis_index0 < 1 || nuis_index0 - 1 + nn > s->np) fail(CMBL_ERR_ARG, "nuisance indices out of range");
+    if (nn > 0 && !nuisance_indices) fail(CMBL_ERR_ARG, "likelihood has %d nuisance parameters: indices needed", nn);
+    std::vector<int> nidx(nn);
+    for (int q = 0; q < nn; q++) {
+        if (nuisance_indices[q] < 1 || nuisance_indices[q] > s->np)
+            fail(CMBL_ERR_ARG, "nuisance index %d out of range 1..%d", nuisance_indices[q], s->np);
+        nidx[q] = nuisance_indices[q] - 1;
+    }
     if ((int)s->likes.size() >= MAXLIKE) fail(CMBL_ERR_ARG, "at most %d likelihoods per sampler", MAXLIKE);
     const int li = (int)s->likes.size();
-    s->likes.push_back({like, nuis_index0 - 1, dl, ld_field, ld_walker});
+    s->likes.push_back({like, nidx, dl, ld_field, ld_walker});
+    // the index list joins the int table (LDS-staged with the proposer tables)
+    s->dc.like_nidx[li] = (int)s->h_tab_i.size();
+    s->h_tab_i.insert(s->h_tab_i.end(), nidx.begin(), nidx.end());
+    s->dc.tl.n_int = (int)s->h_tab_i.size();
+    set_mh_lds(s);
+    upload_tables(s);
     const size_t nlk = (s->likes.size() + 1) & ~size_t(1);
     DevBuf nt(nlk * (size_t)s->dc.ld * 8);
     HIP_CHECK(hipMemset(nt.p, 0, nt.bytes));
@@ -1233,7 +1247,6 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, int nuis_index0, const double
     }
     s->nuis_bufs[li].alloc((size_t)std::max(nn, 1) * s->W * 8);
     s->dc.like_nuis[li] = s->nuis_bufs[li].as<double>();
-    s->dc.like_nuis0[li] = nuis_index0 - 1;
     s->dc.like_nn[li] = nn;
     size_t maxws = 0;
     for (auto &l : s->likes) maxws = std::max(maxws, l.like->like->workspace_size(s->W));
@@ -1269,7 +1282,8 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
         double *nb = s->dc.like_nuis[i];
         if (gather) {   // mh_kernel scatters the nuisance slices itself on every step
             hipLaunchKernelGGL(gather_nuis, dim3((s->W + 255) / 256), dim3(256), 0, st,
-                               s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld, s->W, s->dc.ld, l.nuis0, nn, nb);
+                               s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld, s->W, s->dc.ld,
+                               s->dc.tab_i + s->dc.like_nidx[i], nn, nb);
             HIP_CHECK(hipGetLastError());
         }
         l.like->like->loglike_batch(Wg, l.dl + (size_t)g0 * l.ld_walker, l.ld_field, l.ld_walker,

@@ -146,14 +146,21 @@ class ClikLikelihood(NativeCMBLikelihood):
     against real clik.
     """
 
-    def clik_compute(self, cl_and_pars, clik_lmax):
-        """+lnL for rows of the clik vector (device tensor [W, n])."""
+    def clik_workspace(self, W: int):
+        """A device workspace for clik_compute on W rows (cmbl_clik_workspace_size)."""
+        import torch
+        n = N.lib().cmbl_clik_workspace_size(self._h, W)
+        return torch.empty(max(n, 8), dtype=torch.uint8, device="cuda")
+
+    def clik_compute(self, cl_and_pars, clik_lmax, workspace=None):
+        """+lnL for rows of the clik vector (device tensor [W, n]); asynchronous."""
         import torch
         W = cl_and_pars.shape[0]
         lm = (C.c_int * 6)(*clik_lmax)
         out = torch.empty(W, dtype=torch.float64, device=cl_and_pars.device)
+        ws = workspace.data_ptr() if workspace is not None else None
         rc = N.lib().cmbl_clik_compute_batch(self._h, W, lm, cl_and_pars.data_ptr(), cl_and_pars.stride(0),
-                                             out.data_ptr(), None, N.current_stream_ptr(cl_and_pars.device))
+                                             out.data_ptr(), ws, N.current_stream_ptr(cl_and_pars.device))
         N.check(rc, self._h)
         return out
 

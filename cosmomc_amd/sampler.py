@@ -88,12 +88,11 @@ class BatchedMCMC:
         self._check(N.lib().cmbs_set_test_gaussian(self._h, c.ctypes.data, m.ctypes.data))
 
     def add_likelihood(self, like, dl):
-        """like: NativeCMBLikelihood with nuisance_indices set; dl: cuda tensor [W, nf, L]."""
-        idx = like.nuisance_indices
-        if idx != list(range(idx[0], idx[0] + len(idx))):
-            raise ValueError("nuisance indices must be contiguous")
+        """like: NativeCMBLikelihood with nuisance_indices set (1-based indices
+        into P, any order, GeneralTypes.f90:642-646); dl: cuda tensor [W, nf, L]."""
+        idx = np.ascontiguousarray(list(like.nuisance_indices) or [0], dtype=np.int32)
         self._likes.append((like, dl))
-        self._check(N.lib().cmbs_add_likelihood(self._h, like.handle, idx[0], dl.data_ptr(), dl.stride(1),
+        self._check(N.lib().cmbs_add_likelihood(self._h, like.handle, idx.ctypes.data, dl.data_ptr(), dl.stride(1),
                                                 dl.stride(0)))
 
     def set_start(self, P0, stream=None):

@@ -85,8 +85,13 @@ int  cmbl_loglike_batch(cmbl_t *h, int W,
                         const double *nuis, long long ld_nuis,
                         double *out, void *workspace, void *stream);
 
-/* Same with HOST arrays: stages through device memory over PCIe and
- * synchronises.  For hosts that keep C_l in CPU memory. */
+/* Same with HOST arrays: stages through pinned host memory and device buffers
+ * the handle keeps between calls (no allocation per call once sized), runs on
+ * the handle's own stream and synchronises.  For hosts that keep C_l in CPU
+ * memory, e.g. the reference's LogLike called per evaluation with W = 1
+ * (INTEGRATION.md).  Reads only the theory the likelihood uses: fields up to
+ * the last with cl_lmax > 0, each to its lmax.  One host call at a time per
+ * handle (serialised internally). */
 int  cmbl_loglike_batch_host(cmbl_t *h, int W,
                              const double *dl, long long ld_field, long long ld_walker,
                              const double *nuis, long long ld_nuis, double *out);
@@ -99,6 +104,9 @@ int  cmbl_loglike_batch_host(cmbl_t *h, int W,
 int  cmbl_clik_compute_batch(cmbl_t *h, int W, const int *clik_lmax,
                              const double *cl_and_pars, long long ld,
                              double *lnlike, void *workspace, void *stream);
+/* Device workspace bytes cmbl_clik_compute_batch needs for W walkers
+ * (workspace NULL: the handle's own, grown on demand; asynchronous either way). */
+size_t cmbl_clik_workspace_size(const cmbl_t *h, int W);
 
 /* Per-kernel device timing (HIP events around every library launch; off by
  * default).  cmbl_profile_read: accumulated milliseconds and launch count of
@@ -155,11 +163,13 @@ int  cmbs_set_covariance(cmbs_t *s, const double *cov);
 int  cmbs_set_test_gaussian(cmbs_t *s, const double *cov, const double *center);
 
 /* Add a CMB likelihood evaluated on cached per-walker theory:
- * DataParams = P[nuis_index0 - 1 .. + n_nuis) (1-based nuis_index0, the
- * contiguous nuisance_indices of AddNuisanceParameters, GeneralTypes.f90:618-669).
- * dl is a device array laid out as for cmbl_loglike_batch for this sampler's
- * walkers; it must stay alive while the sampler is used. */
-int  cmbs_add_likelihood(cmbs_t *s, cmbl_t *like, int nuis_index0,
+ * DataParams = P(nuisance_indices) (GeneralTypes.f90:642-646: the indices
+ * AddNuisanceParameters assigns, :618-669, in any order and shared between
+ * likelihoods, e.g. calPlanck for plik_lite and lensing), nuisance_indices
+ * 1-based, n_nuis of them (cmbl_info).  dl is a device array laid out as for
+ * cmbl_loglike_batch for this sampler's walkers; it must stay alive while the
+ * sampler is used. */
+int  cmbs_add_likelihood(cmbs_t *s, cmbl_t *like, const int *nuisance_indices,
                          const double *dl, long long ld_field, long long ld_walker);
 
 /* Initial points (host, W x num_params) -> evaluates the starting -lnL. */

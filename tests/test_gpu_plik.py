@@ -91,6 +91,35 @@ def test_plik_host_entry(data, dataset):
     np.testing.assert_allclose(like.loglike_host(th, cal[:, None]), orc.loglike_batch(th, cal), rtol=RTOL)
 
 
+def test_plik_host_entry_per_eval_loop(data, dataset):
+    """The Fortran LogLike binding calls the host entry once per evaluation
+    (W = 1): buffers persist on the handle, so a call costs tens of
+    microseconds, not allocations; a shared theory (ld_walker = 0) reads only
+    the fields the likelihood uses."""
+    import ctypes as C
+    import time
+    from cosmomc_amd import _native as N
+    like = _open(dataset)
+    orc = po.PlikLite(data)
+    th = syn.walker_theory(40, seed=18, n_fields=3)
+    cal = syn.walker_calibrations(40, seed=19)
+    like.loglike_host(th[:1], cal[:1, None])                  # sizes the staging once
+    t0 = time.perf_counter()
+    got = np.array([like.loglike_host(th[w:w + 1], cal[w:w + 1, None])[0] for w in range(40)])
+    per_call = (time.perf_counter() - t0) / 40
+    np.testing.assert_allclose(got, orc.loglike_batch(th, cal), rtol=RTOL)
+    print(f"host entry W=1: {per_call * 1e6:.1f} us per call")
+    assert per_call < 1e-3
+    one = np.ascontiguousarray(th[3])                          # [3, L]: exactly the fields plik_lite reads
+    W = 7
+    out = np.empty(W)
+    nu = np.ascontiguousarray(cal[:W, None])
+    rc = N.lib().cmbl_loglike_batch_host(like._h, W, one.ctypes.data, one.shape[1], 0, nu.ctypes.data, 1,
+                                         out.ctypes.data)
+    N.check(rc, like._h)
+    np.testing.assert_allclose(out, [orc.loglike(one, c) for c in cal[:W]], rtol=RTOL)
+
+
 def test_plik_zero_theory_property(data, dataset):
     """Zero theory: every walker's -lnL is X^T C^-1 X / 2, independent of cal."""
     like = _open(dataset)
@@ -138,6 +167,12 @@ def test_clik_packing_routes_to_native(data, dataset):
     got = like.clik_compute(v, lmax).cpu().numpy()
     ref = -po.PlikLite(data).loglike_batch(th, cal)
     np.testing.assert_allclose(got, ref, rtol=1e-9)
+    ws = like.clik_workspace(W)                   # caller's workspace, on a side stream, no host sync
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        got2 = like.clik_compute(v, lmax, workspace=ws)
+    s.synchronize()
+    np.testing.assert_allclose(got2.cpu().numpy(), ref, rtol=1e-9)
 
 
 def test_bad_dataset_errors(tmp_path, dataset):
