@@ -103,6 +103,12 @@ def lib():
         L.cmbs_step_drag.argtypes = [vp, i, d, THEORY_FN, vp, vp]
         L.cmbs_step_theory.argtypes = [vp, i, THEORY_FN, vp, vp]
         L.cmbs_refresh_theory.argtypes = [vp, THEORY_FN, vp, vp]
+        L.cmbs_collector_enable.argtypes = [vp, i]
+        L.cmbs_collector_add.argtypes = [vp, vp, i, i, i, vp]
+        L.cmbs_collector_state_host.argtypes = [vp, vp, vp, vp, vp]
+        L.cmbs_collector_thin.argtypes = [vp, i, vp]
+        L.cmbs_collector_moments.argtypes = [vp, vp, vp, vp]
+        L.cmbs_collector_limits.argtypes = [vp, vp, i, d, vp, vp]
         L.cmbs_chain_moments.argtypes = [vp, i, i, vp, vp, vp]
         L.cmbs_enable_history.argtypes = [vp, i]
         L.cmbs_history_stats.argtypes = [vp, i, i, vp, vp, vp]

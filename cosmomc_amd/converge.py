@@ -25,6 +25,11 @@ from dataclasses import dataclass, field
 import numpy as np
 
 
+def _real4(x: float) -> float:
+    """The value a Fortran default REAL holds (TMPIData's MPI_R_Stop etc. are REAL(4))."""
+    return float(np.float32(x))
+
+
 @dataclass
 class CollectorSettings:
     """TMPIData defaults (SampleCollector.f90:12-35) and their ini keys (:115-127)."""
@@ -35,6 +40,10 @@ class CollectorSettings:
     MPI_Max_R_ProposeUpdate: float = 2.0
     MPI_Max_R_ProposeUpdateNew: float = 30.0
     MPI_R_StopProposeUpdate: float = 0.0
+    MPI_Check_Limit_Converge: bool = False
+    MPI_Limit_Converge: float = 0.025
+    MPI_Limit_Converge_Err: float = 0.3
+    MPI_Limit_Param: int = 0                  # full parameter index; 0 = every used parameter
     covariance_is_diagonal: bool = False      # BaseParams%covariance_is_diagonal
 
     @classmethod
@@ -47,6 +56,11 @@ class CollectorSettings:
             s.MPI_Max_R_ProposeUpdate = float(ini.get("MPI_Max_R_ProposeUpdate", s.MPI_Max_R_ProposeUpdate))
             s.MPI_Max_R_ProposeUpdateNew = float(ini.get("MPI_Max_R_ProposeUpdateNew",
                                                          s.MPI_Max_R_ProposeUpdateNew))
+        s.MPI_Check_Limit_Converge = str(ini.get("MPI_Check_Limit_Converge", "F")).upper().startswith("T")
+        if s.MPI_Check_Limit_Converge:
+            s.MPI_Limit_Converge = float(ini.get("MPI_Limit_Converge", s.MPI_Limit_Converge))
+            s.MPI_Limit_Converge_Err = float(ini.get("MPI_Limit_Converge_Err", s.MPI_Limit_Converge_Err))
+            s.MPI_Limit_Param = int(ini.get("MPI_Limit_Param", s.MPI_Limit_Param))
         return s
 
 
@@ -102,7 +116,10 @@ class ConvergenceExchange:
         self.flukecheck = False
 
     def update_cov_and_check_converge(self, provider, first: int, last: int,
-                                      min_sample_update: int | None = None) -> ConvergeResult:
+                                      min_sample_update: int | None = None,
+                                      window_count: int | None = None) -> ConvergeResult:
+        """window_count: the smallest per-chain window size when the chains'
+        windows differ (ChainCollector); else last - first + 1."""
         import torch
         n, st = self.n, self.settings
         p1 = _all_reduce(provider.chain_moments(first, last), self.group)
@@ -115,7 +132,7 @@ class ConvergenceExchange:
         g = torch.as_tensor(mean, dtype=torch.float64, device=_device_of(provider))
         p2 = _all_reduce(provider.chain_moments(first, last, g), self.group).double().cpu().numpy()
         meanscov = p2.reshape(n, n) / norm
-        count = last - first + 1
+        count = last - first + 1 if window_count is None else window_count
         msu = st.MPI_Min_Sample_Update if min_sample_update is None else min_sample_update
         enough = count > msu // 2 + 2                       # all(MPIMeans(0,:) > Min/2 + 2)
         res = ConvergeResult(R=1e6, evals=None, mean=mean, propose_cov=0.5 * (propose_cov + propose_cov.T),
@@ -128,13 +145,13 @@ class ConvergenceExchange:
                 res.evals = ev
                 res.R = float(ev.max())
                 if enough:
-                    res.converged = res.R < st.MPI_R_Stop and self.flukecheck
-                    self.flukecheck = res.R < st.MPI_R_Stop
+                    res.converged = res.R < _real4(st.MPI_R_Stop) and self.flukecheck
+                    self.flukecheck = res.R < _real4(st.MPI_R_Stop)
         if enough:
             # SampleCollector.f90:311-317 (Fortran precedence: .and. before .or.)
             res.update_proposal = st.MPI_LearnPropose and (
-                M == 1 or ((st.covariance_is_diagonal or res.R < st.MPI_Max_R_ProposeUpdate)
-                           and res.R > st.MPI_R_StopProposeUpdate))
+                M == 1 or ((st.covariance_is_diagonal or res.R < _real4(st.MPI_Max_R_ProposeUpdate))
+                           and res.R > _real4(st.MPI_R_StopProposeUpdate)))
         return res
 
 
@@ -148,3 +165,165 @@ def reference_window(count: int) -> tuple[int, int]:
     if count < 2:
         raise ValueError("need at least two samples")
     return count // 2 - 1, count - 1
+
+
+class ChainCollector:
+    """TMpiChainCollector_AddNewPoint / UpdateCovAndCheckConverge
+    (SampleCollector.f90:212-460) for every walker of every rank: each walker
+    is one chain with its own Samples list (cmbs_collector_* on device).
+
+    Per processed block of history steps: AddNewPoint at every output_thin-th
+    step (MCMC.f90:147; output_thin = oversample_fast for the Metropolis
+    sampler, 1 for fast dragging, :235, :460); burn-in per walker; when
+    walker 0 (global; "rank 0") burns, MPI_Sample_update_freq *= num_params_used
+    (num_slow when dragging) and every chain's MPI_Min_Sample_Update becomes
+    50 + 4 num_slow + num_fast, + 4 num_fast (x oversample_fast when dragging)
+    (:391-404); all_burn = every walker on every rank burned (the ISEND/IRECV
+    barrier of :380-389 as an all-reduce); DoUpdates once all_burn and Count >=
+    Min + 1; then walker 0 triggers an exchange whenever its Count is a
+    multiple of the update frequency (:429-446) and the exchange runs once every
+    chain can answer (DoUpdates everywhere).  The block length the host should
+    step next is ``next_block()``: it ends exactly at walker 0's next trigger.
+
+    Chains are stepped in lock step, so every chain enters the exchange at the
+    same step; in the reference each rank enters when the trigger reaches it,
+    a few samples apart -- a timing the reference itself does not fix."""
+
+    def __init__(self, sampler, settings: CollectorSettings | None = None, num_slow: int = 0, num_fast: int = 0,
+                 dragging: bool = False, oversample_fast: int = 1, output_thin: int | None = None, group=None,
+                 sample_capacity: int | None = None, thin_limit: int = 500000, root: str | None = None):
+        self.s = sampler
+        self.settings = settings or CollectorSettings()
+        self.n = len(sampler.params_used)
+        self.num_slow, self.num_fast = num_slow, num_fast
+        self.dragging = dragging
+        self.oversample_fast = max(1, oversample_fast)
+        self.output_thin = output_thin if output_thin is not None else (1 if dragging else self.oversample_fast)
+        self.group = group
+        self.thin_limit = thin_limit
+        self.root = root
+        cap = sample_capacity or getattr(sampler, "_hist_cap", 0)
+        sampler.collector_enable(cap)
+        self.cap = cap
+        self.min_update = self.settings.MPI_Min_Sample_Update
+        self.update_freq = self.settings.MPI_Sample_update_freq
+        self.min_after_burn = 50 + 4 * num_slow + num_fast
+        if dragging:
+            self.min_after_burn *= self.oversample_fast
+        else:
+            self.min_after_burn += 4 * num_fast
+        self.next_step = 0
+        self.burn0 = False
+        self.all_burn = False
+        self.waiting = False
+        self.done = False
+        self.count0 = 0
+        self.min_count = 0
+        self.exchange = ConvergenceExchange(self.n, self.settings, group)
+        self.results: list[ConvergeResult] = []
+        import torch.distributed as dist
+        self._world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self._rank = dist.get_rank(group) if self._world > 1 else 0
+
+    # -- cross-rank reductions of the per-walker collector state
+    def _reduce(self, burned, total, count0, mincount):
+        import torch
+        if self._world == 1:
+            return burned, total, count0, mincount
+        import torch.distributed as dist
+        dev = "cuda" if torch.cuda.is_available() and dist.get_backend(self.group) == "nccl" else "cpu"
+        a = torch.tensor([burned, total, count0], dtype=torch.float64, device=dev)
+        dist.all_reduce(a, op=dist.ReduceOp.SUM, group=self.group)
+        b = torch.tensor([mincount], dtype=torch.float64, device=dev)
+        dist.all_reduce(b, op=dist.ReduceOp.MIN, group=self.group)
+        return int(a[0].item()), int(a[1].item()), int(a[2].item()), int(b[0].item())
+
+    def next_block(self) -> int:
+        """History steps to run before the next ``process`` call: up to walker
+        0's next trigger once it can trigger, else one update period."""
+        if self.burn0 and self.all_burn and not self.waiting and self.count0 >= self.min_update + 1:
+            k = self.update_freq - self.count0 % self.update_freq
+            return max(1, k) * self.output_thin
+        return max(1, self.update_freq) * self.output_thin
+
+    def process(self) -> ConvergeResult | None:
+        """AddNewPoint for every history step recorded since the last call, then
+        the exchange if one is due.  Returns its ConvergeResult (or None)."""
+        s = self.s
+        total_steps = s.history_count()
+        steps = [t for t in range(self.next_step, total_steps) if (t + 1) % self.output_thin == 0]
+        self.next_step = total_steps
+        s.collector_add(steps, self.min_after_burn, check_burn=True)
+        _, count, burn, _ = s.collector_state()
+        c0 = int(count[0]) if self._rank == 0 else 0
+        b0 = int(burn[0]) if self._rank == 0 else 0
+        burned, total, c0, minc = self._reduce(int(burn.sum()), s.W, c0, int(count.min()))
+        b0 = self._reduce(b0, 0, 0, 0)[0] if self._world > 1 else b0
+        self.count0, self.min_count = c0, minc
+        if b0 and not self.burn0:                  # walker 0's own burn (:391-404)
+            self.burn0 = True
+            self.update_freq *= self.num_slow if self.dragging else self.n
+            self.min_update = self.min_after_burn
+        if not self.all_burn and burned == total:
+            self.all_burn = True
+        do0 = self.all_burn and self.count0 >= self.min_update + 1
+        if do0 and not self.waiting and self.count0 % max(1, self.update_freq) == 0:
+            self.waiting = True                     # rank 0's ISSEND trigger (:436-441)
+        if not (self.waiting and self.all_burn and self.min_count >= self.min_update + 1):
+            return None
+        self.waiting = False
+        return self._update_cov_and_check_converge()
+
+    def _update_cov_and_check_converge(self) -> ConvergeResult:
+        st = self.settings
+        wc = self.min_count - self.min_count // 2 + 1
+        prov = _CollectorMoments(self.s)
+        res = self.exchange.update_cov_and_check_converge(prov, 0, 0, self.min_update, window_count=wc)
+        if res.converged and st.MPI_Check_Limit_Converge:
+            ok, worst, _ = self.check_limits(res.propose_cov)
+            res.extras["limit_err"] = worst
+            res.converged = ok
+        self.done = self.done or res.converged
+        if res.evals is not None:                   # Samples%Thin(2), MPI_thin_fac * 2 where Count > 500000
+            self.s.collector_thin(self.thin_limit)   # (:300-304; per walker on device)
+        if self.root and self._rank == 0:           # ConvergeStatus (:461-475)
+            with open(self.root + ".converge_stat", "w") as f:
+                f.write(f"{res.R!r}\n" + ("Done\n" if res.converged else ""))
+        self.results.append(res)
+        return res
+
+    def check_limits(self, propose_cov):
+        """CheckLimitsConverge: every chain's ConfidVal limits (device), all
+        gathered, against the pooled standard deviations."""
+        import torch
+        st = self.settings
+        if st.MPI_Limit_Param:
+            params = [self.s.params_used.index(st.MPI_Limit_Param)]
+        else:
+            params = list(range(self.n))
+        lim = self.s.collector_limits(params, st.MPI_Limit_Converge)
+        if self._world > 1:
+            import torch.distributed as dist
+            if dist.get_backend(self.group) != "nccl":
+                lim = lim.cpu()
+            parts = [torch.empty_like(lim) for _ in range(self._world)]
+            dist.all_gather(parts, lim, group=self.group)
+            lim = torch.cat(parts)
+        lim = lim.double().cpu().numpy()
+        M = lim.shape[0]
+        mean_lim = lim.sum(axis=0) / M
+        var = ((lim - mean_lim[None]) ** 2).sum(axis=0) / (M - 1)
+        err = np.sqrt(var / np.diag(propose_cov)[params][:, None])
+        worst = float(err.max())
+        return worst < _real4(st.MPI_Limit_Converge_Err), worst, err
+
+
+class _CollectorMoments:
+    """chain_moments provider over each walker's own collector window."""
+
+    def __init__(self, sampler):
+        self.s = sampler
+        self.device = "cuda"
+
+    def chain_moments(self, first, last, gmean=None):
+        return self.s.collector_moments(gmean)

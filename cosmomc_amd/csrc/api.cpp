@@ -325,6 +325,40 @@ int cmbs_refresh_theory(cmbs_t *s, cmbs_theory_fn theory_fn, void *user, void *s
                    [&] { cmamd::sampler_refresh_theory(s, theory_fn, user, (hipStream_t)stream); });
 }
 
+int cmbs_collector_enable(cmbs_t *s, int sample_capacity) {
+    if (!s) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_collector_enable(s, sample_capacity); });
+}
+
+int cmbs_collector_add(cmbs_t *s, const int *steps, int n_steps, int min_sample_update, int check_burn, void *stream) {
+    if (!s || (n_steps > 0 && !steps)) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] {
+        cmamd::sampler_collector_add(s, steps, n_steps, min_sample_update, check_burn, (hipStream_t)stream);
+    });
+}
+
+int cmbs_collector_state_host(cmbs_t *s, int *start, int *count, int *burn_done, int *thin_fac) {
+    if (!s) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_collector_state_host(s, start, count, burn_done, thin_fac); });
+}
+
+int cmbs_collector_thin(cmbs_t *s, int limit, void *stream) {
+    if (!s) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_collector_thin(s, limit, (hipStream_t)stream); });
+}
+
+int cmbs_collector_moments(cmbs_t *s, const double *gmean, double *out, void *stream) {
+    if (!s || !out) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] { cmamd::sampler_collector_moments(s, gmean, out, (hipStream_t)stream); });
+}
+
+int cmbs_collector_limits(cmbs_t *s, const int *params, int n_check, double limfrac, double *out, void *stream) {
+    if (!s || (n_check > 0 && (!params || !out))) return CMBL_ERR_ARG;
+    return guarded(&s->last_error, [&] {
+        cmamd::sampler_collector_limits(s, params, n_check, limfrac, out, (hipStream_t)stream);
+    });
+}
+
 int cmbs_set_groups(cmbs_t *s, int n_groups) {
     if (!s) return CMBL_ERR_ARG;
     return guarded(&s->last_error, [&] { cmamd::sampler_set_groups(s, n_groups); });

@@ -109,6 +109,12 @@ struct cmbs {
     // (cmbs_step_theory / cmbs_step_drag); after a resume those rows must be
     // recomputed at the restored points (cmbs_refresh_theory) before stepping
     bool theory_moved = false, theory_stale = false;
+    // sample collector (collector.hip): per-walker Samples lists over the history ring
+    struct Collector {
+        cmamd::DevBuf samp, state, flag, wcount, steps;
+        int cap = 0;
+        bool enabled = false;
+    } coll;
     // likelihoods of one step run concurrently: likelihood i > 0 on its own
     // stream (forked from / joined to the caller's) with its own workspace
     hipStream_t like_streams[cmamd::MAXLIKE] = {};
@@ -136,4 +142,13 @@ void sampler_set_trial_theory(cmbs *s, int like_index, double *dl_end, long long
 void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_fn fn, void *user, hipStream_t stream);
 void sampler_step_theory(cmbs *s, int n_steps, cmbs_theory_fn fn, void *user, hipStream_t stream);
 void sampler_refresh_theory(cmbs *s, cmbs_theory_fn fn, void *user, hipStream_t stream);
+void sampler_collector_enable(cmbs *s, int samp_capacity);
+void sampler_collector_add(cmbs *s, const int *steps, int nsteps, int min_update, int check_burn, hipStream_t st);
+void sampler_collector_state_host(cmbs *s, int *start, int *count, int *burn, int *thin);
+void sampler_collector_thin(cmbs *s, int limit, hipStream_t st);
+void sampler_collector_moments(cmbs *s, const double *gmean, double *out, hipStream_t stream);
+void sampler_collector_limits(cmbs *s, const int *params, int ncheck, double limfrac, double *out, hipStream_t stream);
+size_t sampler_collector_bytes(const cmbs *s);
+void sampler_collector_save(cmbs *s, void *buf);
+void sampler_collector_load(cmbs *s, const void *buf);
 }

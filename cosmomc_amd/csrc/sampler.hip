@@ -880,8 +880,9 @@ __global__ __launch_bounds__(64 * HS_PH) void hist_cov_kernel(const double *hist
 // One block; each thread owns a fixed strided set of walkers and the partials
 // are combined in a fixed tree order, so the sums are deterministic.
 __global__ __launch_bounds__(256) void chain_moments_kernel(const double *means, const double *covs, int W, int n,
-                                                           double count, const double *gmean, double *out)
-{
+                                                           double count, const int *wcount, const double *gmean,
+                                                           double *out)
+{   // wcount (may be null): each walker's own sample count (collector windows)
     __shared__ double red[256];
     const int nout = gmean ? n * n : 2 + n + 2 * n * n;
     for (int o = 0; o < nout; o++) {
@@ -889,16 +890,17 @@ __global__ __launch_bounds__(256) void chain_moments_kernel(const double *means,
         for (int w = threadIdx.x; w < W; w += 256) {
             const double *m = means + (size_t)w * n;
             const double *C = covs + (size_t)w * n * n;
+            const double cw = wcount ? (double)wcount[w] : count;
             double v;
             if (gmean) {
                 const int i = o / n, j = o % n;
-                v = count * (m[i] - gmean[i]) * (m[j] - gmean[j]);
+                v = cw * (m[i] - gmean[i]) * (m[j] - gmean[j]);
             } else if (o == 0) {
-                v = count;
+                v = cw;
             } else if (o <= n) {
-                v = count * m[o - 1];
+                v = cw * m[o - 1];
             } else if (o <= n + n * n) {
-                v = count * C[o - 1 - n];
+                v = cw * C[o - 1 - n];
             } else if (o <= n + 2 * n * n) {
                 v = C[o - 1 - n - n * n];
             } else {
@@ -915,6 +917,13 @@ __global__ __launch_bounds__(256) void chain_moments_kernel(const double *means,
         if (threadIdx.x == 0) out[o] = red[0];
         __syncthreads();
     }
+}
+
+void chain_moments_launch(const double *means, const double *covs, int W, int n, double count, const int *wcount,
+                          const double *gmean, double *out, hipStream_t stream) {
+    hipLaunchKernelGGL(chain_moments_kernel, dim3(1), dim3(256), 0, stream, means, covs, W, n, count, wcount, gmean,
+                       out);
+    HIP_CHECK(hipGetLastError());
 }
 
 // ------------------------------------------------------------ host side
@@ -1628,9 +1637,7 @@ void sampler_chain_moments(cmbs *s, int first, int last, const double *gmean, do
     s->mom.grow((size_t)s->W * (n + n * n) * 8);
     double *means = s->mom.as<double>(), *covs = means + (size_t)s->W * n;
     sampler_history_stats(s, first, last, means, covs, stream);
-    hipLaunchKernelGGL(chain_moments_kernel, dim3(1), dim3(256), 0, stream, means, covs, s->W, n,
-                       (double)(last - first + 1), gmean, out);
-    HIP_CHECK(hipGetLastError());
+    chain_moments_launch(means, covs, s->W, n, (double)(last - first + 1), nullptr, gmean, out, stream);
 }
 
 void sampler_history_host(cmbs *s, int first, int count, double *out) {
@@ -1718,19 +1725,22 @@ void sampler_get_state_host(cmbs *s, double *P, double *cur_like, double *mult, 
 struct StateHeader {
     unsigned magic, version;
     int W, np, n_used, nblocks, all_n, slow_n, fast_n, R_total, ND, NI, n_like, theory_moved;
+    int coll_cap, pad;      // sample-collector ring (0: not enabled) appended after the terms
     long long num_drag;
 };
 static constexpr unsigned STATE_MAGIC = 0x53424d43u;   // "CMBS"
 
 size_t sampler_state_bytes(const cmbs *s) {
     const Rows &R = s->dc.rows;
-    return sizeof(StateHeader) + (size_t)(R.ND + s->likes.size()) * s->W * 8 + (size_t)R.NI * s->W * 4;
+    return sizeof(StateHeader) + (size_t)(R.ND + s->likes.size()) * s->W * 8 + (size_t)R.NI * s->W * 4 +
+           sampler_collector_bytes(s);
 }
 
 static StateHeader state_header(const cmbs *s) {
     const Rows &R = s->dc.rows;
     return StateHeader{STATE_MAGIC, 2u, s->W, s->np, s->n_used, s->nblocks, s->all_n, s->slow_n, s->fast_n,
-                       s->R_total, R.ND, R.NI, (int)s->likes.size(), s->theory_moved ? 1 : 0, s->num_drag};
+                       s->R_total, R.ND, R.NI, (int)s->likes.size(), s->theory_moved ? 1 : 0,
+                       s->coll.enabled ? s->coll.cap : 0, 0, s->num_drag};
 }
 
 void sampler_save_state(cmbs *s, void *buf, size_t bytes) {
@@ -1750,6 +1760,8 @@ void sampler_save_state(cmbs *s, void *buf, size_t bytes) {
     p += (size_t)R.NI * W * 4;
     if (!s->likes.empty())
         HIP_CHECK(hipMemcpy2D(p, W * 8, s->dc.cur_terms, ld * 8, W * 8, s->likes.size(), hipMemcpyDeviceToHost));
+    p += s->likes.size() * W * 8;
+    if (s->coll.enabled) sampler_collector_save(s, p);
 }
 
 void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
@@ -1760,7 +1772,7 @@ void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
     const StateHeader m = state_header(s);
     if (h.W != m.W || h.np != m.np || h.n_used != m.n_used || h.nblocks != m.nblocks || h.all_n != m.all_n ||
         h.slow_n != m.slow_n || h.fast_n != m.fast_n || h.R_total != m.R_total || h.ND != m.ND || h.NI != m.NI ||
-        h.n_like != m.n_like)
+        h.n_like != m.n_like || h.coll_cap != m.coll_cap)
         fail(CMBL_ERR_ARG,
              "state image is for a different sampler (W %d np %d blocks %d likelihoods %d; this one W %d np %d "
              "blocks %d likelihoods %d)", h.W, h.np, h.nblocks, h.n_like, m.W, m.np, m.nblocks, m.n_like);
@@ -1775,6 +1787,8 @@ void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
     p += (size_t)R.NI * W * 4;
     if (!s->likes.empty())
         HIP_CHECK(hipMemcpy2D(s->dc.cur_terms, ld * 8, p, W * 8, W * 8, s->likes.size(), hipMemcpyHostToDevice));
+    p += s->likes.size() * W * 8;
+    if (s->coll.enabled) sampler_collector_load(s, p);
     s->num_drag = h.num_drag;
     s->theory_moved = h.theory_moved != 0;
     s->theory_stale = s->theory_moved && !s->likes.empty();

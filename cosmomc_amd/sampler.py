@@ -206,6 +206,43 @@ class BatchedMCMC:
                                                out.data_ptr(), N.current_stream_ptr()))
         return out
 
+    # ---- sample collector (cmbs_collector_*; cosmomc_amd.converge.ChainCollector drives it)
+    def collector_enable(self, sample_capacity: int):
+        self._check(N.lib().cmbs_collector_enable(self._h, int(sample_capacity)))
+
+    def collector_add(self, steps, min_sample_update: int, check_burn: bool = True):
+        st = np.ascontiguousarray(steps, dtype=np.int32)
+        if st.size:
+            self._check(N.lib().cmbs_collector_add(self._h, st.ctypes.data, st.size, int(min_sample_update),
+                                                   int(check_burn), N.current_stream_ptr()))
+
+    def collector_state(self):
+        """Per-walker (start, count, burn_done, thin_fac) host int arrays."""
+        a = [np.empty(self.W, dtype=np.int32) for _ in range(4)]
+        self._check(N.lib().cmbs_collector_state_host(self._h, *[x.ctypes.data for x in a]))
+        return tuple(a)
+
+    def collector_thin(self, limit: int):
+        self._check(N.lib().cmbs_collector_thin(self._h, int(limit), N.current_stream_ptr()))
+
+    def collector_moments(self, gmean=None):
+        import torch
+        n = len(self.params_used)
+        out = torch.empty(2 + n + 2 * n * n if gmean is None else n * n, dtype=torch.float64, device="cuda")
+        g = None if gmean is None else torch.as_tensor(gmean, dtype=torch.float64, device="cuda").contiguous()
+        self._check(N.lib().cmbs_collector_moments(self._h, None if g is None else g.data_ptr(), out.data_ptr(),
+                                                   N.current_stream_ptr()))
+        return out
+
+    def collector_limits(self, params, limfrac: float):
+        """[W, len(params), 2] device tensor of (lower, upper) ConfidVal limits."""
+        import torch
+        p = np.ascontiguousarray(params, dtype=np.int32)
+        out = torch.empty((self.W, p.size, 2), dtype=torch.float64, device="cuda")
+        self._check(N.lib().cmbs_collector_limits(self._h, p.ctypes.data, p.size, float(limfrac), out.data_ptr(),
+                                                  N.current_stream_ptr()))
+        return out
+
     device = "cuda"
 
     def state(self):

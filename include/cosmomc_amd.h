@@ -252,6 +252,34 @@ int  cmbs_history_host(cmbs_t *s, int first, int count, double *out);
  * mean, MPICovMat, mean-of-covariances and covariance-of-means. */
 int  cmbs_chain_moments(cmbs_t *s, int first, int last, const double *gmean, double *out, void *stream);
 
+/* Sample collector (TMpiChainCollector_AddNewPoint, SampleCollector.f90:324-460):
+ * every walker's Samples list -- the thinned points the convergence test
+ * windows over -- kept on device as a ring of history step numbers (the points
+ * stay in the history ring).  cmbs_collector_enable after cmbs_enable_history;
+ * sample_capacity bounds each walker's list (Samples%Thin keeps it below
+ * the reference's 500000).  Part of the cmbs_save_state image once enabled. */
+int  cmbs_collector_enable(cmbs_t *s, int sample_capacity);
+/* AddNewPoint for history steps steps[0..n_steps) (increasing; host array)
+ * of every walker: sample_num++, keep every MPI_thin_fac-th, Samples%Add (points
+ * at logZero are skipped, MCMC.f90:146); with check_burn, the burn-in test
+ * (a used parameter changed > 51 times between consecutive samples once
+ * Count > 51, :352-377) and on burn DeleteRange to the last min_sample_update
+ * samples (:391-397).  Synchronises; fails if a list outgrows its capacity. */
+int  cmbs_collector_add(cmbs_t *s, const int *steps, int n_steps, int min_sample_update, int check_burn,
+                        void *stream);
+/* HOST copies of every walker's list start/count, Burn_done and MPI_thin_fac (any may be NULL). */
+int  cmbs_collector_state_host(cmbs_t *s, int *start, int *count, int *burn_done, int *thin_fac);
+/* Samples%Thin(2) and MPI_thin_fac * 2 for every walker whose Count > limit (:300-304). */
+int  cmbs_collector_thin(cmbs_t *s, int limit, void *stream);
+/* As cmbs_chain_moments, each walker over its own window: items Count/2 .. Count
+ * of its list, Count - Count/2 + 1 samples (:233-246), its weight in the sums. */
+int  cmbs_collector_moments(cmbs_t *s, const double *gmean, double *out, void *stream);
+/* CheckLimitsConverge's per-chain limits (:477-544): ConfidVal (samples.f90:70-110)
+ * of used parameters params[0..n_check) (0-based) over each walker's window at
+ * limfrac (MPI_Limit_Converge): out[W][n_check][2] = (lower, upper), device
+ * pointer; synchronises. */
+int  cmbs_collector_limits(cmbs_t *s, const int *params, int n_check, double limfrac, double *out, void *stream);
+
 /* Device pointers of the walker state (valid until destroy), walker-minor:
  * P [num_params][W], cur_like [W], mult [W] (double), num_accept [W] (int). */
 int  cmbs_state(cmbs_t *s, double **P, double **cur_like, double **mult, int **num_accept);

@@ -253,6 +253,30 @@ def gen_gr():
         json.dump(out, f, indent=0)
 
 
+# ConfidVal cases: (name, samples, columns, ix1, ix2, limfrac, seed)
+CONFID_CASES = [("confid_gauss_window", 401, 3, 200, 401, 0.025, 611), ("confid_all_0p05", 97, 2, 1, 97, 0.05, 612),
+                ("confid_ties", 120, 2, 60, 120, 0.025, 613), ("confid_small", 7, 1, 3, 7, 0.3, 614)]
+
+
+def gen_confid():
+    """TSampleList%ConfidVal of the compiled reference (CheckLimitsConverge's
+    per-chain limits) on seeded synthetic sample columns."""
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for name, ns, nc, ix1, ix2, frac, seed in CONFID_CASES:
+            v = syn.gaussians(seed, ns * nc).reshape(ns, nc)
+            if "ties" in name:
+                v = np.round(v * 3) / 3                  # many equal values
+            cfg = f"{ns} {nc} {ix1} {ix2} {frac!r}\n{_fmt(v)}\n"
+            lines = [x for x in run_rng("confid", cfg, td) if x.strip()]
+            lims = [[float(a) for a in l.split()] for l in lines]
+            out[name] = {"samples": ns, "columns": nc, "ix1": ix1, "ix2": ix2, "limfrac": frac, "seed": seed,
+                         "ties": "ties" in name, "limits": lims}
+            print(f"{name}: {lims[0]}")
+    with open(os.path.join(GOLDEN, "confid_ref.json"), "w") as f:
+        json.dump(out, f, indent=0)
+
+
 # CMBlikes cases on the reference's own data (tests/golden/refdata.tar.xz):
 # (name, tag, dataset, overrides, walkers, lmax, nuisance kind)
 LENS = "planck_lensing_2018/smicadx12_Dec5_ftl_mv2_ndclpp_p_teb_consext8.dataset"
@@ -411,6 +435,8 @@ if __name__ == "__main__":
         gen_rng()
     if not only or "gr" in only:
         gen_gr()
+    if not only or "confid" in only:
+        gen_confid()
     if not only or "cmblikes" in only:
         gen_cmblikes()
     if not only or "sptpol" in only:

@@ -224,3 +224,56 @@ def move_done_rows(like0, P0, accept, cur_like, P, burn_in=2, thin=1):
             mult += 1.0
         cur_l, cur_p = float(cur_like[k]), np.asarray(P[k], dtype=np.float64)
     return rows, (max_like, max_p)
+
+
+def confid_val(values, limfrac, ix1=None, ix2=None):
+    """TSampleList%ConfidVal (samples.f90:70-110) of one column: sort items
+    ix1..ix2 (1-based, inclusive), interpolate the order statistics at
+    pos = (samps-1)*limfrac + 1 and (samps-1)*(1-limfrac) + 1."""
+    v = np.asarray(values, dtype=np.float64)
+    b0 = 1 if ix1 is None else ix1
+    t0 = v.size if ix2 is None else ix2
+    x = np.sort(v[b0 - 1:t0])
+    samps = t0 - b0 + 1
+    out = []
+    for frac in (limfrac, 1.0 - limfrac):
+        pos = (samps - 1) * frac + 1
+        b = max(int(pos), 1)
+        val = x[b - 1]
+        if b < samps and pos > b:
+            d = pos - b
+            val = val * (1 - d) + d * x[b]
+        out.append(val)
+    return out[0], out[1]
+
+
+def collector_samples(rows, steps, min_update, check_burn=True, thin=1, state=None):
+    """One chain's TMpiChainCollector Samples list (SampleCollector.f90:324-397)
+    restated item by item: rows[t] = (P_used..., like) of history step t;
+    AddNewPoint at each step in `steps` (logZero points skipped, MCMC.f90:146):
+    sample_num++, keep every thin-th, Add, burn-in test once Count > 51
+    (every parameter changed > 51 times between consecutive items), then
+    DeleteRange(1, Count - min_update).  state (dict, updated in place):
+    items (history steps), sample_num, burn, changes."""
+    st = state if state is not None else {"items": [], "sample_num": 0, "burn": False, "changes": None}
+    n = rows.shape[1] - 1
+    for t in steps:
+        if rows[t, n] == 1e30:
+            continue
+        st["sample_num"] += 1
+        if st["sample_num"] % thin != 0:
+            continue
+        st["items"].append(t)
+        cnt = len(st["items"])
+        if st["burn"] or not check_burn or cnt <= 51:
+            continue
+        if st["changes"] is None:
+            st["changes"] = np.zeros(n, dtype=int)
+        a, b = rows[st["items"][-1], :n], rows[st["items"][-2], :n]
+        st["changes"] += (a != b)
+        if np.all(st["changes"] > 51):
+            st["burn"] = True
+            if cnt > min_update:
+                del st["items"][:cnt - min_update]
+            st["changes"] = None
+    return st

@@ -8,6 +8,8 @@
 !   mode "stream" : ranmar / Gaussian1 / randexp1 / RandIndices / RandRotationD
 !   mode "gr"     : GelmanRubinEvalues (samples.f90:41-67) on a given
 !                   (mean-of-covariances, covariance-of-means) pair
+!   mode "confid" : TSampleList%ConfidVal (samples.f90:70-110), the per-chain
+!                   limits of CheckLimitsConverge (SampleCollector.f90:515-517)
 !   mode "chain"  : (fast_only = 2: TFastDraggingSampler_GetNewSample,
 !                   MCMC.f90:338-452, restated inline on the reference's
 !                   BlockedProposer GetProposalSlow / GetProposalFastDelta)
@@ -30,7 +32,7 @@ program rng_harness
     use GeneralTypes
     use MatrixUtils
     use propose
-    use Samples, only: GelmanRubinEvalues
+    use Samples, only: GelmanRubinEvalues, TSampleList
     use BaseParameters
     use CalcLike
     implicit none
@@ -49,7 +51,9 @@ program rng_harness
     real(mcp), allocatable :: cend(:), cstart(:), tend(:), tstart(:), delta(:)
     real(mcp) :: cendlike, cstartlike, elike, slike, sum_s, sum_e, frac, cintlike, intlike, mult
     integer :: num_drag, num_fast, interp, istep
-    integer :: n_used, incl_fixed, nlin
+    integer :: n_used, incl_fixed, nlin, ix1, ix2
+    Type(TSampleList) :: SL
+    real(mcp) :: limfrac, lower, upper
     Type(TGenericLikeCalculator) :: Calc
     Type(TCalculationAtParamPoint) :: Pt
 
@@ -78,6 +82,19 @@ program rng_harness
         accpt = GelmanRubinEvalues(cov, mcov, evals, n)
         write(u_out, '(I2)') merge(1, 0, accpt)
         if (accpt) write(u_out, '(ES25.17)') evals
+    case ('confid')
+        open(newunit=u_in, file=trim(cfg), status='old')
+        read(u_in, *) n, nidx, ix1, ix2, limfrac
+        allocate(R(nidx, n))
+        read(u_in, *) ((R(j, i), j=1,nidx), i=1,n)
+        close(u_in)
+        do i = 1, n
+            call SL%Add(R(:, i))
+        end do
+        do j = 1, nidx
+            call SL%ConfidVal(j, limfrac, ix1, ix2, lower, upper)
+            write(u_out, '(2ES25.17)') lower, upper
+        end do
     case ('stream')
         open(newunit=u_in, file=trim(cfg), status='old')
         read(u_in, *) ij, kl, n, nidx, nrot

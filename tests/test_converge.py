@@ -129,3 +129,19 @@ def test_multirank_exchange_gloo(gr_golden, world):
         assert R == pytest.approx(case["R"], rel=1e-9)
         np.testing.assert_allclose(pc, case["propose_cov"], rtol=1e-11, atol=1e-15)
         np.testing.assert_allclose(mc, case["meanscov"], rtol=1e-9, atol=1e-15)
+
+
+def test_confid_val_restatement_vs_reference():
+    """pyoracle.confid_val == the compiled TSampleList%ConfidVal (samples.f90:70-110)."""
+    import pyoracle as po
+    from conftest import load_golden
+    from cosmomc_amd import synthetic as syn
+    g = load_golden("confid_ref.json")
+    for name, c in g.items():
+        v = syn.gaussians(c["seed"], c["samples"] * c["columns"]).reshape(c["samples"], c["columns"])
+        if c["ties"]:
+            v = np.round(v * 3) / 3
+        for j in range(c["columns"]):
+            lo, hi = po.confid_val(v[:, j], c["limfrac"], c["ix1"], c["ix2"])
+            assert lo == pytest.approx(c["limits"][j][0], rel=1e-14, abs=1e-15), name
+            assert hi == pytest.approx(c["limits"][j][1], rel=1e-14, abs=1e-15), name

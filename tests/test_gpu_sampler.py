@@ -467,3 +467,42 @@ def test_chain_files_from_history(tmp_path):
         assert np.all(np.any(np.diff(c[:, 2:], axis=0) != 0, axis=1))
         np.testing.assert_allclose(open_runs[w][0][1:], P[w], rtol=1e-15)
         assert open_runs[w][0][0] == pytest.approx(like[w], rel=1e-15)
+
+
+def test_interleaved_nuisance_indices(tmp_path):
+    """Two likelihoods whose nuisance_indices are not contiguous and not in
+    parameter order (GeneralTypes.f90:642-646): plik_lite TTTEEE reads P(4),
+    plik_lite TT reads P(2); the fixed parameters between them are never
+    passed.  Every walker's CurLike and per-likelihood terms equal the oracle's
+    at its final point."""
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    data = syn.make_plik_lite(12345)
+    ds = data.write(str(tmp_path))
+    l1 = NativeCMBLikelihood("PLIK_LITE", ds)
+    l2 = NativeCMBLikelihood("PLIK_LITE", ds, {"use_cl": "TT"})
+    l1.nuisance_indices, l2.nuisance_indices = [4], [2]
+    W, steps = 130, 30
+    th = syn.walker_theory(W, seed=21, n_fields=3)
+    dl = torch.tensor(th, device="cuda")
+    P0 = np.array([7.0, 1.0, -3.0, 1.0, 5.0])
+    pmin = np.array([7.0, 0.9, -3.0, 0.9, 5.0])
+    pmax = np.array([7.0, 1.1, -3.0, 1.1, 5.0])
+    pm, ps = np.array([0, 1.0, 0, 1.0, 0]), np.array([0, 0.0025, 0, 0.003, 0])
+    s = BatchedMCMC(W, 5, [2, 4], [[1], [2]], 0, pmin, pmax, pm, ps, seed_ij=31, seed_kl=32)
+    s.set_covariance(np.diag([0.002 ** 2, 0.002 ** 2]))
+    s.add_likelihood(l1, dl)
+    s.add_likelihood(l2, dl)
+    s.enable_history(steps)
+    s.set_start(np.tile(P0, (W, 1)))
+    s.step(steps, fast_only=True)
+    P, lk, _, nacc = s.state()
+    assert np.all(nacc > 0)
+    terms = s.history_terms(steps - 1, 1)[0]
+    o1, o2 = po.PlikLite(data), po.PlikLite(data, use_cl="TT")
+    for w in (0, 1, 64, 129):
+        t1, t2 = o1.loglike(th[w], P[w, 3]), o2.loglike(th[w], P[w, 1])
+        pri = 0.5 * (((P[w, 1] - 1) / 0.0025) ** 2 + ((P[w, 3] - 1) / 0.003) ** 2)
+        assert terms[0, w] == pytest.approx(t1, rel=1e-9)
+        assert terms[1, w] == pytest.approx(t2, rel=1e-9)
+        assert lk[w] == pytest.approx(t1 + t2 + pri, rel=1e-9)
