@@ -323,7 +323,7 @@ class _CollectorMoments:
 
     def __init__(self, sampler):
         self.s = sampler
-        self.device = "cuda"
+        self.device = getattr(sampler, "device", "cuda")
 
     def chain_moments(self, first, last, gmean=None):
         return self.s.collector_moments(gmean)

@@ -145,3 +145,60 @@ def test_confid_val_restatement_vs_reference():
             lo, hi = po.confid_val(v[:, j], c["limfrac"], c["ix1"], c["ix2"])
             assert lo == pytest.approx(c["limits"][j][0], rel=1e-14, abs=1e-15), name
             assert hi == pytest.approx(c["limits"][j][1], rel=1e-14, abs=1e-15), name
+
+
+def _collector_run(W_total, world, rank, q):
+    """ChainCollector over FakeCollectorSampler walkers [rank*W, (rank+1)*W):
+    returns the (history step, R, Count of walker 0) of every exchange."""
+    from collector_fake import FakeCollectorSampler
+    from cosmomc_amd.converge import ChainCollector, CollectorSettings
+    W = W_total // world
+    s = FakeCollectorSampler(W, first_walker=rank * W)
+    st = CollectorSettings(MPI_R_Stop=0.02, MPI_Sample_update_freq=5, MPI_Check_Limit_Converge=True,
+                           MPI_Limit_Converge_Err=0.5)
+    col = ChainCollector(s, st, num_slow=2, num_fast=1, sample_capacity=100000)
+    log = []
+    while s.history_count() < 1500 and not col.done:
+        s.step(col.next_block())
+        r = col.process()
+        if r is not None:
+            log.append((s.history_count(), r.R, col.count0, bool(r.converged)))
+    q.put((rank, log, col.burn0, col.update_freq))
+
+
+def _collector_rank(rank, world, port, W_total, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        _collector_run(W_total, world, rank, q)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_chain_collector_two_ranks_match_one(tmp_path):
+    """ChainCollector sharded over 2 gloo ranks (all_burn and the minimum
+    count as all-reduces, walker 0 on rank 0 triggering) exchanges at the same
+    steps with the same R-1 as one rank holding every walker; burn-in scales
+    the update frequency by num_params_used; CheckLimitsConverge ends the run."""
+    import queue as _q
+    import torch.multiprocessing as mp
+    W_total = 16
+    q1 = _q.Queue()
+    _collector_run(W_total, 1, 0, q1)
+    _, ref_log, burn0, freq = q1.get()
+    assert burn0 and freq == 15 and len(ref_log) > 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_collector_rank, args=(r, 2, port, W_total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, log, _, _ in res:
+        assert [x[0] for x in log] == [x[0] for x in ref_log]
+        assert [x[2] for x in log] == [x[2] for x in ref_log]
+        np.testing.assert_allclose([x[1] for x in log], [x[1] for x in ref_log], rtol=1e-9)
+        assert [x[3] for x in log] == [x[3] for x in ref_log]
