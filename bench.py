@@ -126,16 +126,51 @@ def build_problem(W, rank, tmpdir, groups=1, lensing=True):
     return smp, likes, theory, names
 
 
+def run_to_convergence(smp, num_slow, num_fast, seconds, world, cap, fast_only=True):
+    """R-1 vs wall-clock with the reference's collector logic (ChainCollector:
+    per-walker burn-in, all_burn, MPI_Min_Sample_Update = 50 + 4 num_slow +
+    5 num_fast and update frequency 40 x num_params_used after burn-in,
+    walker-0 triggered exchanges, SampleCollector.f90:324-460) and proposal
+    learning, until R-1 < 0.01 twice running or `seconds` pass.  Every rank
+    steps the same blocks (ChainCollector.next_block is rank-agreed)."""
+    import torch
+    from cosmomc_amd.converge import ChainCollector, CollectorSettings
+    smp.enable_history(cap)
+    col = ChainCollector(smp, CollectorSettings(MPI_R_Stop=0.01, covariance_is_diagonal=True), num_slow=num_slow,
+                         num_fast=num_fast, sample_capacity=cap)
+    trace, t0, done_at = [], time.perf_counter(), None
+    while smp.history_count() + col.next_block() <= cap:
+        smp.step(col.next_block(), fast_only=fast_only)
+        r = col.process()
+        el = time.perf_counter() - t0
+        if r is not None:
+            trace.append([round(el, 4), smp.history_count(), r.R])
+            if r.update_proposal:
+                smp.set_covariance(r.propose_cov)
+            if r.converged:
+                done_at = el
+                break
+        stop = el > seconds
+        if world > 1:
+            import torch.distributed as dist
+            flag = torch.tensor([1.0 if stop else 0.0], dtype=torch.float64, device="cuda")
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            stop = flag.item() > 0
+        if stop:
+            break
+    return {"target_r_minus_1": 0.01, "min_sample_update": col.min_update, "update_freq": col.update_freq,
+            "converged_wall_s": done_at, "trace_wall_s_steps_R": trace}
+
+
 def convergence_run(W, rank, world, tmpdir, seconds, lensing=True):
     """R-1 vs wall-clock (the metric's second half): every walker samples the
     same posterior -- one shared cached slow point (theory stride 0), calPlanck
     fast, plik_lite (+ lensing) + the calPlanck prior -- from an overdispersed
-    start; every MPI_Sample_update_freq samples the GPUs exchange chain moments
-    (ConvergenceExchange: all_reduce over RCCL) and learn the proposal,
-    until R-1 < 0.01 twice in a row (SampleCollector.f90:289-299) or time out."""
+    start; the collector's exchanges (ChainCollector: all_reduce over RCCL)
+    learn the proposal until R-1 < 0.01 twice in a row
+    (SampleCollector.f90:289-299) or time out."""
     import torch
     from cosmomc_amd import synthetic as syn
-    from cosmomc_amd.converge import CollectorSettings, ConvergenceExchange, reference_window
     from cosmomc_amd.likelihood import NativeCMBLikelihood
     from cosmomc_amd.sampler import BatchedMCMC
     likes = [NativeCMBLikelihood("PLIK_LITE", syn.make_plik_lite(12345).write(tmpdir))]
@@ -148,8 +183,6 @@ def convergence_run(W, rank, world, tmpdir, seconds, lensing=True):
     pmin[6], pmax[6] = 0.9, 1.1
     pm, ps = np.zeros(7), np.zeros(7)
     pm[6], ps[6] = 1.0, 0.0025
-    steps_block = 40                                   # MPI_Sample_update_freq x num_params_used (1)
-    cap = 20000
     smp = BatchedMCMC(W, 7, [7], [[1]], 0, pmin, pmax, pm, ps, propose_scale=2.4, seed_ij=2002 + rank,
                       seed_kl=9373, first_walker=rank * W)
     smp.set_covariance(np.array([[0.0025 ** 2]]))
@@ -160,31 +193,10 @@ def convergence_run(W, rank, world, tmpdir, seconds, lensing=True):
     start = np.tile(P0, (W, 1))
     start[:, 6] = 1.0 + 0.01 * syn.gaussians(77 + rank, W)
     smp.set_start(start)
-    smp.enable_history(cap)
-    ex = ConvergenceExchange(1, CollectorSettings(MPI_R_Stop=0.01, MPI_Min_Sample_Update=55))
-    trace, t0, done_at = [], time.perf_counter(), None
-    while smp.history_count() + steps_block <= cap:
-        smp.step(steps_block, fast_only=True)
-        r = ex.update_cov_and_check_converge(smp, *reference_window(smp.history_count()))
-        el = time.perf_counter() - t0
-        trace.append([round(el, 4), smp.history_count(), r.R])
-        if r.update_proposal:
-            smp.set_covariance(r.propose_cov)
-        if r.converged:
-            done_at = el
-            break
-        if world > 1:                                  # every rank must leave the exchange loop together
-            import torch.distributed as dist
-            flag = torch.tensor([1.0 if el > seconds else 0.0], dtype=torch.float64, device="cuda")
-            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-            if flag.item() > 0:
-                break
-        elif el > seconds:
-            break
-    return {"workload": "plik_lite_TTTEEE" + (" + lensing" if lensing else "") + " on one shared slow point, "
-                        "calPlanck fast, overdispersed start (1 +- 0.01)",
-            "walkers_total": W * world, "target_r_minus_1": 0.01, "exchange_every_steps": steps_block,
-            "converged_wall_s": done_at, "trace_wall_s_steps_R": trace}
+    out = run_to_convergence(smp, 0, 1, seconds, world, 20000)
+    out.update({"workload": "plik_lite_TTTEEE" + (" + lensing" if lensing else "") + " on one shared slow point, "
+                            "calPlanck fast, overdispersed start (1 +- 0.01)", "walkers_total": W * world})
+    return out
 
 
 def kernel_profile(smp, steps):
@@ -218,7 +230,6 @@ def config4_run(W, rank, world, tmpdir, seconds, steps=200):
     seconds > 0, R-1 vs wall-clock with the exchange every 40 x 21 samples."""
     import torch
     from cosmomc_amd import synthetic as syn
-    from cosmomc_amd.converge import CollectorSettings, ConvergenceExchange, reference_window
     from cosmomc_amd.likelihood import NativeCMBLikelihood
     from cosmomc_amd.sampler import BatchedMCMC
     n = 21
@@ -264,32 +275,7 @@ def config4_run(W, rank, world, tmpdir, seconds, steps=200):
            "walkers_total": W * world, "evals_per_s": W * world * steps / dt, "ms_per_step": dt / steps * 1e3,
            "avg_kernel_us": kernel_profile(smp, 50)}
     if seconds > 0:
-        steps_block = 40 * n
-        cap = 60 * steps_block
-        smp.enable_history(cap)
-        ex = ConvergenceExchange(n, CollectorSettings(MPI_R_Stop=0.01, MPI_Min_Sample_Update=55,
-                                                      covariance_is_diagonal=True))
-        trace, t0, done_at = [], time.perf_counter(), None
-        while smp.history_count() + steps_block <= cap:
-            smp.step(steps_block, fast_only=True)
-            r = ex.update_cov_and_check_converge(smp, *reference_window(smp.history_count()))
-            el = time.perf_counter() - t0
-            trace.append([round(el, 3), smp.history_count(), r.R])
-            if r.update_proposal:
-                smp.set_covariance(r.propose_cov)
-            if r.converged:
-                done_at = el
-                break
-            stop = el > seconds
-            if world > 1:
-                import torch.distributed as dist
-                flag = torch.tensor([1.0 if stop else 0.0], dtype=torch.float64, device="cuda")
-                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-                stop = flag.item() > 0
-            if stop:
-                break
-        out.update({"target_r_minus_1": 0.01, "exchange_every_steps": steps_block, "converged_wall_s": done_at,
-                    "trace_wall_s_steps_R": trace})
+        out.update(run_to_convergence(smp, 0, n, seconds, world, 60 * 40 * n))
     return out
 
 
@@ -308,7 +294,6 @@ def config5_run(W, rank, world, tmpdir, seconds, steps=100):
     wall-clock with the cross-GPU exchange every 40 x n_used samples."""
     import torch
     from cosmomc_amd import synthetic as syn
-    from cosmomc_amd.converge import CollectorSettings, ConvergenceExchange, reference_window
     from cosmomc_amd.likelihood import NativeCMBLikelihood
     from cosmomc_amd.sampler import BatchedMCMC
     rd = extract_refdata(os.path.join(tmpdir, "c5"))
@@ -359,32 +344,7 @@ def config5_run(W, rank, world, tmpdir, seconds, steps=100):
            "walkers_total": W * world, "evals_per_s": W * world * steps / dt, "ms_per_step": dt / steps * 1e3,
            "avg_kernel_us": kernel_profile(smp, 20)}
     if seconds > 0:
-        steps_block = 40 * len(used)                   # MPI_Sample_update_freq (SampleCollector.f90:399-403)
-        cap = 100 * steps_block
-        smp.enable_history(cap)
-        ex = ConvergenceExchange(len(used), CollectorSettings(MPI_R_Stop=0.01, MPI_Min_Sample_Update=55,
-                                                              covariance_is_diagonal=True))
-        trace, t0, done_at = [], time.perf_counter(), None
-        while smp.history_count() + steps_block <= cap:
-            smp.step(steps_block, fast_only=True)
-            r = ex.update_cov_and_check_converge(smp, *reference_window(smp.history_count()))
-            el = time.perf_counter() - t0
-            trace.append([round(el, 3), smp.history_count(), r.R])
-            if r.update_proposal:
-                smp.set_covariance(r.propose_cov)
-            if r.converged:
-                done_at = el
-                break
-            stop = el > seconds
-            if world > 1:
-                import torch.distributed as dist
-                flag = torch.tensor([1.0 if stop else 0.0], dtype=torch.float64, device="cuda")
-                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-                stop = flag.item() > 0
-            if stop:
-                break
-        out.update({"target_r_minus_1": 0.01, "exchange_every_steps": steps_block, "converged_wall_s": done_at,
-                    "trace_wall_s_steps_R": trace})
+        out.update(run_to_convergence(smp, 0, len(used), seconds, world, 100 * 40 * len(used)))
     return out
 
 
