@@ -6,7 +6,7 @@ set -u
 mkdir -p gpurun_out
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 export PYTHONUNBUFFERED=1
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/gpu_tests.log
 ok $rc || exit $rc
 timeout -k 10 300 python bench.py "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err
