@@ -87,6 +87,7 @@ def lib():
         L.cmbl_clik_compute_batch.argtypes = [vp, i, vp, vp, ll, vp, vp, vp]
         L.cmbl_clik_workspace_size.argtypes = [vp, i]
         L.cmbl_clik_workspace_size.restype = sz
+        L.cmbl_status.argtypes = [vp, C.POINTER(i), i]
         L.cmbs_walker_seed.argtypes = [i, i, i, C.POINTER(i), C.POINTER(i)]
         L.cmbs_create.argtypes = [C.POINTER(CmbsConfig), C.POINTER(vp), C.c_char_p, sz]
         L.cmbs_destroy.argtypes = [vp]

@@ -180,6 +180,25 @@ int cmbl_loglike_batch_host(cmbl_t *h, int W, const double *dl, long long ld_fie
         HIP_CHECK(hipMemcpyAsync(pout, h->h_out.p, (size_t)W * 8, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         std::memcpy(out, pout, (size_t)W * 8);
+        int flags = 0;
+        if (h->like->status_buf.p) {
+            HIP_CHECK(hipMemcpy(&flags, h->like->status_buf.p, sizeof flags, hipMemcpyDeviceToHost));
+            if (flags) {
+                HIP_CHECK(hipMemset(h->like->status_buf.p, 0, sizeof flags));
+                cmamd::fail(CMBL_ERR_NUMERIC, "%s: HL eigensolve did not converge (status %d)", L.name.c_str(), flags);
+            }
+        }
+    });
+}
+
+int cmbl_status(cmbl_t *h, int *flags, int clear) {
+    if (!h || !h->like || !flags) return CMBL_ERR_ARG;
+    return guarded(&h->like->last_error, [&] {
+        *flags = 0;
+        if (!h->like->status_buf.p) return;
+        HIP_CHECK(hipDeviceSynchronize());
+        HIP_CHECK(hipMemcpy(flags, h->like->status_buf.p, sizeof(int), hipMemcpyDeviceToHost));
+        if (clear && *flags) HIP_CHECK(hipMemset(h->like->status_buf.p, 0, sizeof(int)));
     });
 }
 

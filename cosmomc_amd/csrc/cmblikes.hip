@@ -11,15 +11,17 @@
 //                                    gaussian: X_b = C - Chat_b
 //   -lnL         = (bigX^T C^-1 bigX + (ln cal / sigma)^2) / 2         (:1220-1225)
 //
-// Kernels:
-//   cmbl_bin_kernel   one 256-thread workgroup per walker: foreground SEDs,
-//                     per map pair the spectrum in LDS, every window column as
-//                     a wave dot product, then the binned Cls per (bin, cl);
-//                     gaussian writes bigX rows, HL writes the C matrices.
-//   cmbl_hl_kernel    one wave per (walker, bin): two symmetric
-//                     eigendecompositions (parallel-order cyclic Jacobi in
-//                     LDS) and the HL transform, writes the bigX entries.
-//   quadform_ksplit   bigX^T C^-1 bigX / 2 on the f64 MFMA (quadform.hip).
+// Kernels (DESIGN.md section 4):
+//   cmbl_bk_prologue        BK foreground SEDs and l profiles per walker
+//   cmbl_window_direct /    every window column as a dot product with one map
+//   cmbl_window_kernel /    spectrum: a skinny f64 MFMA GEMM over l chunks
+//   cmbl_window_group       (grouped map pairs for the BK foregrounds)
+//   cmbl_gauss_small_kernel gaussian datasets with <= 64 bandpowers: chi^2 in one kernel
+//   cmbl_reduce_kernel      binned C matrices / bigX rows
+//   cmbl_hl_rows_kernel<M>  the HL transform per (walker, bin): two symmetric
+//                           eigendecompositions by register-resident cyclic Jacobi
+//   cmbl_exact_kernel       like_approx = exact (unbinned): ExactChiSq per (walker, l)
+//   quadform_ksplit         bigX^T C^-1 bigX / 2 on the f64 MFMA (quadform.hip).
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -822,179 +824,18 @@ __global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev
     }
 }
 
-// ---------------------------------------------------------------- HL (one wave)
-// Symmetric eigen-decomposition of the m x m (m even, <= 16) LDS matrix A by
-// cyclic Jacobi in round-robin order: every round rotates m/2 disjoint (p, q)
-// pairs at once; lanes own matrix elements.  V accumulates the rotations
-// (eigenvector k in column k).  A and V are double-buffered (A, A2), (V, V2);
-// the result is left in A / V.
-__device__ void wave_jacobi(double *A, double *A2, double *V, double *V2, double *cs, int *partner, int m, int lane)
-{
-    const int mm = m * m;
-    for (int e = lane; e < mm; e += 64) V[e] = (e / m == e % m) ? 1.0 : 0.0;
-    __syncthreads();
-    for (int sweep = 0; sweep < 40; sweep++) {
-        // convergence: all off-diagonal elements negligible against their diagonals
-        bool big = false;
-        for (int e = lane; e < mm; e += 64) {
-            const int i = e / m, j = e % m;
-            if (i < j) {
-                const double a = A[e];
-                if (a != 0.0 && fabs(a) > 1e-18 * sqrt(fabs(A[i * m + i] * A[j * m + j]))) big = true;
-            }
-        }
-        if (!__any(big)) break;
-        for (int r = 0; r < m - 1; r++) {
-            // pairs of this round (circle method): k = 0: (r, m-1); k > 0: ((r+k)%(m-1), (r-k)%(m-1))
-            if (lane < m / 2) {
-                int p, q;
-                if (lane == 0) { p = r; q = m - 1; }
-                else { p = (r + lane) % (m - 1); q = (r - lane + (m - 1)) % (m - 1); }
-                if (p > q) { const int t = p; p = q; q = t; }
-                const double apq = A[p * m + q], app = A[p * m + p], aqq = A[q * m + q];
-                double cc = 1.0, ss = 0.0;
-                if (apq != 0.0 && fabs(apq) > 1e-300) {
-                    const double theta = (aqq - app) / (2.0 * apq);
-                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                    cc = 1.0 / sqrt(t * t + 1.0);
-                    ss = t * cc;
-                }
-                partner[p] = q; partner[q] = p;
-                cs[2 * p] = cc; cs[2 * p + 1] = -ss;   // J[p][p] = c, J[q][p] = -s
-                cs[2 * q] = cc; cs[2 * q + 1] = ss;    // J[q][q] = c, J[p][q] = s
-            }
-            __syncthreads();
-            // A' = J^T A J ; element (i, j) mixes rows {i, i'} and columns {j, j'}
-            for (int e = lane; e < mm; e += 64) {
-                const int i = e / m, j = e % m, ip = partner[i], jp = partner[j];
-                const double ci = cs[2 * i], si = cs[2 * i + 1], cj = cs[2 * j], sj = cs[2 * j + 1];
-                // column i of J: J[i][i] = ci, J[ip][i] = si
-                const double v = ci * (A[i * m + j] * cj + A[i * m + jp] * sj) + si * (A[ip * m + j] * cj + A[ip * m + jp] * sj);
-                A2[e] = v;
-                V2[e] = V[i * m + j] * cj + V[i * m + jp] * sj;
-            }
-            __syncthreads();
-            for (int e = lane; e < mm; e += 64) {
-                A[e] = A2[e];
-                V[e] = V2[e];
-            }
-            __syncthreads();
-        }
-    }
-}
-
-// C <- A B (n x n, row stride m), all in LDS
-__device__ inline void wave_matmul(double *C, const double *A, const double *B, int n, int m, int lane, bool transA,
-                                   bool transB)
-{
-    for (int e = lane; e < n * n; e += 64) {
-        const int i = e / n, j = e % n;
-        double s = 0.0;
-        for (int k = 0; k < n; k++) {
-            const double a = transA ? A[k * m + i] : A[i * m + k];
-            const double b = transB ? B[j * m + k] : B[k * m + j];
-            s += a * b;
-        }
-        C[i * m + j] = s;
-    }
-}
-
+// ---------------------------------------------------------------- HL
 struct HLDev {
     int n, m, nb, ncl, ncl_used, nX, Np;
     const double *chat;     // [nb][n][n]
     const double *cfhalf;   // [nb][n][n]
     const int *cl_use;
+    int *status;            // sticky CMBL_STATUS_* bits (cmbl_status)
 };
 
-__global__ __launch_bounds__(64) void cmbl_hl_kernel(HLDev h, const double *__restrict__ cmat, double *__restrict__ xrows,
-                                                    int W)
-{
-    // LDS sized by the padded matrix edge m (9 m^2 + 3 m doubles; 10.7 KB at
-    // m = 12 instead of 18.8 KB at the 16 x 16 maximum), so about twice as many
-    // of these latency-bound single-wave blocks are resident per CU
-    extern __shared__ double S[];
-    __shared__ int partner[CL_MAXMAPS];
-    const int lane = threadIdx.x;
-    const int w = blockIdx.x / h.nb, b = blockIdx.x % h.nb;
-    if (w >= W) return;
-    const int n = h.n, m = h.m, MM = m * m;
-    double *A = S, *A2 = S + MM, *U = S + 2 * MM, *V2 = S + 3 * MM, *T = S + 4 * MM, *R = S + 5 * MM;
-    double *Vb = S + 6 * MM, *Ch = S + 7 * MM, *Cf = S + 8 * MM;
-    double *cs = S + 9 * MM, *dg = cs + 2 * CL_MAXMAPS;
-    const double *cm = cmat + ((long long)w * h.nb + b) * h.ncl;
-    // C from its lower-triangle elements (ElementsToMatrix :950-965), padded to m with zeros
-    for (int e = lane; e < m * m; e += 64) {
-        const int i = e / m, j = e % m;
-        double v = 0.0;
-        if (i < n && j < n) {
-            const int a = i > j ? i : j, bb = i > j ? j : i;
-            v = cm[a * (a + 1) / 2 + bb];
-        }
-        A[e] = v;
-        Ch[e] = (i < n && j < n) ? h.chat[((long long)b * n + i) * n + j] : 0.0;
-        Cf[e] = (i < n && j < n) ? h.cfhalf[((long long)b * n + i) * n + j] : 0.0;
-    }
-    __syncthreads();
-    // (1) C = U diag U^T
-    wave_jacobi(A, A2, U, V2, cs, partner, m, lane);
-    if (lane < m) dg[lane] = A[lane * m + lane];
-    __syncthreads();
-    // (2) Rot = U^T Chat U, scaled by 1/sqrt(diag) on rows and columns (:878-889)
-    wave_matmul(T, Ch, U, n, m, lane, false, false);
-    __syncthreads();
-    wave_matmul(R, U, T, n, m, lane, true, false);
-    __syncthreads();
-    for (int e = lane; e < n * n; e += 64) {
-        const int i = e / n, j = e % n;
-        const int lo = i < j ? i : j, hi = i < j ? j : i;
-        double v = R[i * m + j];
-        v = v / sqrt(dg[lo]);
-        v = v / sqrt(dg[hi]);
-        R[i * m + j] = v;
-    }
-    __syncthreads();
-    // (3) Rot = U Rot U^T (:891)
-    wave_matmul(T, R, U, n, m, lane, false, true);
-    __syncthreads();
-    wave_matmul(A, U, T, n, m, lane, false, false);
-    __syncthreads();
-    for (int e = lane; e < m * m; e += 64) {
-        const int i = e / m, j = e % m;
-        if (i >= n || j >= n) A[e] = 0.0;
-    }
-    __syncthreads();
-    // (4) Rot = V diag V^T; g(x) = sign(sqrt(2 max(0, x - ln x - 1)), x - 1)  (:892-894)
-    wave_jacobi(A, A2, Vb, V2, cs, partner, m, lane);
-    if (lane < n) {
-        const double x = A[lane * m + lane];
-        const double g = sqrt(2 * fmax(0.0, x - log(x) - 1));
-        dg[lane] = (x - 1 >= 0) ? g : -g;
-    }
-    __syncthreads();
-    // (5) U = Cfhalf V ; C = U diag(g) U^T (:907-912)
-    wave_matmul(T, Cf, Vb, n, m, lane, false, false);
-    __syncthreads();
-    for (int e = lane; e < n * n; e += 64) {
-        const int i = e / n, j = e % n;
-        R[i * m + j] = T[i * m + j] * dg[j];
-    }
-    __syncthreads();
-    wave_matmul(A, R, T, n, m, lane, false, true);
-    __syncthreads();
-    // vecp = lower-triangle elements (MatrixToElements :917-931); bigX entries of this bin
-    double *x = xrows + (long long)w * h.Np + (long long)b * h.ncl_used;
-    for (int u = lane; u < h.ncl_used; u += 64) {
-        const int k = h.cl_use[u];
-        int i = 0;
-        while ((i + 1) * (i + 2) / 2 <= k) i++;
-        const int j = k - i * (i + 1) / 2;
-        x[u] = A[i * m + j];
-    }
-}
-
 // ------------------------------------------- HL, register-resident (16 lanes / matrix)
-// The same two cyclic-Jacobi eigensolves and HL transform as cmbl_hl_kernel
-// (CMBLikes_Transform :861-914), with the matrices in registers: lane r of a
+// The two symmetric eigensolves and HL transform of CMBLikes_Transform
+// (:861-914) by cyclic Jacobi, with the matrices in registers: lane r of a
 // 16-lane group owns row r of the working matrix and of the eigenvector
 // matrix, and a 64-lane block runs four (walker, bin) problems.  A Jacobi
 // round is a column rotation of the lane's own row (the round's (c, s) of
@@ -1074,15 +915,19 @@ __device__ __forceinline__ void hl_colrot_round(int rr, double (&A)[M], double (
 }
 
 // cyclic Jacobi of the group's M x M matrix (row r in A), eigenvectors in V (row r)
+static constexpr int HL_MAX_SWEEPS = 40;   // as DSYEV's own iteration limit, a cap that fails loudly
+
+// cyclic Jacobi of the group's M x M matrix (row r in A), eigenvectors in V (row r).
+// Returns true on the lanes whose row still fails the convergence test after
+// HL_MAX_SWEEPS sweeps (the caller marks that problem failed: NaN and a status bit).
 template <int M>
-__device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, int grp, int r, int lane,
-                               int max_sweeps)
+__device__ bool hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, int grp, int r, int lane)
 {
     const bool on = grp < HLRowsLds<M>::G;        // lanes past G*M idle
 #pragma unroll
     for (int k = 0; k < M; k++) V[k] = (k == r) ? 1.0 : 0.0;
-    for (int sweep = 0; sweep < max_sweeps; sweep++) {
-        // convergence (as cmbl_hl_kernel): every off-diagonal |a_rk| <= 1e-18 sqrt(|a_rr a_kk|) or 0;
+    for (int sweep = 0;; sweep++) {
+        // convergence: every off-diagonal |a_rk| <= 1e-18 sqrt(|a_rr a_kk|) or 0;
         // the diagonal and a_{r p} written here also serve round 0
         if (on) {
 #pragma unroll
@@ -1099,7 +944,8 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
             }
         }
         __syncthreads();
-        if (!__any(big)) break;        // wave-uniform: converged groups keep rotating by ~0
+        if (!__any(big)) return false;   // wave-uniform: converged groups keep rotating by ~0
+        if (sweep == HL_MAX_SWEEPS) return big;
 #pragma unroll 1
         for (int rr = 0; rr < M - 1; rr++) {
 #ifdef CMAMD_STAMPS
@@ -1162,7 +1008,7 @@ __device__ void hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
 
 template <int M>
 __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLDev h, const double *__restrict__ cmat,
-                                                         double *__restrict__ xrows, int W, int max_sweeps)
+                                                         double *__restrict__ xrows, int W)
 {
     __shared__ HLRowsLds<M> S;
     constexpr int G = HLRowsLds<M>::G;
@@ -1188,7 +1034,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
         A[j] = v;
     }
     // (1) C = U diag U^T
-    hl_jacobi_rows<M>(A, V, S, grp, r, lane, max_sweeps);
+    bool unconverged = hl_jacobi_rows<M>(A, V, S, grp, r, lane);
     const double dgr = hl_pick<M>(A, r);
     if (on) {
         S.dg[grp][r] = dgr;
@@ -1251,7 +1097,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
     }
     __syncthreads();
     // (4) Rot = V diag V^T; g(x) = sign(x - 1) sqrt(2 max(0, x - ln x - 1))  (:892-894)
-    hl_jacobi_rows<M>(A, V, S, grp, r, lane, max_sweeps);
+    unconverged = hl_jacobi_rows<M>(A, V, S, grp, r, lane) || unconverged;
     if (on) {
         const double x = hl_pick<M>(A, r);
         const double g = sqrt(2 * fmax(0.0, x - log(x) - 1));
@@ -1288,6 +1134,11 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
 #pragma unroll
         for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = A[k];
     __syncthreads();
+    // an eigensolve that hit the sweep cap fails its (walker, bin): NaN bigX entries
+    // (so -lnL is NaN) and a sticky status bit (cmbl_status); the reference stops the run
+    const unsigned long long gmask = ((1ull << M) - 1) << (on ? grp * M : 0);
+    const bool failed = on && (__ballot(unconverged) & gmask) != 0;
+    if (live && failed && r == 0) atomicOr(h.status, CMBL_STATUS_HL_NOCONV);
     // vecp = lower-triangle elements (MatrixToElements :917-931); bigX entries of this bin
     if (live) {
         double *x = xrows + (long long)w * h.Np + (long long)b * h.ncl_used;
@@ -1296,8 +1147,111 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
             int i = 0;
             while ((i + 1) * (i + 2) / 2 <= k) i++;
             const int j = k - i * (i + 1) / 2;
-            x[u] = S.rows[grp][0][i][j];
+            x[u] = failed ? __builtin_nan("") : S.rows[grp][0][i][j];
         }
+    }
+}
+
+// ------------------------------------------------------- exact (unbinned)
+// like_approx = exact: per l, C = MapCl(l) + N_l (n x n over the used maps) and
+// ExactChiSq (CMBlikes.f90:967-979)
+//   chi2_l = (2l+1) fksy (tr M - n - ln det M),  M = C^-1/2 Chat_l C^-1/2.
+// tr M = tr(C^-1 Chat) = |L^-1 R|_F^2 with C = L L^T and Chat = R R^T (R and
+// ln det Chat = 2 sum ln R_ii from the host), and ln det M = ln det Chat - ln det C,
+// so a thread needs one n x n Cholesky and a triangular solve instead of two
+// eigendecompositions.  A C that is not positive definite gives NaN (the
+// reference's C^-1/2 takes a negative eigenvalue to the power -1/2).
+struct ExactDev {
+    int n, ncl, lmin, lmax, bmin, nb, K;   // K: doubles per l row of tab
+    int field[10], cmb[10];                // per element of the lower triangle (ElementsToMatrix order)
+    const double *tab;                     // [nb][K]: N_l (ncl), R (ncl, lower packed), ln det Chat, (2l+1) fksy
+    double aberration, log_cal_prior;
+    int cal_index;
+};
+static constexpr int EXACT_MAXMAPS = 4;    // T, E, B, P
+static constexpr int EXACT_WPB = 4;        // walkers per 256-thread block: one wave each
+
+template <int N>
+__global__ __launch_bounds__(256) void cmbl_exact_kernel(ExactDev x, const double *__restrict__ dl, long long ld_field,
+                                                         long long ld_walker, const double *__restrict__ nuis,
+                                                         long long ld_nuis, double *__restrict__ out, int W)
+{
+    constexpr int NC = N * (N + 1) / 2;
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * EXACT_WPB + (threadIdx.x >> 6);
+    if (w >= W) return;                                   // wave-uniform
+    double calsq = 1.0;
+    if (x.cal_index >= 0) {
+        const double cal = nuis[(long long)w * ld_nuis + x.cal_index];
+        calsq = cal * cal;
+    }
+    const double *Dw = dl + (long long)w * ld_walker;
+    double acc = 0.0;
+    for (int b = lane; b < x.nb; b += 64) {
+        const int l = x.bmin + b;
+        const double *t = x.tab + (long long)b * x.K;
+        double C[NC];
+#pragma unroll
+        for (int e = 0; e < NC; e++) {                    // GetTheoryMapCls + AdaptTheoryForMaps :1022-1126
+            const double *Df = Dw + (long long)x.field[e] * ld_field;
+            double v = Df[l];
+            if (x.aberration != 0.0 && x.cmb[e]) {        // AddAberration :1062-1101
+                int la = l - 1, lb = l + 1;
+                if (l == x.lmin) { la = l; lb = l + 2; }
+                else if (l == x.lmax) { la = l - 2; lb = l; }
+                const double ea = la, eb = lb, el = l;
+                const double ca = Df[la] / (ea * (ea + 1)), cb = Df[lb] / (eb * (eb + 1));
+                const double deriv = 0.5 * (cb - ca);
+                v = v + x.aberration * (el * el * (el + 1) * deriv);
+            }
+            if (x.cal_index >= 0 && x.cmb[e]) v = v / calsq;
+            C[e] = v + t[e];                              // C + NoiseM(bin) :1200-1202
+        }
+        // C = L L^T (lower packed, in place); ln det C
+        double lndet_c = 0.0;
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            double d = C[j * (j + 1) / 2 + j];
+#pragma unroll
+            for (int k = 0; k < j; k++) d -= C[j * (j + 1) / 2 + k] * C[j * (j + 1) / 2 + k];
+            d = sqrt(d);                                  // NaN when C is not positive definite
+            C[j * (j + 1) / 2 + j] = d;
+            lndet_c += log(d);
+#pragma unroll
+            for (int i = j + 1; i < N; i++) {
+                double s = C[i * (i + 1) / 2 + j];
+#pragma unroll
+                for (int k = 0; k < j; k++) s -= C[i * (i + 1) / 2 + k] * C[j * (j + 1) / 2 + k];
+                C[i * (i + 1) / 2 + j] = s / d;
+            }
+        }
+        // tr(C^-1 Chat) = |L^-1 R|_F^2, column by column of R (lower triangular)
+        double tr = 0.0;
+#pragma unroll
+        for (int c = 0; c < N; c++) {
+            double y[N];
+#pragma unroll
+            for (int i = 0; i < N; i++) {
+                double s = (i >= c) ? t[x.ncl + i * (i + 1) / 2 + c] : 0.0;
+#pragma unroll
+                for (int k = 0; k < i; k++) s -= C[i * (i + 1) / 2 + k] * y[k];
+                y[i] = s / C[i * (i + 1) / 2 + i];
+                tr += y[i] * y[i];
+            }
+        }
+        const double lndet_m = t[2 * x.ncl] - 2.0 * lndet_c;
+        acc += t[2 * x.ncl + 1] * (tr - N - lndet_m);
+    }
+    // fixed-order wave reduction (deterministic)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) {
+        double chisq = acc;
+        if (x.log_cal_prior > 0 && x.cal_index >= 0) {   // :1222-1223
+            const double lc = log(nuis[(long long)w * ld_nuis + x.cal_index]) / x.log_cal_prior;
+            chisq = chisq + lc * lc;
+        }
+        out[w] = chisq / 2;
     }
 }
 
@@ -1380,7 +1334,9 @@ struct CMBLikes final : Like {
     bool has_map_names = false, bk = false;
     std::vector<std::string> map_names, used_map_order;
     std::vector<int> map_fields, use_map, require_map, map_used_index, map_required_index, required_order;
-    int approx = 0, nmaps = 0, nreq = 0, ncl = 0, ncl_used = 0;
+    int approx = 0, nmaps = 0, nreq = 0, ncl = 0, ncl_used = 0;   // approx: 1 HL, 2 gaussian, 3 exact
+    bool binned = true;
+    double fksy = 1.0;                                              // fullsky_exact_fksy
     int lmin = 0, lmax = 0, nbins = 0, bin_min = 1, bin_max = 0, nb = 0;
     double aberration = 0.0, log_cal_prior = -1.0;
     int cal_index = -1;
@@ -1620,7 +1576,7 @@ struct CMBLikes final : Like {
         std::string la = ini.str_required("like_approx");
         if (la == "HL") approx = 1;
         else if (la == "gaussian") approx = 2;
-        else if (la == "exact") fail(CMBL_ERR_UNSUPPORTED, "CMBlikes: like_approx = exact is not supported");
+        else if (la == "exact") approx = 3;
         else fail(CMBL_ERR_FORMAT, "CMBlikes: unknown like_approx %s", la.c_str());
         for (int i = 0; i < nm; i++) {
             nmaps += use_map[i];
@@ -1628,6 +1584,9 @@ struct CMBLikes final : Like {
         }
         if (nmaps < 1) fail(CMBL_ERR_FORMAT, "CMBlikes: no maps used");
         if (approx == 1 && nmaps > CL_MAXMAPS) fail(CMBL_ERR_UNSUPPORTED, "CMBlikes HL: at most %d maps", CL_MAXMAPS);
+        if (approx == 3 && nmaps > EXACT_MAXMAPS)
+            fail(CMBL_ERR_UNSUPPORTED, "CMBlikes exact: at most %d maps", EXACT_MAXMAPS);
+        if (approx == 3 && bk) fail(CMBL_ERR_UNSUPPORTED, "BKPLANCK with like_approx = exact is not supported");
         if (nreq > CL_MAXREQ) fail(CMBL_ERR_UNSUPPORTED, "CMBlikes: at most %d required maps", CL_MAXREQ);
         map_required_index.assign(nm, 0);
         map_used_index.assign(nm, 0);
@@ -1646,18 +1605,36 @@ struct CMBLikes final : Like {
         ncl = nmaps * (nmaps + 1) / 2;
         lmin = ini_int(ini, "cl_lmin", true, 0);
         lmax = ini_int(ini, "cl_lmax", true, 0);
-        if (!ini_logical(ini, "binned", false))
-            fail(CMBL_ERR_UNSUPPORTED, "CMBlikes: unbinned likelihoods are not supported (untested in the reference)");
-        nbins = ini_int(ini, "nbins", false, 0);
+        if (!ini.has("binned")) fail(CMBL_ERR_FORMAT, "CMBlikes: binned not given");   // Read_Logical('binned') :597
+        binned = ini_logical(ini, "binned", false);
         aberration = ini_double(ini, "aberration_coeff", 0.0);
-        bin_min = ini_int(ini, "use_min", false, 1);
-        bin_max = ini_int(ini, "use_max", false, nbins);
-        if (bin_min < 1 || bin_min > nbins || bin_max < bin_min || bin_max > nbins)
-            fail(CMBL_ERR_FORMAT, "CMBlikes: use_min/use_max outside 1..nbins");
+        if (binned) {
+            if (approx == 3) fail(CMBL_ERR_FORMAT, "CMBLikes: exact like cannot be binned!");   // :1185
+            nbins = ini_int(ini, "nbins", false, 0);
+            bin_min = ini_int(ini, "use_min", false, 1);
+            bin_max = ini_int(ini, "use_max", false, nbins);
+            if (bin_min < 1 || bin_min > nbins || bin_max < bin_min || bin_max > nbins)
+                fail(CMBL_ERR_FORMAT, "CMBlikes: use_min/use_max outside 1..nbins");
+        } else {
+            // unbinned (:601-605, :636-637): one "bin" per l; only the exact
+            // likelihood (the reference marks unbinned HL / gaussian untested)
+            if (approx != 3)
+                fail(CMBL_ERR_UNSUPPORTED, "CMBlikes: unbinned HL / gaussian likelihoods are not supported "
+                                           "(untested in the reference)");
+            if (nmaps != nreq) fail(CMBL_ERR_FORMAT, "CMBlikes: Unbinned must have required==used");   // :1188
+            nbins = lmax - lmin + 1;
+            bin_min = ini_int(ini, "use_min", false, lmin);
+            bin_max = ini_int(ini, "use_max", false, lmax);
+            if (bin_min < lmin || bin_min > lmax || bin_max < bin_min || bin_max > lmax)
+                fail(CMBL_ERR_FORMAT, "CMBlikes: use_min/use_max outside cl_lmin..cl_lmax");
+            if (lmax - lmin < 2 && aberration != 0.0)
+                fail(CMBL_ERR_FORMAT, "CMBlikes: aberration needs cl_lmax >= cl_lmin + 2");
+        }
         nb = bin_max - bin_min + 1;
-        read_bin_windows(ini, "bin_window", bw);
+        if (binned) read_bin_windows(ini, "bin_window", bw);
         read_cl_arr(ini, "cl_hat", clhat, false);
         if (approx == 1) read_cl_arr(ini, "cl_fiducial", clfid, false);
+        if (approx == 3) fksy = ini_double(ini, "fullsky_exact_fksy", 1.0);      // :645-648
         const bool includes_noise = ini_logical(ini, "cl_hat_includes_noise", false);
         bool have_noise = false;
         if (approx != 2 || includes_noise) {
@@ -1696,8 +1673,10 @@ struct CMBLikes final : Like {
                 std::copy(M.begin(), M.end(), cfh.begin() + (size_t)b * nmaps * nmaps);
             }
         }
-        read_covmat(ini);
+        if (approx != 3) read_covmat(ini);        // :726-728
         std::vector<double> fc;
+        if (!binned && ini.has("linear_correction_fiducial_file"))
+            fail(CMBL_ERR_UNSUPPORTED, "CMBlikes: linear corrections of an unbinned likelihood are not supported");
         if (read_cl_arr(ini, "linear_correction_fiducial", fc, true)) {
             fidcorr = fc;
             read_bin_windows(ini, "linear_correction_bin_window", cw);
@@ -1764,7 +1743,62 @@ struct CMBLikes final : Like {
                 bkm.push_back(m);
             }
         }
-        build_device(have_noise, chatM, cfh, bkm, bnu, bR, bdnu);
+        if (approx == 3) build_exact(chatM);
+        else build_device(have_noise, chatM, cfh, bkm, bnu, bR, bdnu);
+    }
+
+    // like_approx = exact: per-l table [nb][K] = N_l (ncl) | chol(Chat_l) (ncl) | ln det Chat_l | (2l+1) fksy
+    ExactDev xdev{};
+    DevBuf d_xtab;
+    void build_exact(const std::vector<double> &chatM) {
+        xdev.n = nmaps;
+        xdev.ncl = ncl;
+        xdev.lmin = lmin;
+        xdev.lmax = lmax;
+        xdev.bmin = bin_min;
+        xdev.nb = nb;
+        xdev.K = 2 * ncl + 2;
+        std::vector<double> tab((size_t)nb * xdev.K, 0.0);
+        for (int b = 0; b < nb; b++) {
+            double *t = &tab[(size_t)b * xdev.K];
+            for (int e = 0; e < ncl; e++) t[e] = clnoise[(size_t)b * ncl + e];
+            // Chat = R R^T (Matrix_Cholesky, as MatrixSym_LogDet :619-634 does for M)
+            const double *M = &chatM[(size_t)b * nmaps * nmaps];
+            std::vector<double> R((size_t)nmaps * nmaps, 0.0);
+            double lndet = 0.0;
+            for (int j = 0; j < nmaps; j++) {
+                double d = M[j * nmaps + j];
+                for (int k = 0; k < j; k++) d -= R[j * nmaps + k] * R[j * nmaps + k];
+                if (!(d > 0)) fail(CMBL_ERR_NUMERIC, "CMBlikes exact: cl_hat at l = %d is not positive definite", bin_min + b);
+                d = std::sqrt(d);
+                R[j * nmaps + j] = d;
+                lndet += std::log(d);
+                for (int i = j + 1; i < nmaps; i++) {
+                    double v = M[i * nmaps + j];
+                    for (int k = 0; k < j; k++) v -= R[i * nmaps + k] * R[j * nmaps + k];
+                    R[i * nmaps + j] = v / d;
+                }
+            }
+            for (int i = 0, q = 0; i < nmaps; i++)
+                for (int j = 0; j <= i; j++, q++) t[ncl + q] = R[i * nmaps + j];
+            t[2 * ncl] = 2.0 * lndet;
+            t[2 * ncl + 1] = (2.0 * (bin_min + b) + 1.0) * fksy;
+        }
+        // element (i, j), i >= j, of the lower triangle -> theory field (MapPair_to_Theory_i_j :284-299)
+        for (int i = 1, q = 0; i <= nmaps; i++)
+            for (int j = 1; j <= i; j++, q++) {
+                int f1 = map_fields[required_order[i - 1] - 1], f2 = map_fields[required_order[j - 1] - 1];
+                if (f2 > f1) std::swap(f1, f2);
+                xdev.field[q] = f1 * (f1 - 1) / 2 + (f2 - 1);
+                xdev.cmb[q] = (f1 <= 3 && f2 <= 3);
+                max_field = std::max(max_field, xdev.field[q]);
+            }
+        d_xtab.alloc(tab.size() * 8);
+        d_xtab.upload(tab.data(), tab.size() * 8);
+        xdev.tab = d_xtab.as<double>();
+        xdev.aberration = aberration;
+        xdev.cal_index = cal_index;
+        xdev.log_cal_prior = log_cal_prior;
     }
 
     std::vector<double> invcov;
@@ -1855,7 +1889,7 @@ struct CMBLikes final : Like {
         const int nseg = (L + SEG - 1) / SEG;
         // BK foregrounds without aberration: grouped-pair items (cmbl_window_group),
         // when no pair has more than 16 window columns
-        use_group = bk && aberration == 0.0 && !std::getenv("CMAMD_BK_STAGED");
+        use_group = bk && aberration == 0.0;
         if (use_group) {
             std::vector<int> per_pair(pairs.size(), 0);
             for (auto &cc : cols)
@@ -2093,6 +2127,7 @@ struct CMBLikes final : Like {
         hl.chat = d_hlchat.as<double>();
         hl.cfhalf = d_hlcf.as<double>();
         hl.cl_use = d_cluse.as<int>();
+        hl.status = status_word();
     }
 
     // workspace: quadratic form | partial dots [rows][W] | C matrices [W][nE] (HL) |
@@ -2109,7 +2144,7 @@ struct CMBLikes final : Like {
         o.total = o.add + al((size_t)W * 8);
         return o;
     }
-    size_t workspace_size(int W) const override { return layout(W).total; }
+    size_t workspace_size(int W) const override { return approx == 3 ? 256 : layout(W).total; }
 
     void loglike_batch(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis,
                        long long ld_nuis, double *out, void *ws, hipStream_t stream) override {
@@ -2121,6 +2156,24 @@ struct CMBLikes final : Like {
         if (!ws) {
             own_ws.grow(workspace_size(W));
             ws = own_ws.p;
+        }
+        if (approx == 3) {
+            timed_launch("cmbl_exact_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+                const dim3 g((W + EXACT_WPB - 1) / EXACT_WPB), bl(256);
+                const double *nu = nuis ? nuis : dl;   // never read without a calibration parameter
+                switch (nmaps) {
+#define CMBL_EXACT(N)                                                                                     \
+    case N:                                                                                               \
+        hipExtLaunchKernelGGL(cmbl_exact_kernel<N>, g, bl, 0, stream, e0, e1, 0, xdev, dl, ld_field, ld_walker, \
+                              nu, ld_nuis, out, W);                                                       \
+        break;
+                    CMBL_EXACT(1) CMBL_EXACT(2) CMBL_EXACT(3) CMBL_EXACT(4)
+#undef CMBL_EXACT
+                    default: break;
+                }
+            });
+            HIP_CHECK(hipGetLastError());
+            return;
         }
         const WsLayout o = layout(W);
         char *base = static_cast<char *>(ws);
@@ -2143,7 +2196,6 @@ struct CMBLikes final : Like {
         // 16-byte theory loads need aligned rows and even chunk starts
         bool vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0 &&
                       items_even && (lmax + 1 < ld_field || (lmax % 2 == 1 && lmax + 1 <= ld_field));
-        static const bool staged = std::getenv("CMAMD_WINDOW_STAGED") != nullptr;   // A/B measurement switch
         if (use_group) {
             const bool gvec = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0;
             const int nblk = 8 * tiles * ((n_gitem + 7) / 8);
@@ -2153,7 +2205,7 @@ struct CMBLikes final : Like {
                                       ld_nuis, (const double *)coef, (const double *)prof, dev.LP, partial, W, tiles,
                                       (int)gvec);
             });
-        } else if (!bk && aberration == 0.0 && !staged) {
+        } else if (!bk && aberration == 0.0) {
             const int nblk = 8 * tiles * ((dev.nitem + 7) / 8);
             timed_launch("cmbl_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
                 hipExtLaunchKernelGGL(cmbl_window_direct, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, dev, dl,
@@ -2178,13 +2230,10 @@ struct CMBLikes final : Like {
         HIP_CHECK(hipGetLastError());
         if (small_gauss) {
             timed_launch("cmbl_gauss_small_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                static const int wt = std::getenv("CMAMD_SMALL_WT") ? atoi(std::getenv("CMAMD_SMALL_WT")) : SMALL_WT;
 #define CMBL_SMALL(T)                                                                                             \
     hipExtLaunchKernelGGL(cmbl_gauss_small_kernel<T>, dim3((W + T - 1) / T), dim3(256), 0, stream, e0, e1, 0, dev, \
                           sdev, (const double *)partial, nu, ld_nuis, d_invcov.as<double>(), out, W)
-                if (wt == 2) CMBL_SMALL(2);
-                else if (wt == 8) CMBL_SMALL(8);
-                else CMBL_SMALL(4);
+                CMBL_SMALL(SMALL_WT);
 #undef CMBL_SMALL
             });
             HIP_CHECK(hipGetLastError());
@@ -2198,26 +2247,17 @@ struct CMBLikes final : Like {
         HIP_CHECK(hipGetLastError());
         if (approx == 1) {
             timed_launch("cmbl_hl_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                static const bool lds_hl = std::getenv("CMAMD_HL_LDS") != nullptr;   // A/B measurement switch
-                if (!lds_hl) {
-                    static const int sweeps = std::getenv("CMAMD_HL_SWEEPS") ? atoi(std::getenv("CMAMD_HL_SWEEPS")) : 40;
-                    const dim3 bl(64);
-                    switch (hl.m) {
+                const dim3 bl(64);
+                switch (hl.m) {
 #define CMBL_HLR(MM)                                                                                              \
     case MM:                                                                                                      \
         hipExtLaunchKernelGGL(cmbl_hl_rows_kernel<MM>, dim3((W * nb + 64 / MM - 1) / (64 / MM)), bl, 0, stream,    \
-                              e0, e1, 0, hl, (const double *)cmat,                                                \
-                              qf.x_rows(qws), W, sweeps);                                                         \
+                              e0, e1, 0, hl, (const double *)cmat, qf.x_rows(qws), W);                           \
         break;
-                        CMBL_HLR(2) CMBL_HLR(4) CMBL_HLR(6) CMBL_HLR(8) CMBL_HLR(10) CMBL_HLR(12) CMBL_HLR(14)
-                        CMBL_HLR(16)
+                    CMBL_HLR(2) CMBL_HLR(4) CMBL_HLR(6) CMBL_HLR(8) CMBL_HLR(10) CMBL_HLR(12) CMBL_HLR(14)
+                    CMBL_HLR(16)
 #undef CMBL_HLR
-                        default: break;
-                    }
-                } else {
-                    const size_t lds = (size_t)(9 * hl.m * hl.m + 3 * hl.m) * sizeof(double);
-                    hipExtLaunchKernelGGL(cmbl_hl_kernel, dim3(W * nb), dim3(64), lds, stream, e0, e1, 0, hl,
-                                          (const double *)cmat, qf.x_rows(qws), W);
+                    default: break;
                 }
             });
             HIP_CHECK(hipGetLastError());

@@ -170,6 +170,12 @@ struct Like {
                                hipStream_t stream) = 0;
     // internal workspace for ws == nullptr
     DevBuf own_ws;
+    // sticky CMBL_STATUS_* bits set by the kernels (cmbl_status)
+    DevBuf status_buf;
+    int *status_word() {
+        if (!status_buf.p) status_buf.alloc(256);
+        return status_buf.as<int>();
+    }
 };
 
 std::unique_ptr<Like> make_plik_lite(const Ini &ini);

@@ -225,10 +225,6 @@ unsigned int *QuadForm::counters(void *ws, int W) const {
 int QuadForm::choose_kb(int tiles) {
     auto itk = kb_for_tiles.find(tiles);
     if (itk != kb_for_tiles.end()) return itk->second;
-    if (const char *ov = std::getenv("CMAMD_QF_KB")) {   // measurement override
-        const int kb = std::atoi(ov);
-        if (kb >= 1 && kb <= MAXKB) return kb_for_tiles[tiles] = kb;
-    }
     const int slots = 512;
     int best_kb = 1;
     double best = 1e300;

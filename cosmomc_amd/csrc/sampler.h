@@ -115,18 +115,7 @@ struct cmbs {
         int cap = 0;
         bool enabled = false;
     } coll;
-    // likelihoods of one step run concurrently: likelihood i > 0 on its own
-    // stream (forked from / joined to the caller's) with its own workspace
-    hipStream_t like_streams[cmamd::MAXLIKE] = {};
-    hipEvent_t like_join[cmamd::MAXLIKE] = {};
-    hipEvent_t like_fork = nullptr;
-    cmamd::DevBuf ws_like[cmamd::MAXLIKE];
     ~cmbs() {
-        for (auto &st : like_streams)
-            if (st) (void)hipStreamDestroy(st);
-        for (auto &e : like_join)
-            if (e) (void)hipEventDestroy(e);
-        if (like_fork) (void)hipEventDestroy(like_fork);
         for (auto &st : streams)
             if (st) (void)hipStreamDestroy(st);
         for (auto &e : events)

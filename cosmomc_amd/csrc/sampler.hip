@@ -1260,12 +1260,6 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, const int *nuisance_indices, 
     size_t maxws = 0;
     for (auto &l : s->likes) maxws = std::max(maxws, l.like->like->workspace_size(s->W));
     s->ws.alloc(maxws);
-    s->ws_like[li].alloc(like->like->workspace_size(s->W));
-    if (li > 0 && !s->like_streams[li]) {
-        HIP_CHECK(hipStreamCreateWithFlags(&s->like_streams[li], hipStreamNonBlocking));
-        HIP_CHECK(hipEventCreateWithFlags(&s->like_join[li], hipEventDisableTiming));
-    }
-    if (!s->like_fork) HIP_CHECK(hipEventCreateWithFlags(&s->like_fork, hipEventDisableTiming));
     if (s->n_groups > 1) sampler_set_groups(s, s->n_groups);   // resize the group workspaces
 }
 
@@ -1273,19 +1267,11 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, const int *nuisance_indices, 
 static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1, void *ws) {
     const int Wg = g1 - g0;
     const size_t nl = s->likes.size();
-    // one walker group: the likelihoods are independent, run them side by side
-    // measured on MI355X (W = 1024, plik_lite + lensing): side by side the memory-bound
-    // likelihood kernels slow each other more than they overlap (91.7 vs 89.7 us/step),
-    // so the default is in order; CMBS_CONCURRENT_LIKES=1 forks them onto streams
-    static const bool concurrent = std::getenv("CMBS_CONCURRENT_LIKES") != nullptr;
-    const bool fork = nl > 1 && g0 == 0 && g1 == s->W && concurrent;
-    if (fork) {
-        HIP_CHECK(hipEventRecord(s->like_fork, stream));
-        for (size_t i = 1; i < nl; i++) HIP_CHECK(hipStreamWaitEvent(s->like_streams[i], s->like_fork, 0));
-    }
+    // the likelihoods run in order on the caller's stream: side by side on forked
+    // streams the memory-bound likelihood kernels slowed each other more than they
+    // overlapped (measured on MI355X, W = 1024, plik_lite + lensing: 91.7 vs 89.7 us/step)
     for (size_t i = 0; i < nl; i++) {
-        hipStream_t st = (fork && i > 0) ? s->like_streams[i] : stream;
-        void *wsi = fork ? s->ws_like[i].p : ws;
+        hipStream_t st = stream;
         auto &l = s->likes[i];
         const int nn = l.like->like->n_nuis;
         double *nb = s->dc.like_nuis[i];
@@ -1297,13 +1283,8 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
         }
         l.like->like->loglike_batch(Wg, l.dl + (size_t)g0 * l.ld_walker, l.ld_field, l.ld_walker,
                                     nb + (size_t)g0 * nn, nn, s->like_terms.as<double>() + i * (size_t)s->dc.ld + g0,
-                                    wsi, st);
+                                    ws, st);
     }
-    if (fork)
-        for (size_t i = 1; i < nl; i++) {
-            HIP_CHECK(hipEventRecord(s->like_join[i], s->like_streams[i]));
-            HIP_CHECK(hipStreamWaitEvent(stream, s->like_join[i], 0));
-        }
 }
 
 // the history ring slots of the next recorded step (none when history is off)

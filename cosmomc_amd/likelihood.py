@@ -114,6 +114,14 @@ class NativeCMBLikelihood(DataLikelihood):
         N.check(rc, self._h)
         return out
 
+    def status(self, clear: bool = True) -> int:
+        """Sticky numerical status bits of the handle (cmbl_status; synchronises):
+        CMBL_STATUS_HL_NOCONV = 1 when an HL eigensolve hit its sweep cap since
+        the last clear (that walker's -lnL is NaN)."""
+        f = C.c_int()
+        N.check(N.lib().cmbl_status(self._h, C.byref(f), int(clear)), self._h)
+        return f.value
+
     def loglike_host(self, dl, nuis):
         """Host numpy arrays in/out (PCIe-staged; cmbl_loglike_batch_host)."""
         import numpy as np

@@ -495,3 +495,69 @@ def write_bk15_covmat(bk15_dir: str, seed: int = 1515, rank: int = 24) -> str:
             f.write(" ".join(row))
             f.write("\n")
     return path
+
+
+# ------------------------------------------------------------------ unbinned exact
+# CMBlikes like_approx = exact (ExactChiSq, CMBlikes.f90:967-979) needs an
+# unbinned dataset: per-l observed spectra cl_hat and noise cl_noise.  No such
+# dataset ships with the reference, so this writes one in the CMBLike2 format
+# ReadClArr reads (:146-193): Chat_l is a Wishart draw with round((2l+1) fksy)
+# degrees of freedom around theory + noise (a full-sky estimator's scatter).
+EXACT_PAIRS = ("TT", "TE", "EE", "TB", "EB", "BB")     # i >= j over T E B (ElementsToMatrix order)
+_EXACT_FIELD = {"TT": FIELD_TT, "TE": FIELD_TE, "EE": FIELD_EE, "TB": FIELD_BT, "EB": FIELD_BE, "BB": FIELD_BB}
+
+
+@dataclass
+class ExactData:
+    lmin: int
+    lmax: int
+    clhat: np.ndarray       # [lmax+1, 6] (EXACT_PAIRS columns), zero below lmin
+    noise: np.ndarray       # [lmax+1, 6]
+
+    def write(self, directory: str, fields: str = "T E B", extra: dict | None = None,
+              hat_includes_noise: bool = False) -> str:
+        d = os.path.abspath(directory)
+        os.makedirs(d, exist_ok=True)
+        hdr = "#    L " + " ".join(f"{p:>24s}" for p in EXACT_PAIRS)
+        ell = np.arange(self.lmin, self.lmax + 1)
+        hat = self.clhat + (self.noise if hat_includes_noise else 0.0)
+        for fn, arr in (("exact_clhat.dat", hat), ("exact_noise.dat", self.noise)):
+            with open(os.path.join(d, fn), "w") as f:
+                f.write(hdr + "\n")
+                for l in ell:
+                    f.write(f"{l:6d} " + " ".join(f"{v:24.17e}" for v in arr[l]) + "\n")
+        with open(os.path.join(d, "exact_cal.paramnames"), "w") as f:
+            f.write("calPlanck    y_{\\rm cal}\n")
+        lines = ["dataset_format = CMBLike2", "like_approx = exact", f"fields_use = {fields}",
+                 f"cl_lmin = {self.lmin}", f"cl_lmax = {self.lmax}", "binned = F",
+                 "cl_hat_file = exact_clhat.dat", "cl_noise_file = exact_noise.dat",
+                 f"cl_hat_includes_noise = {'T' if hat_includes_noise else 'F'}"]
+        for k, v in (extra or {}).items():
+            lines.append(f"{k} = {v}")
+        path = os.path.join(d, "exact.dataset")
+        with open(path, "w") as f:
+            f.write("\n".join(lines) + "\n")
+        return path
+
+
+def make_exact(lmin: int = 2, lmax: int = 400, fksy: float = 1.0, seed: int = 1979) -> ExactData:
+    base = base_theory(max(lmax, 2))
+    ell = np.arange(lmax + 1, dtype=np.float64)
+    white = ell * (ell + 1) / (2 * np.pi)
+    noise = np.zeros((lmax + 1, 6))
+    noise[:, 0] = 1e-4 * white                  # TT
+    noise[:, 2] = 2e-4 * white                  # EE
+    noise[:, 5] = 2e-4 * white                  # BB
+    clhat = np.zeros((lmax + 1, 6))
+    for l in range(lmin, lmax + 1):
+        C = np.zeros((3, 3))
+        for k, p in enumerate(EXACT_PAIRS):
+            i, j = "TEB".index(p[0]), "TEB".index(p[1])
+            C[i, j] = C[j, i] = base[_EXACT_FIELD[p], l] + noise[l, k]
+        nu = max(3, int(round((2 * l + 1) * fksy)))
+        x = np.linalg.cholesky(C) @ gaussians(seed + l, 3 * nu).reshape(3, nu)
+        S = x @ x.T / nu
+        for k, p in enumerate(EXACT_PAIRS):
+            i, j = "TEB".index(p[0]), "TEB".index(p[1])
+            clhat[l, k] = S[i, j] - noise[l, k]
+    return ExactData(lmin, lmax, clhat, noise)

@@ -55,7 +55,8 @@ typedef struct cmbl cmbl_t;
  * the SPTpol TE/EE 2017 and BB 2019 likelihoods (CMB_SPTpol_TEEE_2017.f90,
  * CMB_SPTpol_BB_2019.f90; sptpol_blind_r is CMBL_ERR_UNSUPPORTED),
  * "WMAP" / "SMICA" CMBL_ERR_UNSUPPORTED, any other tag a CMBlikes
- * dataset (CMBlikes.f90; like_approx HL or gaussian, binned).
+ * dataset (CMBlikes.f90; like_approx HL or gaussian, binned, or exact,
+ * unbinned: ExactChiSq CMBlikes.f90:967-979, up to 4 maps).
  * override_ini: "key = value" lines applied over the dataset file, as
  * cmb_dataset[TAG,key] = value (source/CMB.f90:71-74); may be NULL. */
 int  cmbl_open(const char *tag, const char *dataset_path, const char *override_ini,
@@ -107,6 +108,17 @@ int  cmbl_clik_compute_batch(cmbl_t *h, int W, const int *clik_lmax,
 /* Device workspace bytes cmbl_clik_compute_batch needs for W walkers
  * (workspace NULL: the handle's own, grown on demand; asynchronous either way). */
 size_t cmbl_clik_workspace_size(const cmbl_t *h, int W);
+
+/* Sticky numerical status of a handle, set on device by the likelihood
+ * kernels (their -lnL output for the affected walker is NaN):
+ *   CMBL_STATUS_HL_NOCONV  an HL eigensolve (CMBLikes_Transform, CMBlikes.f90:
+ *                          861-914) did not converge in 40 Jacobi sweeps; the
+ *                          reference's LAPACK call would stop the run
+ * cmbl_status synchronises the device, writes the bits accumulated since the
+ * last clear to *flags and clears them when clear != 0.  The host entry
+ * (cmbl_loglike_batch_host) checks them itself and returns CMBL_ERR_NUMERIC. */
+#define CMBL_STATUS_HL_NOCONV 1
+int  cmbl_status(cmbl_t *h, int *flags, int clear);
 
 /* Per-kernel device timing (HIP events around every library launch; off by
  * default).  cmbl_profile_read: accumulated milliseconds and launch count of

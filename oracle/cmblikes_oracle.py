@@ -171,15 +171,24 @@ class CMBLikesOracle:
         self.ncl = self.nmaps * (self.nmaps + 1) // 2
         self.lmin = int(ini.get("cl_lmin"))
         self.lmax = int(ini.get("cl_lmax"))
-        self.nbins = int(ini.get("nbins", 0))
+        self.binned = ini.logical("binned", False)
         self.aberration = float(ini.get("aberration_coeff", 0.0))
-        self.bin_min = int(ini.get("use_min", 1))
-        self.bin_max = int(ini.get("use_max", self.nbins))
+        if self.binned:
+            self.nbins = int(ini.get("nbins", 0))
+            self.bin_min = int(ini.get("use_min", 1))
+            self.bin_max = int(ini.get("use_max", self.nbins))
+        else:                                              # unbinned (:601-605, :636-637): bins are l
+            self.nbins = self.lmax - self.lmin + 1
+            self.bin_min = int(ini.get("use_min", self.lmin))
+            self.bin_max = int(ini.get("use_max", self.lmax))
         self.bins = list(range(self.bin_min, self.bin_max + 1))
-        self.W_main = self._read_windows(ini, "bin_window")
+        if self.binned:
+            self.W_main = self._read_windows(ini, "bin_window")
         self.clhat = self._read_cl(ini, "cl_hat")
         if self.like_approx == 1:
             self.clfid = self._read_cl(ini, "cl_fiducial")
+        elif self.like_approx == 3:
+            self.fksy = float(ini.get("fullsky_exact_fksy", 1.0))
         inc = ini.logical("cl_hat_includes_noise", False)
         self.clnoise = None
         if self.like_approx != 2 or inc:
@@ -198,7 +207,8 @@ class CMBLikesOracle:
             if self.like_approx == 1:
                 f = self.clfid[b] + (0 if fid_noise else self.clnoise[b])
                 self.sqrt_fid[b] = _mat_root(self._to_matrix(f), 0.5)
-        self._read_covmat(ini)
+        if self.like_approx != 3:
+            self._read_covmat(ini)
         self.fidcorr = None
         if ini.get("linear_correction_fiducial_file"):
             self.fidcorr = self._read_cl(ini, "linear_correction_fiducial")
@@ -445,9 +455,28 @@ class CMBLikesOracle:
         U2 = CfHalf @ V
         return (U2 * g) @ U2.T
 
+    def _exact_chisq(self, C, Chat, l):                  # ExactChiSq :967-979
+        R = _mat_root(C, -0.5)
+        M = R @ (Chat @ R)
+        L = np.linalg.cholesky(M)                          # MatrixSym_LogDet (Matrix_utils_new.f90:619-634)
+        logdet = 2.0 * np.sum(np.log(np.diag(L)))
+        return (2 * l + 1) * self.fksy * (np.trace(M) - self.nmaps - logdet)
+
     def loglike(self, dl, nuis):
         """-lnL (CMBLikes_LogLike, CMBlikes.f90:1165-1227)."""
         mc = self.map_cls(dl, nuis)
+        if self.like_approx == 3:                          # unbinned exact (:1187-1206)
+            chisq = 0.0
+            for l in self.bins:
+                C = np.zeros((self.nmaps, self.nmaps))
+                for i in range(1, self.nmaps + 1):
+                    for j in range(1, i + 1):
+                        C[i - 1, j - 1] = C[j - 1, i - 1] = mc[i, j][l - self.lmin]
+                C = C + self.noiseM[l]
+                chisq += self._exact_chisq(C, self.chatM[l], l)
+            if self.log_cal_prior > 0 and self.cal_index is not None:
+                chisq += (np.log(nuis[self.cal_index]) / self.log_cal_prior) ** 2
+            return chisq / 2
         X = []
         for b in self.bins:
             cls = self._bin(self.W_main, mc, b)

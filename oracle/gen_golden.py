@@ -425,6 +425,43 @@ def gen_sptpol():
         json.dump(out, f, indent=1)
 
 
+# like_approx = exact on the synthetic unbinned datasets (cosmomc_amd.synthetic.make_exact):
+# (name, make_exact kwargs, fields, dataset keys, hat_includes_noise, walkers, nuisance kind)
+EXACT_CASES = [
+    ("exact_TE_lowl", {"lmin": 2, "lmax": 29, "fksy": 1.0}, "T E", {}, False, 4, None),
+    ("exact_TEB_cal_aberration", {"lmin": 2, "lmax": 400, "fksy": 0.6, "seed": 1980}, "T E B",
+     {"fullsky_exact_fksy": "0.6", "calibration_param": "exact_cal.paramnames", "log_calibration_prior": "0.0025",
+      "aberration_coeff": "-0.0013"}, False, 4, "cal"),
+    ("exact_T_userange_hatnoise", {"lmin": 2, "lmax": 300, "fksy": 0.8, "seed": 1981}, "T",
+     {"fullsky_exact_fksy": "0.8", "use_min": "10", "use_max": "250", "calibration_param": "exact_cal.paramnames"},
+     True, 3, "cal"),
+    ("exact_EB_pol", {"lmin": 2, "lmax": 200, "fksy": 0.5, "seed": 1982}, "E B",
+     {"fullsky_exact_fksy": "0.5"}, False, 3, None),
+]
+
+
+def exact_dataset(case, td):
+    name, kw, fields, keys, incl, W, kind = case
+    return syn.make_exact(**kw).write(os.path.join(td, name), fields=fields, extra=keys, hat_includes_noise=incl)
+
+
+def gen_exact():
+    out = {"theory_seed": 0xE8AC7, "generator": "cosmomc_amd.synthetic.make_exact", "cases": {}}
+    with tempfile.TemporaryDirectory() as td:
+        for ci, case in enumerate(EXACT_CASES):
+            name, kw, fields, keys, incl, W, kind = case
+            path = exact_dataset(case, td)
+            lmax = kw["lmax"]
+            th = syn.walker_theory(W, seed=out["theory_seed"] + 100 * ci, lmax=lmax, n_fields=6)
+            nu = cmbl_nuisance(kind, W, 7070 + ci) if kind else np.zeros((W, 0))
+            ref = run_cmb_harness(f"cmb_dataset[exact] = {path}\n", th, nu, td)
+            out["cases"][name] = {"walkers": W, "lmax": lmax, "theory_seed": out["theory_seed"] + 100 * ci,
+                                  "nuis": nu.tolist(), "minus_lnL": ref.tolist()}
+            print(f"{name:28s} -lnL = {ref}")
+    with open(os.path.join(GOLDEN, "exact_ref.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
     if not os.path.exists(os.path.join(REF_DIR, "plik_harness")):
         sys.exit("build the reference first: make -C oracle ref")
@@ -441,3 +478,5 @@ if __name__ == "__main__":
         gen_cmblikes()
     if not only or "sptpol" in only:
         gen_sptpol()
+    if not only or "exact" in only:
+        gen_exact()

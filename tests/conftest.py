@@ -78,3 +78,17 @@ def sptpol_overrides(case, dataset):
     """Golden-case overrides with @DIR@ -> the dataset's directory."""
     d = os.path.dirname(dataset)
     return {k: v.replace("@DIR@", d) for k, v in case["overrides"].items()}
+
+
+@pytest.fixture(scope="session")
+def exact_golden():
+    return load_golden("exact_ref.json")
+
+
+@pytest.fixture(scope="session")
+def exact_data(tmp_path_factory):
+    """The synthetic unbinned like_approx = exact datasets of oracle/gen_golden.py
+    EXACT_CASES, written once per session: {case name: dataset path}."""
+    import gen_golden as gg
+    d = str(tmp_path_factory.mktemp("exact"))
+    return {c[0]: gg.exact_dataset(c, d) for c in gg.EXACT_CASES}

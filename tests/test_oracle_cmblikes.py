@@ -24,3 +24,18 @@ def test_cmblikes_oracle_vs_reference(cmbl_golden, refdata, case):
     nu = np.array(c["nuis"])
     got = np.array([o.loglike(th[w], nu[w]) for w in range(c["walkers"])])
     np.testing.assert_allclose(got, c["minus_lnL"], rtol=1e-11, atol=1e-9)
+
+
+EXACT = ["exact_TE_lowl", "exact_TEB_cal_aberration", "exact_T_userange_hatnoise", "exact_EB_pol"]
+
+
+@pytest.mark.parametrize("case", EXACT)
+def test_exact_oracle_vs_reference(exact_golden, exact_data, case):
+    """like_approx = exact (ExactChiSq, CMBlikes.f90:967-979) on the synthetic
+    unbinned datasets vs the compiled reference (tests/golden/exact_ref.json)."""
+    c = exact_golden["cases"][case]
+    o = co.CMBLikesOracle(exact_data[case], None, "exact")
+    th = syn.walker_theory(c["walkers"], seed=c["theory_seed"], lmax=c["lmax"], n_fields=6)
+    nu = np.array(c["nuis"]).reshape(c["walkers"], -1)
+    got = np.array([o.loglike(th[w], nu[w]) for w in range(c["walkers"])])
+    np.testing.assert_allclose(got, c["minus_lnL"], rtol=1e-11, atol=1e-9)
