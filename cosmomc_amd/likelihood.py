@@ -106,11 +106,12 @@ class NativeCMBLikelihood(DataLikelihood):
             out = torch.empty(W, dtype=torch.float64, device=dl.device)
         if dl.dtype != torch.float64 or nuis.dtype != torch.float64 or not (dl.is_cuda and nuis.is_cuda):
             raise TypeError("dl and nuis must be float64 cuda tensors")
-        if dl.stride(2) != 1 or nuis.stride(1) != 1:
+        if dl.stride(2) != 1 or (nuis.numel() > 0 and nuis.stride(1) != 1):
             raise ValueError("dl rows (l) and nuisance rows must be contiguous")
         ws = workspace.data_ptr() if workspace is not None else None
-        rc = N.lib().cmbl_loglike_batch(self._h, W, dl.data_ptr(), dl.stride(1), dl.stride(0), nuis.data_ptr(),
-                                        nuis.stride(0), out.data_ptr(), ws, N.current_stream_ptr(dl.device))
+        nptr, nld = (nuis.data_ptr(), nuis.stride(0)) if nuis.numel() > 0 else (None, 0)
+        rc = N.lib().cmbl_loglike_batch(self._h, W, dl.data_ptr(), dl.stride(1), dl.stride(0), nptr, nld,
+                                        out.data_ptr(), ws, N.current_stream_ptr(dl.device))
         N.check(rc, self._h)
         return out
 

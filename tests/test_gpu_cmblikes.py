@@ -41,6 +41,7 @@ def test_cmblikes_vs_reference_golden(cmbl_golden, refdata, case):
     got = like.loglike_batch(th, nu).cpu().numpy()
     rtol, atol = _tol(case)
     np.testing.assert_allclose(got, c["minus_lnL"], rtol=rtol, atol=atol)
+    assert like.status() == 0          # every HL eigensolve converged within the sweep cap
 
 
 @pytest.mark.parametrize("case", ["lensing_consext8", "bkplanck_3map_bins1to5", "sptsz_aberration_calprior",
