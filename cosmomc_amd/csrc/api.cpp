@@ -134,18 +134,6 @@ int cmbl_loglike_batch(cmbl_t *h, int W, const double *dl, long long ld_field, l
     });
 }
 
-// Doubles of one walker's theory the likelihood reads: fields in
-// cmbl_loglike_batch order (TT, TE, EE, TB, EB, BB, PT, PE, PB, PP), each
-// l = 0..cl_lmax of its pair; the last used field ends at its lmax.
-static long long theory_extent(const cmamd::Like &L, long long ld_field) {
-    static const int fi[10] = {1, 2, 2, 3, 3, 3, 4, 4, 4, 4}, fj[10] = {1, 1, 2, 1, 2, 3, 1, 2, 3, 4};
-    long long ext = 0;
-    for (int f = 0; f < 10; f++) {
-        const int lm = L.cl_lmax[(fi[f] - 1) * 4 + (fj[f] - 1)];
-        if (lm > 0) ext = std::max(ext, f * ld_field + lm + 1);
-    }
-    return ext;
-}
 
 int cmbl_loglike_batch_host(cmbl_t *h, int W, const double *dl, long long ld_field, long long ld_walker,
                             const double *nuis, long long ld_nuis, double *out) {
@@ -155,7 +143,7 @@ int cmbl_loglike_batch_host(cmbl_t *h, int W, const double *dl, long long ld_fie
         if (!dl || !out) cmamd::fail(CMBL_ERR_ARG, "cmbl_loglike_batch_host: bad arguments");
         std::lock_guard<std::mutex> lock(h->host_mu);
         const auto &L = *h->like;
-        const size_t nd = (size_t)((W - 1) * ld_walker + theory_extent(L, ld_field));
+        const size_t nd = (size_t)((W - 1) * ld_walker + cmamd::theory_extent(L, ld_field));
         const size_t nn = nuis ? (size_t)((W - 1) * ld_nuis + L.n_nuis) : 0;
         if (!h->host_stream) HIP_CHECK(hipStreamCreateWithFlags(&h->host_stream, hipStreamNonBlocking));
         const size_t pin_need = (nd + nn + (size_t)W) * 8;

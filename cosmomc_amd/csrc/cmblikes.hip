@@ -101,7 +101,13 @@ struct CLDev {
     const double *log_l80;          // log(l / 80), l = 0 .. LP-1
     double fpivot_dust, fpivot_sync, decorr_dust[2], decorr_sync[2];
     int lform_dust, lform_sync;     // 0 flat, 1 lin, 2 quad
+    // sparse evaluation (the sampler's per-likelihood change mask): walkers
+    // [0, *wcount) of the launch are live, the rest exit; null = all W
+    const int *wcount;
 };
+
+// live walkers of a launch over W (wcount: device count, or null)
+__device__ __forceinline__ int live_walkers(const int *wcount, int W) { return wcount ? min(W, *wcount) : W; }
 
 static constexpr double BK_TCMB = 2.72548;
 static constexpr double BK_H = 6.62606957e-34;
@@ -138,6 +144,7 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int w = blockIdx.x;
+    if (w >= live_walkers(c.wcount, W)) return;
     const double *P = nuis + (long long)w * ld_nuis;
     const double Adust = P[0], Async = P[1], alphadust = P[2], betadust = P[3], Tdust = P[4];
     const double alphasync = P[5], betasync = P[6], dustsync_corr = P[7];
@@ -210,6 +217,8 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
     __shared__ __attribute__((aligned(16))) double tsh[64 * WK_TS];           // spectra [walker][l]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int w0 = blockIdx.x * 64;
+    const int Wc = live_walkers(c.wcount, W);
+    if (w0 >= Wc) return;
     const WItem it = c.items[blockIdx.y];
     const CLPair pr = c.pairs[it.pair];
     const bool aber = ABER && c.aberration != 0.0 && pr.cmb;
@@ -224,7 +233,7 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
     bool dd_l = false, ds_l = false;     // l-dependent decorrelation (lform lin / quad) in use
 #pragma unroll
     for (int u = 0; u < PER; u++) {
-        const int w = min(w0 + rbase + 8 * u, W - 1);
+        const int w = min(w0 + rbase + 8 * u, Wc - 1);
         const double *P = nuis + (long long)w * ld_nuis;
         const double cl = c.cal_index >= 0 ? P[c.cal_index] : 1.0;
         calsq[u] = cl * cl;
@@ -273,7 +282,7 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
         for (int u = 0; u < PER; u++) {
             const int w = w0 + rbase + 8 * u;
             raw[u] = make_double2(0.0, 0.0);
-            if (w < W && lq <= it.l1) {
+            if (w < Wc && lq <= it.l1) {
                 const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
                 if (vec_ok) {
                     raw[u] = *reinterpret_cast<const double2 *>(Df + lq);
@@ -298,7 +307,7 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
         for (int u = 0; u < PER; u++) {
             const int r = rbase + 8 * u, w = w0 + r;
             double v2[2] = {raw[u].x, raw[u].y};
-            if (w < W && lq <= it.l1) {
+            if (w < Wc && lq <= it.l1) {
                 const double *Df = dl + (long long)w * ld_walker + (long long)pr.field * ld_field;
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
@@ -357,7 +366,7 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
     }
     // D: walker = lane&15, col = (lane>>4) + 4 r
     const int w = w0 + 16 * wave + li;
-    if (w < W) {
+    if (w < Wc) {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int c0 = lk + 4 * r, c1 = 16 + lk + 4 * r;
@@ -390,12 +399,14 @@ __global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double 
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
     const int item = xcd + 8 * (j / tiles), tile = j % tiles;
     if (item >= c.nitem) return;
+    const int Wc = live_walkers(c.wcount, W);
+    if (tile * 64 >= Wc) return;
     const WItem it = c.items[item];
     const CLPair pr = c.pairs[it.pair];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, kq = lane >> 4;
     const int w = tile * 64 + wave * 16 + li;
-    const int wl = min(w, W - 1);
+    const int wl = min(w, Wc - 1);
     const double *Df = dl + (long long)wl * ld_walker + (long long)pr.field * ld_field;
     const int ncb = (it.ncol + 15) >> 4;
     const int nstep = it.nch * NSUB;
@@ -466,7 +477,7 @@ __global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double 
             for (int s = 0; s < LPL; s++) t[s] = tn[s];
         }
     }
-    if (w < W) {
+    if (w < Wc) {
         double inv = 1.0;
         if (c.cal_index >= 0 && pr.cmb) {
             const double cl = nuis[(long long)w * ld_nuis + c.cal_index];
@@ -523,11 +534,13 @@ __global__ __launch_bounds__(256, 2) void cmbl_window_group(CLDev c, const GItem
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
     const int item = xcd + 8 * (j / tiles), tile = j % tiles;   // all walker tiles of an item on one XCD
     if (item >= ngitem) return;
+    const int Wc = live_walkers(c.wcount, W);
+    if (tile * 64 >= Wc) return;
     const GItem &it = gitems[item];
     const int np = it.npair;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     {   // staged kernel :226-258, one (walker, pair) per thread and pass
-        const int ws = min(tile * 64 + lane, W - 1);
+        const int ws = min(tile * 64 + lane, Wc - 1);
         const double *P = nuis + (long long)ws * ld_nuis;
         const double *cw = coef + (long long)ws * 3 * c.nreq;
         const double Delta_dust = P[10], Delta_sync = P[11];
@@ -570,7 +583,7 @@ __global__ __launch_bounds__(256, 2) void cmbl_window_group(CLDev c, const GItem
     const int li = lane & 15, kq = lane >> 4;
     const int wr_ = wave * 16 + li;                // walker within the tile
     const int w = tile * 64 + wr_;
-    const int wl = min(w, W - 1);
+    const int wl = min(w, Wc - 1);
     const double *P = nuis + (long long)wl * ld_nuis;
     const double Delta_dust = P[10], Delta_sync = P[11];
     const double *Df = dl + (long long)wl * ld_walker + (long long)it.field * ld_field;
@@ -666,7 +679,7 @@ __global__ __launch_bounds__(256, 2) void cmbl_window_group(CLDev c, const GItem
                 for (int s = 0; s < LPL; s++) t[q][s] = tn[q][s];
         }
     }
-    if (w < W) {
+    if (w < Wc) {
 #pragma unroll
         for (int g = 0; g < GP; g++) {
             if (g >= np) break;
@@ -703,12 +716,14 @@ __global__ __launch_bounds__(256) void cmbl_reduce_kernel(CLDev c, const double 
     const int w = blockIdx.x * 64 + lane;
     if (blockIdx.x == 0 && e == 0)
         for (int i = threadIdx.x; i < n_counters; i += 256) counters[i] = 0u;
+    const int Wc = live_walkers(c.wcount, W);
+    if (blockIdx.x * 64 >= Wc) return;
     // window columns in window order, each the l-chunk partials in order (flattened on
     // the host); wave v sums rows v, v+4, ... eight loads at a time, the four wave sums
     // are combined in fixed order: deterministic
     auto rows_sum = [&](const int *off, const int *rows) {
         double v = 0.0;
-        if (w < W) {
+        if (w < Wc) {
             const int q0 = off[e], q1 = off[e + 1];
             for (int q = q0 + wave; q < q1; q += 32) {
                 double t[8];
@@ -724,7 +739,7 @@ __global__ __launch_bounds__(256) void cmbl_reduce_kernel(CLDev c, const double 
     red[0][wave][lane] = rows_sum(c.e_main_off, c.e_main_rows);
     red[1][wave][lane] = c.has_corr ? rows_sum(c.e_corr_off, c.e_corr_rows) : 0.0;
     __syncthreads();
-    if (wave != 0 || w >= W) return;
+    if (wave != 0 || w >= Wc) return;
     double s = c.e_main_const[e] + (((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane]);
     if (c.has_corr) {
         const double cs = c.e_corr_const[e] + (((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane]);
@@ -778,8 +793,10 @@ __global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev
     __shared__ double Msh[SMALL_NX * SMALL_NX];
     const int wl = threadIdx.x % WT, g = threadIdx.x / WT;
     const int w = blockIdx.x * WT + wl;
+    const int Wc = live_walkers(c.wcount, W);
+    if (blockIdx.x * WT >= Wc) return;
     for (int i = threadIdx.x; i < c.nX * c.nX; i += 256) Msh[i] = M[i];   // in flight with the partial loads
-    const bool act = w < W;
+    const bool act = w < Wc;
     for (int t = g; t < sd.ntask; t += NG) {
         const SmallTask tk = sd.tasks[t];
         double v[8];
@@ -831,6 +848,7 @@ struct HLDev {
     const double *cfhalf;   // [nb][n][n]
     const int *cl_use;
     int *status;            // sticky CMBL_STATUS_* bits (cmbl_status)
+    const int *wcount;      // live walkers (CLDev::wcount)
 };
 
 // ------------------------------------------- HL, register-resident (16 lanes / matrix)
@@ -1015,7 +1033,8 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
     const int lane = threadIdx.x, grp = lane / M, r = lane % M;
     const bool on = grp < G;                      // lanes past G*M idle
     const int prob = blockIdx.x * G + grp;
-    const int nprob = W * h.nb;
+    const int nprob = live_walkers(h.wcount, W) * h.nb;
+    if (blockIdx.x * G >= nprob) return;          // block-uniform: no live problem
     const bool live = on && prob < nprob;
     const int w = live ? prob / h.nb : 0, b = live ? prob % h.nb : 0;
     const int n = h.n;
@@ -2148,7 +2167,20 @@ struct CMBLikes final : Like {
 
     void loglike_batch(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis,
                        long long ld_nuis, double *out, void *ws, hipStream_t stream) override {
+        run(W, dl, ld_field, ld_walker, nuis, ld_nuis, out, ws, stream, nullptr);
+    }
+    bool sparse_capable() const override { return approx != 3; }
+    void loglike_batch_sparse(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis,
+                              long long ld_nuis, double *out, void *ws, hipStream_t stream,
+                              const int *wcount) override {
+        run(W, dl, ld_field, ld_walker, nuis, ld_nuis, out, ws, stream, wcount);
+    }
+
+    void run(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis, long long ld_nuis,
+             double *out, void *ws, hipStream_t stream, const int *wcount) {
         if (W <= 0) return;
+        dev.wcount = wcount;
+        hl.wcount = wcount;
         if (n_nuis > 0 && !nuis) fail(CMBL_ERR_ARG, "%s needs its %d nuisance parameters", name.c_str(), n_nuis);
         if (ld_field < lmax + 1) fail(CMBL_ERR_ARG, "ld_field %lld < cl_lmax+1 = %d", ld_field, lmax + 1);
         if (W > 1 && ld_walker != 0 && ld_walker < (long long)(max_field + 1) * ld_field)
@@ -2262,7 +2294,7 @@ struct CMBLikes final : Like {
             });
             HIP_CHECK(hipGetLastError());
         }
-        qf.launch(W, qws, use_add ? addend : nullptr, out, stream, "cmbl_quadform");
+        qf.launch(W, qws, use_add ? addend : nullptr, out, stream, "cmbl_quadform", wcount);
     }
 };
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <map>
@@ -168,6 +169,18 @@ struct Like {
     virtual void loglike_batch(int W, const double *dl, long long ld_field, long long ld_walker,
                                const double *nuis, long long ld_nuis, double *out, void *ws,
                                hipStream_t stream) = 0;
+    // Sparse evaluation for the sampler's per-likelihood change mask: the same
+    // launch over W walker slots, of which only [0, *wcount) (a device count)
+    // are live; the caller has compacted the live walkers' inputs into those
+    // slots.  Likelihoods without it are evaluated densely.
+    virtual bool sparse_capable() const { return false; }
+    virtual void loglike_batch_sparse(int W, const double *dl, long long ld_field, long long ld_walker,
+                                      const double *nuis, long long ld_nuis, double *out, void *ws,
+                                      hipStream_t stream, const int *wcount) {
+        (void)W, (void)dl, (void)ld_field, (void)ld_walker, (void)nuis, (void)ld_nuis, (void)out, (void)ws;
+        (void)stream, (void)wcount;
+        fail(CMBL_ERR_UNSUPPORTED, "%s: no sparse evaluation", name.c_str());
+    }
     // internal workspace for ws == nullptr
     DevBuf own_ws;
     // sticky CMBL_STATUS_* bits set by the kernels (cmbl_status)
@@ -177,6 +190,19 @@ struct Like {
         return status_buf.as<int>();
     }
 };
+
+// Doubles of one walker's theory the likelihood reads: fields in
+// cmbl_loglike_batch order (TT, TE, EE, TB, EB, BB, PT, PE, PB, PP), each
+// l = 0..cl_lmax of its pair; the last used field ends at its lmax.
+inline long long theory_extent(const Like &L, long long ld_field) {
+    static const int fi[10] = {1, 2, 2, 3, 3, 3, 4, 4, 4, 4}, fj[10] = {1, 1, 2, 1, 2, 3, 1, 2, 3, 4};
+    long long ext = 0;
+    for (int f = 0; f < 10; f++) {
+        const int lm = L.cl_lmax[(fi[f] - 1) * 4 + (fj[f] - 1)];
+        if (lm > 0) ext = std::max(ext, f * ld_field + lm + 1);
+    }
+    return ext;
+}
 
 std::unique_ptr<Like> make_plik_lite(const Ini &ini);
 std::unique_ptr<Like> make_cmblikes(const Ini &ini, const std::string &tag);

@@ -54,7 +54,8 @@ __global__ __launch_bounds__(256) void plik_bin_delta(
     const double *__restrict__ wts,          // by absolute l, zero outside the bins
     const BinInfo *__restrict__ bins, const double *__restrict__ X,
     int nused, int Np, FieldRanges fr, int vec_ok,
-    double *__restrict__ delta, unsigned int *__restrict__ counters, int n_counters)
+    double *__restrict__ delta, unsigned int *__restrict__ counters, int n_counters,
+    const int *__restrict__ wcount)   // sparse evaluation: walkers [0, *wcount) live (null: all)
 {
     extern __shared__ __attribute__((aligned(16))) double prod[];
     const int w = blockIdx.x, f = blockIdx.y;
@@ -65,6 +66,7 @@ __global__ __launch_bounds__(256) void plik_bin_delta(
             for (int i = tid; i < n_counters; i += blockDim.x) counters[i] = 0u;
         for (int i = nused + tid; i < Np; i += blockDim.x) out[i] = 0.0;
     }
+    if (wcount && w >= *wcount) return;
     const int lo = fr.lo[f], hi = fr.hi[f];
     if (hi < lo) return;
     const double *Df = dl + (long long)w * ld_walker + f * ld_field;
@@ -313,6 +315,17 @@ struct PlikLite final : Like {
     void loglike_batch(int W, const double *dl, long long ld_field, long long ld_walker,
                        const double *nuis, long long ld_nuis, double *out, void *ws,
                        hipStream_t stream) override {
+        run(W, dl, ld_field, ld_walker, nuis, ld_nuis, out, ws, stream, nullptr);
+    }
+    bool sparse_capable() const override { return true; }
+    void loglike_batch_sparse(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis,
+                              long long ld_nuis, double *out, void *ws, hipStream_t stream,
+                              const int *wcount) override {
+        run(W, dl, ld_field, ld_walker, nuis, ld_nuis, out, ws, stream, wcount);
+    }
+
+    void run(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis, long long ld_nuis,
+             double *out, void *ws, hipStream_t stream, const int *wcount) {
         if (W <= 0) return;
         if (n_nuis < 1 || !nuis) fail(CMBL_ERR_ARG, "plik_lite needs the calibration nuisance parameter");
         if (ld_field < lmax_needed + 1) fail(CMBL_ERR_ARG, "ld_field %lld < lmax+1 = %d", ld_field, lmax_needed + 1);
@@ -331,10 +344,10 @@ struct PlikLite final : Like {
         timed_launch("plik_bin_delta", stream, [&](hipEvent_t e0, hipEvent_t e1) {
             hipExtLaunchKernelGGL(plik_bin_delta, dim3(W, 3), dim3(256), (size_t)lds_doubles * 8, stream, e0, e1, 0, dl, ld_field,
                                ld_walker, nuis, ld_nuis, d_wts.as<double>(), d_bins.as<BinInfo>(), d_X.as<double>(),
-                               nused, Np, fr, vec_ok, delta, counters, qf.n_counters(W));
+                               nused, Np, fr, vec_ok, delta, counters, qf.n_counters(W), wcount);
         });
         HIP_CHECK(hipGetLastError());
-        qf.launch(W, ws, nullptr, out, stream, "plik_quadform_ksplit");
+        qf.launch(W, ws, nullptr, out, stream, "plik_quadform_ksplit", wcount);
     }
 };
 

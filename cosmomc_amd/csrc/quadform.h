@@ -33,7 +33,9 @@ class QuadForm {
     unsigned int *counters(void *ws, int W) const;
     int n_counters(int W) const { return wpad(W) / QF_TILE; }
     // out[w] = x_w^T M x_w / 2 + (addend ? addend[w] : 0)
-    void launch(int W, void *ws, const double *addend, double *out, hipStream_t stream, const char *prof_name);
+    // wcount (device int, or null): only walkers [0, *wcount) are live
+    void launch(int W, void *ws, const double *addend, double *out, hipStream_t stream, const char *prof_name,
+                const int *wcount = nullptr);
 
   private:
     static constexpr int MAXKB = 5;

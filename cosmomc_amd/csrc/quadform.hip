@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
     const double *__restrict__ Ct, int Np, const double *__restrict__ delta, int W,
     const QFItem *__restrict__ items, int n_items, int xcd_map,
     double *__restrict__ partial, unsigned int *__restrict__ counters, const double *__restrict__ addend,
-    double *__restrict__ out)
+    double *__restrict__ out, const int *__restrict__ wcount)
 {
     __shared__ __attribute__((aligned(16))) double smem[2 * 2 * QF_TILE * BK];   // [buf][A|B][64][BK], 64 KB
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -67,8 +67,13 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
         tile = x + 8 * (j / n_items);
         item_ix = j % n_items;
     }
-    const QFItem it = items[item_ix];
     const int w0 = tile * QF_TILE;
+    if (wcount) {                                     // sparse evaluation: walkers [0, *wcount) live
+        const int wc = *wcount;
+        if (w0 >= wc) return;                         // the whole tile: no ticket taken
+        W = min(W, wc);
+    }
+    const QFItem it = items[item_ix];
     const int nsteps = it.nJ * (QF_TILE / BK);
     const int kbase0 = it.J0 * QF_TILE;
     const double *Arow = Ct + (size_t)(it.I * QF_TILE) * Np;      // rows of the I panel
@@ -245,7 +250,8 @@ int QuadForm::choose_kb(int tiles) {
     return best_kb;
 }
 
-void QuadForm::launch(int W, void *ws, const double *addend, double *out, hipStream_t stream, const char *prof_name) {
+void QuadForm::launch(int W, void *ws, const double *addend, double *out, hipStream_t stream, const char *prof_name,
+                      const int *wcount) {
     const int tiles = wpad(W) / QF_TILE;
     const int kb = choose_kb(tiles);
     const int n_items = (int)items[kb].size();
@@ -255,7 +261,7 @@ void QuadForm::launch(int W, void *ws, const double *addend, double *out, hipStr
     timed_launch(prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
         hipExtLaunchKernelGGL(quadform_ksplit, dim3(n_items, tiles), dim3(256), 0, stream, e0, e1, 0,
                               d_ct.as<double>(), Np, (const double *)x, W, d_items[kb].as<QFItem>(), n_items,
-                              (int)(tiles % 8 == 0), partial, cnt, addend, out);
+                              (int)(tiles % 8 == 0), partial, cnt, addend, out, wcount);
     });
     HIP_CHECK(hipGetLastError());
 }

@@ -63,6 +63,14 @@ struct DevCfg {
     int like_nidx[MAXLIKE], like_nn[MAXLIKE];   // offset in tab_i of each likelihood's nuisance_indices
                                                 //   (0-based indices into P), and their count
     double *like_nuis[MAXLIKE];     // [W][like_nn] DataParams buffers written by mh_kernel
+    // per-likelihood change mask (LogLikeWithTheorySet, calclike.f90:374-386): a
+    // likelihood is re-evaluated only for walkers whose trial moved one of its
+    // dependent parameters (its nuisance parameters and every theory parameter);
+    // the others keep their current-point term (TCalculationAtParamPoint%Likelihoods)
+    unsigned long long like_dep[MAXLIKE];   // dependent-parameter bits (0-based parameter index)
+    int mask_on;                            // this launch uses the mask (set per launch)
+    int *like_flag;                         // [n_like][ld]: 0 unchanged, else 1 (dense) or compact slot + 1 (sparse)
+    const double *like_out[MAXLIKE];        // sparse likelihoods: terms by compact slot; null = dense (like_terms)
 };
 
 struct LikeSlot {
@@ -115,6 +123,12 @@ struct cmbs {
         int cap = 0;
         bool enabled = false;
     } coll;
+    // change mask: flags, per sparse likelihood the compacted walker slots
+    // (count, DataParams rows, theory rows when per walker, terms)
+    cmamd::DevBuf like_flag, like_cnt;
+    cmamd::DevBuf like_outc[cmamd::MAXLIKE], like_nuisc[cmamd::MAXLIKE], like_dlc[cmamd::MAXLIKE];
+    std::vector<int> sparse_likes;          // likelihood indices evaluated sparsely
+    bool mask_on = false;                   // some likelihood can skip walkers (SetMask at add_likelihood)
     ~cmbs() {
         for (auto &st : streams)
             if (st) (void)hipStreamDestroy(st);

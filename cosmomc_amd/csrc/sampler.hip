@@ -388,6 +388,21 @@ __device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size
     for (int r = r0 + wave; r < r1; r += nw) dst[(size_t)r * ld + w] = src[(size_t)(src_r0 + r - r0) * NB + lane];
 }
 
+// changeMask of the trial (TheoryLike_GetLogLikeMain, calclike.f90:302-306):
+// likelihood l must be recomputed iff a parameter it depends on moved
+// (LogLikeWithTheorySet :377); 1 = recompute, 0 = keep the current term
+template <class QT, class QP>
+__device__ inline void write_like_flags(const DevCfg &c, const QT &trial, const QP &P, int w)
+{
+    for (int l = 0; l < c.n_like; l++) {
+        const unsigned long long m = c.like_dep[l];
+        bool ch = false;
+        for (int i = 0; i < c.np; i++)
+            if (((m >> i) & 1ull) && trial[i] != P[i]) ch = true;
+        c.like_flag[(size_t)l * c.ld + w] = ch ? 1 : 0;
+    }
+}
+
 // One launch per Metropolis step boundary: accept/reject the pending trial
 // (MetropolisAccept MCMC.f90:119-131 + MoveDone :166-190), then propose the
 // next trial (GetProposal / GetProposalFast) and scatter its nuisance
@@ -482,6 +497,16 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     int &nacc = si[(size_t)R.NACC * NB + lane];
 
     if (ACCEPT) {
+        if (c.mask_on) {   // unchanged likelihoods keep the current point's term (calclike.f90:377-384)
+            for (int l = 0; l < c.n_like; l++) {
+                const int f = c.like_flag[(size_t)l * W + w];
+                double v;
+                if (f == 0) v = c.cur_terms[(size_t)l * W + w];
+                else if (c.like_out[l]) v = c.like_out[l][f - 1];        // sparse: compacted slot
+                else v = lk[(size_t)l * NB + lane];
+                lk[(size_t)l * NB + lane] = v;
+            }
+        }
         const double like = target_like(c, t, k.trial, Col<double>{lk + lane, NB}, par_test ? tq + lane : nullptr);
         bool acc = false;
         if (like != LOGZERO) {
@@ -520,10 +545,12 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
         if (fast_only) proposal_fast(c, t, k);
         else proposal(c, t, k);
         if (par_map) tq[lane] = (double)k.pend_b;                    // the block, for the mapping waves
-        else
+        else {
             for (int l = 0; l < c.n_like; l++)
                 for (int q = 0; q < c.like_nn[l]; q++)
                     c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = k.trial[t.ti[c.like_nidx[l] + q]];
+            if (c.mask_on) write_like_flags(c, k.trial, k.P, w);
+        }
     }
     STAMP(4);
     sd[(size_t)R.C * NB + lane] = k.r.c;
@@ -555,6 +582,9 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
             for (int l = 0; l < c.n_like; l++)
                 for (int q = 0; q < c.like_nn[l]; q++)
                     c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = trial[(size_t)ti[c.like_nidx[l] + q] * NB];
+            if (c.mask_on)
+                write_like_flags(c, Col<const double>{trial, NB}, Col<const double>{sd + (size_t)SROW(R.P) * NB + lane, NB},
+                                 w);
         }
     }
     __syncthreads();
@@ -792,6 +822,58 @@ __global__ void gather_nuis(const double *trial, int W, int ld, const int *nidx,
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
     for (int k = 0; k < n_nuis; k++) out[(size_t)w * n_nuis + k] = trial[(size_t)nidx[k] * ld + w];
+}
+
+// Change mask, sparse likelihoods: the walkers whose flag is set get compact
+// slots in walker order (a deterministic block scan; one 1024-thread block per
+// sparse likelihood); the flag becomes slot + 1, slot -> walker goes to map,
+// the walker's DataParams row is copied to its slot, and cnt[b] is the count.
+struct SparseSet {
+    int like[MAXLIKE], nn[MAXLIKE];
+    double *nuisc[MAXLIKE];
+    int *map[MAXLIKE];
+};
+
+__global__ __launch_bounds__(1024) void like_compact_kernel(DevCfg c, SparseSet ss, int *__restrict__ cnt)
+{
+    __shared__ int wsum[16];
+    const int b = blockIdx.x, l = ss.like[b], nn = ss.nn[b];
+    int *flag = c.like_flag + (size_t)l * c.ld;
+    const double *nuis = c.like_nuis[l];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int chunk = (c.W + 1023) / 1024, w0 = t * chunk, w1 = min(c.W, w0 + chunk);
+    int n = 0;
+    for (int w = w0; w < w1; w++) n += flag[w] != 0;
+    int v = n;                                       // inclusive scan: wave, then the 16 wave totals
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o);
+        if (lane >= o) v += y;
+    }
+    if (lane == 63) wsum[wave] = v;
+    __syncthreads();
+    int before = 0;
+    for (int q = 0; q < wave; q++) before += wsum[q];
+    int off = before + v - n;
+    for (int w = w0; w < w1; w++)
+        if (flag[w] != 0) {
+            flag[w] = off + 1;
+            ss.map[b][off] = w;
+            for (int q = 0; q < nn; q++) ss.nuisc[b][(size_t)off * nn + q] = nuis[(size_t)w * nn + q];
+            off++;
+        }
+    if (t == 1023) cnt[b] = before + v;
+}
+
+// theory rows of the compacted walkers (sparse likelihood with per-walker theory)
+__global__ __launch_bounds__(256) void gather_theory_kernel(const double *__restrict__ dl, long long ld_walker,
+                                                            long long ext, const int *__restrict__ map,
+                                                            const int *__restrict__ cnt, double *__restrict__ dlc)
+{
+    const int w = blockIdx.x;
+    if (w >= *cnt) return;
+    const double *src = dl + (long long)map[w] * ld_walker;
+    double *dst = dlc + (long long)w * ld_walker;
+    for (long long i = threadIdx.x; i < ext; i += 256) dst[i] = src[i];
 }
 
 // Per-chain mean and covariance over history rows first..last
@@ -1214,6 +1296,8 @@ void sampler_set_test_gaussian(cmbs *s, const double *cov, const double *center)
     upload_tables(s);
 }
 
+static void set_change_mask(cmbs *s);
+
 void sampler_add_likelihood(cmbs *s, cmbl_t *like, const int *nuisance_indices, const double *dl, long long ld_field,
                             long long ld_walker) {
     if (!like) fail(CMBL_ERR_ARG, "null likelihood");
@@ -1260,7 +1344,88 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, const int *nuisance_indices, 
     size_t maxws = 0;
     for (auto &l : s->likes) maxws = std::max(maxws, l.like->like->workspace_size(s->W));
     s->ws.alloc(maxws);
+    set_change_mask(s);
     if (s->n_groups > 1) sampler_set_groups(s, s->n_groups);   // resize the group workspaces
+}
+
+// Change mask set-up (recomputed as likelihoods are added).  dependent_params
+// of a CMB likelihood are its nuisance parameters (GeneralTypes.f90:648) and
+// every theory parameter (CosmologyTypes.f90:154); here the theory parameters
+// are the ones no likelihood owns as a nuisance parameter.  A likelihood whose
+// dependent set misses some varying parameter can be skipped for walkers that
+// did not move it; those that support it are evaluated on compacted walker
+// slots (sparse), the others densely with the same keep-the-current-term rule.
+static void set_change_mask(cmbs *s) {
+    const int nl = (int)s->likes.size(), W = s->W;
+    const size_t ld = s->dc.ld;
+    unsigned long long nuis_all = 0;
+    for (auto &l : s->likes)
+        for (int i : l.nidx) nuis_all |= 1ull << i;
+    const unsigned long long all = (s->np >= 64) ? ~0ull : ((1ull << s->np) - 1);
+    const unsigned long long theory = all & ~nuis_all;
+    s->sparse_likes.clear();
+    for (int li = 0; li < nl; li++) {
+        unsigned long long dep = theory;
+        for (int i : s->likes[li].nidx) dep |= 1ull << i;
+        s->dc.like_dep[li] = dep;
+        bool maskable = false;
+        for (int u : s->params_used) maskable |= !((dep >> (u - 1)) & 1ull);
+        s->dc.like_out[li] = nullptr;
+        if (maskable && s->likes[li].like->like->sparse_capable()) s->sparse_likes.push_back(li);
+    }
+    s->mask_on = !s->sparse_likes.empty();
+    if (!s->mask_on) return;
+    s->like_flag.alloc((size_t)nl * ld * 4);
+    s->dc.like_flag = s->like_flag.as<int>();
+    s->like_cnt.alloc(256);
+    for (int li : s->sparse_likes) {
+        const int nn = std::max(1, s->likes[li].like->like->n_nuis);
+        s->like_outc[li].alloc((size_t)W * 8);
+        s->like_nuisc[li].alloc((size_t)W * nn * 8 + (size_t)ld * 4);   // + the slot -> walker map
+        s->dc.like_out[li] = s->like_outc[li].as<double>();
+        if (s->likes[li].ld_walker != 0) s->like_dlc[li].alloc((size_t)W * s->likes[li].ld_walker * 8);
+    }
+}
+
+// the likelihoods of a masked step: compaction of the sparse likelihoods'
+// changed walkers, then every likelihood (sparse ones on the compacted slots)
+static void eval_likes_masked(cmbs *s, hipStream_t stream) {
+    SparseSet ss{};
+    const int ns = (int)s->sparse_likes.size();
+    for (int b = 0; b < ns; b++) {
+        const int li = s->sparse_likes[b];
+        const int nn = s->likes[li].like->like->n_nuis;
+        ss.like[b] = li;
+        ss.nn[b] = nn;
+        ss.nuisc[b] = s->like_nuisc[li].as<double>();
+        ss.map[b] = reinterpret_cast<int *>(ss.nuisc[b] + (size_t)s->W * std::max(1, nn));
+    }
+    int *cnt = s->like_cnt.as<int>();
+    hipLaunchKernelGGL(like_compact_kernel, dim3(ns), dim3(1024), 0, stream, s->dc, ss, cnt);
+    HIP_CHECK(hipGetLastError());
+    for (size_t i = 0; i < s->likes.size(); i++) {
+        auto &l = s->likes[i];
+        const int nn = l.like->like->n_nuis;
+        int b = -1;
+        for (int q = 0; q < ns; q++)
+            if (ss.like[q] == (int)i) b = q;
+        if (b < 0) {
+            l.like->like->loglike_batch(s->W, l.dl, l.ld_field, l.ld_walker, s->dc.like_nuis[i], nn,
+                                        s->like_terms.as<double>() + i * (size_t)s->dc.ld, s->ws.p, stream);
+            continue;
+        }
+        const double *dl = l.dl;
+        if (l.ld_walker != 0) {
+            double *dlc = s->like_dlc[i].as<double>();
+            hipLaunchKernelGGL(gather_theory_kernel, dim3(s->W), dim3(256), 0, stream, l.dl, l.ld_walker,
+                               theory_extent(*l.like->like, l.ld_field), (const int *)ss.map[b], (const int *)(cnt + b),
+                               dlc);
+            HIP_CHECK(hipGetLastError());
+            dl = dlc;
+        }
+        l.like->like->loglike_batch_sparse(s->W, dl, l.ld_field, l.ld_walker, ss.nuisc[b], nn,
+                                           s->like_outc[i].as<double>(), s->ws.p, stream, cnt + b);
+    }
 }
 
 // likelihood terms of walkers [g0, g1) at their trial points
@@ -1304,17 +1469,19 @@ static HistRow next_hist(cmbs *s) {
 }
 
 static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const HistRow &row, hipStream_t stream,
-                      int g0, int g1) {
+                      int g0, int g1, bool masked = false) {
     const dim3 g((g1 - g0 + NB - 1) / NB), b(NB * MH_WAVES);
     const int blk0 = g0 / NB;
     const size_t lds = s->mh_lds;
+    DevCfg dc = s->dc;
+    dc.mask_on = masked ? 1 : 0;
     timed_launch("mh_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
         if (accept && propose)
-            hipExtLaunchKernelGGL(mh_kernel<true, true>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row.p, row.t, blk0);
+            hipExtLaunchKernelGGL(mh_kernel<true, true>, g, b, lds, stream, e0, e1, 0, dc, fast_only, row.p, row.t, blk0);
         else if (accept)
-            hipExtLaunchKernelGGL(mh_kernel<true, false>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row.p, row.t, blk0);
+            hipExtLaunchKernelGGL(mh_kernel<true, false>, g, b, lds, stream, e0, e1, 0, dc, fast_only, row.p, row.t, blk0);
         else
-            hipExtLaunchKernelGGL(mh_kernel<false, true>, g, b, lds, stream, e0, e1, 0, s->dc, fast_only, row.p, row.t, blk0);
+            hipExtLaunchKernelGGL(mh_kernel<false, true>, g, b, lds, stream, e0, e1, 0, dc, fast_only, row.p, row.t, blk0);
     });
     HIP_CHECK(hipGetLastError());
 }
@@ -1349,13 +1516,16 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     // propose(1) | likes | accept(1)+propose(2) | likes | ... | likes | accept(n)
     const int G = s->n_groups;
     if (G == 1) {
-        launch_mh(s, false, true, fast_only, HistRow{}, stream, 0, s->W);
-        eval_likes(s, stream, false, 0, s->W, s->ws.p);
+        const bool m = s->mask_on;
+        launch_mh(s, false, true, fast_only, HistRow{}, stream, 0, s->W, m);
+        if (m) eval_likes_masked(s, stream);
+        else eval_likes(s, stream, false, 0, s->W, s->ws.p);
         for (int k = 1; k < n_steps; k++) {
-            launch_mh(s, true, true, fast_only, next_hist(s), stream, 0, s->W);
-            eval_likes(s, stream, false, 0, s->W, s->ws.p);
+            launch_mh(s, true, true, fast_only, next_hist(s), stream, 0, s->W, m);
+            if (m) eval_likes_masked(s, stream);
+            else eval_likes(s, stream, false, 0, s->W, s->ws.p);
         }
-        launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W);
+        launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W, m);
         return;
     }
     // groups are independent chains: fork from the caller's stream, issue the
@@ -1442,9 +1612,11 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
     for (int step = 0; step < n_steps; step++) {
         s->num_drag++;
         if (s->num_drag % s->dc.oversample_fast != 0) {   // FastParameterSample (:357-361)
-            launch_mh(s, false, true, 1, HistRow{}, stream, 0, s->W);
-            eval_likes(s, stream, false, 0, s->W, s->ws.p);
-            launch_mh(s, true, false, 1, next_hist(s), stream, 0, s->W);
+            const bool m = s->mask_on;
+            launch_mh(s, false, true, 1, HistRow{}, stream, 0, s->W, m);
+            if (m) eval_likes_masked(s, stream);
+            else eval_likes(s, stream, false, 0, s->W, s->ws.p);
+            launch_mh(s, true, false, 1, next_hist(s), stream, 0, s->W, m);
             continue;
         }
         g.istep = 0;

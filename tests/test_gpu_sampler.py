@@ -506,3 +506,66 @@ def test_interleaved_nuisance_indices(tmp_path):
         assert terms[0, w] == pytest.approx(t1, rel=1e-9)
         assert terms[1, w] == pytest.approx(t2, rel=1e-9)
         assert lk[w] == pytest.approx(t1 + t2 + pri, rel=1e-9)
+
+
+@pytest.mark.parametrize("shared_theory", [True, False])
+def test_change_mask_matches_dense(cmbl_golden, refdata, tmp_path, shared_theory):
+    """Per-likelihood change mask (LogLikeWithTheorySet, calclike.f90:374-386):
+    plik_lite (calPlanck) + BICEP/Keck/Planck (6 varying foreground parameters)
+    in separate fast blocks, so every step each walker re-evaluates only the
+    likelihood whose parameters moved; the sparse path compacts those walkers
+    (plik and the HL CMBlikes kernels on compacted slots, theory rows gathered
+    when they are per walker).  Walker groups (cmbs_set_groups) take the dense
+    path, which evaluates every likelihood for every walker: both runs must
+    make the same accept decisions and end at the same points and terms."""
+    import os
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    bc = cmbl_golden["cases"]["bkplanck_3map_bins1to5"]
+    plik = NativeCMBLikelihood("PLIK_LITE", syn.make_plik_lite(12345).write(str(tmp_path)))
+    bk = NativeCMBLikelihood(bc["tag"], os.path.join(refdata, bc["dataset"]), bc["overrides"])
+    plik.nuisance_indices = [2]
+    bk.nuisance_indices = list(range(3, 19))
+    W, steps = 130, 24
+    th = syn.walker_theory(1 if shared_theory else W, seed=8, n_fields=10, ld_field=2512)
+    dl = torch.tensor(th, device="cuda")
+    if shared_theory:
+        dl = dl.expand(W, -1, -1)                     # ld_walker = 0: one slow point
+    bk0 = np.array(bc["nuis"][0])
+    bk0[1] = 0.5                                      # Async > 0
+    P0 = np.concatenate([[0.0222, 1.0], bk0])
+    vary = [2, 3, 4, 5, 6, 8, 9]                      # calPlanck, Adust, Async, alphadust, betadust, alphasync, betasync
+    pmin, pmax = P0.copy(), P0.copy()
+    for i, wdt in zip(vary, [0.1, 2.0, 1.0, 0.5, 0.5, 1.0, 1.0]):
+        pmin[i - 1], pmax[i - 1] = P0[i - 1] - wdt, P0[i - 1] + wdt
+    pm, ps = np.zeros(18), np.zeros(18)
+    pm[1], ps[1] = 1.0, 0.0025
+    sig = np.array([0.002, 0.1, 0.05, 0.02, 0.02, 0.05, 0.05])
+    runs = []
+    for g in (1, 2):
+        s = BatchedMCMC(W, 18, vary, [[1], [2, 3, 4, 5, 6, 7]], 0, pmin, pmax, pm, ps, seed_ij=41, seed_kl=42)
+        s.set_covariance(np.diag(sig ** 2))
+        s.set_groups(g)
+        s.add_likelihood(plik, dl)
+        s.add_likelihood(bk, dl)
+        s.enable_history(steps)
+        s.set_start(np.tile(P0, (W, 1)))
+        s.step(steps, fast_only=True)
+        P, lk, mult, nacc = s.state()
+        runs.append((P.copy(), lk.copy(), mult.copy(), nacc.copy(), s.history_terms(0, steps)))
+        s.close()
+    a, b = runs
+    assert np.all(a[3] > 0)
+    np.testing.assert_array_equal(a[3], b[3])
+    np.testing.assert_array_equal(a[2], b[2])
+    np.testing.assert_allclose(a[0], b[0], rtol=1e-12)
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-10)
+    np.testing.assert_allclose(a[4], b[4], rtol=1e-10)
+    # the terms at the final points are the oracles' values there
+    import cmblikes_oracle as co
+    ob = co.CMBLikesOracle(os.path.join(refdata, bc["dataset"]), bc["overrides"], bc["tag"])
+    op = po.PlikLite(syn.make_plik_lite(12345))
+    for w in (0, 77, W - 1):
+        t = th[0 if shared_theory else w]
+        assert a[4][-1, 0, w] == pytest.approx(op.loglike(t, a[0][w, 1]), rel=1e-9)
+        assert a[4][-1, 1, w] == pytest.approx(ob.loglike(t, a[0][w, 2:]), rel=1e-9)
