@@ -313,10 +313,21 @@ def config5_run(W, rank, world, tmpdir, seconds, steps=100):
     pm[4], ps[4] = 1.59, 0.11
     pm[7], ps[7] = -3.1, 0.3
     used = [1, 2, 3, 4, 5, 7, 8, 9]
+    # blocks as the reference's SetFastSlowParams makes them for this list
+    # (block_fast_likelihood_params, BaseParameters.f90:360-418): no theory
+    # parameter varies (one cached slow point), plik_lite then BK15
+    from cosmomc_amd.likelihood import LikelihoodList
+    from cosmomc_amd.params import set_fast_slow_params
+    ll = LikelihoodList()
+    ll.add(plik)
+    ll.add(bk)
+    ll.add_nuisance_parameters([])
+    varying = [i + 1 in used for i in range(17)]
+    blk = set_fast_slow_params(17, varying, list(ll), num_theory_params=0)
     # starting proposal: a diagonal guess of the posterior widths (no covmat; the
     # reference then learns the proposal freely, covariance_is_diagonal)
     width = np.array([0.0025, 0.5, 1.0, 0.1, 0.1, 0.1, 0.3, 0.2])
-    smp = BatchedMCMC(W, 17, used, [[1], [2, 3, 4, 5, 6, 7, 8]], 0, pmin, pmax, pm, ps, propose_scale=2.4,
+    smp = BatchedMCMC(W, 17, used, blk.param_blocks, blk.slow_block_max, pmin, pmax, pm, ps, propose_scale=2.4,
                       seed_ij=3003 + rank, seed_kl=9373, first_walker=rank * W)
     smp.set_covariance(np.diag(width ** 2))
     th = torch.tensor(syn.walker_theory(1, n_fields=10, ld_field=2512), device="cuda")
@@ -341,6 +352,7 @@ def config5_run(W, rank, world, tmpdir, seconds, steps=100):
         dt = float(t.item())
     out = {"workload": "BK15 (12 B maps x 9 bins, HL, synthetic covariance) + plik_lite_TTTEEE joint, "
                        "8 fast parameters (calPlanck + 7 BK15 foreground), one shared slow point",
+           "param_blocks": blk.param_blocks,
            "walkers_total": W * world, "evals_per_s": W * world * steps / dt, "ms_per_step": dt / steps * 1e3,
            "avg_kernel_us": kernel_profile(smp, 20)}
     if seconds > 0:

@@ -249,14 +249,19 @@ class LikelihoodList:
         contiguous 1-based nuisance indices; returns the extended name list."""
         self.items.sort(key=lambda l: l.speed)
         names = list(param_names)
+        self.first_fast_param = 0
         for like in self.items:
+            like.new_param_block_start = len(names) + 1          # :638
             idx = []
             for nm in like.nuisance_names:
                 if nm in names:
                     idx.append(names.index(nm) + 1)
                 else:
-                    names.append(nm)
+                    names.append(nm)                             # ParamNames_Add: new names only
                     idx.append(len(names))
+            like.new_params = len(names) - like.new_param_block_start + 1   # :641
             like.nuisance_indices = idx
             like.dependent_params = set(idx)
+            if self.first_fast_param == 0 and like.speed >= 0 and like.new_params > 0 and idx:   # :650-651
+                self.first_fast_param = like.new_param_block_start
         return names

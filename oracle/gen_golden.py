@@ -425,6 +425,51 @@ def gen_sptpol():
         json.dump(out, f, indent=1)
 
 
+# TBaseParameters_SetFastSlowParams (BaseParameters.f90:302-433) through the
+# compiled reference (rng_harness "blocks"): (name, config dict); likes =
+# [(new_param_block_start, new_params, speed)] in the sorted list order
+BLOCK_CASES = [
+    ("bk15_plik_default", {"num_params": 23, "num_theory_params": 6, "varying": [1] * 6 + [1] * 8 + [0] * 9,
+                           "likes": [(7, 1, 0), (8, 16, 0)]}),
+    ("three_likes_shared_cal", {"num_params": 30, "num_theory_params": 6,
+                                "varying": [1] * 7 + [0] * 3 + [1] * 9 + [0] * 3 + [1] * 8,
+                                "likes": [(7, 1, 0), (8, 0, 0), (8, 15, 0), (23, 8, 0)]}),
+    ("semi_fast_semi_slow", {"num_params": 12, "num_theory_params": 6, "index_semislow": 4, "fast_param_index": 5,
+                             "varying": [1] * 12, "likes": [(7, 2, 0), (9, 4, 0)]}),
+    ("no_likelihood_blocks", {"num_params": 23, "num_theory_params": 6, "varying": [1] * 14 + [0] * 9,
+                              "likes": [(7, 1, 0), (8, 16, 0)], "block_fast_likelihood_params": "F"}),
+    ("slow_first_likelihood", {"num_params": 20, "num_theory_params": 6, "varying": [1] * 20,
+                               "likes": [(7, 3, -1), (10, 5, 0), (15, 6, 0)], "block_semi_fast": "F"}),
+    ("no_fast_slow", {"num_params": 14, "num_theory_params": 6, "varying": [1] * 14, "likes": [(7, 1, 0), (8, 7, 0)],
+                      "use_fast_slow": "F"}),
+]
+
+
+def blocks_config_text(cfg):
+    lines = [f"num_params = {cfg['num_params']}", f"num_theory_params = {cfg['num_theory_params']}",
+             "varying = " + " ".join(str(v) for v in cfg["varying"]), f"num_likes = {len(cfg['likes'])}"]
+    lines += [f"like{i + 1} = {a} {b} {c}" for i, (a, b, c) in enumerate(cfg["likes"])]
+    for k in ("index_semislow", "fast_param_index", "block_semi_fast", "block_fast_likelihood_params",
+              "use_fast_slow"):
+        if k in cfg:
+            lines.append(f"{k} = {cfg[k]}")
+    return "\n".join(lines) + "\n"
+
+
+def gen_blocks():
+    out = {"cases": {}}
+    with tempfile.TemporaryDirectory() as td:
+        for name, cfg in BLOCK_CASES:
+            rows = run_rng("blocks", blocks_config_text(cfg), td)
+            head = [int(x) for x in rows[0].split()]
+            blocks = [[int(x) for x in r.split()][1:] for r in rows[1:1 + head[0]]]
+            out["cases"][name] = {"config": cfg, "param_blocks": blocks, "num_slow": head[1], "num_fast": head[2],
+                                  "num_semi_slow": head[3], "num_semi_fast": head[4]}
+            print(f"{name:26s} {blocks}")
+    with open(os.path.join(GOLDEN, "blocks_ref.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 # like_approx = exact on the synthetic unbinned datasets (cosmomc_amd.synthetic.make_exact):
 # (name, make_exact kwargs, fields, dataset keys, hat_includes_noise, walkers, nuisance kind)
 EXACT_CASES = [
@@ -480,3 +525,5 @@ if __name__ == "__main__":
         gen_sptpol()
     if not only or "exact" in only:
         gen_exact()
+    if not only or "blocks" in only:
+        gen_blocks()

@@ -24,10 +24,17 @@
 !                   three-line MetropolisAccept of MCMC.f90:119-131 is restated
 !                   inline; the RNG, proposer, Cholesky and inverse are the
 !                   reference's own code.
+!   mode "blocks" : TBaseParameters_SetFastSlowParams (BaseParameters.f90:302-433)
+!                   on BaseParams%varying and a DataLikelihoods list of plain
+!                   TDataLikelihood items carrying new_param_block_start /
+!                   new_params / speed, the blocking keys read from the config
+!                   itself (an ini file); writes every param_blocks entry
 !
-! usage: rng_harness kat|stream|chain|gr <config.txt> <out.txt>
+! usage: rng_harness kat|stream|chain|gr|confid|blocks <config> <out.txt>
 program rng_harness
     use settings
+    use StringUtils, only: numcat
+    use IniObjects
     use RandUtils
     use GeneralTypes
     use MatrixUtils
@@ -56,6 +63,10 @@ program rng_harness
     real(mcp) :: limfrac, lower, upper
     Type(TGenericLikeCalculator) :: Calc
     Type(TCalculationAtParamPoint) :: Pt
+    Type(TSettingIni) :: BIni
+    class(TDataLikelihood), pointer :: BLike
+    logical :: bad
+    integer, allocatable :: ivec(:)
 
     call get_command_argument(1, mode)
     call get_command_argument(2, cfg)
@@ -263,6 +274,47 @@ program rng_harness
                 curlike = like
             end if
             write(u_out, '(I2,*(ES25.17))') merge(1, 0, accpt), like, curlike, P
+        end do
+    case ('blocks')
+        Feedback = 0
+        call BIni%Open(trim(cfg), bad, .false.)
+        if (bad) stop 'cannot open blocks config'
+        num_params = BIni%Read_Int('num_params')
+        num_theory_params = BIni%Read_Int('num_theory_params')
+        index_data = num_theory_params + 1
+        index_semislow = BIni%Read_Int('index_semislow', -1)
+        allocate(ivec(num_params))
+        read(BIni%Read_String('varying'), *) ivec
+        allocate(BaseParams%varying(num_params))
+        BaseParams%varying = ivec /= 0
+        num_params_used = count(BaseParams%varying)
+        allocate(params_used(num_params_used))
+        j = 0
+        do i = 1, num_params
+            if (BaseParams%varying(i)) then
+                j = j + 1
+                params_used(j) = i
+            end if
+        end do
+        n = BIni%Read_Int('num_likes')
+        DataLikelihoods%first_fast_param = 0
+        do i = 1, n
+            allocate(TDataLikelihood :: BLike)
+            deallocate(ivec)
+            allocate(ivec(3))
+            read(BIni%Read_String(numcat('like', i)), *) ivec
+            BLike%new_param_block_start = ivec(1)
+            BLike%new_params = ivec(2)
+            BLike%speed = ivec(3)
+            call DataLikelihoods%Add(BLike)         ! already in speed order (AddNuisanceParameters sorts)
+            if (DataLikelihoods%first_fast_param == 0 .and. BLike%speed >= 0 .and. BLike%new_params > 0) &
+                DataLikelihoods%first_fast_param = BLike%new_param_block_start   ! GeneralTypes.f90:650-651
+        end do
+        call BaseParams%SetFastSlowParams(BIni, BIni%Read_Logical('use_fast_slow', .true.))
+        write(u_out, '(*(I6))') size(BaseParams%param_blocks), BaseParams%num_slow, BaseParams%num_fast, &
+            BaseParams%num_semi_slow, BaseParams%num_semi_fast
+        do i = 1, size(BaseParams%param_blocks)
+            write(u_out, '(*(I6))') size(BaseParams%param_blocks(i)%P), BaseParams%param_blocks(i)%P
         end do
     end select
     close(u_out)
