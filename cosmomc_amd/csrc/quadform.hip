@@ -12,6 +12,20 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 static constexpr int BK = 32;            // k depth staged per pipeline step (16 chunks of 16 B per row)
 
+#ifdef CMAMD_STAMPS
+// per-workgroup phase timestamps (s_memtime; instrumented build only, tools/qf_stamps.py):
+// start, first tile landed, K loop done, partial + ticket done, end; item nJ
+__device__ unsigned long long g_qf_stamps[1024][6];
+#define QSTAMP(k)                                                                                  \
+    do {                                                                                           \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                               \
+        const int b_ = blockIdx.x + blockIdx.y * gridDim.x;                                        \
+        if (tid == 0 && b_ < 1024) g_qf_stamps[b_][k] = t_;                                        \
+    } while (0)
+#else
+#define QSTAMP(k) ((void)0)
+#endif
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void gbl_void_t;
 
@@ -58,6 +72,7 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
     __shared__ __attribute__((aligned(16))) double smem[2 * 2 * QF_TILE * BK];   // [buf][A|B][64][BK], 64 KB
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
+    QSTAMP(0);
     // XCD-aware placement: blocks b and b+8 share an XCD; give each XCD whole
     // walker tiles so a tile's Delta stays in one L2 (speed only)
     int item_ix = blockIdx.x, tile = blockIdx.y;
@@ -82,24 +97,26 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
     f64x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-    // the epilogue's Delta_I tile is independent of the K loop: its loads are
-    // issued first and land while the MFMAs run (one HBM round trip fewer)
+    // the epilogue's Delta_I tile is loaded during the last K step (issued
+    // behind that step's barrier, so the first tiles' wait does not include it)
     double2 dI[QF_TILE * QF_TILE / 2 / 256];
-#pragma unroll
-    for (int u = 0; u < QF_TILE * QF_TILE / 2 / 256; u++) {
-        const int e = tid + 256 * u, r = e >> 5, c2 = (e & 31) * 2;
-        dI[u] = *reinterpret_cast<const double2 *>(delta + (size_t)(w0 + r) * Np + it.I * QF_TILE + c2);
-    }
     dma_tile(smem, Arow, Np, kbase0, wave, lane);
     dma_tile(smem + QF_TILE * BK, Brow, Np, kbase0, wave, lane);
     for (int s = 0; s < nsteps; s++) {
         const int buf = s & 1;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();                              // tile s landed for every wave; buf^1 free
+        if (s == 0) QSTAMP(1);
         if (s + 1 < nsteps) {
             double *nb = smem + (buf ^ 1) * 2 * QF_TILE * BK;
             dma_tile(nb, Arow, Np, kbase0 + (s + 1) * BK, wave, lane);
             dma_tile(nb + QF_TILE * BK, Brow, Np, kbase0 + (s + 1) * BK, wave, lane);
+        } else {
+#pragma unroll
+            for (int u = 0; u < QF_TILE * QF_TILE / 2 / 256; u++) {
+                const int e = tid + 256 * u, r = e >> 5, c2 = (e & 31) * 2;
+                dI[u] = *reinterpret_cast<const double2 *>(delta + (size_t)(w0 + r) * Np + it.I * QF_TILE + c2);
+            }
         }
         const double *A = smem + buf * 2 * QF_TILE * BK;
         const double *B = A + QF_TILE * BK;
@@ -130,6 +147,10 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
         }
     }
     __syncthreads();                                  // all waves done with the operand buffers
+    QSTAMP(2);
+#ifdef CMAMD_STAMPS
+    if (tid == 0 && blockIdx.x + blockIdx.y * gridDim.x < 1024) g_qf_stamps[blockIdx.x + blockIdx.y * gridDim.x][5] = it.nJ;
+#endif
     // Delta_I tile: smem[n][i] (row stride QF_TILE+2)
 #pragma unroll
     for (int u = 0; u < QF_TILE * QF_TILE / 2 / 256; u++) {
@@ -148,19 +169,22 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
     sacc += __shfl_xor(sacc, 16);
     sacc += __shfl_xor(sacc, 32);
     double *tile_part = partial + (size_t)tile * n_items * QF_TILE;
-    if (lk == 0) tile_part[(size_t)item_ix * QF_TILE + n] = sacc;
-
     // ---- in-launch hand-off of the tile's partials to its last-arriving workgroup
+    // (cdna_hip_programming.md section 5 split-K recipe, write-through form): the
+    // partials are stored sc1 (agent-scope relaxed atomic stores), drained by
+    // every storing wave, then one relaxed ticket; no release fence, so no L2
+    // write-back of the tile's other dirty lines
+    if (lk == 0)
+        __hip_atomic_store(tile_part + (size_t)item_ix * QF_TILE + n, sacc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     unsigned int *flag = reinterpret_cast<unsigned int *>(smem + 64 * (QF_TILE + 2));
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned int t = __hip_atomic_fetch_add(counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         flag[0] = (t == (unsigned int)n_items - 1u) ? 1u : 0u;
     }
     __syncthreads();
+    QSTAMP(3);
     if (flag[0] == 0u) return;
     if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -179,7 +203,14 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
         if (w0 + lane < W) out[w0 + lane] = addend ? v + addend[w0 + lane] : v;
         if (lane == 0) counters[tile] = 0u;
     }
+    QSTAMP(4);
 }
+
+#ifdef CMAMD_STAMPS
+extern "C" int cmamd_debug_qf_stamps(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_qf_stamps), sizeof(g_qf_stamps)) == hipSuccess ? 0 : -5;
+}
+#endif
 
 
 // ------------------------------------------------------------------ host side
