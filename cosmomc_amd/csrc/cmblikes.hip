@@ -865,6 +865,7 @@ struct HLDev {
 // phase timestamps (s_memtime) of the first Jacobi rounds of block 0, lane 0
 // (instrumented build only; tools/hl_stamps.py)
 __device__ unsigned long long g_hl_stamps[32][6];
+__device__ unsigned int g_hl_sweeps[2][64];      // waves per sweep count, first / second eigensolve
 #define HSTAMP(k)                                                                                      \
     do {                                                                                               \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                   \
@@ -939,13 +940,16 @@ static constexpr int HL_MAX_SWEEPS = 40;   // as DSYEV's own iteration limit, a 
 // Returns true on the lanes whose row still fails the convergence test after
 // HL_MAX_SWEEPS sweeps (the caller marks that problem failed: NaN and a status bit).
 template <int M>
-__device__ bool hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, int grp, int r, int lane)
+__device__ bool hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, int grp, int r, int lane,
+                               int which)
 {
+    (void)which;
     const bool on = grp < HLRowsLds<M>::G;        // lanes past G*M idle
 #pragma unroll
     for (int k = 0; k < M; k++) V[k] = (k == r) ? 1.0 : 0.0;
     for (int sweep = 0;; sweep++) {
-        // convergence: every off-diagonal |a_rk| <= 1e-18 sqrt(|a_rr a_kk|) or 0;
+        // convergence: every off-diagonal |a_rk| <= 1e-18 sqrt(|a_rr a_kk|) or 0 (a 1e-16
+        // threshold measured no fewer sweeps: 4.6 and 6.0 for the two BK15 solves);
         // the diagonal and a_{r p} written here also serve round 0
         if (on) {
 #pragma unroll
@@ -962,6 +966,10 @@ __device__ bool hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, 
             }
         }
         __syncthreads();
+#ifdef CMAMD_STAMPS
+        if (!__any(big) || sweep == HL_MAX_SWEEPS)
+            if (lane == 0) atomicAdd(&g_hl_sweeps[which][sweep < 63 ? sweep : 63], 1u);
+#endif
         if (!__any(big)) return false;   // wave-uniform: converged groups keep rotating by ~0
         if (sweep == HL_MAX_SWEEPS) return big;
 #pragma unroll 1
@@ -1053,7 +1061,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
         A[j] = v;
     }
     // (1) C = U diag U^T
-    bool unconverged = hl_jacobi_rows<M>(A, V, S, grp, r, lane);
+    bool unconverged = hl_jacobi_rows<M>(A, V, S, grp, r, lane, 0);
     const double dgr = hl_pick<M>(A, r);
     if (on) {
         S.dg[grp][r] = dgr;
@@ -1116,7 +1124,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
     }
     __syncthreads();
     // (4) Rot = V diag V^T; g(x) = sign(x - 1) sqrt(2 max(0, x - ln x - 1))  (:892-894)
-    unconverged = hl_jacobi_rows<M>(A, V, S, grp, r, lane) || unconverged;
+    unconverged = hl_jacobi_rows<M>(A, V, S, grp, r, lane, 1) || unconverged;
     if (on) {
         const double x = hl_pick<M>(A, r);
         const double g = sqrt(2 * fmax(0.0, x - log(x) - 1));
@@ -2305,6 +2313,9 @@ std::unique_ptr<Like> make_cmblikes(const Ini &ini, const std::string &tag) {
 }  // namespace cmamd
 
 #ifdef CMAMD_STAMPS
+extern "C" int cmamd_debug_hl_sweeps(unsigned int *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_hl_sweeps), sizeof(cmamd::g_hl_sweeps)) == hipSuccess ? 0 : -5;
+}
 extern "C" int cmamd_debug_hl_stamps(unsigned long long *host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_hl_stamps), sizeof(cmamd::g_hl_stamps)) == hipSuccess ? 0 : -5;
 }

@@ -33,3 +33,10 @@ if __name__ == "__main__":
     for i, n in enumerate(names):
         print(f"{n:16s} median {np.median(d[:, i + 1] - d[:, i]):8.0f}  max {(d[:, i + 1] - d[:, i]).max():8.0f}")
     print(f"{'round':16s} median {np.median(d[1:, 0] - d[:-1, 0]):8.0f} (s_memtime ticks)")
+    sw = np.zeros((2, 64), dtype=np.uint32)
+    assert N.lib().cmamd_debug_hl_sweeps(sw.ctypes.data_as(C.c_void_p)) == 0
+    for k, lab in enumerate(("first eigensolve", "second eigensolve")):
+        h = sw[k]
+        nz = np.nonzero(h)[0]
+        print(f"{lab}: waves by sweeps (incl. the final check sweep) " +
+              " ".join(f"{i}:{h[i]}" for i in nz) + f"  mean {(h * np.arange(64)).sum() / max(h.sum(), 1):.2f}")
