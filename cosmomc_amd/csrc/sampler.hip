@@ -183,6 +183,11 @@ __device__ int cyc_next(Walker &k, int which, int n, int base)
     return k.cyc[base + lp - 1];
 }
 
+// Rows of R may live in HBM (blocks too big for the LDS image): every pass over
+// a row loads it RCH elements at a time, all in flight together, instead of one
+// dependent round trip per element.  The sums keep the reference's q order.
+static constexpr int RCH = 8;
+
 __device__ void rot_matrix(Walker &k, int off, int n)
 {   // RotMatrix propose.f90:88-102 -> RandRotationD RandUtils.f90:133-153
     // element (j,i) (row j) of this block's R at R[off + j*n + i]
@@ -191,10 +196,29 @@ __device__ void rot_matrix(Walker &k, int off, int n)
             double norm;
             for (;;) {
                 for (int i = 0; i < n; i++) k.vec[i] = gaussian1(k.r);
-                for (int i = 0; i < j; i++) {
+                for (int i = 0; i < j; i++) {   // vec = vec - sum(vec*R(i,:))*R(i,:)
+                    const int base = off + i * n;
                     double s = 0.0;
-                    for (int q = 0; q < n; q++) s += k.vec[q] * k.R[off + i * n + q];
-                    for (int q = 0; q < n; q++) k.vec[q] = k.vec[q] - s * k.R[off + i * n + q];
+                    for (int q0 = 0; q0 < n; q0 += RCH) {
+                        double rv[RCH], vv[RCH];
+#pragma unroll
+                        for (int u = 0; u < RCH; u++) {
+                            const int q = q0 + u;
+                            rv[u] = q < n ? k.R[base + q] : 0.0;
+                            vv[u] = q < n ? k.vec[q] : 0.0;
+                        }
+#pragma unroll
+                        for (int u = 0; u < RCH; u++)
+                            if (q0 + u < n) s += vv[u] * rv[u];
+                    }
+                    for (int q0 = 0; q0 < n; q0 += RCH) {
+                        double rv[RCH];
+#pragma unroll
+                        for (int u = 0; u < RCH; u++) rv[u] = q0 + u < n ? k.R[base + q0 + u] : 0.0;
+#pragma unroll
+                        for (int u = 0; u < RCH; u++)
+                            if (q0 + u < n) k.vec[q0 + u] = k.vec[q0 + u] - s * rv[u];
+                    }
                 }
                 norm = 0.0;
                 for (int q = 0; q < n; q++) norm += k.vec[q] * k.vec[q];
@@ -239,7 +263,14 @@ __device__ void block_proposal(const DevCfg &c, const Tabs &t, Walker &k, int bi
     const int nc = t.blk_nchanged[b];
     const double *M = t.mapping + t.blk_map_off[b];
     const int *chg = t.changed + t.blk_changed_off[b];
-    for (int q = 0; q < n; q++) k.vec[q] = k.R[off + q * n + (lp - 1)] * scale;
+    for (int q0 = 0; q0 < n; q0 += RCH) {
+        double rv[RCH];
+#pragma unroll
+        for (int u = 0; u < RCH; u++) rv[u] = q0 + u < n ? k.R[off + (q0 + u) * n + (lp - 1)] : 0.0;
+#pragma unroll
+        for (int u = 0; u < RCH; u++)
+            if (q0 + u < n) k.vec[q0 + u] = rv[u] * scale;
+    }
     if (k.defer) {
         k.pend_b = b;
         return;
