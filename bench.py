@@ -204,7 +204,7 @@ def kernel_profile(smp, steps):
     more fast steps (HIP events on the launch stream)."""
     import torch
     from cosmomc_amd import _native as N
-    names = ("plik_bin_delta", "plik_quadform_ksplit", "mh_kernel", "cmbl_bk_prologue", "cmbl_window_kernel",
+    names = ("plik_bin_delta", "plik_quadform_ksplit", "mh_kernel", "rot_kernel", "cmbl_bk_prologue", "cmbl_window_kernel",
              "cmbl_reduce_kernel", "cmbl_hl_kernel", "cmbl_quadform", "cmbl_gauss_small_kernel")
     N.profile_reset()
     N.profile_enable(True)

@@ -27,6 +27,7 @@ struct Rows {
     int CYCLP = 5;      // 3 rows: All, Slow, Fast CyclicIndexRandomizer%loopix
     int BLKLP = 8;      // nblocks rows: RandDirectionProposer%loopix
     int ACCF;           // 1 if the last accept of this walker moved it (theory swap for slow steps)
+    int PROT;           // b + 1 while block b's new random rotation is pending for rot_kernel, else 0
     int CYC;            // multiple of 4; all_n + slow_n + fast_n rows: the three index permutations
                         //   (last, so an LDS image without them is the prefix [0, CYC))
     int NI;             // multiple of 4: rows are moved four at a time
@@ -45,6 +46,7 @@ struct DevCfg {
     int ld;                 // row stride of sd / si / like_terms: W rounded up to 64
     double propose_scale, temperature;
     int has_priors, test_like, n_lin;
+    int rot_defer;          // mh_kernel leaves new rotations of blocks >= ROT_DEFER_MIN to rot_kernel
     Rows rows;
     TabLayout tl;
     const int *tab_i;       // [tl.n_int] (allocation padded to a multiple of 64 words)

@@ -161,6 +161,8 @@ struct Walker {
     int fast_ix;
     int defer = 0;    // leave the mapping product to the caller (block index in pend_b, vec filled)
     int pend_b = -1;
+    int defer_rot = 0;   // leave a new rotation of a wide block to rot_kernel (block index in pend_rot)
+    int pend_rot = -1;
 };
 
 __device__ int cyc_next(Walker &k, int which, int n, int base)
@@ -233,6 +235,10 @@ __device__ void rot_matrix(Walker &k, int off, int n)
     }
 }
 
+static constexpr int ROT_DEFER_MIN = 8;   // blocks this wide get their rotations from rot_kernel
+
+__device__ void proposal_tail(const DevCfg &c, const Tabs &t, Walker &k, int b, int lp);
+
 __device__ void block_proposal(const DevCfg &c, const Tabs &t, Walker &k, int bi /*1-based*/)
 {   // GetBlockProposal :247-254 -> ProposeVec :105-120 -> Propose_r :122-139 -> UpdateParams :142-149
     const int b = bi - 1;
@@ -240,9 +246,21 @@ __device__ void block_proposal(const DevCfg &c, const Tabs &t, Walker &k, int bi
     const int off = t.blk_R_off[b];
     int lp = k.blklp[b];
     if (lp % n == 0) {
+        if (k.defer_rot && n >= ROT_DEFER_MIN) {   // rot_kernel draws it and finishes this proposal
+            k.pend_rot = b;
+            return;
+        }
         rot_matrix(k, off, n);
         lp = 0;
     }
+    proposal_tail(c, t, k, b, lp);
+}
+
+// ProposeVec after the rotation check: loop index, step length, UpdateParams
+__device__ void proposal_tail(const DevCfg &c, const Tabs &t, Walker &k, int b, int lp)
+{
+    const int n = t.blk_n[b];
+    const int off = t.blk_R_off[b];
     lp++;
     k.blklp[b] = lp;
     double rf;
@@ -573,9 +591,13 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     if (PROPOSE) {
         for (int i = 0; i < c.np; i++) k.trial[i] = k.P[i];          // Trial = CurParams
         k.defer = par_map;
+        k.defer_rot = c.rot_defer;
         if (fast_only) proposal_fast(c, t, k);
         else proposal(c, t, k);
-        if (par_map) tq[lane] = (double)k.pend_b;                    // the block, for the mapping waves
+        si[(size_t)R.PROT * NB + lane] = k.pend_rot + 1;             // rot_kernel finishes this walker
+        if (k.pend_rot >= 0) {
+            if (par_map) tq[lane] = -1.0;
+        } else if (par_map) tq[lane] = (double)k.pend_b;             // the block, for the mapping waves
         else {
             for (int l = 0; l < c.n_like; l++)
                 for (int q = 0; q < c.like_nn[l]; q++)
@@ -593,7 +615,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     }
     if (par_map) {   // UpdateParams' mapping product, rows spread over the waves (one thread per row, same order)
         __syncthreads();
-        if (act) {
+        if (act && tq[lane] >= 0.0) {
             const Tabs t = make_tabs(c, ti, td, c.stage_cov ? td : c.tab_d);
             const int b = (int)tq[lane];
             const int n = t.blk_n[b], nc = t.blk_nchanged[b];
@@ -608,7 +630,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
             }
         }
         __syncthreads();
-        if (wave == 0 && act) {
+        if (wave == 0 && act && si[(size_t)R.PROT * NB + lane] == 0) {
             const double *trial = sd + (size_t)SROW(R.T) * NB + lane;
             for (int l = 0; l < c.n_like; l++)
                 for (int q = 0; q < c.like_nn[l]; q++)
@@ -633,6 +655,105 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     STAMP(6);
 #endif
 #undef SROW
+}
+
+// ------------------------------------------------------- deferred rotations
+// A new random rotation of a block of ROT_DEFER_MIN or more parameters
+// (RotMatrix propose.f90:88-102 -> RandRotationD RandUtils.f90:133-153) is too
+// big for one lane: mh_kernel stops that walker's proposal at the rotation
+// (Rows::PROT) and this kernel, one wave per walker, finishes it.  Lane q owns
+// column q of the new R in registers; lane 0 draws the Gaussians and forms
+// every sum of the modified Gram-Schmidt from the lanes' products in q order,
+// as rot_matrix does, so R is bit-identical.  Then the rest of ProposeVec
+// (proposal_tail), the nuisance scatter and the change-mask flags.
+__global__ __launch_bounds__(64) void rot_kernel(DevCfg c, int w0)
+{
+    const int w = w0 + blockIdx.x, lane = threadIdx.x;
+    if (w >= c.W) return;
+    const size_t ld = c.ld;
+    const Rows &R = c.rows;
+    const int pend = c.si[(size_t)R.PROT * ld + w];
+    if (pend == 0) return;                              // block-uniform
+    const int b = pend - 1;
+    __shared__ double u_s[97], g[MAXBLK], pr[64], vec_s[MAXBLK];
+    __shared__ double bc;
+    const Tabs t = make_tabs(c, c.tab_i, c.tab_d, c.tab_d);
+    const int n = t.blk_n[b], off = t.blk_R_off[b];
+    for (int i = lane; i < 97; i += 64) u_s[i] = c.sd[(size_t)(R.U + i) * ld + w];
+    Walker k;
+    k.r.u = Col<double>{u_s, 1};
+    k.r.c = c.sd[(size_t)R.C * ld + w];
+    k.r.gset = c.sd[(size_t)R.G * ld + w];
+    k.r.i97 = c.si[(size_t)R.I97 * ld + w];
+    k.r.j97 = c.si[(size_t)R.J97 * ld + w];
+    k.r.iset = c.si[(size_t)R.ISET * ld + w];
+    __syncthreads();
+    double rcol[MAXBLK];
+#pragma unroll
+    for (int i = 0; i < MAXBLK; i++) rcol[i] = 0.0;
+    for (int j = 0; j < n; j++) {
+        double v, norm;
+        for (;;) {
+            if (lane == 0)
+                for (int q = 0; q < n; q++) g[q] = gaussian1(k.r);
+            __syncthreads();
+            v = lane < n ? g[lane] : 0.0;
+#pragma unroll
+            for (int i = 0; i < MAXBLK; i++) {
+                if (i < j) {                            // vec = vec - sum(vec*R(i,:))*R(i,:)
+                    pr[lane] = v * rcol[i];
+                    __syncthreads();
+                    if (lane == 0) {
+                        double s = 0.0;
+                        for (int q = 0; q < n; q++) s += pr[q];
+                        bc = s;
+                    }
+                    __syncthreads();
+                    v = v - bc * rcol[i];
+                    __syncthreads();
+                }
+            }
+            pr[lane] = v * v;
+            __syncthreads();
+            if (lane == 0) {
+                double s = 0.0;
+                for (int q = 0; q < n; q++) s += pr[q];
+                bc = s;
+            }
+            __syncthreads();
+            norm = bc;
+            __syncthreads();
+            if (norm > 1e-3) break;
+        }
+        const double rv = v / sqrt(norm);
+#pragma unroll
+        for (int i = 0; i < MAXBLK; i++)
+            if (i == j) rcol[i] = rv;
+    }
+    if (lane < n)
+#pragma unroll
+        for (int i = 0; i < MAXBLK; i++)
+            if (i < n) c.sd[(size_t)(R.R + off + i * n + lane) * ld + w] = rcol[i];
+    if (lane == 0) {   // R(:, 1) is lane 0's own column: the tail reads its own stores
+        k.R = Col<double>{c.sd + (size_t)R.R * ld + w, (int)ld};
+        k.trial = Col<double>{c.sd + (size_t)R.T * ld + w, (int)ld};
+        k.P = Col<double>{c.sd + (size_t)R.P * ld + w, (int)ld};
+        k.vec = Col<double>{vec_s, 1};
+        k.blklp = Col<int>{c.si + (size_t)R.BLKLP * ld + w, (int)ld};
+        proposal_tail(c, t, k, b, 0);
+        for (int l = 0; l < c.n_like; l++)
+            for (int q = 0; q < c.like_nn[l]; q++)
+                c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = k.trial[t.ti[c.like_nidx[l] + q]];
+        if (c.mask_on) write_like_flags(c, k.trial, k.P, w);
+        c.sd[(size_t)R.C * ld + w] = k.r.c;
+        c.sd[(size_t)R.G * ld + w] = k.r.gset;
+        c.si[(size_t)R.I97 * ld + w] = k.r.i97;
+        c.si[(size_t)R.J97 * ld + w] = k.r.j97;
+        c.si[(size_t)R.ISET * ld + w] = k.r.iset;
+        c.si[(size_t)R.PROT * ld + w] = 0;
+    }
+    __syncthreads();
+    for (int i = lane; i < 97; i += 64) c.sd[(size_t)(R.U + i) * ld + w] = u_s[i];
 }
 
 // ---------------------------------------------------------------- fast dragging
@@ -1160,6 +1281,7 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     d.R_total = s->R_total;
     d.max_blk = 1;
     for (int bn : s->blk_n) d.max_blk = std::max(d.max_blk, bn);
+    d.rot_defer = d.max_blk >= ROT_DEFER_MIN ? 1 : 0;
 
     // ---- shared tables
     TabLayout &tl = d.tl;
@@ -1226,7 +1348,8 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     R.M = R.L + 1;
     R.ND = (R.M + 2) & ~1;
     R.ACCF = R.BLKLP + nb;
-    R.CYC = (R.ACCF + 1 + 3) & ~3;
+    R.PROT = R.ACCF + 1;
+    R.CYC = (R.PROT + 1 + 3) & ~3;
     R.NI = (R.CYC + s->all_n + s->slow_n + s->fast_n + 3) & ~3;
     d.ld = (W + NB - 1) / NB * NB;
     s->sd.alloc((size_t)R.ND * d.ld * 8);
@@ -1514,6 +1637,12 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
         else
             hipExtLaunchKernelGGL(mh_kernel<false, true>, g, b, lds, stream, e0, e1, 0, dc, fast_only, row.p, row.t, blk0);
     });
+    if (propose && dc.rot_defer) {   // the walkers whose proposal waits on a new rotation
+        HIP_CHECK(hipGetLastError());
+        timed_launch("rot_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            hipExtLaunchKernelGGL(rot_kernel, dim3(g1 - g0), dim3(64), 0, stream, e0, e1, 0, dc, g0);
+        });
+    }
     HIP_CHECK(hipGetLastError());
 }
 
