@@ -851,28 +851,14 @@ struct HLDev {
     const int *wcount;      // live walkers (CLDev::wcount)
 };
 
-// ------------------------------------------- HL, register-resident (16 lanes / matrix)
+// ------------------------------------------- HL, register-resident (M lanes / matrix)
 // The two symmetric eigensolves and HL transform of CMBLikes_Transform
-// (:861-914) by cyclic Jacobi, with the matrices in registers: lane r of a
-// 16-lane group owns row r of the working matrix and of the eigenvector
-// matrix, and a 64-lane block runs four (walker, bin) problems.  A Jacobi
-// round is a column rotation of the lane's own row (the round's (c, s) of
-// every column read from LDS) followed by the row rotation with the partner
-// row (one LDS exchange); the column rotation is dispatched per round to a
-// compile-time instance, so every register index is static.  The matrix
-// products go through per-group LDS row buffers.
+// (:861-914) by one-sided cyclic Jacobi (hl_ojacobi), with the matrices in
+// registers: lane r of an M-lane group owns column r of the working matrix
+// and of the eigenvector matrix, and a 64-lane block packs 64/M (walker, bin)
+// problems.  The matrix products go through per-group LDS row buffers.
 #ifdef CMAMD_STAMPS
-// phase timestamps (s_memtime) of the first Jacobi rounds of block 0, lane 0
-// (instrumented build only; tools/hl_stamps.py)
-__device__ unsigned long long g_hl_stamps[32][6];
-__device__ unsigned int g_hl_sweeps[2][64];      // waves per sweep count, first / second eigensolve
-#define HSTAMP(k)                                                                                      \
-    do {                                                                                               \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                   \
-        if (blockIdx.x == 0 && lane == 0 && nst < 32) g_hl_stamps[nst][k] = t_;                      \
-    } while (0)
-#else
-#define HSTAMP(k) ((void)0)
+__device__ unsigned int g_hl_sweeps[2][64];      // waves per sweep count, first / second eigensolve (tools/hl_stamps.py)
 #endif
 
 template <int M>
@@ -880,17 +866,8 @@ struct HLRowsLds {
     static constexpr int G = 64 / M;   // problems per wave: M lanes each, packed (5 for M = 12)
     double rows[G][2][M][M + 1];    // two row buffers per problem (odd stride: fewer bank conflicts);
                                     // in the Jacobi, buffer 1 holds each row as of the round start
-    double cs[G][M][2];             // (c, s) of each column in the current round
     double dg[G][M];                // a diagonal / g(x) broadcast
 };
-
-template <int M>
-__device__ inline double hl_pick(const double (&a)[M], int k) {   // a[k] for a runtime k (no scratch)
-    double v = 0.0;
-#pragma unroll
-    for (int j = 0; j < M; j++) v = (j == k) ? a[j] : v;
-    return v;
-}
 
 template <int M>
 __device__ inline int hl_partner(int rr, int r) {   // round-robin pairing of round rr (circle method)
@@ -899,141 +876,120 @@ __device__ inline int hl_partner(int rr, int r) {   // round-robin pairing of ro
     return ((2 * rr - r) % (M - 1) + (M - 1)) % (M - 1);
 }
 
-// column rotation of one row for round RR (compile-time, so the partner
-// column of every column is a static register index): B = A J, V = V J
-template <int M, int RR>
-__device__ __forceinline__ void hl_colrot(double (&A)[M], double (&V)[M], const double (*cs)[2])
-{
-    if constexpr (RR < M - 1) {
-        double An[M], Vn[M];
-#pragma unroll
-        for (int k = 0; k < M; k++) {
-            const int pk = (k == M - 1) ? RR : (k == RR ? M - 1 : ((2 * RR - k) % (M - 1) + (M - 1)) % (M - 1));
-            const double ck = cs[k][0], sk = cs[k][1];
-            An[k] = A[k] * ck + A[pk] * sk;
-            Vn[k] = V[k] * ck + V[pk] * sk;
-        }
-#pragma unroll
-        for (int k = 0; k < M; k++) {
-            A[k] = An[k];
-            V[k] = Vn[k];
-        }
-    }
-}
-
-template <int M>
-__device__ __forceinline__ void hl_colrot_round(int rr, double (&A)[M], double (&V)[M], const double (*cs)[2])
-{
-    switch (rr) {
-#define HLC(R) case R: hl_colrot<M, R>(A, V, cs); break;
-        HLC(0) HLC(1) HLC(2) HLC(3) HLC(4) HLC(5) HLC(6) HLC(7) HLC(8) HLC(9) HLC(10) HLC(11) HLC(12) HLC(13)
-        HLC(14)
-#undef HLC
-        default: break;
-    }
-}
-
-// cyclic Jacobi of the group's M x M matrix (row r in A), eigenvectors in V (row r)
 static constexpr int HL_MAX_SWEEPS = 40;   // as DSYEV's own iteration limit, a cap that fails loudly
 
-// cyclic Jacobi of the group's M x M matrix (row r in A), eigenvectors in V (row r).
-// Returns true on the lanes whose row still fails the convergence test after
-// HL_MAX_SWEEPS sweeps (the caller marks that problem failed: NaN and a status bit).
+// One-sided (Hestenes) cyclic Jacobi of the group's symmetric M x M matrix C:
+// lane r owns column r of G (initially C's column r, i.e. its row r) and
+// column r of V (initially e_r).  A round pairs lanes (lo, hi) by the
+// round-robin circle schedule; both lanes of a pair read the other's columns
+// from LDS, form a_ll = g_l.g_l, a_hh = g_h.g_h, a_lh = g_l.g_h (the same sums
+// in the same order, so both derive the same rotation) and rotate their own
+// columns: g_l' = c g_l - s g_h, g_h' = s g_l + c g_h, with tan of the angle
+// the smaller root of t^2 + 2 zeta t - 1 = 0, zeta = (a_hh - a_ll) / (2 a_lh).
+// At convergence G = C V and V holds orthonormal eigenvectors in its columns;
+// lam = v_r . g_r = v_r^T C v_r is eigenvalue r, signed.  One column exchange
+// per round (two barriers) replaces the two-sided form's row exchange plus
+// broadcast of every column's rotation (three barriers, about twice the LDS
+// traffic); the column norms are carried across rounds, so a round forms one
+// dot product, and the arithmetic is fused multiply-adds (the eigensolver is
+// not the reference's DSYEV, so no operation order is there to follow).  Pairs
+// with |a_lh| > 1e-15 sqrt(a_ll a_hh) are rotated; a sweep in which no pair had
+// |a_lh| > 1e-9 sqrt(a_ll a_hh) ends the solve (its own rotations, by the
+// quadratic convergence of cyclic Jacobi, leave every pair near 1e-18: no
+// separate check sweep).
+// Returns true on lanes whose pair still needed rotating in sweep
+// HL_MAX_SWEEPS (the caller fails that problem: NaN and a status bit).
 template <int M>
-__device__ bool hl_jacobi_rows(double (&A)[M], double (&V)[M], HLRowsLds<M> &S, int grp, int r, int lane,
-                               int which)
+__device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int grp, int r, int lane, int which,
+                           double &lam)
 {
     (void)which;
+    (void)lane;
     const bool on = grp < HLRowsLds<M>::G;        // lanes past G*M idle
 #pragma unroll
     for (int k = 0; k < M; k++) V[k] = (k == r) ? 1.0 : 0.0;
+    bool failed = false;
     for (int sweep = 0;; sweep++) {
-        // convergence: every off-diagonal |a_rk| <= 1e-18 sqrt(|a_rr a_kk|) or 0 (a 1e-16
-        // threshold measured no fewer sweeps: 4.6 and 6.0 for the two BK15 solves);
-        // the diagonal and a_{r p} written here also serve round 0
-        if (on) {
-#pragma unroll
-            for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = A[k];   // the whole row: no runtime-index picks
-        }
-        __syncthreads();
         bool big = false;
-        if (on) {
-            const double arr = S.rows[grp][1][r][r];
+        // the column's squared norm, recomputed every sweep and updated exactly
+        // as Rutishauser's a_ll' = a_ll - t a_lh, a_hh' = a_hh + t a_lh in between
+        double nrm = 0.0;
 #pragma unroll
-            for (int k = 0; k < M; k++) {
-                const double a = A[k];
-                if (k != r && a != 0.0 && a * a > 1e-36 * fabs(arr * S.rows[grp][1][k][k])) big = true;   // squared: no sqrt
-            }
-        }
-        __syncthreads();
-#ifdef CMAMD_STAMPS
-        if (!__any(big) || sweep == HL_MAX_SWEEPS)
-            if (lane == 0) atomicAdd(&g_hl_sweeps[which][sweep < 63 ? sweep : 63], 1u);
-#endif
-        if (!__any(big)) return false;   // wave-uniform: converged groups keep rotating by ~0
-        if (sweep == HL_MAX_SWEEPS) return big;
+        for (int k = 0; k < M; k++) nrm = fma(G[k], G[k], nrm);
 #pragma unroll 1
         for (int rr = 0; rr < M - 1; rr++) {
-#ifdef CMAMD_STAMPS
-            const int nst = sweep * (M - 1) + rr;
-#endif
-            HSTAMP(0);
-            // (1) this row's pair and rotation (the lower row's a_pq for both lanes); the
-            // diagonal and a_{r p} were exchanged at the end of the previous round
-            double c = 1.0, s = 0.0;
-            int p = r;
-            if (on) p = hl_partner<M>(rr, r);
-            HSTAMP(1);
+            const int p = on ? hl_partner<M>(rr, r) : r;
             if (on) {
-                const int lo = r < p ? r : p, hi = r < p ? p : r;
-                const double apq = S.rows[grp][1][lo][hi], app = S.rows[grp][1][lo][lo], aqq = S.rows[grp][1][hi][hi];
-                double cc = 1.0, ss = 0.0;
-                if (apq != 0.0 && fabs(apq) > 1e-300) {
-                    // t = sign(theta) / (|theta| + sqrt(theta^2 + 1)), theta = d / e, written with
-                    // one division; c = rsqrt(t^2 + 1).  The round's dependent chain of f64
-                    // divides and square roots is what a round waits on.
-                    const double d = aqq - app, e = 2.0 * apq;
+#pragma unroll
+                for (int k = 0; k < M; k++) {
+                    S.rows[grp][0][r][k] = G[k];
+                    S.rows[grp][1][r][k] = V[k];
+                }
+                S.dg[grp][r] = nrm;
+            }
+            __syncthreads();
+            double Gp[M], Vp[M];
+#pragma unroll
+            for (int k = 0; k < M; k++) {        // every load in flight together
+                Gp[k] = on ? S.rows[grp][0][p][k] : 0.0;
+                Vp[k] = on ? S.rows[grp][1][p][k] : 0.0;
+            }
+            if (on) {
+                const bool low = r < p;
+                const double np = S.dg[grp][p];
+                const double all = low ? nrm : np, ahh = low ? np : nrm;
+                double alh = 0.0;
+#pragma unroll
+                for (int k = 0; k < M; k++) alh = fma(low ? G[k] : Gp[k], low ? Gp[k] : G[k], alh);
+                if (alh != 0.0 && alh * alh > 1e-30 * (all * ahh)) {
+                    // cos^2 > 1e-18: columns this far from orthogonal need another sweep;
+                    // below it this sweep's rotation leaves them at ~1e-18 (quadratic convergence)
+                    big = big || alh * alh > 1e-18 * (all * ahh);
+                    const double d = ahh - all, e = 2.0 * alh;
                     const double den = fabs(d) + sqrt(d * d + e * e);
                     double q = __builtin_amdgcn_rcp(den);           // reciprocal + two Newton steps
                     q = fma(q, fma(-den, q, 1.0), q);
                     q = fma(q, fma(-den, q, 1.0), q);
                     const double t = ((d >= 0) == (e >= 0) ? fabs(e) : -fabs(e)) * q;
-                    cc = rsqrt(t * t + 1.0);
-                    ss = t * cc;
+                    const double c = rsqrt(t * t + 1.0), s = t * c;
+                    if (low) {
+#pragma unroll
+                        for (int k = 0; k < M; k++) {
+                            G[k] = fma(-s, Gp[k], c * G[k]);
+                            V[k] = fma(-s, Vp[k], c * V[k]);
+                        }
+                        nrm = fma(-t, alh, all);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < M; k++) {
+                            G[k] = fma(s, Gp[k], c * G[k]);
+                            V[k] = fma(s, Vp[k], c * V[k]);
+                        }
+                        nrm = fma(t, alh, ahh);
+                    }
                 }
-                c = cc;
-                s = (r == lo) ? -ss : ss;      // J[r][r] = c, J[p][r] = s (column r of J)
-                S.cs[grp][r][0] = c;
-                S.cs[grp][r][1] = s;
             }
-            __syncthreads();
-            HSTAMP(2);
-            // (2) B = A J, V = V J on this lane's row; (3) A' = J^T B: row r = c B_r + s B_p
-            if (on) {
-                hl_colrot_round<M>(rr, A, V, S.cs[grp]);
-#pragma unroll
-                for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = A[k];
-            }
-            __syncthreads();
-            HSTAMP(3);
-            if (on) {
-                const double *Bp = S.rows[grp][0][p];
-                // the rotated-away a_rp is exactly 0 (standard Jacobi; computing it leaves
-                // O(eps) noise that the convergence test would keep rotating)
-#pragma unroll
-                for (int k = 0; k < M; k++) A[k] = (k == p) ? 0.0 : c * A[k] + s * Bp[k];
-                if (rr + 1 < M - 1)         // the next round's exchange, one barrier early
-#pragma unroll
-                    for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = A[k];
-            }
-            __syncthreads();
-            HSTAMP(4);
+            __syncthreads();                           // partners' columns read: the next round may write
+        }
+#ifdef CMAMD_STAMPS
+        if (!__any(big) || sweep == HL_MAX_SWEEPS)
+            if (lane == 0) atomicAdd(&g_hl_sweeps[which][sweep < 63 ? sweep : 63], 1u);
+#endif
+        if (!__any(big)) break;          // wave-uniform: converged groups keep checking
+        if (sweep == HL_MAX_SWEEPS) {
+            failed = big;
+            break;
         }
     }
+    double l = 0.0;
+#pragma unroll
+    for (int k = 0; k < M; k++) l = fma(V[k], G[k], l);
+    lam = l;
+    return failed;
 }
 
 template <int M>
-__global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLDev h, const double *__restrict__ cmat,
+__global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLDev h, const double *__restrict__ cmat,
                                                          double *__restrict__ xrows, int W)
 {
     __shared__ HLRowsLds<M> S;
@@ -1060,13 +1016,13 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
         }
         A[j] = v;
     }
-    // (1) C = U diag U^T
-    bool unconverged = hl_jacobi_rows<M>(A, V, S, grp, r, lane, 0);
-    const double dgr = hl_pick<M>(A, r);
+    // (1) C = U diag U^T (lane r: eigenvector r, i.e. column r of U)
+    double dgr;
+    bool unconverged = hl_ojacobi<M>(A, V, S, grp, r, lane, 0, dgr);
     if (on) {
         S.dg[grp][r] = dgr;
 #pragma unroll
-        for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = V[k];     // U rows
+        for (int k = 0; k < M; k++) S.rows[grp][0][k][r] = V[k];     // U rows, from its columns
     }
     __syncthreads();
     // (2) T = Chat U ; R = U^T T scaled by 1/sqrt(diag) (:878-889)
@@ -1124,13 +1080,14 @@ __global__ __launch_bounds__(64, (M <= 12 ? 3 : 1)) void cmbl_hl_rows_kernel(HLD
     }
     __syncthreads();
     // (4) Rot = V diag V^T; g(x) = sign(x - 1) sqrt(2 max(0, x - ln x - 1))  (:892-894)
-    unconverged = hl_jacobi_rows<M>(A, V, S, grp, r, lane, 1) || unconverged;
+    double x;
+    unconverged = hl_ojacobi<M>(A, V, S, grp, r, lane, 1, x) || unconverged;
+    __syncthreads();                               // the solve's last reads of the row buffers
     if (on) {
-        const double x = hl_pick<M>(A, r);
         const double g = sqrt(2 * fmax(0.0, x - log(x) - 1));
         S.dg[grp][r] = (x - 1 >= 0) ? g : -g;
 #pragma unroll
-        for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = V[k];     // V rows
+        for (int k = 0; k < M; k++) S.rows[grp][0][k][r] = V[k];     // V rows, from its columns
     }
     __syncthreads();
     // (5) U = Cfhalf V ; C = U diag(g) U^T (:907-912)
@@ -2315,8 +2272,5 @@ std::unique_ptr<Like> make_cmblikes(const Ini &ini, const std::string &tag) {
 #ifdef CMAMD_STAMPS
 extern "C" int cmamd_debug_hl_sweeps(unsigned int *host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_hl_sweeps), sizeof(cmamd::g_hl_sweeps)) == hipSuccess ? 0 : -5;
-}
-extern "C" int cmamd_debug_hl_stamps(unsigned long long *host) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_hl_stamps), sizeof(cmamd::g_hl_stamps)) == hipSuccess ? 0 : -5;
 }
 #endif
