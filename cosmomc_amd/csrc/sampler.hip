@@ -662,10 +662,31 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
 // (RotMatrix propose.f90:88-102 -> RandRotationD RandUtils.f90:133-153) is too
 // big for one lane: mh_kernel stops that walker's proposal at the rotation
 // (Rows::PROT) and this kernel, one wave per walker, finishes it.  Lane q owns
-// column q of the new R in registers; lane 0 draws the Gaussians and forms
-// every sum of the modified Gram-Schmidt from the lanes' products in q order,
-// as rot_matrix does, so R is bit-identical.  Then the rest of ProposeVec
+// column q of the new R in registers; lane 0 draws the Gaussians, and every
+// sum of the modified Gram-Schmidt is formed from the lanes' products in q
+// order (readlane broadcasts), as rot_matrix does, so R is bit-identical.  Then the rest of ProposeVec
 // (proposal_tail), the nuisance scatter and the change-mask flags.
+// sum of x over lanes 0..n-1 in lane order, formed identically on every lane
+// from v_readlane broadcasts (no LDS round trip, no divergent lane-0 section)
+__device__ __forceinline__ double lane_sum_ordered(double x, int n)
+{
+    const long long bits = __double_as_longlong(x);
+    const int lo = (int)bits, hi = (int)(bits >> 32);
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < MAXBLK; q++)
+        if (q < n) {
+            const unsigned l = (unsigned)__builtin_amdgcn_readlane(lo, q);
+            const long long h = __builtin_amdgcn_readlane(hi, q);
+            s += __longlong_as_double((h << 32) | l);
+        }
+    return s;
+}
+
+#ifdef CMAMD_STAMPS
+__device__ unsigned long long g_rot_ticks[3];     // block 0: total, Gaussian draws, Gram-Schmidt + norms
+#endif
+
 __global__ __launch_bounds__(64) void rot_kernel(DevCfg c, int w0)
 {
     const int w = w0 + blockIdx.x, lane = threadIdx.x;
@@ -675,8 +696,7 @@ __global__ __launch_bounds__(64) void rot_kernel(DevCfg c, int w0)
     const int pend = c.si[(size_t)R.PROT * ld + w];
     if (pend == 0) return;                              // block-uniform
     const int b = pend - 1;
-    __shared__ double u_s[97], g[MAXBLK], pr[64], vec_s[MAXBLK];
-    __shared__ double bc;
+    __shared__ double u_s[97], g[MAXBLK], vec_s[MAXBLK];
     const Tabs t = make_tabs(c, c.tab_i, c.tab_d, c.tab_d);
     const int n = t.blk_n[b], off = t.blk_R_off[b];
     for (int i = lane; i < 97; i += 64) u_s[i] = c.sd[(size_t)(R.U + i) * ld + w];
@@ -691,38 +711,34 @@ __global__ __launch_bounds__(64) void rot_kernel(DevCfg c, int w0)
     double rcol[MAXBLK];
 #pragma unroll
     for (int i = 0; i < MAXBLK; i++) rcol[i] = 0.0;
+#ifdef CMAMD_STAMPS
+    unsigned long long t_start = __builtin_amdgcn_s_memtime(), t_g = 0, t_m = 0, t0;
+#endif
     for (int j = 0; j < n; j++) {
         double v, norm;
         for (;;) {
+#ifdef CMAMD_STAMPS
+            t0 = __builtin_amdgcn_s_memtime();
+#endif
             if (lane == 0)
                 for (int q = 0; q < n; q++) g[q] = gaussian1(k.r);
             __syncthreads();
+#ifdef CMAMD_STAMPS
+            t_g += __builtin_amdgcn_s_memtime() - t0;
+            t0 = __builtin_amdgcn_s_memtime();
+#endif
             v = lane < n ? g[lane] : 0.0;
 #pragma unroll
             for (int i = 0; i < MAXBLK; i++) {
                 if (i < j) {                            // vec = vec - sum(vec*R(i,:))*R(i,:)
-                    pr[lane] = v * rcol[i];
-                    __syncthreads();
-                    if (lane == 0) {
-                        double s = 0.0;
-                        for (int q = 0; q < n; q++) s += pr[q];
-                        bc = s;
-                    }
-                    __syncthreads();
-                    v = v - bc * rcol[i];
-                    __syncthreads();
+                    const double s = lane_sum_ordered(v * rcol[i], n);
+                    v = v - s * rcol[i];
                 }
             }
-            pr[lane] = v * v;
-            __syncthreads();
-            if (lane == 0) {
-                double s = 0.0;
-                for (int q = 0; q < n; q++) s += pr[q];
-                bc = s;
-            }
-            __syncthreads();
-            norm = bc;
-            __syncthreads();
+            norm = lane_sum_ordered(v * v, n);
+#ifdef CMAMD_STAMPS
+            t_m += __builtin_amdgcn_s_memtime() - t0;
+#endif
             if (norm > 1e-3) break;
         }
         const double rv = v / sqrt(norm);
@@ -754,7 +770,20 @@ __global__ __launch_bounds__(64) void rot_kernel(DevCfg c, int w0)
     }
     __syncthreads();
     for (int i = lane; i < 97; i += 64) c.sd[(size_t)(R.U + i) * ld + w] = u_s[i];
+#ifdef CMAMD_STAMPS
+    if (w == 0 && lane == 0) {
+        g_rot_ticks[0] = __builtin_amdgcn_s_memtime() - t_start;
+        g_rot_ticks[1] = t_g;
+        g_rot_ticks[2] = t_m;
+    }
+#endif
 }
+
+#ifdef CMAMD_STAMPS
+extern "C" int cmamd_debug_rot_ticks(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rot_ticks), sizeof(g_rot_ticks)) == hipSuccess ? 0 : -5;
+}
+#endif
 
 // ---------------------------------------------------------------- fast dragging
 // TFastDraggingSampler_GetNewSample (MCMC.f90:338-452) in four launch stages,
@@ -1587,8 +1616,9 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
     const int Wg = g1 - g0;
     const size_t nl = s->likes.size();
     // the likelihoods run in order on the caller's stream: side by side on forked
-    // streams the memory-bound likelihood kernels slowed each other more than they
-    // overlapped (measured on MI355X, W = 1024, plik_lite + lensing: 91.7 vs 89.7 us/step)
+    // streams the memory-bound likelihood kernels slow each other more than they
+    // overlap (MI355X, W = 1024, plik_lite + lensing: 77.1 vs 71.9 us/step; the
+    // binning kernel alone 12.5 -> 26.2 us next to the lensing windows)
     for (size_t i = 0; i < nl; i++) {
         hipStream_t st = stream;
         auto &l = s->likes[i];
