@@ -19,7 +19,7 @@
 //   cmbl_gauss_small_kernel gaussian datasets with <= 64 bandpowers: chi^2 in one kernel
 //   cmbl_reduce_kernel      binned C matrices / bigX rows
 //   cmbl_hl_rows_kernel<M>  the HL transform per (walker, bin): two symmetric
-//                           eigendecompositions by register-resident cyclic Jacobi
+//                           eigendecompositions by one-sided (Hestenes) cyclic Jacobi
 //   cmbl_exact_kernel       like_approx = exact (unbinned): ExactChiSq per (walker, l)
 //   quadform_ksplit         bigX^T C^-1 bigX / 2 on the f64 MFMA (quadform.hip).
 #include <algorithm>
