@@ -480,9 +480,9 @@ def pmc_traffic(kernel, W):
         return None, None
     if d.get("walkers") != W:
         return None, None
-    symbol = {"plik_quadform_ksplit": "quadform_ksplit",                    # profiler label -> kernel
-              "cmbl_window_kernel": "cmbl_window_direct"}.get(kernel, kernel)
-    t = d["per_launch"].get(symbol)
+    symbols = {"plik_quadform_ksplit": ("quadform_ksplit<false>", "quadform_ksplit"),   # profiler label -> kernel
+               "cmbl_window_kernel": ("cmbl_window_direct",)}.get(kernel, (kernel,))
+    t = next((d["per_launch"][k] for k in symbols if k in d["per_launch"]), None)
     if not t:
         return None, None
     return t["fetch_bytes"] + t["write_bytes"], "profiles/pmc_traffic.json"

@@ -2141,9 +2141,19 @@ struct CMBLikes final : Like {
         run(W, dl, ld_field, ld_walker, nuis, ld_nuis, out, ws, stream, wcount);
     }
 
-    void run(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis, long long ld_nuis,
-             double *out, void *ws, hipStream_t stream, const int *wcount) {
-        if (W <= 0) return;
+    // the quadratic-form datasets (HL and large gaussian) can leave the combine to the sampler
+    bool deferred_capable() const override { return approx != 3 && !small_gauss; }
+    QFDeferred loglike_batch_deferred(int W, const double *dl, long long ld_field, long long ld_walker,
+                                      const double *nuis, long long ld_nuis, void *ws, hipStream_t stream) override {
+        if (!deferred_capable()) fail(CMBL_ERR_UNSUPPORTED, "%s: no deferred evaluation", name.c_str());
+        if (!ws) fail(CMBL_ERR_ARG, "deferred evaluation needs a caller workspace");
+        return run(W, dl, ld_field, ld_walker, nuis, ld_nuis, nullptr, ws, stream, nullptr, true);
+    }
+
+    QFDeferred run(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis,
+                   long long ld_nuis, double *out, void *ws, hipStream_t stream, const int *wcount,
+                   bool defer = false) {
+        if (W <= 0) return QFDeferred{};
         dev.wcount = wcount;
         hl.wcount = wcount;
         if (n_nuis > 0 && !nuis) fail(CMBL_ERR_ARG, "%s needs its %d nuisance parameters", name.c_str(), n_nuis);
@@ -2170,7 +2180,7 @@ struct CMBLikes final : Like {
                 }
             });
             HIP_CHECK(hipGetLastError());
-            return;
+            return QFDeferred{};
         }
         const WsLayout o = layout(W);
         char *base = static_cast<char *>(ws);
@@ -2234,7 +2244,7 @@ struct CMBLikes final : Like {
 #undef CMBL_SMALL
             });
             HIP_CHECK(hipGetLastError());
-            return;
+            return QFDeferred{};
         }
         timed_launch("cmbl_reduce_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
             hipExtLaunchKernelGGL(cmbl_reduce_kernel, dim3(tiles, dev.nE), dim3(256), 0, stream, e0, e1, 0, dev,
@@ -2259,7 +2269,9 @@ struct CMBLikes final : Like {
             });
             HIP_CHECK(hipGetLastError());
         }
+        if (defer) return qf.launch_deferred(W, qws, use_add ? addend : nullptr, stream, "cmbl_quadform");
         qf.launch(W, qws, use_add ? addend : nullptr, out, stream, "cmbl_quadform", wcount);
+        return QFDeferred{};
     }
 };
 

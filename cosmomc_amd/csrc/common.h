@@ -157,6 +157,16 @@ std::vector<std::string> split_ws(const std::string &s);
 // .paramnames file -> space-separated names (derived '*' stripped), count
 std::string load_paramnames(const std::string &path, int *count);
 
+// What a deferred quadratic-form launch (QuadForm::launch_deferred) leaves
+// for the kernel that consumes it: -lnL of walker w is the fixed-order combine
+// of quadform.h (qf_group_sum / qf_tree) over the partials of walker tile
+// w / 64 at lane w % 64, + addend[w] when addend is not null.
+struct QFDeferred {
+    const double *partial = nullptr;   // [tiles][n_items][64]
+    int n_items = 0;
+    const double *addend = nullptr;
+};
+
 // ---------------- likelihood object ----------------
 struct Like {
     virtual ~Like() = default;
@@ -180,6 +190,16 @@ struct Like {
         (void)W, (void)dl, (void)ld_field, (void)ld_walker, (void)nuis, (void)ld_nuis, (void)out, (void)ws;
         (void)stream, (void)wcount;
         fail(CMBL_ERR_UNSUPPORTED, "%s: no sparse evaluation", name.c_str());
+    }
+    // Deferred evaluation for the sampler's fast steps: the same launches as
+    // loglike_batch except the quadratic form's split-K combine, which the
+    // sampler's next mh_kernel performs (QFDeferred).  ws must stay untouched
+    // until then.
+    virtual bool deferred_capable() const { return false; }
+    virtual QFDeferred loglike_batch_deferred(int W, const double *dl, long long ld_field, long long ld_walker,
+                                              const double *nuis, long long ld_nuis, void *ws, hipStream_t stream) {
+        (void)W, (void)dl, (void)ld_field, (void)ld_walker, (void)nuis, (void)ld_nuis, (void)ws, (void)stream;
+        fail(CMBL_ERR_UNSUPPORTED, "%s: no deferred evaluation", name.c_str());
     }
     // internal workspace for ws == nullptr
     DevBuf own_ws;

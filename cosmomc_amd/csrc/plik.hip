@@ -324,9 +324,17 @@ struct PlikLite final : Like {
         run(W, dl, ld_field, ld_walker, nuis, ld_nuis, out, ws, stream, wcount);
     }
 
-    void run(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis, long long ld_nuis,
-             double *out, void *ws, hipStream_t stream, const int *wcount) {
-        if (W <= 0) return;
+    bool deferred_capable() const override { return true; }
+    QFDeferred loglike_batch_deferred(int W, const double *dl, long long ld_field, long long ld_walker,
+                                      const double *nuis, long long ld_nuis, void *ws, hipStream_t stream) override {
+        if (!ws) fail(CMBL_ERR_ARG, "deferred evaluation needs a caller workspace");
+        return run(W, dl, ld_field, ld_walker, nuis, ld_nuis, nullptr, ws, stream, nullptr, true);
+    }
+
+    QFDeferred run(int W, const double *dl, long long ld_field, long long ld_walker, const double *nuis,
+                   long long ld_nuis, double *out, void *ws, hipStream_t stream, const int *wcount,
+                   bool defer = false) {
+        if (W <= 0) return QFDeferred{};
         if (n_nuis < 1 || !nuis) fail(CMBL_ERR_ARG, "plik_lite needs the calibration nuisance parameter");
         if (ld_field < lmax_needed + 1) fail(CMBL_ERR_ARG, "ld_field %lld < lmax+1 = %d", ld_field, lmax_needed + 1);
         // ld_walker == 0: every walker reads the same theory (a shared slow point)
@@ -347,7 +355,9 @@ struct PlikLite final : Like {
                                nused, Np, fr, vec_ok, delta, counters, qf.n_counters(W), wcount);
         });
         HIP_CHECK(hipGetLastError());
+        if (defer) return qf.launch_deferred(W, ws, nullptr, stream, "plik_quadform_ksplit");
         qf.launch(W, ws, nullptr, out, stream, "plik_quadform_ksplit", wcount);
+        return QFDeferred{};
     }
 };
 

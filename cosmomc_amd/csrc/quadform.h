@@ -22,6 +22,42 @@ struct QFItem {   // one workgroup's share: row block I x column blocks J0 .. J0
     int I, J0, nJ, pad;
 };
 
+// Split-K combine, one fixed order shared by the in-launch reducer and by a
+// deferred consumer (the sampler's mh_kernel), so both give the same bits:
+// partials p[tile][k][64]; group g sums k = g, g+16, ... ascending from 0.0
+// (loads issued 8 at a time); the 16 group sums meet in a fixed pairwise
+// tree; then + addend.
+static constexpr int QF_GROUPS = 16;
+static constexpr int QF_GROUP_DEPTH = 8;
+
+__device__ inline double qf_group_sum(const double *tile_part, int n_items, int g, int lane) {
+    double r = 0.0;
+    for (int k0 = g; k0 < n_items; k0 += QF_GROUPS * QF_GROUP_DEPTH) {
+        double v[QF_GROUP_DEPTH];
+#pragma unroll
+        for (int j = 0; j < QF_GROUP_DEPTH; j++) {      // every load in flight before the first add
+            const int k = k0 + QF_GROUPS * j;
+            v[j] = (k < n_items) ? tile_part[(size_t)k * QF_TILE + lane] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < QF_GROUP_DEPTH; j++) r += v[j];
+    }
+    return r;
+}
+
+// r[g * stride]: the 16 group sums
+__device__ inline double qf_tree(const double *r, int stride) {
+    double a[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) a[i] = r[i * stride] + r[(i + 8) * stride];
+#pragma unroll
+    for (int i = 0; i < 4; i++) a[i] = a[i] + a[i + 4];
+    a[0] = a[0] + a[2];
+    a[1] = a[1] + a[3];
+    return a[0] + a[1];
+}
+
+
 class QuadForm {
   public:
     // M: n x n row-major symmetric
@@ -36,6 +72,9 @@ class QuadForm {
     // wcount (device int, or null): only walkers [0, *wcount) are live
     void launch(int W, void *ws, const double *addend, double *out, hipStream_t stream, const char *prof_name,
                 const int *wcount = nullptr);
+    // the same launch without the combine: the workgroups store their partials
+    // and exit; the returned descriptor tells a later kernel how to finish
+    QFDeferred launch_deferred(int W, void *ws, const double *addend, hipStream_t stream, const char *prof_name);
 
   private:
     static constexpr int MAXKB = 5;

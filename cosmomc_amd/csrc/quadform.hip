@@ -14,8 +14,9 @@ static constexpr int BK = 32;            // k depth staged per pipeline step (16
 
 #ifdef CMAMD_STAMPS
 // per-workgroup phase timestamps (s_memtime; instrumented build only, tools/qf_stamps.py):
-// start, first tile landed, K loop done, partial + ticket done, end; item nJ
-__device__ unsigned long long g_qf_stamps[1024][6];
+// start, first tile landed, K loop done, partial + ticket done, end; item nJ,
+// partial stored and drained (before the ticket), XCC id
+__device__ unsigned long long g_qf_stamps[1024][8];
 #define QSTAMP(k)                                                                                  \
     do {                                                                                           \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();                               \
@@ -63,6 +64,9 @@ __device__ __forceinline__ void dma_tile(double *lds_tile, const double *g, size
 // Partials are handed off in-launch: the last workgroup of each walker tile
 // (agent-scope release / ticket / acquire, cdna_hip_programming.md section 5
 // split-K recipe) sums them in fixed item order: deterministic results.
+// Without TICKET the partials are only stored: the consumer kernel that runs
+// next on the stream combines them (QFDeferred), with no in-launch hand-off.
+template <bool TICKET>
 __global__ __launch_bounds__(256, 2) void quadform_ksplit(
     const double *__restrict__ Ct, int Np, const double *__restrict__ delta, int W,
     const QFItem *__restrict__ items, int n_items, int xcd_map,
@@ -149,7 +153,12 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
     __syncthreads();                                  // all waves done with the operand buffers
     QSTAMP(2);
 #ifdef CMAMD_STAMPS
-    if (tid == 0 && blockIdx.x + blockIdx.y * gridDim.x < 1024) g_qf_stamps[blockIdx.x + blockIdx.y * gridDim.x][5] = it.nJ;
+    if (tid == 0 && blockIdx.x + blockIdx.y * gridDim.x < 1024) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_qf_stamps[blockIdx.x + blockIdx.y * gridDim.x][5] = it.nJ;
+        g_qf_stamps[blockIdx.x + blockIdx.y * gridDim.x][7] = xcc & 15;
+    }
 #endif
     // Delta_I tile: smem[n][i] (row stride QF_TILE+2)
 #pragma unroll
@@ -169,6 +178,10 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
     sacc += __shfl_xor(sacc, 16);
     sacc += __shfl_xor(sacc, 32);
     double *tile_part = partial + (size_t)tile * n_items * QF_TILE;
+    if (!TICKET) {                                    // the kernel boundary publishes them
+        if (lk == 0) tile_part[(size_t)item_ix * QF_TILE + n] = sacc;
+        return;
+    }
     // ---- in-launch hand-off of the tile's partials to its last-arriving workgroup
     // (cdna_hip_programming.md section 5 split-K recipe, write-through form): the
     // partials are stored sc1 (agent-scope relaxed atomic stores), drained by
@@ -178,6 +191,7 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
         __hip_atomic_store(tile_part + (size_t)item_ix * QF_TILE + n, sacc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    QSTAMP(6);
     unsigned int *flag = reinterpret_cast<unsigned int *>(smem + 64 * (QF_TILE + 2));
     if (tid == 0) {
         const unsigned int t = __hip_atomic_fetch_add(counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -191,15 +205,16 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    // four item groups per walker, combined in fixed order
-    const int g = tid >> 6;
-    double part = 0.0;
-    for (int k = g; k < n_items; k += 4) part += tile_part[(size_t)k * QF_TILE + lane];
+    // the fixed combine order of quadform.h: wave q takes groups q, q+4, q+8, q+12
     double *red = smem + 64 * (QF_TILE + 2) + 8;
-    red[g * QF_TILE + lane] = part;
+#pragma unroll
+    for (int j = 0; j < QF_GROUPS / 4; j++) {
+        const int g = wave + 4 * j;
+        red[g * QF_TILE + lane] = qf_group_sum(tile_part, n_items, g, lane);
+    }
     __syncthreads();
     if (tid < QF_TILE) {
-        const double v = ((red[lane] + red[QF_TILE + lane]) + red[2 * QF_TILE + lane]) + red[3 * QF_TILE + lane];
+        const double v = qf_tree(red + lane, QF_TILE);
         if (w0 + lane < W) out[w0 + lane] = addend ? v + addend[w0 + lane] : v;
         if (lane == 0) counters[tile] = 0u;
     }
@@ -290,11 +305,31 @@ void QuadForm::launch(int W, void *ws, const double *addend, double *out, hipStr
     double *partial = x + (size_t)wpad(W) * Np;
     unsigned int *cnt = counters(ws, W);
     timed_launch(prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
-        hipExtLaunchKernelGGL(quadform_ksplit, dim3(n_items, tiles), dim3(256), 0, stream, e0, e1, 0,
+        hipExtLaunchKernelGGL(quadform_ksplit<true>, dim3(n_items, tiles), dim3(256), 0, stream, e0, e1, 0,
                               d_ct.as<double>(), Np, (const double *)x, W, d_items[kb].as<QFItem>(), n_items,
                               (int)(tiles % 8 == 0), partial, cnt, addend, out, wcount);
     });
     HIP_CHECK(hipGetLastError());
+}
+
+QFDeferred QuadForm::launch_deferred(int W, void *ws, const double *addend, hipStream_t stream, const char *prof_name) {
+    const int tiles = wpad(W) / QF_TILE;
+    const int kb = choose_kb(tiles);
+    const int n_items = (int)items[kb].size();
+    double *x = x_rows(ws);
+    double *partial = x + (size_t)wpad(W) * Np;
+    timed_launch(prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
+        hipExtLaunchKernelGGL(quadform_ksplit<false>, dim3(n_items, tiles), dim3(256), 0, stream, e0, e1, 0,
+                              d_ct.as<double>(), Np, (const double *)x, W, d_items[kb].as<QFItem>(), n_items,
+                              (int)(tiles % 8 == 0), partial, (unsigned int *)nullptr, (const double *)nullptr,
+                              (double *)nullptr, (const int *)nullptr);
+    });
+    HIP_CHECK(hipGetLastError());
+    QFDeferred d;
+    d.partial = partial;
+    d.n_items = n_items;
+    d.addend = addend;
+    return d;
 }
 
 // Cholesky inverse of an SPD matrix (Matrix_Inverse: dpotrf 'L' + dpotri,

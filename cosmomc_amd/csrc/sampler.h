@@ -7,6 +7,7 @@ namespace cmamd {
 
 static constexpr int MAXLIKE = 8;
 static constexpr int MAXGROUPS = 8;
+static constexpr int MAXDEF = 2;        // likelihoods whose split-K combine mh_kernel can take over
 
 // Per-walker state is two row-major SoA arrays in HBM, sd[ND][W] (doubles)
 // and si[NI][W] (ints): row r of walker w at sd[r*W + w].  mh_kernel copies
@@ -73,6 +74,14 @@ struct DevCfg {
     int mask_on;                            // this launch uses the mask (set per launch)
     int *like_flag;                         // [n_like][ld]: 0 unchanged, else 1 (dense) or compact slot + 1 (sparse)
     const double *like_out[MAXLIKE];        // sparse likelihoods: terms by compact slot; null = dense (like_terms)
+    // deferred quadratic-form combines (QFDeferred): the accepting mh_kernel
+    // finishes these likelihoods' -lnL from the split-K partials the step's
+    // evaluation left (one kernel boundary and no in-launch hand-off)
+    int def_cap;                            // LDS room: group-sum rows for this many likelihoods
+    int n_def;                              // this launch: deferred likelihoods to finish (set per launch)
+    int def_like[MAXDEF], def_items[MAXDEF];
+    const double *def_part[MAXDEF];         // [tiles][def_items][64]
+    const double *def_add[MAXDEF];          // [W] or null
 };
 
 struct LikeSlot {
@@ -131,6 +140,12 @@ struct cmbs {
     cmamd::DevBuf like_outc[cmamd::MAXLIKE], like_nuisc[cmamd::MAXLIKE], like_dlc[cmamd::MAXLIKE];
     std::vector<int> sparse_likes;          // likelihood indices evaluated sparsely
     bool mask_on = false;                   // some likelihood can skip walkers (SetMask at add_likelihood)
+    // deferred combines: the likelihoods that may defer (each with a workspace
+    // of its own, which must survive until the accepting mh_kernel), and how
+    // many the last evaluation left pending in dc.def_*
+    std::vector<int> defer_likes;
+    cmamd::DevBuf like_ws[cmamd::MAXLIKE];
+    int pending_def = 0;
     ~cmbs() {
         for (auto &st : streams)
             if (st) (void)hipStreamDestroy(st);

@@ -22,6 +22,7 @@
 
 #include <cstdlib>
 
+#include "quadform.h"
 #include "sampler.h"
 
 namespace cmamd {
@@ -475,7 +476,8 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     double *lk = sd + (size_t)nd_st * NB;                        // [nlk][NB]
     double *vc = lk + (size_t)nlk * NB;                          // [max_blk][NB]
     double *tq = vc + (size_t)c.max_blk * NB;                    // [tq_rows][NB] test-Gaussian row sums / block
-    double *td = tq + (size_t)c.tq_rows * NB;                    // [ntd rounded to 32]
+    double *dq = tq + (size_t)c.tq_rows * NB;                    // [def_cap][QF_GROUPS + 1][NB] deferred combines
+    double *td = dq + (size_t)c.def_cap * (QF_GROUPS + 1) * NB;  // [ntd rounded to 32]
     int *si = reinterpret_cast<int *>(td + ((ntd + 31) & ~31));  // [ni_st][NB]
     int *it = si + (size_t)ni_st * NB;                           // [all_n][NB] when stage_cyc
     int *ti = it + (size_t)(c.stage_cyc ? c.all_n : 0) * NB;     // [n_int rounded to 64]
@@ -505,9 +507,32 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
         for (int l = 0; l < MAXLIKE; l++)
             if (l < c.n_like) ct[l] = c.cur_terms[(size_t)l * W + w];
     }
+    // deferred split-K combines: the 16 group sums of this walker tile's
+    // partials, one group per wave, loaded beside the state image
+    if (ACCEPT && c.n_def) {
+        const int tile = wb / NB;
+        for (int d = 0; d < MAXDEF; d++) {
+            if (d >= c.n_def) break;
+            const double *tp = c.def_part[d] + (size_t)tile * c.def_items[d] * QF_TILE;
+            double *row = dq + (size_t)d * (QF_GROUPS + 1) * NB;
+            for (int g = wave; g < QF_GROUPS; g += MH_WAVES) row[(size_t)g * NB + lane] = qf_group_sum(tp, c.def_items[d], g, lane);
+            if (wave == MH_WAVES - 1) row[(size_t)QF_GROUPS * NB + lane] = (c.def_add[d] && act) ? c.def_add[d][w] : 0.0;
+        }
+    }
     STAMP(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (ACCEPT && c.n_def && wave == 0 && act) {   // finish them in quadform.h's fixed order
+        for (int d = 0; d < MAXDEF; d++) {
+            if (d >= c.n_def) break;
+            const double *row = dq + (size_t)d * (QF_GROUPS + 1) * NB;
+            double v = qf_tree(row + lane, NB);
+            if (c.def_add[d]) v = v + row[(size_t)QF_GROUPS * NB + lane];
+            const int l = c.def_like[d];
+            lk[(size_t)l * NB + lane] = v;
+            const_cast<double *>(c.like_terms)[(size_t)l * W + w] = v;
+        }
+    }
     // the test-Gaussian rows of covinv . (trial - center) are spread over the
     // waves (each row summed by one thread, in order) instead of run serially
     // by the chain wave
@@ -1196,7 +1221,8 @@ static size_t mh_lds_bytes(const cmbs *s) {
     const int nd_st = d.stage_R ? d.rows.ND : d.rows.ND - d.rows.RR;
     const int ni_st = d.stage_cyc ? d.rows.NI : d.rows.CYC;
     const int ntd = d.stage_cov ? d.tl.n_dbl : d.tl.covinv;
-    return (size_t)(nd_st + MAXLIKE + d.max_blk + d.tq_rows) * NB * 8 + (size_t)((ntd + 31) & ~31) * 8 +
+    return (size_t)(nd_st + MAXLIKE + d.max_blk + d.tq_rows + d.def_cap * (QF_GROUPS + 1)) * NB * 8 +
+           (size_t)((ntd + 31) & ~31) * 8 +
            (size_t)(ni_st + (d.stage_cyc ? d.all_n : 0)) * NB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 + 64;
 }
 
@@ -1209,6 +1235,11 @@ static void set_mh_lds(cmbs *s) {
     const size_t cap = 160 * 1024;
     d.stage_R = d.stage_cyc = d.stage_cov = 1;
     d.tq_rows = d.test_like ? s->n_used : 1;   // a row per test-Gaussian row, or one (the proposal's block)
+    d.def_cap = (int)s->defer_likes.size();
+    if (mh_lds_bytes(s) > cap) {               // the deferred combines go first: the likelihoods combine in-launch
+        d.def_cap = 0;
+        s->defer_likes.clear();
+    }
     if (mh_lds_bytes(s) > cap) d.stage_R = 0;
     if (mh_lds_bytes(s) > cap) d.stage_cyc = 0;
     if (mh_lds_bytes(s) > cap) d.stage_cov = 0;
@@ -1528,6 +1559,17 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, const int *nuisance_indices, 
     for (auto &l : s->likes) maxws = std::max(maxws, l.like->like->workspace_size(s->W));
     s->ws.alloc(maxws);
     set_change_mask(s);
+    // likelihoods whose quadratic-form combine the accepting mh_kernel can take
+    // over (dense evaluation only: the sparse ones write compacted slots)
+    s->defer_likes.clear();
+    for (int i = 0; i < (int)s->likes.size() && (int)s->defer_likes.size() < MAXDEF; i++) {
+        bool sparse = false;
+        for (int q : s->sparse_likes) sparse |= q == i;
+        if (!sparse && s->likes[i].like->like->deferred_capable()) s->defer_likes.push_back(i);
+    }
+    for (int i = 0; i < MAXLIKE; i++) s->like_ws[i].release();
+    set_mh_lds(s);
+    for (int i : s->defer_likes) s->like_ws[i].alloc(s->likes[i].like->like->workspace_size(s->W));
     if (s->n_groups > 1) sampler_set_groups(s, s->n_groups);   // resize the group workspaces
 }
 
@@ -1572,7 +1614,25 @@ static void set_change_mask(cmbs *s) {
 
 // the likelihoods of a masked step: compaction of the sparse likelihoods'
 // changed walkers, then every likelihood (sparse ones on the compacted slots)
-static void eval_likes_masked(cmbs *s, hipStream_t stream) {
+// a deferrable likelihood's evaluation for the accepting mh_kernel that follows:
+// the launches up to the quadratic form's partials, recorded in s->dc.def_*
+static bool eval_deferred(cmbs *s, size_t i, const double *nuis, hipStream_t stream) {
+    int k = -1;
+    for (size_t q = 0; q < s->defer_likes.size(); q++)
+        if (s->defer_likes[q] == (int)i) k = (int)q;
+    if (k < 0) return false;
+    auto &l = s->likes[i];
+    const QFDeferred d = l.like->like->loglike_batch_deferred(s->W, l.dl, l.ld_field, l.ld_walker, nuis,
+                                                              l.like->like->n_nuis, s->like_ws[i].p, stream);
+    const int p = s->pending_def++;
+    s->dc.def_like[p] = (int)i;
+    s->dc.def_items[p] = d.n_items;
+    s->dc.def_part[p] = d.partial;
+    s->dc.def_add[p] = d.addend;
+    return true;
+}
+
+static void eval_likes_masked(cmbs *s, hipStream_t stream, bool defer = false) {
     SparseSet ss{};
     const int ns = (int)s->sparse_likes.size();
     for (int b = 0; b < ns; b++) {
@@ -1593,6 +1653,7 @@ static void eval_likes_masked(cmbs *s, hipStream_t stream) {
         for (int q = 0; q < ns; q++)
             if (ss.like[q] == (int)i) b = q;
         if (b < 0) {
+            if (defer && eval_deferred(s, i, s->dc.like_nuis[i], stream)) continue;
             l.like->like->loglike_batch(s->W, l.dl, l.ld_field, l.ld_walker, s->dc.like_nuis[i], nn,
                                         s->like_terms.as<double>() + i * (size_t)s->dc.ld, s->ws.p, stream);
             continue;
@@ -1612,8 +1673,11 @@ static void eval_likes_masked(cmbs *s, hipStream_t stream) {
 }
 
 // likelihood terms of walkers [g0, g1) at their trial points
-static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1, void *ws) {
+// defer: the accepting mh_kernel launched next finishes the deferrable
+// likelihoods (all walkers, one group)
+static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1, void *ws, bool defer = false) {
     const int Wg = g1 - g0;
+    if (defer && (g0 != 0 || g1 != s->W)) fail(CMBL_ERR_ARG, "internal: deferred evaluation of a walker group");
     const size_t nl = s->likes.size();
     // the likelihoods run in order on the caller's stream: side by side on forked
     // streams the memory-bound likelihood kernels slow each other more than they
@@ -1630,6 +1694,7 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
                                s->dc.tab_i + s->dc.like_nidx[i], nn, nb);
             HIP_CHECK(hipGetLastError());
         }
+        if (defer && eval_deferred(s, i, nb, st)) continue;
         l.like->like->loglike_batch(Wg, l.dl + (size_t)g0 * l.ld_walker, l.ld_field, l.ld_walker,
                                     nb + (size_t)g0 * nn, nn, s->like_terms.as<double>() + i * (size_t)s->dc.ld + g0,
                                     ws, st);
@@ -1659,6 +1724,9 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
     const size_t lds = s->mh_lds;
     DevCfg dc = s->dc;
     dc.mask_on = masked ? 1 : 0;
+    if (s->pending_def && !accept) fail(CMBL_ERR_ARG, "internal: deferred likelihoods without an accepting step");
+    dc.n_def = s->pending_def;
+    s->pending_def = 0;
     timed_launch("mh_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
         if (accept && propose)
             hipExtLaunchKernelGGL(mh_kernel<true, true>, g, b, lds, stream, e0, e1, 0, dc, fast_only, row.p, row.t, blk0);
@@ -1708,12 +1776,12 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (G == 1) {
         const bool m = s->mask_on;
         launch_mh(s, false, true, fast_only, HistRow{}, stream, 0, s->W, m);
-        if (m) eval_likes_masked(s, stream);
-        else eval_likes(s, stream, false, 0, s->W, s->ws.p);
+        if (m) eval_likes_masked(s, stream, true);
+        else eval_likes(s, stream, false, 0, s->W, s->ws.p, true);
         for (int k = 1; k < n_steps; k++) {
             launch_mh(s, true, true, fast_only, next_hist(s), stream, 0, s->W, m);
-            if (m) eval_likes_masked(s, stream);
-            else eval_likes(s, stream, false, 0, s->W, s->ws.p);
+            if (m) eval_likes_masked(s, stream, true);
+            else eval_likes(s, stream, false, 0, s->W, s->ws.p, true);
         }
         launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W, m);
         return;

@@ -3,7 +3,9 @@
 in-kernel s_memtime stamps of every workgroup (instrumented build,
 tools/_stamps/, -DCMAMD_STAMPS):
   0 start, 1 first operand tiles landed, 2 K loop done, 3 partial + ticket
-  done, 4 end of the last arriver's reduction.
+  done, 4 end of the last arriver's reduction, 6 partial stored and drained.
+s_memtime counters are per XCD, so cross-workgroup times are compared within
+one XCD only (slot 7).
 Run once without arguments on the dev box (builds), then with --no-build on
 the GPU."""
 import os
@@ -36,24 +38,27 @@ if __name__ == "__main__":
         for _ in range(20):
             like.loglike_batch(th, cal)
         torch.cuda.synchronize()
-        st = np.zeros((1024, 6), dtype=np.uint64)
+        st = np.zeros((1024, 8), dtype=np.uint64)
         fn = N.lib().cmamd_debug_qf_stamps
         fn.argtypes = [C.c_void_p]
         assert fn(st.ctypes.data) == 0
     d = st.astype(np.int64)
-    live = d[:, 0] > 0
-    d = d[live]
-    t0 = d[:, 0].min()
-    for k in range(5):
-        d[:, k] = np.where(d[:, k] > 0, d[:, k] - t0, -1)
-    print(f"workgroups {len(d)}; ticks relative to the first start")
-    for lab, a, b in (("start", None, 0), ("first tiles", 0, 1), ("K loop", 1, 2), ("partial+ticket", 2, 3)):
-        v = d[:, b] if a is None else d[:, b] - d[:, a]
-        print(f"{lab:16s} min {v.min():7d} median {np.median(v):9.0f} max {v.max():7d}")
-    last = d[d[:, 4] >= 0]
-    print(f"{'reduction':16s} median {np.median(last[:, 4] - last[:, 3]):9.0f}  end max {last[:, 4].max()}")
+    d = d[d[:, 0] > 0]
+    print(f"workgroups {len(d)}; per-workgroup phase lengths (ticks)")
+    for lab, a, b in (("first tiles", 0, 1), ("K loop", 1, 2), ("dot+partial drain", 2, 6), ("ticket", 6, 3)):
+        v = d[:, b] - d[:, a]
+        print(f"{lab:18s} min {v.min():7d} median {np.median(v):9.0f} max {v.max():7d}")
+    last = d[d[:, 4] > 0]
+    print(f"{'reduction':18s} median {np.median(last[:, 4] - last[:, 3]):9.0f}")
     for nj in sorted(set(d[:, 5])):
         m = d[:, 5] == nj
-        print(f"nJ={nj}: {m.sum()} wgs, K loop median {np.median(d[m, 2] - d[m, 1]):.0f}, "
-              f"end-of-K median {np.median(d[m, 2]):.0f}")
-    print("end of every K loop (sorted, deciles):", np.percentile(d[:, 2], [0, 10, 50, 90, 100]).astype(int))
+        print(f"nJ={nj}: {m.sum()} wgs, K loop median {np.median(d[m, 2] - d[m, 1]):.0f}")
+    print("per XCD, relative to its first start: start / first tiles / K done / ticket done / end (max over wgs)")
+    for x in sorted(set(d[:, 7])):
+        e = d[d[:, 7] == x]
+        t0 = e[:, 0].min()
+        ends = e[e[:, 4] > 0][:, 4]
+        print(f"  xcc {x}: {len(e)} wgs  start max {e[:, 0].max() - t0:6d}  first tiles med {np.median(e[:, 1] - t0):7.0f}"
+              f"  K done med {np.median(e[:, 2] - t0):7.0f} max {e[:, 2].max() - t0:7d}"
+              f"  ticket med {np.median(e[:, 3] - t0):7.0f} max {e[:, 3].max() - t0:7d}"
+              f"  end max {(ends.max() - t0) if len(ends) else -1:7d}")
