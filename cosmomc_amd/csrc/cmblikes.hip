@@ -378,10 +378,12 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
 
 // Window contraction without aberration or foregrounds (TBinWindows_bin
 // :1230-1256 on GetTheoryMapCls :1022-1052).  The spectrum operand comes
-// straight from global memory: lane (walker li, quarter kq) of a wave holds 8
-// consecutive l of its walker's spectrum, l = l0 + 32 st + 8 kq + s, and MFMA
-// step s contracts the four l {8 kq + s}; every load is a 16-byte vector and
-// the next step's spectra are in flight during this step's MFMAs.  The weights
+// straight from global memory: lane (walker li, quarter kq) of a wave holds the
+// 8 l {l0 + 32 st + 8 j + 2 kq + h : j < 4, h < 2} of its walker's spectrum in
+// slot 2 j + h, and MFMA step s = 2 j + h contracts the four l {8 j + 2 kq + h};
+// every load is a 16-byte vector, and the four kq lanes of a walker read 64
+// contiguous bytes per load instruction (one half line, not four scattered
+// quarters), and the next step's spectra are in flight during this step's MFMAs.  The weights
 // (8 KB per 64 l) are shared by the block's four waves through a
 // double-buffered LDS tile: read per wave from L2 they cost 24.2 vs 17.7 us per
 // launch (lensing, W = 1024, MI355X).  The calibration (AdaptTheoryForMaps
@@ -411,19 +413,24 @@ __global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double 
     const int ncb = (it.ncol + 15) >> 4;
     const int nstep = it.nch * NSUB;
     double t[LPL], tn[LPL], a[LPL], a2[LPL];
+    static_assert(LPL == 8, "slot 2 j + h holds l = 8 j + 2 kq + h");
     auto load_t = [&](int st, double *dst) {
-        const int lb = it.l0 + st * STEP + LPL * kq;
-        if (vec_ok && lb + LPL - 1 <= it.l1) {
-            const double2 *src = reinterpret_cast<const double2 *>(Df + lb);
+        const int lb = it.l0 + st * STEP + 2 * kq;
+        if (vec_ok && it.l0 + st * STEP + STEP - 1 <= it.l1) {
 #pragma unroll
-            for (int s = 0; s < LPL / 2; s++) {
-                const double2 v = src[s];
-                dst[2 * s] = v.x;
-                dst[2 * s + 1] = v.y;
+            for (int j = 0; j < LPL / 2; j++) {
+                const double2 v = *reinterpret_cast<const double2 *>(Df + lb + 8 * j);
+                dst[2 * j] = v.x;
+                dst[2 * j + 1] = v.y;
             }
         } else {
 #pragma unroll
-            for (int s = 0; s < LPL; s++) dst[s] = (lb + s <= it.l1) ? Df[lb + s] : 0.0;
+            for (int j = 0; j < LPL / 2; j++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int l = lb + 8 * j + h;
+                    dst[2 * j + h] = (l <= it.l1) ? Df[l] : 0.0;
+                }
         }
     };
     // weights [nch][ncb][16][WK_CHUNK]; thread tid moves column tid/16, l 2 (tid%16) .. +1
@@ -441,13 +448,13 @@ __global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double 
         *reinterpret_cast<double2 *>(wsh + ((buf * 2 + 0) * 16 + wc) * WROW + wp) = wr0;
         if (ncb > 1) *reinterpret_cast<double2 *>(wsh + ((buf * 2 + 1) * 16 + wc) * WROW + wp) = wr1;
     };
-    auto read_w = [&](int buf, int cb, double *dst) {   // A operand: column li, the lane's LPL l
-        const double *src = wsh + ((buf * 2 + cb) * 16 + li) * WROW + LPL * kq;
+    auto read_w = [&](int buf, int cb, double *dst) {   // A operand: column li at the lane's LPL l
+        const double *src = wsh + ((buf * 2 + cb) * 16 + li) * WROW + 2 * kq;
 #pragma unroll
-        for (int s = 0; s < LPL / 2; s++) {
-            const double2 v = *reinterpret_cast<const double2 *>(src + 2 * s);
-            dst[2 * s] = v.x;
-            dst[2 * s + 1] = v.y;
+        for (int j = 0; j < LPL / 2; j++) {
+            const double2 v = *reinterpret_cast<const double2 *>(src + 8 * j);
+            dst[2 * j] = v.x;
+            dst[2 * j + 1] = v.y;
         }
     };
     f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};

@@ -382,6 +382,35 @@ def test_history_terms_and_chi2_chain_files(tmp_path):
     assert open(tmp_path / "run.likelihoods").read().split("\t")[:3] == ["1", "CMB", "PLIK_LITE"]
 
 
+@pytest.mark.gpu
+def test_deferred_combine_bitwise(tmp_path):
+    """In fast steps the plik quadratic form leaves its split-K partials to the
+    accepting mh_kernel (QFDeferred); the terms it finishes are bit-identical
+    to cmbl_loglike_batch's in-launch combine at the same points (W = 512:
+    eight walker tiles, XCD-aware item placement)."""
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    data = syn.make_plik_lite(12345)
+    like = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    like.nuisance_indices = [2]
+    W, steps = 512, 12
+    th = syn.walker_theory(W, seed=5, n_fields=3)
+    dl = torch.tensor(th, device="cuda")
+    s = BatchedMCMC(W, 3, [2], [[1]], 0, [0.0222, 0.9, 3.05], [0.0222, 1.1, 3.05], [0.0, 1.0, 0.0],
+                    [0.0, 0.0025, 0.0], seed_ij=57, seed_kl=68)
+    s.set_covariance(np.array([[0.002 ** 2]]))
+    s.add_likelihood(like, dl)
+    s.enable_history(steps)
+    s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
+    s.step(steps, fast_only=True)
+    hist = s.history_host(0, steps)
+    terms = s.history_terms(0, steps)
+    for k in (0, steps // 2, steps - 1):
+        cal = torch.tensor(hist[k, 0, :].copy(), device="cuda").reshape(-1, 1)
+        ref = like.loglike_batch(dl, cal).cpu().numpy()
+        assert np.array_equal(terms[k, 0], ref), np.abs(terms[k, 0] - ref).max()
+
+
 @pytest.mark.parametrize("oversample", [1, 3])
 def test_full_steps_with_theory_callback(tmp_path, oversample):
     """cmbs_step_theory: full GetNewSample steps (slow amplitude A and fast
