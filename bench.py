@@ -446,11 +446,16 @@ def cpu_baseline(seconds, lensing=True, repeats=5):
                 "sample": f"C restatement oracle/liboracle.so (plik_lite only), 1 thread, {seconds:g} s"}
 
 
-def lensing_window_bytes(refdir):
+PLIK_RANGES = {"TT": (30, 2508), "TE": (30, 1996), "EE": (30, 1996)}   # plik_lite's binned l (CMB.f90:315-325)
+
+
+def lensing_window_bytes(refdir, with_plik=False):
     """Algorithmic bytes of one lensing window-contraction launch, split into
     per-walker theory bytes (each field's D_l over the union of its windows'
     nonzero l ranges, read once) and per-launch window bytes (nonzero weights,
-    read once): CMBlikes.f90:1230-1256 over the consext8 windows."""
+    read once): CMBlikes.f90:1230-1256 over the consext8 windows.  with_plik:
+    the fused window pass (theorypass.hip), which also reads plik_lite's binned
+    l (the union per field, once) and its 6413 weights."""
     base = os.path.join(refdir, LENS_DATASET.replace(".dataset", ""))
     ranges = {}
     wbytes = 0
@@ -464,6 +469,11 @@ def lensing_window_bytes(refdir):
                     r = ranges.get(f, (lo, hi))
                     ranges[f] = (min(r[0], lo), max(r[1], hi))
                     wbytes += 8 * len(nz)
+    if with_plik:
+        for f, (lo, hi) in PLIK_RANGES.items():
+            r = ranges.get(f, (lo, hi))
+            ranges[f] = (min(r[0], lo), max(r[1], hi))     # the lensing ranges contain or adjoin plik's
+        wbytes += 8 * N_L
     per_walker = 8 * sum(hi - lo + 1 for lo, hi in ranges.values())
     return per_walker, wbytes
 
@@ -509,6 +519,7 @@ def main():
     with tempfile.TemporaryDirectory() as td:
         smp, likes, theory, _ = build_problem(W, rank, td, args.groups, lensing=not args.no_lensing)
         lens_bytes = lensing_window_bytes(os.path.join(td, "refdata")) if not args.no_lensing else (0, 0)
+        fused_bytes = lensing_window_bytes(os.path.join(td, "refdata"), True) if not args.no_lensing else (0, 0)
 
         def barrier():
             if world > 1:
@@ -536,7 +547,7 @@ def main():
         smp.step(args.steps, fast_only=True)
         torch.cuda.synchronize()
         N.profile_enable(False)
-        kern = {k: N.profile_read(k) for k in ("plik_bin_delta", "plik_quadform_ksplit", "mh_kernel",
+        kern = {k: N.profile_read(k) for k in ("theory_window_kernel", "plik_bin_delta", "plik_quadform_ksplit", "mh_kernel",
                                                 "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_gauss_small_kernel",
                                                 "cmbl_quadform")}
         kern = {k: v for k, v in kern.items() if v[1]}
@@ -564,6 +575,8 @@ def main():
             ach = W * BYTES_BIN / (avg_ms[dom] * 1e-3) / 1e9
         elif dom == "cmbl_window_kernel":
             ach = (W * lens_bytes[0] + lens_bytes[1]) / (avg_ms[dom] * 1e-3) / 1e9
+        elif dom == "theory_window_kernel":
+            ach = (W * fused_bytes[0] + fused_bytes[1]) / (avg_ms[dom] * 1e-3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": (ach / PEAK_HBM_GBS) if ach else None, "traffic": None}
     roof["avg_kernel_us"] = {k: (v * 1e3 if v else None) for k, v in avg_ms.items()}

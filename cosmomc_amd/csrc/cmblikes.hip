@@ -390,7 +390,7 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
 // :1113-1124, D_l / cal^2 for T/E/B pairs) is linear and is applied to the
 // sums.  Blocks are dealt to the 8 XCDs round-robin; the remap puts all walker
 // tiles of an item on one XCD so its weights are fetched into one L2 (17.9 vs
-// 18.7 us with the linear order).
+// 18.7 us with the linear order; 17.5 vs 17.7 us against an XCD-balanced split).
 __global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double *__restrict__ dl, long long ld_field,
                                                          long long ld_walker, const double *__restrict__ nuis,
                                                          long long ld_nuis, double *__restrict__ partial, int W,
@@ -398,6 +398,8 @@ __global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double 
 {
     constexpr int LPL = 8, STEP = 4 * LPL, NSUB = WK_CHUNK / STEP, WROW = STEP + 2;
     __shared__ __attribute__((aligned(16))) double wsh[2 * 2 * 16 * WROW];   // [buf][col block][col][l]
+    // blocks are dealt to the XCDs round-robin: all walker tiles of an item on one XCD
+    // (its weights in one L2); measured faster than an XCD-balanced split of the units
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
     const int item = xcd + 8 * (j / tiles), tile = j % tiles;
     if (item >= c.nitem) return;
@@ -412,7 +414,7 @@ __global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double 
     const double *Df = dl + (long long)wl * ld_walker + (long long)pr.field * ld_field;
     const int ncb = (it.ncol + 15) >> 4;
     const int nstep = it.nch * NSUB;
-    double t[LPL], tn[LPL], a[LPL], a2[LPL];
+    double t[LPL], tn[LPL], tnn[LPL], a[LPL], a2[LPL];
     static_assert(LPL == 8, "slot 2 j + h holds l = 8 j + 2 kq + h");
     auto load_t = [&](int st, double *dst) {
         const int lb = it.l0 + st * STEP + 2 * kq;
@@ -458,17 +460,18 @@ __global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double 
         }
     };
     f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    // the spectra run two steps ahead (measured neutral: the read pattern itself
+    // gives 4.2-4.5 TB/s here with the MFMAs removed, tools/membench2.hip 6.2)
     load_t(0, t);
     fetch_w(0);
+    if (nstep > 1) load_t(1, tn);
     store_w(0);
     __syncthreads();
     for (int st = 0; st < nstep; st++) {
         const bool more = st + 1 < nstep;
         const int cur = st & 1;
-        if (more) {                                    // in flight across this step's MFMAs
-            load_t(st + 1, tn);
-            fetch_w(st + 1);
-        }
+        if (more) fetch_w(st + 1);                     // in flight across this step's MFMAs
+        if (st + 2 < nstep) load_t(st + 2, tnn);
         read_w(cur, 0, a);
         if (ncb > 1) read_w(cur, 1, a2);
 #pragma unroll
@@ -481,7 +484,10 @@ __global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double 
             store_w(cur ^ 1);      // buffer cur ^ 1 was last read before the previous barrier
             __syncthreads();
 #pragma unroll
-            for (int s = 0; s < LPL; s++) t[s] = tn[s];
+            for (int s = 0; s < LPL; s++) {
+                t[s] = tn[s];
+                tn[s] = tnn[s];
+            }
         }
     }
     if (w < Wc) {
@@ -538,8 +544,10 @@ __global__ __launch_bounds__(256, 2) void cmbl_window_group(CLDev c, const GItem
     // the item's window weights of one step, double-buffered: [GP * 16 columns][STEP (+2 pad)]
     constexpr int WR = STEP + 2;
     __shared__ __attribute__((aligned(16))) double wsh[2][GP * 16 * WR];
+    // blocks are dealt to the XCDs round-robin: all walker tiles of an item on one XCD
+    // (its weights in one L2); measured faster than an XCD-balanced split of the units
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
-    const int item = xcd + 8 * (j / tiles), tile = j % tiles;   // all walker tiles of an item on one XCD
+    const int item = xcd + 8 * (j / tiles), tile = j % tiles;
     if (item >= ngitem) return;
     const int Wc = live_walkers(c.wcount, W);
     if (tile * 64 >= Wc) return;
@@ -1349,6 +1357,16 @@ struct CMBLikes final : Like {
     int small_ntask = 0;
     SmallDev sdev{};
     DevBuf d_invcov, d_stasks, d_srows, d_smt, d_sct;
+    // window columns (one per bin and window entry with an output; main then
+    // correction), the map pairs they read, and per element its columns; kept
+    // so the work items can be rebuilt on other segment boundaries (window_resegment)
+    struct HCol { int pair, lo, hi; const double *W; double cst; bool fixed; };
+    std::vector<HCol> wcols;
+    std::vector<CLPair> pairs;
+    std::vector<std::vector<int>> w_emain, w_ecorr;
+    std::vector<WItem> h_items;                     // direct-path work items (host copy)
+    std::vector<std::vector<int>> h_item_cols;      // their columns (indices into wcols)
+    std::map<int, std::vector<int>> seg_starts;     // theory field -> segment starts (relative l); default 256
 
     std::string cl_name(const std::vector<std::string> &names, int i, int j) const {   // Cl_i_j_name (:328-343)
         return has_map_names ? names[i - 1] + "x" + names[j - 1] : names[i - 1] + names[j - 1];
@@ -1824,60 +1842,21 @@ struct CMBLikes final : Like {
         spd_inverse(invcov, nX);
     }
 
-    void build_device(bool have_noise, const std::vector<double> &chatM, const std::vector<double> &cfh,
-                      const std::vector<BKMap> &bkm, const std::vector<double> &bnu, const std::vector<double> &bR,
-                      const std::vector<double> &bdnu) {
+    // Work items of the window stage, their partial rows, and the per-element
+    // row lists and small-gaussian tasks that consume them (re-run by
+    // window_resegment; the results depend on the segment boundaries only
+    // through the summation split of each window's dot product).
+    void build_items() {
         const int L = lmax - lmin + 1;
-        // required map pairs (InitMapCls :997-1019, MapPair_to_Theory_i_j :284-299)
-        std::vector<CLPair> pairs;
-        auto pair_index = [&](int i, int j) { return (i - 1) * i / 2 + (j - 1); };   // i >= j, 1-based
-        for (int i = 1; i <= nreq; i++)
-            for (int j = 1; j <= i; j++) {
-                int f1 = map_fields[required_order[i - 1] - 1], f2 = map_fields[required_order[j - 1] - 1];
-                if (f2 > f1) std::swap(f1, f2);
-                CLPair p{};
-                p.field = f1 * (f1 - 1) / 2 + (f2 - 1);
-                p.cmb = (f1 <= 3 && f2 <= 3);
-                p.fg = bk ? ((f1 == 2 && f2 == 2) ? 1 : (f1 == 3 && f2 == 3) ? 2 : 0) : 0;
-                p.mi = i - 1;
-                p.mj = j - 1;
-                pairs.push_back(p);
-            }
-        // window columns: one per (bin, window entry with an output); main then correction
-        struct HCol { int pair, lo, hi; const double *W; double cst; bool fixed; };
-        std::vector<HCol> cols;
         const int nE = nb * ncl;
-        std::vector<std::vector<int>> e_main(nE), e_corr(nE);
-        auto add_windows = [&](const Windows &wn, std::vector<std::vector<int>> &lists) {
-            const int norder = (int)wn.in_i.size();
-            for (int b = 0; b < nb; b++)
-                for (int k = 0; k < norder; k++) {
-                    if (wn.out[k] <= 0) continue;
-                    const double *Wk = &wn.W[((size_t)b * norder + k) * L];
-                    HCol c{-1, L, -1, Wk, 0.0, false};
-                    for (int l = 0; l < L; l++)
-                        if (Wk[l] != 0.0) { c.lo = std::min(c.lo, l); c.hi = l; }
-                    if (!wn.fix[k].empty()) {              // fix_cl: walker-independent dot
-                        c.fixed = true;
-                        for (int l = 0; l < L; l++) c.cst += Wk[l] * wn.fix[k][l];
-                    } else {
-                        if (wn.in_i[k] == 0 || wn.in_j[k] == 0)
-                            fail(CMBL_ERR_FORMAT, "CMBlikes: bin window uses a spectrum of a map that is not required");
-                        c.pair = pair_index(wn.in_i[k], wn.in_j[k]);
-                    }
-                    lists[(size_t)b * ncl + (wn.out[k] - 1)].push_back((int)cols.size());
-                    cols.push_back(c);
-                }
-        };
-        add_windows(bw, e_main);
-        if (cw.present) add_windows(cw, e_corr);
+        auto &cols = wcols;
+        max_field = 0;
         // work items: per pair, per l chunk, the overlapping columns in groups of WK_COLS
         std::vector<WItem> items;
         std::vector<double> wdense, wdirect;
         std::vector<std::vector<int>> col_parts(cols.size());
         int nrows = 0;
         const int SEG = WK_CHUNK * WK_NCH;
-        const int nseg = (L + SEG - 1) / SEG;
         // BK foregrounds without aberration: grouped-pair items (cmbl_window_group),
         // when no pair has more than 16 window columns
         use_group = bk && aberration == 0.0;
@@ -1937,9 +1916,17 @@ struct CMBLikes final : Like {
         if (!gitems.empty()) d_gitems.upload(gitems.data(), gitems.size() * sizeof(GItem));
         d_gw.alloc(std::max<size_t>(16, gw.size() * 8));
         if (!gw.empty()) d_gw.upload(gw.data(), gw.size() * 8);
-        for (size_t p = 0; p < (use_group ? 0 : pairs.size()); p++)
-            for (int sg = 0; sg < nseg; sg++) {
-                const int c0 = sg * SEG, c1 = std::min(L - 1, c0 + SEG - 1);
+        h_items.clear();
+        h_item_cols.clear();
+        for (size_t p = 0; p < (use_group ? 0 : pairs.size()); p++) {
+            std::vector<int> segs;
+            auto fs = seg_starts.find(pairs[p].field);
+            if (fs != seg_starts.end()) segs = fs->second;
+            else
+                for (int c = 0; c < L; c += SEG) segs.push_back(c);
+            for (size_t sg = 0; sg < segs.size(); sg++) {
+                const int c0 = segs[sg], c1 = std::min(L - 1, sg + 1 < segs.size() ? segs[sg + 1] - 1 : L - 1);
+                if (c1 < c0) continue;
                 std::vector<int> sel;
                 for (size_t ci = 0; ci < cols.size(); ci++)
                     if (!cols[ci].fixed && cols[ci].pair == (int)p && cols[ci].hi >= c0 && cols[ci].lo <= c1)
@@ -1974,8 +1961,11 @@ struct CMBLikes final : Like {
                                 }
                     for (size_t g = g0; g < g1; g++) col_parts[sel[g]].push_back(nrows++);
                     items.push_back(it);
+                    h_item_cols.emplace_back(sel.begin() + g0, sel.begin() + g1);
                 }
             }
+        }
+        h_items = items;
         n_part_rows = nrows;
         items_even = true;
         for (auto &it : items) items_even = items_even && (it.l0 % 2 == 0);
@@ -1996,8 +1986,8 @@ struct CMBLikes final : Like {
         };
         std::vector<int> main_off, main_rows, corr_off, corr_rows;
         std::vector<double> main_cst, corr_cst;
-        flatten(e_main, main_off, main_rows, main_cst);
-        flatten(e_corr, corr_off, corr_rows, corr_cst);
+        flatten(w_emain, main_off, main_rows, main_cst);
+        flatten(w_ecorr, corr_off, corr_rows, corr_cst);
         {   // small-gaussian tasks: each element's rows in runs of <= 8 (main rows, then corr rows)
             std::vector<SmallTask> tasks;
             std::vector<int> rows_all(main_rows);
@@ -2026,6 +2016,88 @@ struct CMBLikes final : Like {
             up2(d_smt, mt.data(), mt.size() * 4);
             up2(d_sct, ct.data(), ct.size() * 4);
         }
+        auto up = [](DevBuf &d, const void *p, size_t bytes) {
+            d.alloc(std::max<size_t>(bytes, 16));
+            if (bytes) d.upload(p, bytes);
+        };
+        up(d_items, items.data(), items.size() * sizeof(WItem));
+        up(d_wts, wdense.data(), wdense.size() * 8);
+        up(d_wdir, wdirect.data(), wdirect.size() * 8);
+        up(d_sumoff, main_off.data(), main_off.size() * 4);
+        up(d_sumcols, main_rows.data(), main_rows.size() * 4);
+        up(d_sumconst, main_cst.data(), main_cst.size() * 8);
+        up(d_corroff, corr_off.data(), corr_off.size() * 4);
+        up(d_corrcols, corr_rows.data(), corr_rows.size() * 4);
+        up(d_corrconst, corr_cst.data(), corr_cst.size() * 8);
+        small_gauss = approx == 2 && nX <= SMALL_NX && small_ntask <= SMALL_MAXTASK;
+        sdev.ntask = small_ntask;
+        sdev.tasks = d_stasks.as<SmallTask>();
+        sdev.rows = d_srows.as<int>();
+        sdev.e_main_t = d_smt.as<int>();
+        sdev.e_corr_t = d_sct.as<int>();
+        dev.nitem = (int)items.size();
+        dev.items = d_items.as<WItem>();
+        dev.wdense = d_wts.as<double>();
+        dev.wdirect = d_wdir.as<double>();
+        dev.e_main_off = d_sumoff.as<int>();
+        dev.e_main_rows = d_sumcols.as<int>();
+        dev.e_main_const = d_sumconst.as<double>();
+        dev.e_corr_off = d_corroff.as<int>();
+        dev.e_corr_rows = d_corrcols.as<int>();
+        dev.e_corr_const = d_corrconst.as<double>();
+        dev.pairs = d_pairs.as<CLPair>();
+    }
+
+    void build_device(bool have_noise, const std::vector<double> &chatM, const std::vector<double> &cfh,
+                      const std::vector<BKMap> &bkm, const std::vector<double> &bnu, const std::vector<double> &bR,
+                      const std::vector<double> &bdnu) {
+        const int L = lmax - lmin + 1;
+        // required map pairs (InitMapCls :997-1019, MapPair_to_Theory_i_j :284-299)
+        pairs.clear();
+        auto pair_index = [&](int i, int j) { return (i - 1) * i / 2 + (j - 1); };   // i >= j, 1-based
+        for (int i = 1; i <= nreq; i++)
+            for (int j = 1; j <= i; j++) {
+                int f1 = map_fields[required_order[i - 1] - 1], f2 = map_fields[required_order[j - 1] - 1];
+                if (f2 > f1) std::swap(f1, f2);
+                CLPair p{};
+                p.field = f1 * (f1 - 1) / 2 + (f2 - 1);
+                p.cmb = (f1 <= 3 && f2 <= 3);
+                p.fg = bk ? ((f1 == 2 && f2 == 2) ? 1 : (f1 == 3 && f2 == 3) ? 2 : 0) : 0;
+                p.mi = i - 1;
+                p.mj = j - 1;
+                pairs.push_back(p);
+            }
+        // window columns: one per (bin, window entry with an output); main then correction
+        auto &cols = wcols;
+        cols.clear();
+        const int nE = nb * ncl;
+        w_emain.assign(nE, {});
+        w_ecorr.assign(nE, {});
+        auto &e_main = w_emain, &e_corr = w_ecorr;
+        auto add_windows = [&](const Windows &wn, std::vector<std::vector<int>> &lists) {
+            const int norder = (int)wn.in_i.size();
+            for (int b = 0; b < nb; b++)
+                for (int k = 0; k < norder; k++) {
+                    if (wn.out[k] <= 0) continue;
+                    const double *Wk = &wn.W[((size_t)b * norder + k) * L];
+                    HCol c{-1, L, -1, Wk, 0.0, false};
+                    for (int l = 0; l < L; l++)
+                        if (Wk[l] != 0.0) { c.lo = std::min(c.lo, l); c.hi = l; }
+                    if (!wn.fix[k].empty()) {              // fix_cl: walker-independent dot
+                        c.fixed = true;
+                        for (int l = 0; l < L; l++) c.cst += Wk[l] * wn.fix[k][l];
+                    } else {
+                        if (wn.in_i[k] == 0 || wn.in_j[k] == 0)
+                            fail(CMBL_ERR_FORMAT, "CMBlikes: bin window uses a spectrum of a map that is not required");
+                        c.pair = pair_index(wn.in_i[k], wn.in_j[k]);
+                    }
+                    lists[(size_t)b * ncl + (wn.out[k] - 1)].push_back((int)cols.size());
+                    cols.push_back(c);
+                }
+        };
+        add_windows(bw, e_main);
+        if (cw.present) add_windows(cw, e_corr);
+        build_items();
         std::vector<int> e_to_x(nE, -1);
         for (int b = 0; b < nb; b++)
             for (int u = 0; u < ncl_used; u++) e_to_x[b * ncl + cl_use[u]] = b * ncl_used + u;
@@ -2038,15 +2110,6 @@ struct CMBLikes final : Like {
             if (bytes) d.upload(p, bytes);
         };
         up(d_pairs, pairs.data(), pairs.size() * sizeof(CLPair));
-        up(d_items, items.data(), items.size() * sizeof(WItem));
-        up(d_wts, wdense.data(), wdense.size() * 8);
-        up(d_wdir, wdirect.data(), wdirect.size() * 8);
-        up(d_sumoff, main_off.data(), main_off.size() * 4);
-        up(d_sumcols, main_rows.data(), main_rows.size() * 4);
-        up(d_sumconst, main_cst.data(), main_cst.size() * 8);
-        up(d_corroff, corr_off.data(), corr_off.size() * 4);
-        up(d_corrcols, corr_rows.data(), corr_rows.size() * 4);
-        up(d_corrconst, corr_cst.data(), corr_cst.size() * 8);
         up(d_etox, e_to_x.data(), e_to_x.size() * 4);
         up(d_fidcorr, fc.data(), fc.size() * 8);
         up(d_noise, noise.data(), noise.size() * 8);
@@ -2066,19 +2129,9 @@ struct CMBLikes final : Like {
             up(d_logl80, ll80.data(), ll80.size() * 8);
         }
         qf.init(invcov, nX);
-        small_gauss = approx == 2 && nX <= SMALL_NX && small_ntask <= SMALL_MAXTASK;
-        sdev.ntask = small_ntask;
-        sdev.tasks = d_stasks.as<SmallTask>();
-        sdev.rows = d_srows.as<int>();
-        sdev.e_main_t = d_smt.as<int>();
-        sdev.e_corr_t = d_sct.as<int>();
         up(d_invcov, invcov.data(), invcov.size() * 8);
         dev.lmin = lmin;
         dev.lmax = lmax;
-        dev.nitem = (int)items.size();
-        dev.items = d_items.as<WItem>();
-        dev.wdense = d_wts.as<double>();
-        dev.wdirect = d_wdir.as<double>();
         dev.pairs = d_pairs.as<CLPair>();
         dev.aberration = aberration;
         dev.cal_index = cal_index;
@@ -2089,12 +2142,6 @@ struct CMBLikes final : Like {
         dev.Np = qf.Np;
         dev.approx = approx;
         dev.has_corr = cw.present ? 1 : 0;
-        dev.e_main_off = d_sumoff.as<int>();
-        dev.e_main_rows = d_sumcols.as<int>();
-        dev.e_main_const = d_sumconst.as<double>();
-        dev.e_corr_off = d_corroff.as<int>();
-        dev.e_corr_rows = d_corrcols.as<int>();
-        dev.e_corr_const = d_corrconst.as<double>();
         dev.fidcorr = d_fidcorr.as<double>();
         dev.noise = d_noise.as<double>();
         dev.chat = d_chat.as<double>();
@@ -2148,6 +2195,51 @@ struct CMBLikes final : Like {
         run(W, dl, ld_field, ld_walker, nuis, ld_nuis, out, ws, stream, wcount);
     }
 
+    // window stage: the direct path's work items (no BK foregrounds, no
+    // aberration), one column per (item, window column) writing its partial row
+    bool window_stage(WinStage &st) const override {
+        if (approx == 3 || bk || aberration != 0.0 || use_group || !binned) return false;
+        st.kind = 0;
+        st.cal_index = cal_index;
+        st.cols.clear();
+        for (size_t k = 0; k < h_items.size(); k++) {
+            const WItem &it = h_items[k];
+            const CLPair &pr = pairs[it.pair];
+            for (size_t g = 0; g < h_item_cols[k].size(); g++) {
+                const HCol &c = wcols[h_item_cols[k][g]];
+                st.cols.push_back(WinCol{pr.field, it.l0, it.l1, c.W + (it.l0 - lmin), it.part + (int)g,
+                                         (pr.cmb && cal_index >= 0) ? 1 : 0});
+            }
+        }
+        return true;
+    }
+    double *window_out(void *ws, int W) const override {
+        return reinterpret_cast<double *>(static_cast<char *>(ws) + layout(W).part);
+    }
+    QFDeferred after_window(int W, const double *nuis, long long ld_nuis, double *out, void *ws, hipStream_t stream,
+                            bool defer) override {
+        if (W <= 0) return QFDeferred{};
+        if (n_nuis > 0 && !nuis) fail(CMBL_ERR_ARG, "%s needs its %d nuisance parameters", name.c_str(), n_nuis);
+        if (defer && !deferred_capable()) fail(CMBL_ERR_UNSUPPORTED, "%s: no deferred evaluation", name.c_str());
+        dev.wcount = nullptr;
+        hl.wcount = nullptr;
+        const double *nu = nuis ? nuis : reinterpret_cast<const double *>(ws);   // never read when n_nuis == 0
+        return post_window(W, nu, ld_nuis, out, ws, stream, nullptr, defer);
+    }
+    bool window_resegment(const std::map<int, std::vector<int>> &starts) override {
+        if (approx == 3 || bk || aberration != 0.0 || use_group || !binned) return false;
+        const int L = lmax - lmin + 1;
+        seg_starts.clear();
+        for (auto &kv : starts) {
+            std::vector<int> v{0};
+            for (int c : kv.second)
+                if (c - lmin > v.back() && c - lmin < L) v.push_back(c - lmin);
+            seg_starts[kv.first] = v;
+        }
+        build_items();
+        return true;
+    }
+
     // the quadratic-form datasets (HL and large gaussian) can leave the combine to the sampler
     bool deferred_capable() const override { return approx != 3 && !small_gauss; }
     QFDeferred loglike_batch_deferred(int W, const double *dl, long long ld_field, long long ld_walker,
@@ -2191,13 +2283,9 @@ struct CMBLikes final : Like {
         }
         const WsLayout o = layout(W);
         char *base = static_cast<char *>(ws);
-        void *qws = ws;
         double *partial = reinterpret_cast<double *>(base + o.part);
-        double *cmat = reinterpret_cast<double *>(base + o.cmat);
         double *coef = reinterpret_cast<double *>(base + o.coef);
         double *prof = reinterpret_cast<double *>(base + o.prof);
-        double *addend = reinterpret_cast<double *>(base + o.add);
-        const bool use_add = log_cal_prior > 0 && cal_index >= 0;
         const double *nu = nuis ? nuis : dl;   // never read when n_nuis == 0
         const int tiles = (W + 63) / 64;
         if (bk) {
@@ -2242,6 +2330,21 @@ struct CMBLikes final : Like {
 #undef CMBL_WINDOW
         });
         HIP_CHECK(hipGetLastError());
+        return post_window(W, nu, ld_nuis, out, ws, stream, wcount, defer);
+    }
+
+    // the kernels after the window stage: binned spectra, then chi^2 (small
+    // gaussian) or the HL transform / gaussian residuals and the quadratic form
+    QFDeferred post_window(int W, const double *nu, long long ld_nuis, double *out, void *ws, hipStream_t stream,
+                           const int *wcount, bool defer) {
+        const WsLayout o = layout(W);
+        char *base = static_cast<char *>(ws);
+        void *qws = ws;
+        double *partial = reinterpret_cast<double *>(base + o.part);
+        double *cmat = reinterpret_cast<double *>(base + o.cmat);
+        double *addend = reinterpret_cast<double *>(base + o.add);
+        const bool use_add = log_cal_prior > 0 && cal_index >= 0;
+        const int tiles = (W + 63) / 64;
         if (small_gauss) {
             timed_launch("cmbl_gauss_small_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
 #define CMBL_SMALL(T)                                                                                             \

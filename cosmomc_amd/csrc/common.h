@@ -167,6 +167,25 @@ struct QFDeferred {
     const double *addend = nullptr;
 };
 
+// Window stage of a likelihood: its first kernel contracts every walker's
+// theory rows with fixed weights (plik_lite's binning, CMBlikes' bin windows).
+// Exposed as columns, the stages of several likelihoods that read one theory
+// buffer run as one pass over it (theorypass.hip), each walker's theory read
+// once; each likelihood then runs its remaining kernels (after_window).
+struct WinCol {
+    int field, lo, hi;     // theory field (cmbl_loglike_batch order) and absolute l range
+    const double *w;       // host: hi - lo + 1 weights
+    int row;               // output row (CMBlikes partial row / plik bin)
+    int cal;               // divide the sum by cal^2 (the stage's calibration parameter)
+};
+struct WinStage {
+    int kind = 0;          // 0: out[row * W + w] (CMBlikes partial rows); 1: out[w * ld + row] = X[row] - sum (plik Delta)
+    int cal_index = -1;    // calibration parameter in the likelihood's nuisance vector (-1: none)
+    std::vector<WinCol> cols;
+    const double *X = nullptr;   // kind 1: device data vector
+    int ld = 0;                  // kind 1: Delta row stride
+};
+
 // ---------------- likelihood object ----------------
 struct Like {
     virtual ~Like() = default;
@@ -200,6 +219,28 @@ struct Like {
                                               const double *nuis, long long ld_nuis, void *ws, hipStream_t stream) {
         (void)W, (void)dl, (void)ld_field, (void)ld_walker, (void)nuis, (void)ld_nuis, (void)ws, (void)stream;
         fail(CMBL_ERR_UNSUPPORTED, "%s: no deferred evaluation", name.c_str());
+    }
+    // Window stage (see WinStage): its columns, where the stage writes in ws,
+    // and the likelihood's remaining kernels once a fused pass has run it.
+    virtual bool window_stage(WinStage &st) const {
+        (void)st;
+        return false;
+    }
+    virtual double *window_out(void *ws, int W) const {
+        (void)ws, (void)W;
+        return nullptr;
+    }
+    virtual QFDeferred after_window(int W, const double *nuis, long long ld_nuis, double *out, void *ws,
+                                    hipStream_t stream, bool defer) {
+        (void)W, (void)nuis, (void)ld_nuis, (void)out, (void)ws, (void)stream, (void)defer;
+        fail(CMBL_ERR_UNSUPPORTED, "%s: no window stage", name.c_str());
+    }
+    // Move the l boundaries at which the window stage splits its dot products
+    // to the given segment starts (absolute l, per theory field), so that
+    // another likelihood's columns never straddle one; false if unsupported.
+    virtual bool window_resegment(const std::map<int, std::vector<int>> &starts) {
+        (void)starts;
+        return false;
     }
     // internal workspace for ws == nullptr
     DevBuf own_ws;

@@ -167,6 +167,8 @@ struct PlikLite final : Like {
     FieldRanges fr{};
     int lds_doubles = 0;
     DevBuf d_wts, d_bins, d_X;
+    std::vector<BinInfo> h_bins;   // the used bins (host), for the window stage
+    std::vector<double> h_wts;     // weights by absolute l
     QuadForm qf;
     DevBuf conv;   // clik -> D_l staging
 
@@ -294,6 +296,8 @@ struct PlikLite final : Like {
             }
         }
 
+        h_bins.assign(binfo.begin(), binfo.end());
+        h_wts = wts;
         binfo.resize(Np, BinInfo{0, 1, 0, 0});
         int wmax = lmax_needed;
         for (int f = 0; f < 3; f++) wmax = std::max(wmax, fr.hi[f]);
@@ -325,6 +329,34 @@ struct PlikLite final : Like {
     }
 
     bool deferred_capable() const override { return true; }
+
+    // window stage: bin i = sum_{l in bin} D_l w_l of field TT / TE / EE, then
+    // Delta_i = X_i - bin_i / cal^2 (CMB.f90:315-326), in the quadratic form's rows
+    bool window_stage(WinStage &st) const override {
+        st.kind = 1;
+        st.cal_index = 0;
+        st.X = d_X.as<double>();
+        st.ld = Np;
+        st.cols.clear();
+        for (size_t i = 0; i < h_bins.size(); i++) {
+            const BinInfo &b = h_bins[i];
+            st.cols.push_back(WinCol{b.field, b.lmin, b.lmax, h_wts.data() + b.lmin, (int)i, 1});
+        }
+        return true;
+    }
+    double *window_out(void *ws, int W) const override {
+        (void)W;
+        return qf.x_rows(ws);
+    }
+    QFDeferred after_window(int W, const double *nuis, long long ld_nuis, double *out, void *ws, hipStream_t stream,
+                            bool defer) override {
+        (void)nuis, (void)ld_nuis;
+        if (W <= 0) return QFDeferred{};
+        if (defer) return qf.launch_deferred(W, ws, nullptr, stream, "plik_quadform_ksplit");
+        HIP_CHECK(hipMemsetAsync(qf.counters(ws, W), 0, (size_t)qf.n_counters(W) * 4, stream));
+        qf.launch(W, ws, nullptr, out, stream, "plik_quadform_ksplit");
+        return QFDeferred{};
+    }
     QFDeferred loglike_batch_deferred(int W, const double *dl, long long ld_field, long long ld_walker,
                                       const double *nuis, long long ld_nuis, void *ws, hipStream_t stream) override {
         if (!ws) fail(CMBL_ERR_ARG, "deferred evaluation needs a caller workspace");

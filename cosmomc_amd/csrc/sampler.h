@@ -2,6 +2,7 @@
 #pragma once
 
 #include "common.h"
+#include "theorypass.h"
 
 namespace cmamd {
 
@@ -146,6 +147,13 @@ struct cmbs {
     std::vector<int> defer_likes;
     cmamd::DevBuf like_ws[cmamd::MAXLIKE];
     int pending_def = 0;
+    // fused window pass (theorypass.h): plik_lite and a CMBlikes dataset that
+    // read one theory buffer run their window stages as one pass; each then
+    // continues from its own workspace (like_ws)
+    std::unique_ptr<cmamd::TheoryPass> tpass;
+    int tp_like[2] = {-1, -1};               // [0] plik_lite (Delta rows), [1] CMBlikes (partial rows)
+    cmamd::WinStage tp_stage[2];
+    int tp_why = 0;                          // set-up progress when no pass was built (debug)
     ~cmbs() {
         for (auto &st : streams)
             if (st) (void)hipStreamDestroy(st);

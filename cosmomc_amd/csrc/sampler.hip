@@ -1512,6 +1512,88 @@ void sampler_set_test_gaussian(cmbs *s, const double *cov, const double *center)
 
 static void set_change_mask(cmbs *s);
 
+// Segment starts (absolute l, even) about TP_MAXL apart over [lo, hi] at which
+// none of the bins [b.first, b.second] is split.
+static std::vector<int> bin_safe_cuts(const std::vector<std::pair<int, int>> &bins, int lo, int hi) {
+    auto valid = [&](int c) {
+        if (c % 2 != 0) return false;
+        for (auto &b : bins)
+            if (b.first < c && c <= b.second) return false;
+        return true;
+    };
+    std::vector<int> cuts;
+    int pos = lo;
+    while (pos + TP_MAXL <= hi) {
+        int c = -1;
+        for (int x = pos + TP_MAXL; x > pos && c < 0; x--)
+            if (valid(x)) c = x;
+        for (int x = pos + TP_MAXL + 1; x <= hi && c < 0; x++)
+            if (valid(x)) c = x;
+        if (c < 0) break;
+        cuts.push_back(c);
+        pos = c;
+    }
+    return cuts;
+}
+
+// Fused window pass: a plik_lite likelihood (window stage kind 1) and a
+// CMBlikes likelihood (kind 0) evaluated densely on the same theory buffer.
+// The CMBlikes windows are re-segmented at l where no plik bin is split, so
+// every column of both lies in one work item of the pass.
+static void setup_fusion(cmbs *s) {
+    s->tpass.reset();
+    s->tp_like[0] = s->tp_like[1] = -1;
+    const int nl = (int)s->likes.size();
+    auto sparse = [&](int i) {
+        for (int q : s->sparse_likes)
+            if (q == i) return true;
+        return false;
+    };
+    s->tp_why = 0;
+    for (int i = 0; i < nl; i++)
+        for (int j = 0; j < nl; j++) {
+            if (i == j) continue;
+            s->tp_why = std::max(s->tp_why, 1);
+            if (sparse(i) || sparse(j)) continue;
+            const LikeSlot &P = s->likes[i], &C = s->likes[j];
+            s->tp_why = std::max(s->tp_why, 2);
+            if (P.dl != C.dl || P.ld_field != C.ld_field || P.ld_walker != C.ld_walker) continue;
+            WinStage sp, sc;
+            s->tp_why = std::max(s->tp_why, 3);
+            if (!P.like->like->window_stage(sp) || sp.kind != 1) continue;
+            s->tp_why = std::max(s->tp_why, 4);
+            if (!C.like->like->window_stage(sc) || sc.kind != 0) continue;
+            s->tp_why = std::max(s->tp_why, 5);
+            std::map<int, std::vector<std::pair<int, int>>> bins;
+            for (auto &c : sp.cols) bins[c.field].push_back({c.lo, c.hi});
+            std::map<int, std::vector<int>> starts;
+            for (auto &kv : bins) {
+                int lo = 1 << 30, hi = -1;
+                for (auto &c : sc.cols)
+                    if (c.field == kv.first) {
+                        lo = std::min(lo, c.lo);
+                        hi = std::max(hi, c.hi);
+                    }
+                if (hi < lo) continue;
+                starts[kv.first] = bin_safe_cuts(kv.second, lo & ~1, hi);
+            }
+            if (!C.like->like->window_resegment(starts) || !C.like->like->window_stage(sc)) continue;
+            s->tp_why = std::max(s->tp_why, 6);
+            std::unique_ptr<TheoryPass> tp(new TheoryPass());
+            if (!tp->build({sp, sc})) continue;
+            s->tpass = std::move(tp);
+            s->tp_like[0] = i;
+            s->tp_like[1] = j;
+            s->tp_stage[0] = sp;
+            s->tp_stage[1] = sc;
+            for (int k : s->tp_like) s->like_ws[k].release();
+            size_t maxws = 0;   // the CMBlikes workspace follows its partial rows
+            for (auto &l : s->likes) maxws = std::max(maxws, l.like->like->workspace_size(s->W));
+            if (maxws > s->ws.bytes) s->ws.alloc(maxws);
+            return;
+        }
+}
+
 void sampler_add_likelihood(cmbs *s, cmbl_t *like, const int *nuisance_indices, const double *dl, long long ld_field,
                             long long ld_walker) {
     if (!like) fail(CMBL_ERR_ARG, "null likelihood");
@@ -1569,7 +1651,10 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, const int *nuisance_indices, 
     }
     for (int i = 0; i < MAXLIKE; i++) s->like_ws[i].release();
     set_mh_lds(s);
+    setup_fusion(s);
     for (int i : s->defer_likes) s->like_ws[i].alloc(s->likes[i].like->like->workspace_size(s->W));
+    for (int i : s->tp_like)
+        if (i >= 0 && !s->like_ws[i].p) s->like_ws[i].alloc(s->likes[i].like->like->workspace_size(s->W));
     if (s->n_groups > 1) sampler_set_groups(s, s->n_groups);   // resize the group workspaces
 }
 
@@ -1616,19 +1701,54 @@ static void set_change_mask(cmbs *s) {
 // changed walkers, then every likelihood (sparse ones on the compacted slots)
 // a deferrable likelihood's evaluation for the accepting mh_kernel that follows:
 // the launches up to the quadratic form's partials, recorded in s->dc.def_*
-static bool eval_deferred(cmbs *s, size_t i, const double *nuis, hipStream_t stream) {
-    int k = -1;
-    for (size_t q = 0; q < s->defer_likes.size(); q++)
-        if (s->defer_likes[q] == (int)i) k = (int)q;
-    if (k < 0) return false;
-    auto &l = s->likes[i];
-    const QFDeferred d = l.like->like->loglike_batch_deferred(s->W, l.dl, l.ld_field, l.ld_walker, nuis,
-                                                              l.like->like->n_nuis, s->like_ws[i].p, stream);
+static bool is_deferred(const cmbs *s, size_t i) {
+    for (int q : s->defer_likes)
+        if (q == (int)i) return true;
+    return false;
+}
+
+static void record_deferred(cmbs *s, size_t i, const QFDeferred &d) {
     const int p = s->pending_def++;
     s->dc.def_like[p] = (int)i;
     s->dc.def_items[p] = d.n_items;
     s->dc.def_part[p] = d.partial;
     s->dc.def_add[p] = d.addend;
+}
+
+// the fused window pass over the whole walker set (eval_likes_fused)
+static bool fused(const cmbs *s, size_t i) {
+    return s->tpass && ((int)i == s->tp_like[0] || (int)i == s->tp_like[1]);
+}
+
+static void launch_tpass(cmbs *s, hipStream_t stream) {
+    TPOut o[2];
+    for (int k = 0; k < 2; k++) {
+        const int i = s->tp_like[k];
+        const WinStage &st = s->tp_stage[k];
+        Like &L = *s->likes[i].like->like;
+        o[k] = TPOut{st.kind, st.cal_index, st.ld, 0, L.window_out(s->like_ws[i].p, s->W), st.X, s->dc.like_nuis[i],
+                     (long long)std::max(1, L.n_nuis)};
+    }
+    const LikeSlot &P = s->likes[s->tp_like[0]];
+    s->tpass->launch(P.dl, P.ld_field, P.ld_walker, o, s->W, stream);
+}
+
+// the rest of a fused likelihood after the pass: deferred or into its like_terms row
+static void eval_after_window(cmbs *s, size_t i, bool defer, hipStream_t stream) {
+    Like &L = *s->likes[i].like->like;
+    const bool d = defer && is_deferred(s, i);
+    const QFDeferred q = L.after_window(s->W, s->dc.like_nuis[i], L.n_nuis,
+                                        d ? nullptr : s->like_terms.as<double>() + i * (size_t)s->dc.ld,
+                                        s->like_ws[i].p, stream, d);
+    if (d) record_deferred(s, i, q);
+}
+
+static bool eval_deferred(cmbs *s, size_t i, const double *nuis, hipStream_t stream) {
+    if (!is_deferred(s, i)) return false;
+    auto &l = s->likes[i];
+    const QFDeferred d = l.like->like->loglike_batch_deferred(s->W, l.dl, l.ld_field, l.ld_walker, nuis,
+                                                              l.like->like->n_nuis, s->like_ws[i].p, stream);
+    record_deferred(s, i, d);
     return true;
 }
 
@@ -1646,6 +1766,7 @@ static void eval_likes_masked(cmbs *s, hipStream_t stream, bool defer = false) {
     int *cnt = s->like_cnt.as<int>();
     hipLaunchKernelGGL(like_compact_kernel, dim3(ns), dim3(1024), 0, stream, s->dc, ss, cnt);
     HIP_CHECK(hipGetLastError());
+    if (s->tpass) launch_tpass(s, stream);   // the fused likelihoods are dense (setup_fusion)
     for (size_t i = 0; i < s->likes.size(); i++) {
         auto &l = s->likes[i];
         const int nn = l.like->like->n_nuis;
@@ -1653,6 +1774,10 @@ static void eval_likes_masked(cmbs *s, hipStream_t stream, bool defer = false) {
         for (int q = 0; q < ns; q++)
             if (ss.like[q] == (int)i) b = q;
         if (b < 0) {
+            if (fused(s, i)) {
+                eval_after_window(s, i, defer, stream);
+                continue;
+            }
             if (defer && eval_deferred(s, i, s->dc.like_nuis[i], stream)) continue;
             l.like->like->loglike_batch(s->W, l.dl, l.ld_field, l.ld_walker, s->dc.like_nuis[i], nn,
                                         s->like_terms.as<double>() + i * (size_t)s->dc.ld, s->ws.p, stream);
@@ -1679,6 +1804,19 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
     const int Wg = g1 - g0;
     if (defer && (g0 != 0 || g1 != s->W)) fail(CMBL_ERR_ARG, "internal: deferred evaluation of a walker group");
     const size_t nl = s->likes.size();
+    const bool fuse = s->tpass && g0 == 0 && g1 == s->W;
+    if (fuse) {   // every nuisance slice first: the pass reads both likelihoods'
+        if (gather)
+            for (size_t i = 0; i < nl; i++) {
+                const int nn = s->likes[i].like->like->n_nuis;
+                hipLaunchKernelGGL(gather_nuis, dim3((s->W + 255) / 256), dim3(256), 0, stream,
+                                   s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld, s->W, s->dc.ld,
+                                   s->dc.tab_i + s->dc.like_nidx[i], nn, s->dc.like_nuis[i]);
+                HIP_CHECK(hipGetLastError());
+            }
+        gather = false;
+        launch_tpass(s, stream);
+    }
     // the likelihoods run in order on the caller's stream: side by side on forked
     // streams the memory-bound likelihood kernels slow each other more than they
     // overlap (MI355X, W = 1024, plik_lite + lensing: 77.1 vs 71.9 us/step; the
@@ -1693,6 +1831,10 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
                                s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld, s->W, s->dc.ld,
                                s->dc.tab_i + s->dc.like_nidx[i], nn, nb);
             HIP_CHECK(hipGetLastError());
+        }
+        if (fuse && fused(s, i)) {
+            eval_after_window(s, i, defer, st);
+            continue;
         }
         if (defer && eval_deferred(s, i, nb, st)) continue;
         l.like->like->loglike_batch(Wg, l.dl + (size_t)g0 * l.ld_walker, l.ld_field, l.ld_walker,
@@ -2213,3 +2355,7 @@ extern "C" int cmamd_debug_stamps(unsigned long long *host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_stamps), sizeof(cmamd::g_stamps)) == hipSuccess ? 0 : -5;
 }
 #endif
+
+// number of work items of the sampler's fused window pass (0: none); for tests
+// (without one: minus the last set-up check passed)
+extern "C" int cmamd_debug_fused(const cmbs *s) { return !s ? 0 : s->tpass ? s->tpass->n_items() : -s->tp_why; }

@@ -89,8 +89,10 @@ __global__ __launch_bounds__(256) void sptpol_window_kernel(SPDev c, const doubl
     constexpr int WROW = SP_CH + 2;            // LDS row stride of the weights (doubles)
     __shared__ __attribute__((aligned(16))) double wsh[SP_COLS * WROW];
     __shared__ __attribute__((aligned(16))) double tsh[(SP_CH + 2) * 4];
+    // blocks are dealt to the XCDs round-robin: all walker tiles of an item on one XCD
+    // (its weights in one L2); measured faster than an XCD-balanced split of the units
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
-    const int item = xcd + 8 * (j / tiles), tile = j % tiles;   // all walker tiles of an item on one XCD
+    const int item = xcd + 8 * (j / tiles), tile = j % tiles;
     if (item >= c.nitem) return;
     const SPItem it = c.items[item];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

@@ -1,0 +1,65 @@
+// One pass over the walkers' theory rows for the window stages of several
+// likelihoods that read the same theory buffer (WinStage, common.h): in the
+// headline workload plik_lite's binning (CMB.f90:315-326) and the lensing
+// likelihood's bin windows (CMBlikes.f90:1230-1256) both read TT, TE and EE;
+// run as one pass, each walker's rows leave HBM once instead of twice.
+#pragma once
+
+#include "common.h"
+
+namespace cmamd {
+
+static constexpr int TP_MAXOUT = 2;    // likelihoods per pass
+static constexpr int TP_CHUNK = 64;    // l per weight chunk
+static constexpr int TP_MAXCOL = 64;   // columns per work item (four 16-column MFMA blocks)
+static constexpr int TP_MAXL = 256;    // l per work item, unless overlapping columns force more
+                                       //   (at most TP_MAXSTEP * 32 - 1 in any case)
+
+struct TPOut {            // a stage's output for one launch
+    int kind;             // WinStage::kind
+    int cal_index;        // calibration parameter index in nuis (-1: none)
+    int ld;               // kind 1: row stride of out
+    int pad;
+    double *out;          // kind 0: [row][W]; kind 1: [W][ld]
+    const double *X;      // kind 1
+    const double *nuis;   // [W][ld_nuis]
+    long long ld_nuis;
+};
+
+static constexpr int TP_MAXSTEP = 16;   // 32-l steps per work item (the active-block mask)
+
+struct TPItem {           // one workgroup's l range of one theory field, with <= 64 columns
+    int field, l0, l1, nch, ncol, cdesc;
+    long long woff;       // weights [nch][ncb][16][TP_CHUNK], zero padded
+    unsigned long long act;   // bit 4 step + block: the block has a nonzero weight in the step
+};
+
+struct TPCol {
+    int out, row, cal, pad;
+};
+
+struct TPDev {
+    const TPItem *items;
+    const TPCol *cols;
+    const double *w;
+    int nitem;
+    TPOut out[TP_MAXOUT];
+};
+
+class TheoryPass {
+  public:
+    // pack the stages' columns into work items (no column split between two);
+    // false when some l range needs more than TP_MAXCOL columns
+    bool build(const std::vector<WinStage> &stages);
+    void launch(const double *dl, long long ld_field, long long ld_walker, const TPOut *outs, int W,
+                hipStream_t stream);
+    int n_items() const { return (int)items.size(); }
+    int n_stages() const { return nstage; }
+
+  private:
+    std::vector<TPItem> items;
+    DevBuf d_items, d_cols, d_w;
+    int nstage = 0;
+};
+
+}  // namespace cmamd

@@ -1,0 +1,313 @@
+// Fused window pass (see theorypass.h).
+//
+// A work item is an l range of one theory field with up to 64 columns from
+// any of the stages (four 16-column MFMA blocks); a workgroup takes one item
+// for 64 walkers and walks the range in 32-l steps.  The contraction is
+// cmbl_window_direct's (cmblikes.hip): lane (walker li, quarter kq) holds the 8
+// l {l0 + 32 st + 8 j + 2 kq + h : j < 4, h < 2} of its walker's row in slot
+// 2 j + h (16-byte loads, two steps ahead of the MFMAs), and MFMA step
+// s = 2 j + h contracts the four l {8 j + 2 kq + h} against the weights, which
+// the block's four waves share through a double-buffered LDS tile.  Columns
+// are ordered wide first (CMBlikes windows), then plik bins by l, and a block
+// runs only in the steps where it has weight (the plik bins are narrow).
+// Each column's sum goes to its stage: a CMBlikes partial row (/ cal^2 for
+// calibrated map pairs, AdaptTheoryForMaps CMBlikes.f90:1113-1124), or plik's
+// Delta = X - sum / cal^2 (CMB.f90:315-326; the bin sum in MFMA order, not the
+// reference's l order: rtol 1e-12 against plik_bin_delta).  No column
+// straddles two items, so every output is one workgroup's store.
+//
+// Measured (MI355X, W = 1024, plik_lite + lensing): 27.6 us against 30 us for
+// plik_bin_delta + cmbl_window_direct.  Summing the bins on the VALU from an
+// LDS copy of the tile instead (the reference's order) took 39-42 us.
+#include <algorithm>
+#include <cstdio>
+#include <map>
+
+#include "theorypass.h"
+
+namespace cmamd {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const double *__restrict__ dl, long long ld_field,
+                                                           long long ld_walker, int W, int tiles, int vec_ok)
+{
+    constexpr int LPL = 8, STEP = 4 * LPL, NSUB = TP_CHUNK / STEP, WROW = STEP + 2, NCB = TP_MAXCOL / 16;
+    __shared__ __attribute__((aligned(16))) double wsh[2 * NCB * 16 * WROW];   // [buf][col block][col][l]
+    __shared__ TPCol csh[TP_MAXCOL];      // the item's column descriptors
+    __shared__ double xsh[TP_MAXCOL];     // and their data values (plik X)
+    // blocks are dealt to the XCDs round-robin: all walker tiles of an item on one XCD
+    // (its weights in one L2); measured faster than an XCD-balanced split of the units
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    const int item = xcd + 8 * (j / tiles), tile = j % tiles;
+    if (item >= c.nitem) return;
+    const TPItem it = c.items[item];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, kq = lane >> 4;
+    const int w = tile * 64 + wave * 16 + li;
+    const int wl = min(w, W - 1);
+    const double *Df = dl + (long long)wl * ld_walker + (long long)it.field * ld_field;
+    const int ncb = (it.ncol + 15) >> 4;
+    const int nstep = it.nch * NSUB;
+    double t[LPL], tn[LPL], tnn[LPL], a[LPL];
+    auto load_t = [&](int st, double *dst) {
+        const int lb = it.l0 + st * STEP + 2 * kq;
+        if (vec_ok && it.l0 + st * STEP + STEP - 1 <= it.l1) {
+#pragma unroll
+            for (int q = 0; q < LPL / 2; q++) {
+                const double2 v = *reinterpret_cast<const double2 *>(Df + lb + 8 * q);
+                dst[2 * q] = v.x;
+                dst[2 * q + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < LPL / 2; q++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int l = lb + 8 * q + h;
+                    dst[2 * q + h] = (l <= it.l1) ? Df[l] : 0.0;
+                }
+        }
+    };
+    // weights [nch][ncb][16][TP_CHUNK]; thread tid moves column tid/16, l 2 (tid%16) .. +1 of each block
+    // (named registers, not arrays: a runtime block count would put an array in scratch)
+    const int wc = tid >> 4, wp = 2 * (tid & 15);
+    double2 wr0{}, wr1{}, wr2{}, wr3{};
+    auto fetch_w = [&](int st) {
+        const int ch = st / NSUB, sub = st % NSUB;
+        const double *base = c.w + it.woff + (long long)ch * ncb * 16 * TP_CHUNK + sub * STEP + wc * TP_CHUNK + wp;
+        const unsigned m = (unsigned)(it.act >> (4 * st)) & 15u;
+        if (m & 1u) wr0 = *reinterpret_cast<const double2 *>(base);
+        if (m & 2u) wr1 = *reinterpret_cast<const double2 *>(base + 16 * TP_CHUNK);
+        if (m & 4u) wr2 = *reinterpret_cast<const double2 *>(base + 2 * 16 * TP_CHUNK);
+        if (m & 8u) wr3 = *reinterpret_cast<const double2 *>(base + 3 * 16 * TP_CHUNK);
+    };
+    auto store_w = [&](int buf, int st) {
+        double *d = wsh + (buf * NCB * 16 + wc) * WROW + wp;
+        const unsigned m = (unsigned)(it.act >> (4 * st)) & 15u;
+        if (m & 1u) *reinterpret_cast<double2 *>(d) = wr0;
+        if (m & 2u) *reinterpret_cast<double2 *>(d + 16 * WROW) = wr1;
+        if (m & 4u) *reinterpret_cast<double2 *>(d + 2 * 16 * WROW) = wr2;
+        if (m & 8u) *reinterpret_cast<double2 *>(d + 3 * 16 * WROW) = wr3;
+    };
+    auto read_w = [&](int buf, int cb) {   // A operand: column li of block cb at the lane's LPL l
+        const double *src = wsh + ((buf * NCB + cb) * 16 + li) * WROW + 2 * kq;
+#pragma unroll
+        for (int q = 0; q < LPL / 2; q++) {
+            const double2 v = *reinterpret_cast<const double2 *>(src + 8 * q);
+            a[2 * q] = v.x;
+            a[2 * q + 1] = v.y;
+        }
+    };
+    // two accumulators per block (even / odd MFMA steps), so consecutive MFMAs
+    // of a block do not wait on each other; summed at the end
+    f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+    f64x4 bcc0 = acc0, bcc1 = acc0, bcc2 = acc0, bcc3 = acc0;
+    auto mfma_block = [&](int buf, int cb, f64x4 &acc, f64x4 &bcc) {
+        read_w(buf, cb);
+#pragma unroll
+        for (int s = 0; s < LPL; s += 2) {
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], t[s], acc, 0, 0, 0);
+            bcc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s + 1], t[s + 1], bcc, 0, 0, 0);
+        }
+    };
+    // the theory rows run two steps ahead of the MFMAs, the weights one
+    load_t(0, t);
+    fetch_w(0);
+    if (nstep > 1) load_t(1, tn);
+    // epilogue operands, fetched behind the first step's loads: column
+    // descriptors and X values into LDS, each stage's calibration per lane
+    if (tid < it.ncol) {
+        const TPCol d = c.cols[it.cdesc + tid];
+        csh[tid] = d;
+        const int kind = d.out ? c.out[1].kind : c.out[0].kind;
+        const double *X = d.out ? c.out[1].X : c.out[0].X;
+        xsh[tid] = kind == 1 ? X[d.row] : 0.0;
+    }
+    double c2[TP_MAXOUT];
+#pragma unroll
+    for (int o = 0; o < TP_MAXOUT; o++) {
+        const int ci = o ? c.out[1].cal_index : c.out[0].cal_index;
+        const double *nu = o ? c.out[1].nuis : c.out[0].nuis;
+        const long long ldn = o ? c.out[1].ld_nuis : c.out[0].ld_nuis;
+        double cl = 1.0;
+        if (ci >= 0 && nu) cl = nu[(long long)wl * ldn + ci];
+        c2[o] = cl * cl;
+    }
+    store_w(0, 0);
+    __syncthreads();
+    for (int st = 0; st < nstep; st++) {
+        const bool more = st + 1 < nstep;
+        const int cur = st & 1;
+        if (more) fetch_w(st + 1);                     // in flight across this step's MFMAs
+        if (st + 2 < nstep) load_t(st + 2, tnn);
+        const unsigned m = (unsigned)(it.act >> (4 * st)) & 15u;   // blocks with weight in this step
+        if (m & 1u) mfma_block(cur, 0, acc0, bcc0);
+        if (m & 2u) mfma_block(cur, 1, acc1, bcc1);
+        if (m & 4u) mfma_block(cur, 2, acc2, bcc2);
+        if (m & 8u) mfma_block(cur, 3, acc3, bcc3);
+        if (more) {
+            store_w(cur ^ 1, st + 1);      // buffer cur ^ 1 was last read before the previous barrier
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < LPL; s++) {
+                t[s] = tn[s];
+                tn[s] = tnn[s];
+            }
+        }
+    }
+    if (w >= W) return;
+    // D: walker = lane&15, column = 16 cb + (lane>>4) + 4 r
+    auto emit = [&](int cb, const f64x4 &acc) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int col = 16 * cb + kq + 4 * r;
+            if (col >= it.ncol) continue;
+            const TPCol d = csh[col];
+            const bool o1 = d.out != 0;   // selects, not a dynamically indexed kernel argument
+            const int kind = o1 ? c.out[1].kind : c.out[0].kind;
+            double *out = o1 ? c.out[1].out : c.out[0].out;
+            double v = acc[r];
+            if (d.cal) v = v / (o1 ? c2[1] : c2[0]);
+            if (kind == 0) {
+                out[(long long)d.row * W + w] = v;
+            } else {
+                const int ld = o1 ? c.out[1].ld : c.out[0].ld;
+                out[(long long)w * ld + d.row] = xsh[col] - v;
+            }
+        }
+    };
+    if (ncb > 0) emit(0, acc0 + bcc0);
+    if (ncb > 1) emit(1, acc1 + bcc1);
+    if (ncb > 2) emit(2, acc2 + bcc2);
+    if (ncb > 3) emit(3, acc3 + bcc3);
+}
+
+// ------------------------------------------------------------------ host side
+
+bool TheoryPass::build(const std::vector<WinStage> &stages) {
+    if (stages.empty() || stages.size() > (size_t)TP_MAXOUT) return false;
+    struct C { int lo, hi, stage, col; };
+    std::map<int, std::vector<C>> byf;
+    for (size_t s = 0; s < stages.size(); s++)
+        for (size_t k = 0; k < stages[s].cols.size(); k++) {
+            const WinCol &wc = stages[s].cols[k];
+            if (wc.hi < wc.lo || wc.lo < 0) return false;
+            byf[wc.field].push_back(C{wc.lo, wc.hi, (int)s, (int)k});
+        }
+    std::vector<TPItem> its;
+    std::vector<TPCol> cols;
+    std::vector<double> w;
+    for (auto &kv : byf) {
+        auto &v = kv.second;
+        // by start, the longest first among equal starts: a long column that
+        // opens a new range then starts the new item before the short ones
+        // sharing its start are considered for the previous one
+        std::stable_sort(v.begin(), v.end(),
+                         [](const C &x, const C &y) { return x.lo < y.lo || (x.lo == y.lo && x.hi > y.hi); });
+        std::vector<std::vector<C>> groups;
+        std::vector<C> cur;
+        int a = 0, bnd = -1;
+        for (const C &x : v) {
+            // a column that overlaps the group joins it; otherwise it starts a
+            // new group once the group would pass TP_MAXL l or TP_MAXCOL columns
+            if (!cur.empty() && x.lo > bnd &&
+                (std::max(bnd, x.hi) - a + 1 > TP_MAXL || (int)cur.size() + 1 > TP_MAXCOL)) {
+                groups.push_back(cur);
+                cur.clear();
+            }
+            if (cur.empty()) {
+                a = x.lo;
+                bnd = x.hi;
+            } else {
+                bnd = std::max(bnd, x.hi);
+            }
+            cur.push_back(x);
+            if ((int)cur.size() > TP_MAXCOL) {
+                fprintf(stderr, "theorypass: field %d [%d, %d] needs %zu columns\n", kv.first, a, bnd, cur.size());
+                return false;
+            }
+        }
+        if (!cur.empty()) groups.push_back(cur);
+        for (auto &g : groups) {
+            // columns: the wide ones (CMBlikes windows, every step) first, then by start,
+            // so the narrow ones (plik bins) of one block are active in few steps
+            std::stable_sort(g.begin(), g.end(), [](const C &x, const C &y) {
+                const int wx = x.hi - x.lo, wy = y.hi - y.lo;
+                if ((wx >= TP_CHUNK) != (wy >= TP_CHUNK)) return wx >= TP_CHUNK;
+                return x.lo < y.lo;
+            });
+            TPItem it{};
+            it.field = kv.first;
+            int lo = g[0].lo, hi = g[0].hi;
+            for (auto &x : g) {
+                lo = std::min(lo, x.lo);
+                hi = std::max(hi, x.hi);
+            }
+            it.l0 = lo & ~1;                      // even: 16-byte theory loads
+            it.l1 = hi;
+            it.nch = (it.l1 - it.l0 + TP_CHUNK) / TP_CHUNK;
+            if (it.nch * (TP_CHUNK / 32) > TP_MAXSTEP) {
+                fprintf(stderr, "theorypass: field %d [%d, %d] longer than %d l\n", kv.first, it.l0, it.l1,
+                        TP_MAXSTEP * 32);
+                return false;
+            }
+            it.ncol = (int)g.size();
+            it.cdesc = (int)cols.size();
+            it.woff = (long long)w.size();
+            const int ncb = (it.ncol + 15) / 16;
+            for (int ch = 0; ch < it.nch; ch++)
+                for (int cb = 0; cb < ncb; cb++)
+                    for (int q = 16 * cb; q < 16 * cb + 16; q++)
+                        for (int k = 0; k < TP_CHUNK; k++) {
+                            const int l = it.l0 + ch * TP_CHUNK + k;
+                            double x = 0.0;
+                            if (q < it.ncol) {
+                                const WinCol &wc = stages[g[q].stage].cols[g[q].col];
+                                if (l >= wc.lo && l <= wc.hi) x = wc.w[l - wc.lo];
+                            }
+                            w.push_back(x);
+                        }
+            for (size_t q = 0; q < g.size(); q++) {
+                const WinCol &wc = stages[g[q].stage].cols[g[q].col];
+                cols.push_back(TPCol{g[q].stage, wc.row, wc.cal, 0});
+                for (int st = 0; st < it.nch * (TP_CHUNK / 32); st++) {
+                    const int s0 = it.l0 + 32 * st, s1 = s0 + 31;
+                    if (wc.lo <= s1 && wc.hi >= s0) it.act |= 1ull << (4 * st + (int)q / 16);
+                }
+            }
+            its.push_back(it);
+        }
+    }
+    items = its;
+    nstage = (int)stages.size();
+    auto up = [](DevBuf &d, const void *p, size_t bytes) {
+        d.alloc(std::max<size_t>(16, bytes));
+        if (bytes) d.upload(p, bytes);
+    };
+    up(d_items, items.data(), items.size() * sizeof(TPItem));
+    up(d_cols, cols.data(), cols.size() * sizeof(TPCol));
+    up(d_w, w.data(), w.size() * 8);
+    return true;
+}
+
+void TheoryPass::launch(const double *dl, long long ld_field, long long ld_walker, const TPOut *outs, int W,
+                        hipStream_t stream) {
+    if (W <= 0 || items.empty()) return;
+    TPDev c{};
+    c.items = d_items.as<TPItem>();
+    c.cols = d_cols.as<TPCol>();
+    c.w = d_w.as<double>();
+    c.nitem = (int)items.size();
+    for (int s = 0; s < nstage; s++) c.out[s] = outs[s];
+    const int vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0;
+    const int tiles = (W + 63) / 64;
+    const int nblk = 8 * tiles * ((c.nitem + 7) / 8);
+    timed_launch("theory_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+        hipExtLaunchKernelGGL(theory_window_kernel, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl, ld_field,
+                              ld_walker, W, tiles, vec_ok);
+    });
+    HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace cmamd

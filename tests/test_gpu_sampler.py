@@ -598,3 +598,48 @@ def test_change_mask_matches_dense(cmbl_golden, refdata, tmp_path, shared_theory
         t = th[0 if shared_theory else w]
         assert a[4][-1, 0, w] == pytest.approx(op.loglike(t, a[0][w, 1]), rel=1e-9)
         assert a[4][-1, 1, w] == pytest.approx(ob.loglike(t, a[0][w, 2:]), rel=1e-9)
+
+
+@pytest.mark.parametrize("W", [100, 512])
+def test_fused_window_pass(cmbl_golden, refdata, tmp_path, W):
+    """plik_lite and the Planck lensing likelihood on one theory buffer run
+    their window stages as one pass over it (theorypass.hip; the lensing
+    windows are re-segmented where no plik bin is split).  The per-likelihood
+    terms of the recorded points equal each likelihood's own loglike_batch
+    (rtol 1e-12: only the summation split differs) and the oracles'."""
+    import os
+
+    import cmblikes_oracle as co
+    from cosmomc_amd import _native as N
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    c = cmbl_golden["cases"]["lensing_consext8"]
+    data = syn.make_plik_lite(12345)
+    plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
+    plik.nuisance_indices = [2]
+    lens.nuisance_indices = [2]
+    steps = 10
+    th = syn.walker_theory(W, seed=7, n_fields=10, ld_field=2512)
+    dl = torch.tensor(th, device="cuda")
+    s = BatchedMCMC(W, 3, [2], [[1]], 0, [0.0222, 0.9, 3.05], [0.0222, 1.1, 3.05], [0.0, 1.0, 0.0],
+                    [0.0, 0.0025, 0.0], seed_ij=58, seed_kl=69)
+    s.set_covariance(np.array([[0.002 ** 2]]))
+    s.add_likelihood(plik, dl)
+    s.add_likelihood(lens, dl)
+    assert N.lib().cmamd_debug_fused(s._h) > 0, N.lib().cmamd_debug_fused(s._h)
+    s.enable_history(steps)
+    s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
+    s.step(steps, fast_only=True)
+    hist = s.history_host(0, steps)
+    terms = s.history_terms(0, steps)
+    po_plik = po.PlikLite(data)
+    o_lens = co.CMBLikesOracle(os.path.join(refdata, c["dataset"]), c["overrides"], c["tag"])
+    for k in (0, steps - 1):
+        cal = hist[k, 0, :].copy()
+        nu = torch.tensor(cal, device="cuda").reshape(-1, 1)
+        np.testing.assert_allclose(terms[k, 0], plik.loglike_batch(dl, nu).cpu().numpy(), rtol=1e-12)
+        np.testing.assert_allclose(terms[k, 1], lens.loglike_batch(dl, nu).cpu().numpy(), rtol=1e-12)
+        for w in (0, W // 2, W - 1):
+            assert terms[k, 0, w] == pytest.approx(po_plik.loglike(th[w, :3], cal[w]), rel=1e-9)
+            assert terms[k, 1, w] == pytest.approx(o_lens.loglike(th[w], cal[w:w + 1]), rel=1e-10)
