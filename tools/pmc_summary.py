@@ -14,7 +14,7 @@ for f in sorted(glob.glob(os.path.join(root, "*", "*counter_collection.csv"))):
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 traffic = {}
 for k, v in agg.items():
-    if any(t in k for t in ("plik", "mh_kernel", "cmbl", "quadform")):
+    if any(t in k for t in ("plik", "mh_kernel", "rot_kernel", "cmbl", "quadform", "theory")):
         print(k)
         for c, x in sorted(v.items()):
             print(f"    {c:28s} {sum(x) / len(x):14.0f}")
