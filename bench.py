@@ -21,9 +21,11 @@ per-step collective ("weak" scaling).
 The JSON line also carries, outside the headline value: "convergence" (R-1 vs
 wall-clock for the headline workload), "config4_fast21" (BASELINE configs[3]
 as a sampler-throughput workload: 21 fast parameters, 512 walkers per GPU;
-full plik needs the absent clik) and "config5_bk15_plik" (BASELINE
+full plik needs the absent clik), "config5_bk15_plik" (BASELINE
 configs[4]: BK15 + plik_lite jointly, fast-step throughput and R-1 vs
-wall-clock with the cross-GPU exchange).
+wall-clock with the cross-GPU exchange) and "config2_drag" (BASELINE
+configs[2] with its fast/slow dragging: a slow amplitude whose theory comes
+from a theory function at every drag, plik_lite + lensing at 1024 walkers).
 """
 from __future__ import annotations
 
@@ -68,6 +70,8 @@ def parse():
                    help="21-fast-parameter sampler workload (BASELINE configs[3]) throughput and R-1 run (< 0 = skip)")
     p.add_argument("--config5-seconds", type=float, default=60.0,
                    help="BK15 + plik_lite (BASELINE configs[4]) throughput and R-1 run (< 0 = skip)")
+    p.add_argument("--drag-seconds", type=float, default=30.0,
+                   help="configs[2] with fast/slow dragging: throughput and R-1 run (< 0 = skip)")
     return p.parse_args()
 
 
@@ -126,7 +130,7 @@ def build_problem(W, rank, tmpdir, groups=1, lensing=True):
     return smp, likes, theory, names
 
 
-def run_to_convergence(smp, num_slow, num_fast, seconds, world, cap, fast_only=True):
+def run_to_convergence(smp, num_slow, num_fast, seconds, world, cap, fast_only=True, stepper=None):
     """R-1 vs wall-clock with the reference's collector logic (ChainCollector:
     per-walker burn-in, all_burn, MPI_Min_Sample_Update = 50 + 4 num_slow +
     5 num_fast and update frequency 40 x num_params_used after burn-in,
@@ -140,7 +144,10 @@ def run_to_convergence(smp, num_slow, num_fast, seconds, world, cap, fast_only=T
                          num_fast=num_fast, sample_capacity=cap)
     trace, t0, done_at = [], time.perf_counter(), None
     while smp.history_count() + col.next_block() <= cap:
-        smp.step(col.next_block(), fast_only=fast_only)
+        if stepper is None:
+            smp.step(col.next_block(), fast_only=fast_only)
+        else:
+            stepper(col.next_block())
         r = col.process()
         el = time.perf_counter() - t0
         if r is not None:
@@ -216,6 +223,69 @@ def kernel_profile(smp, steps):
         ms, cnt = N.profile_read(k)
         if cnt:
             out[k] = round(ms / cnt * 1e3, 2)
+    return out
+
+
+def drag_run(W, rank, world, tmpdir, seconds, steps=20, dragging_steps=3.0):
+    """BASELINE configs[2] with its fast/slow dragging (MCMC.f90:357-420):
+    plik_lite TTTEEE + Planck 2018 lensing on per-walker theory rows, one slow
+    parameter (an amplitude A: theory = A x base D_l, computed by a theory
+    function -- the CAMB stand-in -- at every drag's end point) and calPlanck
+    fast; each drag interpolates over round(dragging_steps x num_fast) + 1
+    points, evaluating both likelihoods at the start and end theories
+    (1 + 2 x (interp - 1) evaluations per walker and drag).  Reports drag steps
+    and likelihood evaluations per second and, when seconds > 0, R-1 vs
+    wall-clock of A and calPlanck from an overdispersed start."""
+    import torch
+    from cosmomc_amd import synthetic as syn
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    plik = NativeCMBLikelihood("PLIK_LITE", syn.make_plik_lite(12345).write(os.path.join(tmpdir, "c2p")))
+    lens = NativeCMBLikelihood("lensing", os.path.join(extract_refdata(tmpdir), LENS_DATASET))
+    plik.nuisance_indices = [2]
+    lens.nuisance_indices = [2]
+    base = torch.tensor(syn.walker_theory(1, n_fields=10, ld_field=2512), device="cuda")[0]
+    pmin, pmax = np.array([0.95, 0.9]), np.array([1.05, 1.1])
+    pm, ps = np.array([0.0, 1.0]), np.array([0.0, 0.0025])
+    smp = BatchedMCMC(W, 2, [1, 2], [[1], [2]], 1, pmin, pmax, pm, ps, propose_scale=2.4, seed_ij=3003 + rank,
+                      seed_kl=9373, first_walker=rank * W)
+    smp.set_covariance(np.diag([0.002 ** 2, 0.0025 ** 2]))
+    g = syn.gaussians(55 + rank, 2 * W).reshape(2, W)
+    A0 = 1.0 + 0.005 * g[0]
+    theory = (base.unsqueeze(0) * torch.tensor(A0, device="cuda").reshape(-1, 1, 1)).contiguous()
+    end = torch.empty_like(theory)
+    for lk in (plik, lens):
+        smp.add_likelihood(lk, theory)
+    smp.set_drag_theory(0, end)
+    smp.set_drag_theory(1, end)
+    smp.set_start(np.stack([A0, 1.0 + 0.005 * g[1]], axis=1))
+
+    def theory_fn(P_end):                              # the drag's end-point theory (CAMB's place)
+        torch.mul(base.unsqueeze(0), P_end[0].reshape(-1, 1, 1), out=end)
+
+    def stepper(n):
+        smp.step_drag(n, dragging_steps, theory_fn=theory_fn)
+    stepper(2)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stepper(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    interp = max(2, int(round(dragging_steps * 1)) + 1)
+    evals = 1 + 2 * (interp - 1)
+    out = {"workload": "plik_lite_TTTEEE + Planck2018 lensing, per-walker theory rows, slow amplitude A dragged "
+                       "(theory = A x base from a theory function at every drag) with calPlanck fast, "
+                       f"dragging_steps={dragging_steps:g}",
+           "walkers_total": W * world, "drag_steps_per_s": W * world * steps / dt,
+           "likelihood_evals_per_s": W * world * steps * evals / dt, "evals_per_drag": evals,
+           "ms_per_drag_step": dt / steps * 1e3}
+    if seconds > 0:
+        out.update(run_to_convergence(smp, 1, 1, seconds, world, 40000, stepper=stepper))
     return out
 
 
@@ -562,6 +632,9 @@ def main():
         c5 = None
         if args.config5_seconds >= 0:
             c5 = config5_run(W, rank, world, td, args.config5_seconds)
+        c2d = None
+        if args.drag_seconds >= 0 and not args.no_lensing:
+            c2d = drag_run(W, rank, world, td, args.drag_seconds)
 
     dom = max(kern, key=lambda k: kern[k][0])
     avg_ms = {k: (v[0] / v[1] if v[1] else None) for k, v in kern.items()}
@@ -606,6 +679,8 @@ def main():
             out["config4_fast21"] = c4
         if c5 is not None:
             out["config5_bk15_plik"] = c5
+        if c2d is not None:
+            out["config2_drag"] = c2d
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, lensing=not args.no_lensing)
         print(json.dumps(out), flush=True)

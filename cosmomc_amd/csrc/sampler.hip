@@ -1720,17 +1720,24 @@ static bool fused(const cmbs *s, size_t i) {
     return s->tpass && ((int)i == s->tp_like[0] || (int)i == s->tp_like[1]);
 }
 
-static void launch_tpass(cmbs *s, hipStream_t stream) {
+// the pass over theory rows dl (the walkers' own, or the drag's end points)
+// with nuisance slices nuis[i] of likelihood i
+static void launch_tpass(cmbs *s, hipStream_t stream, const double *dl, long long ld_field, long long ld_walker,
+                         double *const *nuis) {
     TPOut o[2];
     for (int k = 0; k < 2; k++) {
         const int i = s->tp_like[k];
         const WinStage &st = s->tp_stage[k];
         Like &L = *s->likes[i].like->like;
-        o[k] = TPOut{st.kind, st.cal_index, st.ld, 0, L.window_out(s->like_ws[i].p, s->W), st.X, s->dc.like_nuis[i],
+        o[k] = TPOut{st.kind, st.cal_index, st.ld, 0, L.window_out(s->like_ws[i].p, s->W), st.X, nuis[i],
                      (long long)std::max(1, L.n_nuis)};
     }
+    s->tpass->launch(dl, ld_field, ld_walker, o, s->W, stream);
+}
+
+static void launch_tpass(cmbs *s, hipStream_t stream) {
     const LikeSlot &P = s->likes[s->tp_like[0]];
-    s->tpass->launch(P.dl, P.ld_field, P.ld_walker, o, s->W, stream);
+    launch_tpass(s, stream, P.dl, P.ld_field, P.ld_walker, s->dc.like_nuis);
 }
 
 // the rest of a fused likelihood after the pass: deferred or into its like_terms row
@@ -1956,6 +1963,22 @@ void sampler_set_trial_theory(cmbs *s, int like_index, double *dl_end, long long
 
 // likelihood terms of set 1 (T rows, end theory) or set 2 (T2 rows, walker theory)
 static void eval_likes_drag(cmbs *s, int set, hipStream_t stream) {
+    // the fused window pass when both likelihoods read one buffer of this set
+    bool fuse = false;
+    if (s->tpass) {
+        const int p = s->tp_like[0], c = s->tp_like[1];
+        if (set == 1) {
+            const auto &a = s->end_theory[p], &b = s->end_theory[c];
+            fuse = a.dl == b.dl && a.ld_field == b.ld_field && a.ld_walker == b.ld_walker;
+            if (fuse) launch_tpass(s, stream, a.dl, a.ld_field, a.ld_walker, s->dc.like_nuis);
+        } else {
+            double *nb2[MAXLIKE] = {};
+            for (size_t i = 0; i < s->likes.size(); i++) nb2[i] = s->nuis_bufs2[i].as<double>();
+            const LikeSlot &P = s->likes[p];
+            fuse = true;
+            launch_tpass(s, stream, P.dl, P.ld_field, P.ld_walker, nb2);
+        }
+    }
     for (size_t i = 0; i < s->likes.size(); i++) {
         auto &l = s->likes[i];
         const int nn = l.like->like->n_nuis;
@@ -1970,6 +1993,10 @@ static void eval_likes_drag(cmbs *s, int set, hipStream_t stream) {
         } else {
             nb = s->nuis_bufs2[i].as<double>();
             out = s->like_terms2.as<double>() + i * (size_t)s->dc.ld;
+        }
+        if (fuse && fused(s, i)) {
+            l.like->like->after_window(s->W, nb, nn, out, s->like_ws[i].p, stream, false);
+            continue;
         }
         l.like->like->loglike_batch(s->W, dl, ldf, ldw, nb, nn, out, s->ws.p, stream);
     }

@@ -643,3 +643,53 @@ def test_fused_window_pass(cmbl_golden, refdata, tmp_path, W):
         for w in (0, W // 2, W - 1):
             assert terms[k, 0, w] == pytest.approx(po_plik.loglike(th[w, :3], cal[w]), rel=1e-9)
             assert terms[k, 1, w] == pytest.approx(o_lens.loglike(th[w], cal[w:w + 1]), rel=1e-10)
+
+
+def test_dragging_fused_plik_lensing(cmbl_golden, refdata, tmp_path):
+    """Dragging with plik_lite + lensing on one theory buffer (the fused
+    window pass at both the start and the end-point theories): every walker's
+    final theory row is A_w x base and its terms are the oracles' there."""
+    import os
+
+    import cmblikes_oracle as co
+    from cosmomc_amd import _native as N
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    c = cmbl_golden["cases"]["lensing_consext8"]
+    data = syn.make_plik_lite(12345)
+    plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
+    plik.nuisance_indices = [2]
+    lens.nuisance_indices = [2]
+    W = 130
+    base = torch.tensor(syn.walker_theory(1, seed=4, n_fields=10, ld_field=2512), device="cuda")[0]
+    theory = base.unsqueeze(0).repeat(W, 1, 1).contiguous()
+    end = torch.empty_like(theory)
+    pmin, pmax = np.array([0.95, 0.9]), np.array([1.05, 1.1])
+    pm, ps = np.array([0.0, 1.0]), np.array([0.0, 0.0025])
+    s = BatchedMCMC(W, 2, [1, 2], [[1], [2]], 1, pmin, pmax, pm, ps, propose_scale=2.4, seed_ij=93, seed_kl=94)
+    s.set_covariance(np.diag([0.002 ** 2, 0.0025 ** 2]))
+    s.add_likelihood(plik, theory)
+    s.add_likelihood(lens, theory)
+    assert N.lib().cmamd_debug_fused(s._h) > 0
+    s.set_drag_theory(0, end)
+    s.set_drag_theory(1, end)
+    s.set_start(np.tile([1.0, 1.0], (W, 1)))
+    s.enable_history(64)
+
+    def theory_fn(P_end):
+        torch.mul(base.unsqueeze(0), P_end[0].reshape(-1, 1, 1), out=end)
+    s.step_drag(12, theory_fn=theory_fn)
+    P, lk, mult, nacc = s.state()
+    terms = s.history_terms(s.history_count() - 1, 1)[0]
+    assert np.any(np.abs(P[:, 0] - 1.0) > 1e-6), "no drag was accepted"
+    th = theory.cpu().numpy()
+    b = base.cpu().numpy()
+    op = po.PlikLite(data)
+    ol = co.CMBLikesOracle(os.path.join(refdata, c["dataset"]), c["overrides"], c["tag"])
+    for w in (0, 64, W - 1):
+        np.testing.assert_allclose(th[w], P[w, 0] * b, rtol=1e-15, atol=0)
+        assert terms[0, w] == pytest.approx(op.loglike(th[w, :3], P[w, 1]), rel=1e-9)
+        assert terms[1, w] == pytest.approx(ol.loglike(th[w], P[w, 1:2]), rel=1e-10)
+        ref = terms[0, w] + terms[1, w] + 0.5 * ((P[w, 1] - 1.0) / 0.0025) ** 2
+        assert lk[w] == pytest.approx(ref, rel=1e-12)
