@@ -812,6 +812,8 @@ __global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev
     if (blockIdx.x * WT >= Wc) return;
     for (int i = threadIdx.x; i < c.nX * c.nX; i += 256) Msh[i] = M[i];   // in flight with the partial loads
     const bool act = w < Wc;
+    const bool calp = c.log_cal_prior > 0 && c.cal_index >= 0;
+    const double cal = (g == 0 && act && calp) ? nuis[(long long)w * ld_nuis + c.cal_index] : 1.0;   // likewise
     for (int t = g; t < sd.ntask; t += NG) {
         const SmallTask tk = sd.tasks[t];
         double v[8];
@@ -848,8 +850,8 @@ __global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev
     if (g == 0 && act) {
         double chisq = 0.0;
         for (int k = 0; k < NG; k++) chisq += red[k][wl];
-        if (c.log_cal_prior > 0 && c.cal_index >= 0) {
-            const double t = log(nuis[(long long)w * ld_nuis + c.cal_index]) / c.log_cal_prior;
+        if (calp) {
+            const double t = log(cal) / c.log_cal_prior;
             chisq = chisq + t * t;
         }
         out[w] = chisq / 2;

@@ -164,6 +164,7 @@ struct Walker {
     int pend_b = -1;
     int defer_rot = 0;   // leave a new rotation of a wide block to rot_kernel (block index in pend_rot)
     int pend_rot = -1;
+    double r1 = 0.0;     // a one-parameter block's rotation, just drawn (R may live in HBM: no read-back)
 };
 
 __device__ int cyc_next(Walker &k, int which, int n, int base)
@@ -232,13 +233,17 @@ __device__ void rot_matrix(Walker &k, int off, int n)
         }
     } else {
         for (int i = 0; i < n * n; i++) k.R[off + i] = 0.0;
-        for (int i = 0; i < n; i++) k.R[off + i * n + i] = (ranmar(k.r) - 0.5) >= 0.0 ? 1.0 : -1.0;
+        for (int i = 0; i < n; i++) {
+            k.r1 = (ranmar(k.r) - 0.5) >= 0.0 ? 1.0 : -1.0;
+            k.R[off + i * n + i] = k.r1;
+        }
     }
 }
 
 static constexpr int ROT_DEFER_MIN = 8;   // blocks this wide get their rotations from rot_kernel
 
 __device__ void proposal_tail(const DevCfg &c, const Tabs &t, Walker &k, int b, int lp);
+__device__ void proposal_r(const DevCfg &c, const Tabs &t, Walker &k, int b, int n, double r1);
 
 __device__ void block_proposal(const DevCfg &c, const Tabs &t, Walker &k, int bi /*1-based*/)
 {   // GetBlockProposal :247-254 -> ProposeVec :105-120 -> Propose_r :122-139 -> UpdateParams :142-149
@@ -253,6 +258,11 @@ __device__ void block_proposal(const DevCfg &c, const Tabs &t, Walker &k, int bi
         }
         rot_matrix(k, off, n);
         lp = 0;
+        if (n == 1) {   // a fresh one-parameter rotation every step: its sign is in hand
+            k.blklp[b] = 1;
+            proposal_r(c, t, k, b, 1, k.r1);
+            return;
+        }
     }
     proposal_tail(c, t, k, b, lp);
 }
@@ -264,6 +274,23 @@ __device__ void proposal_tail(const DevCfg &c, const Tabs &t, Walker &k, int b, 
     const int off = t.blk_R_off[b];
     lp++;
     k.blklp[b] = lp;
+    // vec(q) = R(q, loopix) (the column of R is read once: R may live in HBM
+    // when it is too big to stage), scaled by Propose_r's step below
+    for (int q0 = 0; q0 < n; q0 += RCH) {
+        double rv[RCH];
+#pragma unroll
+        for (int u = 0; u < RCH; u++) rv[u] = q0 + u < n ? k.R[off + (q0 + u) * n + (lp - 1)] : 0.0;
+#pragma unroll
+        for (int u = 0; u < RCH; u++)
+            if (q0 + u < n) k.vec[q0 + u] = rv[u];
+    }
+    proposal_r(c, t, k, b, n, 0.0);
+}
+
+// Propose_r's step length and UpdateParams: vec *= r * wid (r1: the 1 x 1
+// rotation itself, when n == 1 and it was just drawn), P(changed) += mapping . vec
+__device__ void proposal_r(const DevCfg &c, const Tabs &t, Walker &k, int b, int n, double r1)
+{
     double rf;
     if (ranmar(k.r) < 0.33) {
         rf = (double)randexp1(k.r);
@@ -277,19 +304,12 @@ __device__ void proposal_tail(const DevCfg &c, const Tabs &t, Walker &k, int b, 
         rf = sqrt(rf / m);
     }
     const double scale = rf * c.propose_scale;
-    // vec(q) = R(q, loopix) * (r * wid);  P(changed) += mapping_matrix . vec
-    // (the column of R is read once: R may live in HBM when it is too big to stage)
     const int nc = t.blk_nchanged[b];
     const double *M = t.mapping + t.blk_map_off[b];
     const int *chg = t.changed + t.blk_changed_off[b];
-    for (int q0 = 0; q0 < n; q0 += RCH) {
-        double rv[RCH];
-#pragma unroll
-        for (int u = 0; u < RCH; u++) rv[u] = q0 + u < n ? k.R[off + (q0 + u) * n + (lp - 1)] : 0.0;
-#pragma unroll
-        for (int u = 0; u < RCH; u++)
-            if (q0 + u < n) k.vec[q0 + u] = rv[u] * scale;
-    }
+    if (r1 != 0.0) k.vec[0] = r1 * scale;
+    else
+        for (int q = 0; q < n; q++) k.vec[q] = k.vec[q] * scale;
     if (k.defer) {
         k.pend_b = b;
         return;
@@ -344,8 +364,23 @@ template <class Q, class L>
 __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const L &likes,
                               const double *trows = nullptr)
 {
-    for (int i = 0; i < c.np; i++)
-        if (q[i] > t.pmax[i] || q[i] < t.pmin[i]) return LOGZERO;   // GetLogLikeBounds :97-109
+    // the parameter loops load RCH entries at a time (all in flight together;
+    // the chain wave would otherwise wait out one LDS round trip per entry)
+    bool oob = false;
+    for (int i0 = 0; i0 < c.np; i0 += RCH) {                         // GetLogLikeBounds :97-109
+        double qv[RCH], hi[RCH], lo[RCH];
+#pragma unroll
+        for (int u = 0; u < RCH; u++) {
+            const int i = i0 + u < c.np ? i0 + u : 0;
+            qv[u] = q[i];
+            hi[u] = t.pmax[i];
+            lo[u] = t.pmin[i];
+        }
+#pragma unroll
+        for (int u = 0; u < RCH; u++)
+            if (i0 + u < c.np && (qv[u] > hi[u] || qv[u] < lo[u])) oob = true;
+    }
+    if (oob) return LOGZERO;
     double main = 0.0;
     if (c.test_like) {                                               // TestLikelihoodFunction :180-199
         const int n = c.n_used;
@@ -364,11 +399,22 @@ __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const 
     double like = main / c.temperature;
     if (c.has_priors) {                                              // GetLogPriors :111-134
         double pri = 0.0;
-        for (int i = 0; i < c.np; i++)       // std already 0 where the varying/include_fixed gate (:119) is off
-            if (t.pstd[i] != 0.0) {
-                const double z = (q[i] - t.pmean[i]) / t.pstd[i];
-                pri += z * z;
+        for (int i0 = 0; i0 < c.np; i0 += RCH) {   // std already 0 where the varying/include_fixed gate (:119) is off
+            double qv[RCH], mu[RCH], sd[RCH];
+#pragma unroll
+            for (int u = 0; u < RCH; u++) {
+                const int i = i0 + u < c.np ? i0 + u : 0;
+                qv[u] = q[i];
+                mu[u] = t.pmean[i];
+                sd[u] = t.pstd[i];
             }
+#pragma unroll
+            for (int u = 0; u < RCH; u++)
+                if (i0 + u < c.np && sd[u] != 0.0) {
+                    const double z = (qv[u] - mu[u]) / sd[u];
+                    pri += z * z;
+                }
+        }
         for (int k = 0; k < c.n_lin; k++)    // linear combinations :125-131
             if (t.lin_s[k] != 0.0) {
                 const double *wk = t.lin_w + (size_t)k * c.np;
@@ -385,11 +431,11 @@ __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const 
 // Phase timestamps (s_memtime) of the first 64 mh_kernel blocks, only in the
 // instrumented build (make EXTRA=-DCMAMD_STAMPS; tools/mh_stamps.py).
 #ifdef CMAMD_STAMPS
-__device__ unsigned long long g_stamps[64][8];
+__device__ unsigned long long g_stamps[64][16];
 #define STAMP(i)                                                                                \
     do {                                                                                        \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();                            \
-        if (ACCEPT && PROPOSE && lane == 0 && blockIdx.x < 64) g_stamps[blockIdx.x][i] = t_;                         \
+        if (ACCEPT && PROPOSE && lane == 0 && wave == 0 && blockIdx.x < 64) g_stamps[blockIdx.x][i] = t_;            \
     } while (0)
 #else
 #define STAMP(i) ((void)0)
@@ -581,16 +627,26 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
                 lk[(size_t)l * NB + lane] = v;
             }
         }
+        STAMP(8);
         const double like = target_like(c, t, k.trial, Col<double>{lk + lane, NB}, par_test ? tq + lane : nullptr);
+        STAMP(9);
         bool acc = false;
         if (like != LOGZERO) {
             acc = cur > like;
             if (!acc) acc = (double)randexp1(k.r) > like - cur;
         }
+        STAMP(10);
         if (acc) {
             if (mult > 0) nacc += 1;
             mult = 1.0;
-            for (int i = 0; i < c.np; i++) k.P[i] = k.trial[i];
+            for (int i0 = 0; i0 < c.np; i0 += RCH) {   // P = trial, RCH loads in flight
+                double v[RCH];
+#pragma unroll
+                for (int u = 0; u < RCH; u++) v[u] = k.trial[i0 + u < c.np ? i0 + u : 0];
+#pragma unroll
+                for (int u = 0; u < RCH; u++)
+                    if (i0 + u < c.np) k.P[i0 + u] = v[u];
+            }
             cur = like;
 #pragma unroll
             for (int l = 0; l < MAXLIKE; l++)
@@ -601,6 +657,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
         } else {
             mult += 1.0;
         }
+        STAMP(11);
         si[(size_t)R.ACCF * NB + lane] = acc ? 1 : 0;
         if (hist_row) {
             for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = k.P[t.params_used[i]];
@@ -614,7 +671,14 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     }
     STAMP(3);
     if (PROPOSE) {
-        for (int i = 0; i < c.np; i++) k.trial[i] = k.P[i];          // Trial = CurParams
+        for (int i0 = 0; i0 < c.np; i0 += RCH) {                     // Trial = CurParams, RCH loads in flight
+            double v[RCH];
+#pragma unroll
+            for (int u = 0; u < RCH; u++) v[u] = k.P[i0 + u < c.np ? i0 + u : 0];
+#pragma unroll
+            for (int u = 0; u < RCH; u++)
+                if (i0 + u < c.np) k.trial[i0 + u] = v[u];
+        }
         k.defer = par_map;
         k.defer_rot = c.rot_defer;
         if (fast_only) proposal_fast(c, t, k);
@@ -655,6 +719,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
             }
         }
         __syncthreads();
+        STAMP(12);
         if (wave == 0 && act && si[(size_t)R.PROT * NB + lane] == 0) {
             const double *trial = sd + (size_t)SROW(R.T) * NB + lane;
             for (int l = 0; l < c.n_like; l++)
@@ -666,6 +731,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
         }
     }
     __syncthreads();
+    STAMP(13);
     if (!act) return;
     if (skipR) {
         stage_out(c.sd, sd, 0, 0, R.R, W, w, lane, wave, MH_WAVES);
@@ -1827,7 +1893,10 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
     // the likelihoods run in order on the caller's stream: side by side on forked
     // streams the memory-bound likelihood kernels slow each other more than they
     // overlap (MI355X, W = 1024, plik_lite + lensing: 77.1 vs 71.9 us/step; the
-    // binning kernel alone 12.5 -> 26.2 us next to the lensing windows)
+    // binning kernel alone 12.5 -> 26.2 us next to the lensing windows).  Even
+    // the fused pass's two tails (quadratic form and the lensing chi^2, 13.6 and
+    // 7.1 us) lose: with the chi^2 on a side stream forked and joined by events
+    // the step took 87.5 instead of 63.3 us (round 2)
     for (size_t i = 0; i < nl; i++) {
         hipStream_t st = stream;
         auto &l = s->likes[i];
