@@ -786,12 +786,13 @@ __global__ __launch_bounds__(256) void cmbl_reduce_kernel(CLDev c, const double 
 // Workgroup = 8 walkers x 32 thread groups.  The partial rows of every
 // element are cut into tasks of <= 8 rows (host); groups take tasks
 // round-robin with all loads of a task in flight, then combine them per
-// element in task order (deterministic), then split the rows of M.
-struct SmallTask { int first, count; };      // rows e_*_rows[first .. first+count)
+// element in task order (deterministic), then split the rows of M.  Every
+// table load is issued at the start, beside the others: the partial loads
+// wait on one table level (the task's rows), nothing after them on any.
+struct SmallTask { int first, count; };      // rows e_*_rows[first .. first+count) (host side)
 struct SmallDev {
     int ntask;
-    const SmallTask *tasks;                  // main tasks then corr tasks, element order
-    const int *rows;                         // e_main_rows ++ e_corr_rows
+    const int *trow;                         // [ntask][8]: each task's partial rows, -1 padded
     const int *e_main_t, *e_corr_t;          // [nE+1] task ranges per element
 };
 
@@ -814,12 +815,26 @@ __global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev
     const bool act = w < Wc;
     const bool calp = c.log_cal_prior > 0 && c.cal_index >= 0;
     const double cal = (g == 0 && act && calp) ? nuis[(long long)w * ld_nuis + c.cal_index] : 1.0;   // likewise
+    struct Elem { int ix, m0, m1, c0, c1; double mc, cc, fc, ch; };
+    auto elem = [&](int e) {   // element e's table entries
+        Elem q{c.e_to_x[e], sd.e_main_t[e], sd.e_main_t[e + 1], 0, 0, c.e_main_const[e], 0.0, 0.0, c.chat[e]};
+        if (c.has_corr) {
+            q.c0 = sd.e_corr_t[e];
+            q.c1 = sd.e_corr_t[e + 1];
+            q.cc = c.e_corr_const[e];
+            q.fc = c.fidcorr[e];
+        }
+        return q;
+    };
+    Elem e0{-1, 0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0};
+    if (g < c.nE) e0 = elem(g);   // this group's first element, in flight with the partials
     for (int t = g; t < sd.ntask; t += NG) {
-        const SmallTask tk = sd.tasks[t];
+        const int4 ra = *reinterpret_cast<const int4 *>(sd.trow + 8 * t);
+        const int4 rb = *reinterpret_cast<const int4 *>(sd.trow + 8 * t + 4);
+        const int r[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
         double v[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++)
-            v[u] = (act && u < tk.count) ? partial[(long long)sd.rows[tk.first + u] * W + w] : 0.0;
+        for (int u = 0; u < 8; u++) v[u] = (act && r[u] >= 0) ? partial[(long long)r[u] * W + w] : 0.0;
         double s = 0.0;
 #pragma unroll
         for (int u = 0; u < 8; u++) s += v[u];
@@ -827,16 +842,16 @@ __global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev
     }
     __syncthreads();
     for (int e = g; e < c.nE; e += NG) {
-        const int ix = c.e_to_x[e];
-        if (ix < 0) continue;
-        double s = c.e_main_const[e];
-        for (int t = sd.e_main_t[e]; t < sd.e_main_t[e + 1]; t++) s += tp[t][wl];
+        const Elem q = e == g ? e0 : elem(e);
+        if (q.ix < 0) continue;
+        double s = q.mc;
+        for (int t = q.m0; t < q.m1; t++) s += tp[t][wl];
         if (c.has_corr) {
-            double cs = c.e_corr_const[e];
-            for (int t = sd.e_corr_t[e]; t < sd.e_corr_t[e + 1]; t++) cs += tp[t][wl];
-            s = s + (cs - c.fidcorr[e]);
+            double cs = q.cc;
+            for (int t = q.c0; t < q.c1; t++) cs += tp[t][wl];
+            s = s + (cs - q.fc);
         }
-        xs[ix][wl] = s - c.chat[e];
+        xs[q.ix][wl] = s - q.ch;
     }
     __syncthreads();
     double part = 0.0;
@@ -1358,7 +1373,7 @@ struct CMBLikes final : Like {
     DevBuf d_gitems, d_gw, d_bplnu, d_logl80;
     int small_ntask = 0;
     SmallDev sdev{};
-    DevBuf d_invcov, d_stasks, d_srows, d_smt, d_sct;
+    DevBuf d_invcov, d_stasks, d_smt, d_sct;
     // window columns (one per bin and window entry with an output; main then
     // correction), the map pairs they read, and per element its columns; kept
     // so the work items can be rebuilt on other segment boundaries (window_resegment)
@@ -2013,8 +2028,10 @@ struct CMBLikes final : Like {
                 d.alloc(std::max<size_t>(bytes, 16));
                 if (bytes) d.upload(p, bytes);
             };
-            up2(d_stasks, tasks.data(), tasks.size() * sizeof(SmallTask));
-            up2(d_srows, rows_all.data(), rows_all.size() * 4);
+            std::vector<int> trow(tasks.size() * 8, -1);
+            for (size_t t = 0; t < tasks.size(); t++)
+                for (int u = 0; u < tasks[t].count; u++) trow[8 * t + u] = rows_all[tasks[t].first + u];
+            up2(d_stasks, trow.data(), trow.size() * 4);
             up2(d_smt, mt.data(), mt.size() * 4);
             up2(d_sct, ct.data(), ct.size() * 4);
         }
@@ -2033,8 +2050,7 @@ struct CMBLikes final : Like {
         up(d_corrconst, corr_cst.data(), corr_cst.size() * 8);
         small_gauss = approx == 2 && nX <= SMALL_NX && small_ntask <= SMALL_MAXTASK;
         sdev.ntask = small_ntask;
-        sdev.tasks = d_stasks.as<SmallTask>();
-        sdev.rows = d_srows.as<int>();
+        sdev.trow = d_stasks.as<int>();
         sdev.e_main_t = d_smt.as<int>();
         sdev.e_corr_t = d_sct.as<int>();
         dev.nitem = (int)items.size();
