@@ -891,6 +891,13 @@ struct HLDev {
 // problems.  The matrix products go through per-group LDS row buffers.
 #ifdef CMAMD_STAMPS
 __device__ unsigned int g_hl_sweeps[2][64];      // waves per sweep count, first / second eigensolve (tools/hl_stamps.py)
+// s_memtime ticks per Jacobi round phase, summed over the rounds of lane 0 of
+// every wave: [0] column write + barrier, [1] partner read, dot product and
+// angle, [2] rotation + barrier, [3] rounds
+__device__ unsigned long long g_hl_phase[4];
+#define HL_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define HL_STAMP(v) ((void)0)
 #endif
 
 template <int M>
@@ -941,6 +948,9 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
 #pragma unroll
     for (int k = 0; k < M; k++) V[k] = (k == r) ? 1.0 : 0.0;
     bool failed = false;
+#ifdef CMAMD_STAMPS
+    unsigned long long ph0 = 0, ph1 = 0, ph2 = 0, nround = 0;
+#endif
     for (int sweep = 0;; sweep++) {
         bool big = false;
         // the column's squared norm, recomputed every sweep and updated exactly
@@ -951,6 +961,7 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
 #pragma unroll 1
         for (int rr = 0; rr < M - 1; rr++) {
             const int p = on ? hl_partner<M>(rr, r) : r;
+            HL_STAMP(t0);
             if (on) {
 #pragma unroll
                 for (int k = 0; k < M; k++) {
@@ -960,6 +971,10 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
                 S.dg[grp][r] = nrm;
             }
             __syncthreads();
+            HL_STAMP(t1);
+#ifdef CMAMD_STAMPS
+            unsigned long long t2 = 0;
+#endif
             double Gp[M], Vp[M];
 #pragma unroll
             for (int k = 0; k < M; k++) {        // every load in flight together
@@ -984,6 +999,9 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
                     q = fma(q, fma(-den, q, 1.0), q);
                     const double t = ((d >= 0) == (e >= 0) ? fabs(e) : -fabs(e)) * q;
                     const double c = rsqrt(t * t + 1.0), s = t * c;
+#ifdef CMAMD_STAMPS
+                    t2 = __builtin_amdgcn_s_memtime();
+#endif
                     if (low) {
 #pragma unroll
                         for (int k = 0; k < M; k++) {
@@ -1002,6 +1020,16 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
                 }
             }
             __syncthreads();                           // partners' columns read: the next round may write
+#ifdef CMAMD_STAMPS
+            {
+                const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+                const unsigned long long t2w = __shfl(t2, 0) ? __shfl(t2, 0) : t3;
+                ph0 += t1 - t0;
+                ph1 += t2w - t1;
+                ph2 += t3 - t2w;
+                nround++;
+            }
+#endif
         }
 #ifdef CMAMD_STAMPS
         if (!__any(big) || sweep == HL_MAX_SWEEPS)
@@ -1013,6 +1041,14 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
             break;
         }
     }
+#ifdef CMAMD_STAMPS
+    if (lane == 0) {
+        atomicAdd(&g_hl_phase[0], ph0);
+        atomicAdd(&g_hl_phase[1], ph1);
+        atomicAdd(&g_hl_phase[2], ph2);
+        atomicAdd(&g_hl_phase[3], nround);
+    }
+#endif
     double l = 0.0;
 #pragma unroll
     for (int k = 0; k < M; k++) l = fma(V[k], G[k], l);
@@ -1058,13 +1094,20 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     }
     __syncthreads();
     // (2) T = Chat U ; R = U^T T scaled by 1/sqrt(diag) (:878-889)
-    double T[M];
+    // row r of Chat (and below of Cfhalf) into registers first, every load in
+    // flight together (a runtime-n loop waited on each load in turn); the sums
+    // keep the k order
+    double T[M], hr[M];
     const double *ch = h.chat + (long long)b * n * n;
+#pragma unroll
+    for (int k = 0; k < M; k++) hr[k] = (row_ok && k < n) ? ch[r * n + k] : 0.0;
 #pragma unroll
     for (int j = 0; j < M; j++) {
         double s = 0.0;
         if (row_ok && j < n)
-            for (int k = 0; k < n; k++) s += ch[r * n + k] * U_row(k, j);
+#pragma unroll
+            for (int k = 0; k < M; k++)
+                if (k < n) s += hr[k] * U_row(k, j);
         T[j] = s;
     }
     if (on)
@@ -1076,7 +1119,9 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     for (int j = 0; j < M; j++) {
         double s = 0.0;
         if (row_ok && j < n) {
-            for (int k = 0; k < n; k++) s += U_row(k, r) * S.rows[grp][1][k][j];
+#pragma unroll
+            for (int k = 0; k < M; k++)
+                if (k < n) s += U_row(k, r) * S.rows[grp][1][k][j];
             const int lo = r < j ? r : j, hi = r < j ? j : r;
             s = s / sqrt(S.dg[grp][lo]);
             s = s / sqrt(S.dg[grp][hi]);
@@ -1107,7 +1152,9 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     for (int j = 0; j < M; j++) {        // A[r][j] = sum_k U[r][k] T2[k][j]
         double s = 0.0;
         if (row_ok && j < n)
-            for (int k = 0; k < n; k++) s += U_row(r, k) * S.rows[grp][1][k][j];
+#pragma unroll
+            for (int k = 0; k < M; k++)
+                if (k < n) s += U_row(r, k) * S.rows[grp][1][k][j];
         A[j] = s;
     }
     __syncthreads();
@@ -1125,10 +1172,14 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     // (5) U = Cfhalf V ; C = U diag(g) U^T (:907-912)
     const double *cf = h.cfhalf + (long long)b * n * n;
 #pragma unroll
+    for (int k = 0; k < M; k++) hr[k] = (row_ok && k < n) ? cf[r * n + k] : 0.0;
+#pragma unroll
     for (int j = 0; j < M; j++) {
         double s = 0.0;
         if (row_ok && j < n)
-            for (int k = 0; k < n; k++) s += cf[r * n + k] * U_row(k, j);
+#pragma unroll
+            for (int k = 0; k < M; k++)
+                if (k < n) s += hr[k] * U_row(k, j);
         T[j] = s;
     }
     __syncthreads();
@@ -2412,5 +2463,8 @@ std::unique_ptr<Like> make_cmblikes(const Ini &ini, const std::string &tag) {
 #ifdef CMAMD_STAMPS
 extern "C" int cmamd_debug_hl_sweeps(unsigned int *host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_hl_sweeps), sizeof(cmamd::g_hl_sweeps)) == hipSuccess ? 0 : -5;
+}
+extern "C" int cmamd_debug_hl_phase(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_hl_phase), sizeof(cmamd::g_hl_phase)) == hipSuccess ? 0 : -5;
 }
 #endif

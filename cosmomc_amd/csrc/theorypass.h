@@ -12,8 +12,11 @@ namespace cmamd {
 static constexpr int TP_MAXOUT = 2;    // likelihoods per pass
 static constexpr int TP_CHUNK = 64;    // l per weight chunk
 static constexpr int TP_MAXCOL = 64;   // columns per work item (four 16-column MFMA blocks)
-static constexpr int TP_MAXL = 256;    // l per work item, unless overlapping columns force more
-                                       //   (at most TP_MAXSTEP * 32 - 1 in any case)
+#ifndef CMAMD_TP_MAXL
+#define CMAMD_TP_MAXL 256
+#endif
+static constexpr int TP_MAXL = CMAMD_TP_MAXL;   // l per work item, unless overlapping columns force more
+                                                //   (at most TP_MAXSTEP * 32 - 1 in any case)
 
 struct TPOut {            // a stage's output for one launch
     int kind;             // WinStage::kind
@@ -40,6 +43,7 @@ struct TPCol {
 
 struct TPDev {
     const TPItem *items;
+    const int2 *units;    // per block: (item, walker tile), item -1: no work
     const TPCol *cols;
     const double *w;
     int nitem;
@@ -57,9 +61,12 @@ class TheoryPass {
     int n_stages() const { return nstage; }
 
   private:
+    // the block table for `tiles` walker tiles (plan_units)
+    void plan_units(int tiles);
     std::vector<TPItem> items;
-    DevBuf d_items, d_cols, d_w;
+    DevBuf d_items, d_cols, d_w, d_units;
     int nstage = 0;
+    int unit_tiles = -1, nblk = 0;
 };
 
 }  // namespace cmamd

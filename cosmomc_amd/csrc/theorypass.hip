@@ -29,6 +29,19 @@ namespace cmamd {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
+#ifdef CMAMD_STAMPS
+// per block of the last launch: s_memtime at start, after the prologue, after
+// the step loop, at the end; HW_ID, XCC_ID and the item (tools/tp_stamps.py)
+__device__ unsigned long long g_tp_stamps[4096][10];
+#define TP_STAMP(i)                                                                   \
+    do {                                                                              \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                   \
+        if (threadIdx.x == 0 && b < 4096) g_tp_stamps[b][i] = t_;                     \
+    } while (0)
+#else
+#define TP_STAMP(i) ((void)0)
+#endif
+
 __global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const double *__restrict__ dl, long long ld_field,
                                                            long long ld_walker, int W, int tiles, int vec_ok)
 {
@@ -36,11 +49,16 @@ __global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const doubl
     __shared__ __attribute__((aligned(16))) double wsh[2 * NCB * 16 * WROW];   // [buf][col block][col][l]
     __shared__ TPCol csh[TP_MAXCOL];      // the item's column descriptors
     __shared__ double xsh[TP_MAXCOL];     // and their data values (plik X)
-    // blocks are dealt to the XCDs round-robin: all walker tiles of an item on one XCD
-    // (its weights in one L2); measured faster than an XCD-balanced split of the units
-    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
-    const int item = xcd + 8 * (j / tiles), tile = j % tiles;
-    if (item >= c.nitem) return;
+    // the (item, walker tile) of this block comes from the host's plan (plan_units)
+    const int b = blockIdx.x;
+    const int2 unit = c.units[b];
+    const int item = unit.x, tile = unit.y;
+    (void)tiles;
+    if (item < 0) return;
+    TP_STAMP(0);
+#ifdef CMAMD_STAMPS
+    const unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();
+#endif
     const TPItem it = c.items[item];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, kq = lane >> 4;
@@ -136,6 +154,7 @@ __global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const doubl
     }
     store_w(0, 0);
     __syncthreads();
+    TP_STAMP(1);
     for (int st = 0; st < nstep; st++) {
         const bool more = st + 1 < nstep;
         const int cur = st & 1;
@@ -156,6 +175,15 @@ __global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const doubl
             }
         }
     }
+    TP_STAMP(2);
+#ifdef CMAMD_STAMPS
+    if (threadIdx.x == 0 && b < 4096) {
+        g_tp_stamps[b][4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        g_tp_stamps[b][5] = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+        g_tp_stamps[b][6] = item;
+        g_tp_stamps[b][7] = (unsigned long long)nstep * 1000 + __builtin_popcountll(it.act);
+    }
+#endif
     if (w >= W) return;
     // D: walker = lane&15, column = 16 cb + (lane>>4) + 4 r
     auto emit = [&](int cb, const f64x4 &acc) {
@@ -181,6 +209,14 @@ __global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const doubl
     if (ncb > 1) emit(1, acc1 + bcc1);
     if (ncb > 2) emit(2, acc2 + bcc2);
     if (ncb > 3) emit(3, acc3 + bcc3);
+    TP_STAMP(3);
+#ifdef CMAMD_STAMPS
+    const unsigned long long rt1_ = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && b < 4096) {
+        g_tp_stamps[b][8] = rt0_;
+        g_tp_stamps[b][9] = rt1_;
+    }
+#endif
 }
 
 // ------------------------------------------------------------------ host side
@@ -291,6 +327,64 @@ bool TheoryPass::build(const std::vector<WinStage> &stages) {
     return true;
 }
 
+// Block table.  The blocks are dealt to the XCDs round-robin (block b on XCD
+// b % 8), and within an XCD the measured dispatch puts its j-th block on CU
+// j % (CUs per XCD) while every block fits at once (block stamps,
+// tools/tp_stamps.py).  With walker tiles of an item on consecutive blocks,
+// the CUs that received a third block got two long items (TT / TE ranges with
+// lensing and plik columns: two MFMA blocks per step) and set the kernel's end
+// at 27.8 us against a median CU end of 22.8 us.  So the units (item, tile) are
+// placed by cost instead: the items go to XCDs by longest-processing-time over
+// their summed cost (all tiles of an item on one XCD: its weights in one L2),
+// then each XCD's units to its CUs the same way, and the table lists them round
+// by round (CU c's k-th unit at j = k * ncu + c); a CU with fewer units has an
+// empty entry there.  Cost of a unit: its active 16-column MFMA block-steps +
+// 1.1 per 32-l step (a CU's end time, fitted over the 256 CUs' stamps, was
+// 16.1 us + 148 ns per block-step + 166 ns per step; no per-block term).  The
+// kernel went from 27.7 to 26.2 us (CU ends 22.4-25.4 us instead of
+// 18-27.8).  Every unit appears once, so the outputs do not depend on the plan.
+void TheoryPass::plan_units(int tiles) {
+    int dev = 0, ncu = 256;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const int NX = 8, cpx = std::max(1, ncu / NX);
+    const int ni = (int)items.size();
+    std::vector<double> cost(ni);
+    for (int i = 0; i < ni; i++)
+        cost[i] = __builtin_popcountll(items[i].act) + 1.1 * items[i].nch * (TP_CHUNK / 32);
+    std::vector<int> ord(ni);
+    for (int i = 0; i < ni; i++) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+    std::vector<double> xload(NX, 0.0);
+    std::vector<std::vector<int>> xitems(NX);
+    for (int i : ord) {
+        const int x = (int)(std::min_element(xload.begin(), xload.end()) - xload.begin());
+        xload[x] += cost[i] * tiles;
+        xitems[x].push_back(i);
+    }
+    // per XCD, per CU: its units in placement order
+    std::vector<std::vector<std::vector<int2>>> cu(NX, std::vector<std::vector<int2>>(cpx));
+    int rounds = 0;
+    for (int x = 0; x < NX; x++) {
+        std::vector<double> load(cpx, 0.0);
+        for (int i : xitems[x])          // already by cost, descending
+            for (int t = 0; t < tiles; t++) {
+                const int k = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+                load[k] += cost[i];
+                cu[x][k].push_back(int2{i, t});
+                rounds = std::max(rounds, (int)cu[x][k].size());
+            }
+    }
+    std::vector<int2> table((size_t)NX * cpx * rounds, int2{-1, 0});
+    for (int x = 0; x < NX; x++)
+        for (int k = 0; k < cpx; k++)
+            for (size_t r = 0; r < cu[x][k].size(); r++) table[((size_t)r * cpx + k) * NX + x] = cu[x][k][r];
+    nblk = (int)table.size();
+    d_units.alloc(table.size() * sizeof(int2));
+    d_units.upload(table.data(), table.size() * sizeof(int2));
+    unit_tiles = tiles;
+}
+
 void TheoryPass::launch(const double *dl, long long ld_field, long long ld_walker, const TPOut *outs, int W,
                         hipStream_t stream) {
     if (W <= 0 || items.empty()) return;
@@ -302,7 +396,8 @@ void TheoryPass::launch(const double *dl, long long ld_field, long long ld_walke
     for (int s = 0; s < nstage; s++) c.out[s] = outs[s];
     const int vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0;
     const int tiles = (W + 63) / 64;
-    const int nblk = 8 * tiles * ((c.nitem + 7) / 8);
+    if (tiles != unit_tiles) plan_units(tiles);
+    c.units = d_units.as<int2>();
     timed_launch("theory_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
         hipExtLaunchKernelGGL(theory_window_kernel, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl, ld_field,
                               ld_walker, W, tiles, vec_ok);
@@ -311,3 +406,9 @@ void TheoryPass::launch(const double *dl, long long ld_field, long long ld_walke
 }
 
 }  // namespace cmamd
+
+#ifdef CMAMD_STAMPS
+extern "C" int cmamd_debug_tp_stamps(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_tp_stamps), sizeof(cmamd::g_tp_stamps)) == hipSuccess ? 0 : -5;
+}
+#endif

@@ -31,3 +31,9 @@ if __name__ == "__main__":
         nz = np.nonzero(h)[0]
         print(f"{lab}: waves by sweeps (incl. the final check sweep) " +
               " ".join(f"{i}:{h[i]}" for i in nz) + f"  mean {(h * np.arange(64)).sum() / max(h.sum(), 1):.2f}")
+    ph = np.zeros(4, dtype=np.uint64)
+    assert N.lib().cmamd_debug_hl_phase(ph.ctypes.data_as(C.c_void_p)) == 0
+    n = max(int(ph[3]), 1)
+    print(f"Jacobi rounds (lane 0 of every wave): {n}; s_memtime ticks per round: "
+          f"write+barrier {ph[0] / n:.0f}, read+dot+angle {ph[1] / n:.0f}, rotate+barrier {ph[2] / n:.0f}, "
+          f"total {(ph[0] + ph[1] + ph[2]) / n:.0f}")
