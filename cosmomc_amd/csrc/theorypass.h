@@ -33,7 +33,9 @@ static constexpr int TP_MAXSTEP = 16;   // 32-l steps per work item (the active-
 
 struct TPItem {           // one workgroup's l range of one theory field, with <= 64 columns
     int field, l0, l1, nch, ncol, cdesc;
-    long long woff;       // weights [nch][ncb][16][TP_CHUNK], zero padded
+    int nsb;              // 16-slot MFMA blocks in use (slots are reused: TheoryPass::build)
+    int soff;             // first of its steps in TPDev::emit / cmap
+    long long woff;       // weights [nch][nsb][16 slots][TP_CHUNK], zero padded
     unsigned long long act;   // bit 4 step + block: the block has a nonzero weight in the step
 };
 
@@ -46,6 +48,8 @@ struct TPDev {
     const int2 *units;    // per block: (item, walker tile), item -1: no work
     const TPCol *cols;
     const double *w;
+    const unsigned long long *emit;   // per item step: slots whose column ends there
+    const unsigned char *cmap;        // per item step, [64] slots: the item's column index (255: none)
     int nitem;
     TPOut out[TP_MAXOUT];
 };
@@ -64,9 +68,9 @@ class TheoryPass {
     // the block table for `tiles` walker tiles (plan_units)
     void plan_units(int tiles);
     std::vector<TPItem> items;
-    DevBuf d_items, d_cols, d_w, d_units;
+    DevBuf d_items, d_cols, d_w, d_units, d_emit, d_cmap;
     int nstage = 0;
-    int unit_tiles = -1, nblk = 0;
+    int unit_tiles = -1, nblk = 0, max_nsb = 0;
 };
 
 }  // namespace cmamd

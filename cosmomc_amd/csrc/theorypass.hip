@@ -9,14 +9,22 @@
 // s = 2 j + h contracts the four l {8 j + 2 kq + h} against the weights, which
 // the block's four waves share through a double-buffered LDS tile.  Columns
 // are ordered wide first (CMBlikes windows), then plik bins by l, and a block
-// runs only in the steps where it has weight (the plik bins are narrow).
+// runs only in the steps where it has weight.
 // Each column's sum goes to its stage: a CMBlikes partial row (/ cal^2 for
 // calibrated map pairs, AdaptTheoryForMaps CMBlikes.f90:1113-1124), or plik's
 // Delta = X - sum / cal^2 (CMB.f90:315-326; the bin sum in MFMA order, not the
 // reference's l order: rtol 1e-12 against plik_bin_delta).  No column
 // straddles two items, so every output is one workgroup's store.
 //
-// Measured (MI355X, W = 1024, plik_lite + lensing): 27.6 us against 30 us for
+// Slots: the columns of an item are dealt to the 16-column MFMA blocks' slots
+// by their step ranges (interval colouring), so a plik bin takes a slot only
+// for the steps it covers, and its sum is written (and the slot zeroed) right
+// after the MFMAs of its last step.  The lensing windows (9 slots, every step)
+// and the few plik bins open in one 32-l step then share one block: one
+// active block per step instead of two (act 16 -> 8 on the long TT/TE/EE
+// items), 26.2 -> 24.2 us.
+//
+// Measured (MI355X, W = 1024, plik_lite + lensing): 24.2 us against 30 us for
 // plik_bin_delta + cmbl_window_direct.  Summing the bins on the VALU from an
 // LDS copy of the tile instead (the reference's order) took 39-42 us.
 #include <algorithm>
@@ -42,13 +50,19 @@ __device__ unsigned long long g_tp_stamps[4096][10];
 #define TP_STAMP(i) ((void)0)
 #endif
 
-__global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const double *__restrict__ dl, long long ld_field,
+// NB: the most 16-slot blocks any item uses.  With slot reuse the headline
+// items need at most two, and four accumulators fit three waves per SIMD
+// (168 VGPRs); NB = 4 keeps the general case at two.
+template <int NB>
+__global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_kernel(TPDev c, const double *__restrict__ dl, long long ld_field,
                                                            long long ld_walker, int W, int tiles, int vec_ok)
 {
     constexpr int LPL = 8, STEP = 4 * LPL, NSUB = TP_CHUNK / STEP, WROW = STEP + 2, NCB = TP_MAXCOL / 16;
     __shared__ __attribute__((aligned(16))) double wsh[2 * NCB * 16 * WROW];   // [buf][col block][col][l]
     __shared__ TPCol csh[TP_MAXCOL];      // the item's column descriptors
     __shared__ double xsh[TP_MAXCOL];     // and their data values (plik X)
+    __shared__ unsigned long long esh[TP_MAXSTEP];            // slots ending at each step
+    __shared__ unsigned char msh[TP_MAXSTEP * TP_MAXCOL];     // slot -> column at each step
     // the (item, walker tile) of this block comes from the host's plan (plan_units)
     const int b = blockIdx.x;
     const int2 unit = c.units[b];
@@ -65,7 +79,7 @@ __global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const doubl
     const int w = tile * 64 + wave * 16 + li;
     const int wl = min(w, W - 1);
     const double *Df = dl + (long long)wl * ld_walker + (long long)it.field * ld_field;
-    const int ncb = (it.ncol + 15) >> 4;
+    const int ncb = it.nsb;
     const int nstep = it.nch * NSUB;
     double t[LPL], tn[LPL], tnn[LPL], a[LPL];
     auto load_t = [&](int st, double *dst) {
@@ -142,6 +156,10 @@ __global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const doubl
         const double *X = d.out ? c.out[1].X : c.out[0].X;
         xsh[tid] = kind == 1 ? X[d.row] : 0.0;
     }
+    if (tid < nstep) esh[tid] = c.emit[it.soff + tid];
+    for (int q = tid; q < nstep * (TP_MAXCOL / 4); q += 256)
+        reinterpret_cast<unsigned int *>(msh)[q] =
+            reinterpret_cast<const unsigned int *>(c.cmap + (long long)it.soff * TP_MAXCOL)[q];
     double c2[TP_MAXOUT];
 #pragma unroll
     for (int o = 0; o < TP_MAXOUT; o++) {
@@ -155,6 +173,33 @@ __global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const doubl
     store_w(0, 0);
     __syncthreads();
     TP_STAMP(1);
+    // D: walker = lane&15, slot = 16 cb + (lane>>4) + 4 r.  A column's sum is
+    // written after the MFMAs of its last step, and its slot is zeroed for the
+    // next column: the sum is the same MFMA chain as with a slot of its own
+    // (the steps outside its range only ever added products with zero weight)
+    auto emit = [&](int st, unsigned long long e, int cb, f64x4 &acc, f64x4 &bcc) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int slot = 16 * cb + kq + 4 * r;
+            if (!((e >> slot) & 1ull)) continue;
+            const int col = msh[st * TP_MAXCOL + slot];
+            double v = acc[r] + bcc[r];
+            acc[r] = 0.0;
+            bcc[r] = 0.0;
+            if (w >= W) continue;
+            const TPCol d = csh[col];
+            const bool o1 = d.out != 0;   // selects, not a dynamically indexed kernel argument
+            const int kind = o1 ? c.out[1].kind : c.out[0].kind;
+            double *out = o1 ? c.out[1].out : c.out[0].out;
+            if (d.cal) v = v / (o1 ? c2[1] : c2[0]);
+            if (kind == 0) {
+                out[(long long)d.row * W + w] = v;
+            } else {
+                const int ld = o1 ? c.out[1].ld : c.out[0].ld;
+                out[(long long)w * ld + d.row] = xsh[col] - v;
+            }
+        }
+    };
     for (int st = 0; st < nstep; st++) {
         const bool more = st + 1 < nstep;
         const int cur = st & 1;
@@ -163,8 +208,17 @@ __global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const doubl
         const unsigned m = (unsigned)(it.act >> (4 * st)) & 15u;   // blocks with weight in this step
         if (m & 1u) mfma_block(cur, 0, acc0, bcc0);
         if (m & 2u) mfma_block(cur, 1, acc1, bcc1);
-        if (m & 4u) mfma_block(cur, 2, acc2, bcc2);
-        if (m & 8u) mfma_block(cur, 3, acc3, bcc3);
+        if constexpr (NB > 2) {
+            if (m & 4u) mfma_block(cur, 2, acc2, bcc2);
+            if (m & 8u) mfma_block(cur, 3, acc3, bcc3);
+        }
+        const unsigned long long e = esh[st];
+        if (e & 0xffffull) emit(st, e, 0, acc0, bcc0);
+        if (e & 0xffff0000ull) emit(st, e, 1, acc1, bcc1);
+        if constexpr (NB > 2) {
+            if (e & 0xffff00000000ull) emit(st, e, 2, acc2, bcc2);
+            if (e & 0xffff000000000000ull) emit(st, e, 3, acc3, bcc3);
+        }
         if (more) {
             store_w(cur ^ 1, st + 1);      // buffer cur ^ 1 was last read before the previous barrier
             __syncthreads();
@@ -184,31 +238,6 @@ __global__ __launch_bounds__(256) void theory_window_kernel(TPDev c, const doubl
         g_tp_stamps[b][7] = (unsigned long long)nstep * 1000 + __builtin_popcountll(it.act);
     }
 #endif
-    if (w >= W) return;
-    // D: walker = lane&15, column = 16 cb + (lane>>4) + 4 r
-    auto emit = [&](int cb, const f64x4 &acc) {
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int col = 16 * cb + kq + 4 * r;
-            if (col >= it.ncol) continue;
-            const TPCol d = csh[col];
-            const bool o1 = d.out != 0;   // selects, not a dynamically indexed kernel argument
-            const int kind = o1 ? c.out[1].kind : c.out[0].kind;
-            double *out = o1 ? c.out[1].out : c.out[0].out;
-            double v = acc[r];
-            if (d.cal) v = v / (o1 ? c2[1] : c2[0]);
-            if (kind == 0) {
-                out[(long long)d.row * W + w] = v;
-            } else {
-                const int ld = o1 ? c.out[1].ld : c.out[0].ld;
-                out[(long long)w * ld + d.row] = xsh[col] - v;
-            }
-        }
-    };
-    if (ncb > 0) emit(0, acc0 + bcc0);
-    if (ncb > 1) emit(1, acc1 + bcc1);
-    if (ncb > 2) emit(2, acc2 + bcc2);
-    if (ncb > 3) emit(3, acc3 + bcc3);
     TP_STAMP(3);
 #ifdef CMAMD_STAMPS
     const unsigned long long rt1_ = __builtin_amdgcn_s_memrealtime();
@@ -231,9 +260,12 @@ bool TheoryPass::build(const std::vector<WinStage> &stages) {
             if (wc.hi < wc.lo || wc.lo < 0) return false;
             byf[wc.field].push_back(C{wc.lo, wc.hi, (int)s, (int)k});
         }
+    max_nsb = 0;
     std::vector<TPItem> its;
     std::vector<TPCol> cols;
     std::vector<double> w;
+    std::vector<unsigned long long> emit;
+    std::vector<unsigned char> cmap;
     for (auto &kv : byf) {
         auto &v = kv.second;
         // by start, the longest first among equal starts: a long column that
@@ -291,14 +323,42 @@ bool TheoryPass::build(const std::vector<WinStage> &stages) {
             it.ncol = (int)g.size();
             it.cdesc = (int)cols.size();
             it.woff = (long long)w.size();
-            const int ncb = (it.ncol + 15) / 16;
+            const int nstep = it.nch * (TP_CHUNK / 32);
+            // steps of each column, and its slot: the lowest slot whose previous
+            // column ended before this one's first step (g: wide ones first, then by l)
+            std::vector<int> s0(g.size()), s1(g.size()), slot(g.size());
+            std::vector<int> slot_end;                    // last step of the slot's current column
+            for (size_t q = 0; q < g.size(); q++) {
+                const WinCol &wc = stages[g[q].stage].cols[g[q].col];
+                s0[q] = std::max(0, (wc.lo - it.l0) / 32);
+                s1[q] = std::min(nstep - 1, (wc.hi - it.l0) / 32);
+                int k = 0;
+                while (k < (int)slot_end.size() && slot_end[k] >= s0[q]) k++;
+                if (k == (int)slot_end.size()) slot_end.push_back(0);
+                slot_end[k] = s1[q];
+                slot[q] = k;
+            }
+            it.nsb = ((int)slot_end.size() + 15) / 16;
+            max_nsb = std::max(max_nsb, it.nsb);
+            it.soff = (int)emit.size();
+            // slot -> column per step (255: none), and the slots whose column ends at each step
+            std::vector<unsigned char> sm((size_t)nstep * TP_MAXCOL, 255);
+            std::vector<unsigned long long> em(nstep, 0ull);
+            for (size_t q = 0; q < g.size(); q++) {
+                for (int st = s0[q]; st <= s1[q]; st++) {
+                    sm[(size_t)st * TP_MAXCOL + slot[q]] = (unsigned char)q;
+                    it.act |= 1ull << (4 * st + slot[q] / 16);
+                }
+                em[s1[q]] |= 1ull << slot[q];
+            }
             for (int ch = 0; ch < it.nch; ch++)
-                for (int cb = 0; cb < ncb; cb++)
-                    for (int q = 16 * cb; q < 16 * cb + 16; q++)
+                for (int cb = 0; cb < it.nsb; cb++)
+                    for (int sl = 16 * cb; sl < 16 * cb + 16; sl++)
                         for (int k = 0; k < TP_CHUNK; k++) {
                             const int l = it.l0 + ch * TP_CHUNK + k;
+                            const int q = sm[(size_t)((ch * TP_CHUNK + k) / 32) * TP_MAXCOL + sl];
                             double x = 0.0;
-                            if (q < it.ncol) {
+                            if (q != 255) {
                                 const WinCol &wc = stages[g[q].stage].cols[g[q].col];
                                 if (l >= wc.lo && l <= wc.hi) x = wc.w[l - wc.lo];
                             }
@@ -307,11 +367,9 @@ bool TheoryPass::build(const std::vector<WinStage> &stages) {
             for (size_t q = 0; q < g.size(); q++) {
                 const WinCol &wc = stages[g[q].stage].cols[g[q].col];
                 cols.push_back(TPCol{g[q].stage, wc.row, wc.cal, 0});
-                for (int st = 0; st < it.nch * (TP_CHUNK / 32); st++) {
-                    const int s0 = it.l0 + 32 * st, s1 = s0 + 31;
-                    if (wc.lo <= s1 && wc.hi >= s0) it.act |= 1ull << (4 * st + (int)q / 16);
-                }
             }
+            emit.insert(emit.end(), em.begin(), em.end());
+            cmap.insert(cmap.end(), sm.begin(), sm.end());
             its.push_back(it);
         }
     }
@@ -324,6 +382,8 @@ bool TheoryPass::build(const std::vector<WinStage> &stages) {
     up(d_items, items.data(), items.size() * sizeof(TPItem));
     up(d_cols, cols.data(), cols.size() * sizeof(TPCol));
     up(d_w, w.data(), w.size() * 8);
+    up(d_emit, emit.data(), emit.size() * sizeof(unsigned long long));
+    up(d_cmap, cmap.data(), cmap.size());
     return true;
 }
 
@@ -392,6 +452,8 @@ void TheoryPass::launch(const double *dl, long long ld_field, long long ld_walke
     c.items = d_items.as<TPItem>();
     c.cols = d_cols.as<TPCol>();
     c.w = d_w.as<double>();
+    c.emit = d_emit.as<unsigned long long>();
+    c.cmap = d_cmap.as<unsigned char>();
     c.nitem = (int)items.size();
     for (int s = 0; s < nstage; s++) c.out[s] = outs[s];
     const int vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0;
@@ -399,8 +461,12 @@ void TheoryPass::launch(const double *dl, long long ld_field, long long ld_walke
     if (tiles != unit_tiles) plan_units(tiles);
     c.units = d_units.as<int2>();
     timed_launch("theory_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-        hipExtLaunchKernelGGL(theory_window_kernel, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl, ld_field,
-                              ld_walker, W, tiles, vec_ok);
+        if (max_nsb <= 2)
+            hipExtLaunchKernelGGL(theory_window_kernel<2>, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl,
+                                  ld_field, ld_walker, W, tiles, vec_ok);
+        else
+            hipExtLaunchKernelGGL(theory_window_kernel<4>, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl,
+                                  ld_field, ld_walker, W, tiles, vec_ok);
     });
     HIP_CHECK(hipGetLastError());
 }
