@@ -13,10 +13,13 @@ static constexpr int TP_MAXOUT = 2;    // likelihoods per pass
 static constexpr int TP_CHUNK = 64;    // l per weight chunk
 static constexpr int TP_MAXCOL = 64;   // columns per work item (four 16-column MFMA blocks)
 #ifndef CMAMD_TP_MAXL
-#define CMAMD_TP_MAXL 256
+#define CMAMD_TP_MAXL 288
 #endif
-static constexpr int TP_MAXL = CMAMD_TP_MAXL;   // l per work item, unless overlapping columns force more
-                                                //   (at most TP_MAXSTEP * 32 - 1 in any case)
+// l per work item, unless overlapping columns force more (at most
+// TP_MAXSTEP * 32 - 1 in any case).  288 (9 steps): with slot reuse the
+// headline's 1024 walkers make about 2 blocks per CU; measured 22.7 us
+// against 24.0 (256), 23.2 (272), 23.3 (300), 23.6 (320), 24.9 (384)
+static constexpr int TP_MAXL = CMAMD_TP_MAXL;
 
 struct TPOut {            // a stage's output for one launch
     int kind;             // WinStage::kind

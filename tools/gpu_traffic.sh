@@ -11,7 +11,7 @@ for pass in "fetch FETCH_SIZE" "write WRITE_SIZE"; do
   set -- $pass
   timeout -k 10 300 rocprofv3 --pmc $2 --output-format csv -d "$R/gpurun_out/pmc/$1" -o run \
     -- python3 "$R/bench.py" --no-cpu-baseline --steps 60 --warmup 5 --converge-seconds 0 --config4-seconds -1 \
-       --config5-seconds -1 > "$R/gpurun_out/pmc/$1.log" 2>&1 || exit $?
+       --config5-seconds -1 --drag-seconds -1 > "$R/gpurun_out/pmc/$1.log" 2>&1 || exit $?
 done
 cd "$R" && PMC_WALKERS=1024 python3 tools/pmc_summary.py gpurun_out/pmc gpurun_out/pmc_traffic.json > gpurun_out/pmc_summary.txt
 rc=$?
