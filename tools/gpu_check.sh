@@ -15,7 +15,7 @@ rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.
 if [ "${PROFILE:-1}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run \
-      -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --converge-seconds 0 --config4-seconds -1 --config5-seconds -1 "$@" > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.log" 2>&1
+      -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --converge-seconds 0 --config4-seconds -1 --config5-seconds -1 --drag-seconds -1 "$@" > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; cd "$GRAFT_REPO_ROOT"
   find gpurun_out/prof -name "*stats*" | head
 fi
