@@ -600,13 +600,15 @@ def test_change_mask_matches_dense(cmbl_golden, refdata, tmp_path, shared_theory
         assert a[4][-1, 1, w] == pytest.approx(ob.loglike(t, a[0][w, 2:]), rel=1e-9)
 
 
-@pytest.mark.parametrize("W", [100, 512])
+@pytest.mark.parametrize("W", [1, 100, 512, 1024])
 def test_fused_window_pass(cmbl_golden, refdata, tmp_path, W):
     """plik_lite and the Planck lensing likelihood on one theory buffer run
     their window stages as one pass over it (theorypass.hip; the lensing
     windows are re-segmented where no plik bin is split).  The per-likelihood
     terms of the recorded points equal each likelihood's own loglike_batch
-    (rtol 1e-12: only the summation split differs) and the oracles'."""
+    (rtol 1e-12: only the summation split differs) and the oracles'.
+    W = 1024 runs the bench's block plan (16 walker tiles placed by cost),
+    W = 1 a single tile; every W runs the slot-reusing columns."""
     import os
 
     import cmblikes_oracle as co
