@@ -165,8 +165,13 @@ def run_to_convergence(smp, num_slow, num_fast, seconds, world, cap, fast_only=T
             stop = flag.item() > 0
         if stop:
             break
+    import torch.distributed as dist
+    backend = dist.get_backend() if world > 1 else None
     return {"target_r_minus_1": 0.01, "min_sample_update": col.min_update, "update_freq": col.update_freq,
-            "converged_wall_s": done_at, "trace_wall_s_steps_R": trace}
+            "converged_wall_s": done_at, "trace_wall_s_steps_R": trace, "ranks": world,
+            "exchanges": len(col.results),
+            "exchange": (f"2 all_reduce per exchange over {backend} across {world} ranks "
+                         "(SampleCollector.f90:248-251 MPI_ALLGATHER)") if world > 1 else "single rank, no collective"}
 
 
 def convergence_run(W, rank, world, tmpdir, seconds, lensing=True):
@@ -448,6 +453,28 @@ def host_cores():
     return (min(n, quota) if quota else n), n, quota
 
 
+def node_physical_cores():
+    """Physical cores of the whole node (unique (physical id, core id) pairs in
+    /proc/cpuinfo), whatever share of them this job may use."""
+    pairs, phys, core = set(), None, None
+    try:
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k = k.strip()
+            if k == "physical id":
+                phys = v.strip()
+            elif k == "core id":
+                core = v.strip()
+            elif not k and phys is not None:
+                pairs.add((phys, core))
+                phys = core = None
+        if phys is not None:
+            pairs.add((phys, core))
+    except OSError:
+        return None
+    return len(pairs) or None
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -472,7 +499,8 @@ def cpu_baseline(seconds, lensing=True, repeats=5):
     Wc = 16
     th = syn.walker_theory(Wc, n_fields=3)
     cal = syn.walker_calibrations(Wc)
-    host = {"cpu_model": cpu_model(), "affinity_cores": n_aff, "cgroup_quota_cores": quota}
+    host = {"cpu_model": cpu_model(), "affinity_cores": n_aff, "cgroup_quota_cores": quota,
+            "node_physical_cores": node_physical_cores(), "node_logical_cpus": os.cpu_count()}
     with tempfile.TemporaryDirectory() as td:
         ds = data.write(td)
         if os.path.exists(exe):
@@ -498,7 +526,13 @@ def cpu_baseline(seconds, lensing=True, repeats=5):
                 totals.append(float(sum(rates)))
             what = "TPlikLiteLikelihood_LogLike + CMBLikes_LogLike (lensing)" if lensing else \
                 "TPlikLiteLikelihood_LogLike"
-            return {"value": float(np.median(totals)), "unit": "evals/s", "cores": P, "kind": "reference",
+            med = float(np.median(totals))
+            pc = node_physical_cores()
+            return {"value": med, "unit": "evals/s", "cores": P, "kind": "reference",
+                    "per_core_evals_per_s": med / P,
+                    "node_estimate_evals_per_s": (med / P * pc) if pc else None,
+                    "node_estimate_note": "per-core rate x the node's physical cores (linear; not measured: "
+                                          "the job may use only `cores` of them)",
                     "repeats": [round(x, 1) for x in totals], "host": host,
                     "flags": "amdflang -O3 -ffast-math -march=x86-64-v3 (reference source/Makefile:60 "
                              "-O3 -ffast-math -march=native) + OpenBLAS 1 thread",
@@ -570,17 +604,49 @@ def pmc_traffic(kernel, W):
     return t["fetch_bytes"] + t["write_bytes"], "profiles/pmc_traffic.json"
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) started as a plain process: start the N
+    ranks as child processes (torch.distributed.run, one per GPU, rendezvous on
+    127.0.0.1) and return their exit code.  Runs before anything touches the
+    GPU; device_count() does not initialise it on this image.  With the nccl
+    (RCCL) backend every rank needs its own device, so N above the device count
+    is refused; gloo rehearses N ranks on fewer devices."""
+    import torch
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and args.gpus > ndev:
+        sys.exit(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs for the nccl (RCCL) backend, "
+                 f"this node has {ndev}; use --dist-backend gloo to rehearse ranks on fewer devices")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if "WORLD_SIZE" in os.environ and args.gpus not in (1, world):
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     import torch
     import torch.distributed as dist
     from cosmomc_amd import _native as N
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     N.require_gpu()
-    dev = local % max(1, torch.cuda.device_count())   # rehearsals may put several ranks on one GPU
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > 1 and local >= ndev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} has no GPU of its own ({ndev} visible) for RCCL")
+    dev = local % max(1, ndev)                         # gloo rehearsals may put several ranks on one GPU
     torch.cuda.set_device(dev)
     if world > 1:
         if args.dist_backend == "nccl":
@@ -588,6 +654,12 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
     W = args.walkers
+    devices = [dev]
+    if world > 1:                                      # which device each rank ran on (reported)
+        t = torch.tensor([dev], dtype=torch.int64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        devices = [int(p.item()) for p in parts]
     with tempfile.TemporaryDirectory() as td:
         smp, likes, theory, _ = build_problem(W, rank, td, args.groups, lensing=not args.no_lensing)
         lens_bytes = lensing_window_bytes(os.path.join(td, "refdata")) if not args.no_lensing else (0, 0)
@@ -672,6 +744,7 @@ def main():
                                    " + calPlanck prior + accept",
                        "walkers_per_gpu": W, "stream_groups": args.groups, "global_walkers": W * world, "nbins": N_B, "lmax": 2508,
                        "parallelism": f"walkers sharded over {world} rank(s), no per-step collective",
+                       "rank_devices": devices, "dist_backend": args.dist_backend if world > 1 else None,
                        "accept_rate": acc_rate},
             "roofline": roof,
         }

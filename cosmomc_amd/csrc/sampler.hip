@@ -1969,6 +1969,8 @@ void sampler_set_start(cmbs *s, const double *P0, hipStream_t stream) {
         for (int i = 0; i < s->np; i++) t[(size_t)i * s->W + w] = P0[(size_t)w * s->np + i];
     HIP_CHECK(hipMemcpy2DAsync(s->dc.sd + (size_t)s->dc.rows.T * s->dc.ld, (size_t)s->dc.ld * 8, t.data(),
                                (size_t)s->W * 8, (size_t)s->W * 8, s->np, hipMemcpyHostToDevice, stream));
+    // t is pageable and local: the copy must be complete before anything below can throw and unwind it
+    HIP_CHECK(hipStreamSynchronize(stream));
     eval_likes(s, stream, true, 0, s->W, s->ws.p);
     hipLaunchKernelGGL(start_kernel, dim3((s->W + 255) / 256), dim3(256), 0, stream, s->dc);
     HIP_CHECK(hipGetLastError());
