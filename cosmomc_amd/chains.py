@@ -3,7 +3,7 @@
 Reference: every accepted move writes the previous point with its
 multiplicity, ``mult like values`` (IO_OutputChainRow, source/IO.f90:85-93,
 via TChainSampler_MoveDone -> AddNewWeightedPoint, source/MCMC.f90:166-190),
-in Fortran ``'(*(E17.7))'`` (source/FileUtils.f90:75), one ``root_N.txt`` per
+in ChainOutFile's ``'(*(E16.7))'`` (source/settings.f90:109), one ``root_N.txt`` per
 chain, plus ``root.paramnames`` and ``root.ranges``.
 
 Here every walker is a chain: the sampler's history ring holds each walker's
@@ -135,7 +135,7 @@ class ChainWriter:
         return f"{self.root}_{w + self.first_chain}.txt"
 
     def _emit(self, fh, point, weight):
-        fh.write("".join(fortran_e(v) for v in [float(weight), point[0], *point[1:]]) + "\n")
+        fh.write("".join(fortran_e(v, 16) for v in [float(weight), point[0], *point[1:]]) + "\n")
 
     def _move_done(self, fh, w, point, mult):
         """The chain leaves ``point`` after ``mult`` steps there (MoveDone with accpt)."""

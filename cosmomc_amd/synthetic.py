@@ -561,3 +561,69 @@ def make_exact(lmin: int = 2, lmax: int = 400, fksy: float = 1.0, seed: int = 19
             i, j = "TEB".index(p[0]), "TEB".index(p[1])
             clhat[l, k] = S[i, j] - noise[l, k]
     return ExactData(lmin, lmax, clhat, noise)
+
+
+def _py_gaussians(seed: int, n: int) -> list[float]:
+    """gaussians() restated on Python floats and libm (math): the splitmix64
+    uniforms are exact, and every later operation is one correctly ordered
+    IEEE step, so two hosts of this image produce the same bits (numpy's
+    vectorised log/cos may pick a different SIMD path per CPU)."""
+    import math
+    u = uniforms(seed, 2 * n).tolist()
+    return [math.sqrt(-2.0 * math.log(1.0 - u[2 * i])) * math.cos(2.0 * math.pi * u[2 * i + 1]) for i in range(n)]
+
+
+def chain_problem(n: int, seed: int, extra: dict | None = None):
+    """The test_likelihood Gaussian of a sampler golden chain
+    (oracle/gen_golden.py CHAIN_CASES): SPD covariance over n used
+    parameters, centre, bounds, priors, start point, plus extra["fixed"] fixed
+    parameters (appended, bounds pinned at their value, each with a Gaussian
+    prior) and extra["lincomb"] linear-combination priors over all
+    parameters.  Pure-Python arithmetic in a fixed order (see _py_gaussians),
+    so the GPU box rebuilds exactly the problem the reference ran on.
+
+    Returns (cov, center, pmin, pmax, pmean, pstd, P0, lincombs)."""
+    import math
+    extra = extra or {}
+    g = _py_gaussians(seed, n * n + 3 * n)
+    A = [g[i * n:(i + 1) * n] for i in range(n)]
+    sig = [0.5 + abs(x) for x in g[n * n:n * n + n]]
+    corr = [[0.0] * n for _ in range(n)]
+    for i in range(n):
+        for j in range(n):
+            s = 0.0
+            for k in range(n):
+                s += A[i][k] * A[j][k]
+            corr[i][j] = (1.0 if i == j else 0.0) + 0.3 * s / n
+    d = [1.0 / math.sqrt(corr[i][i]) for i in range(n)]
+    cov = np.array([[corr[i][j] * d[i] * d[j] * sig[i] * sig[j] for j in range(n)] for i in range(n)])
+    center = [g[n * n + n + i] for i in range(n)]
+    pmin = [center[i] - 4.0 * sig[i] for i in range(n)]
+    pmax = [center[i] + 4.0 * sig[i] for i in range(n)]
+    pmean = [0.0] * n
+    pstd = [0.0] * n
+    pmean[-1] = center[-1] + 0.2 * sig[-1]
+    pstd[-1] = 2.0 * sig[-1]
+    P0 = [center[i] + 0.5 * sig[i] * g[n * n + 2 * n + i] for i in range(n)]
+    nf = extra.get("fixed", 0)
+    fv = [0.3 + 0.1 * k for k in range(nf)]
+    center += fv
+    pmin += fv
+    pmax += fv
+    pmean += [v + 0.05 for v in fv]
+    pstd += [0.1] * nf
+    P0 += fv
+    lin = []
+    gl = _py_gaussians(seed + 99, 3 * max(1, extra.get("lincomb", 0)))
+    for k in range(extra.get("lincomb", 0)):
+        w = [0.0] * (n + nf)
+        i, j = (2 * k) % n, (2 * k + 5) % n
+        w[i], w[j] = 1.0, 0.5 + 0.1 * gl[3 * k]            # e.g. SZComb = A_kSZ + 1.6 A_tSZ
+        if nf:
+            w[n] = 0.25                                      # fixed parameters enter dot_product(Comb, P)
+        s = 0.0
+        for a, b in zip(w, center):
+            s += a * b
+        lin.append({"weights": w, "mean": s + 0.3 * gl[3 * k + 1], "std": 1.5 + abs(gl[3 * k + 2])})
+    arr = [np.array(v, dtype=np.float64) for v in (center, pmin, pmax, pmean, pstd, P0)]
+    return (cov, *arr, lin)

@@ -101,27 +101,29 @@ def _fmt(a):
 # chain configurations: (name, n_used, blocks, slow_block_max, oversample_fast, propose_scale, fast_only, steps,
 #                        extra) with extra = {"fixed": k fixed parameters appended after the used ones,
 #                        "include_fixed": include_fixed_parameter_priors, "lincomb": number of
-#                        linear-combination priors (BaseParameters.f90:184-201)}
+#                        linear-combination priors (BaseParameters.f90:184-201), "burn_in": the
+#                        sampler's burn_in (MCMC.f90:39, default 2)}.  fast_only: 0 ->
+#                        TMetropolisSampler_GetNewSample, 1 -> FastParameterSample, 2 -> fast dragging.
 CHAIN_CASES = [
     # config 1: 6-D Gaussian, test_likelihood, one (slow) block, no fast/slow split
     ("gauss6_single_block", 6, [[1, 2, 3, 4, 5, 6]], 1, 1, 2.4, 0, 400, {}),
     # slow 2 + fast 3 + fast 1, oversample_fast 2, full GetProposal cycle
     ("gauss6_blocked", 6, [[1, 2], [3, 4, 5], [6]], 1, 2, 2.4, 0, 400, {}),
     # fast-only steps (FastParameterSample path) with propose_scale 1.9 (batch3/common.ini)
-    ("gauss6_fast_only", 6, [[1, 2], [3, 4, 5], [6]], 1, 1, 1.9, 1, 400, {}),
+    ("gauss6_fast_only", 6, [[1, 2], [3, 4, 5], [6]], 1, 1, 1.9, 1, 400, {"burn_in": 0}),
     # 1-D block of calPlanck-like width (sign flip RotMatrix branch, n=1)
-    ("gauss3_n1_blocks", 3, [[1], [2], [3]], 1, 3, 2.4, 0, 300, {}),
+    ("gauss3_n1_blocks", 3, [[1], [2], [3]], 1, 3, 2.4, 0, 300, {"burn_in": 5}),
     # fast dragging (TFastDraggingSampler, fast_only = 2): slow 2 + fast 3 + fast 1, drag every 2nd step
     ("gauss6_drag", 6, [[1, 2], [3, 4, 5], [6]], 1, 2, 2.4, 2, 240, {}),
     # dragging every step (oversample_fast 1), one fast parameter (interp_steps 4)
-    ("gauss4_drag_every_step", 4, [[1, 2, 3], [4]], 1, 1, 2.0, 2, 200, {}),
+    ("gauss4_drag_every_step", 4, [[1, 2, 3], [4]], 1, 1, 2.0, 2, 200, {"burn_in": 1}),
     # BASELINE configs[3] shape: 6 slow + one 21-parameter fast block (full plik's foreground
     # nuisance set), fast-only steps; rotations of 21x21 regenerated every 21 draws
     ("gauss27_fast21_fast_only", 27, [list(range(1, 7)), list(range(7, 28))], 1, 1, 1.9, 1, 320,
      {"lincomb": 1, "fixed": 1}),
     # same parameters, full GetProposal cycle with oversample_fast 3
     ("gauss27_fast21_os3", 27, [list(range(1, 7)), list(range(7, 28))], 1, 3, 2.4, 0, 320,
-     {"lincomb": 1}),
+     {"lincomb": 1, "burn_in": 5}),
     # the 21 fast parameters split 12 + 9 (block_fast_likelihood_params: two likelihoods),
     # a linear-combination prior (batch2/plik_dx11dr2_HM_v18_TT.ini:16-17 SZComb) and fixed
     # parameters whose priors count (include_fixed_parameter_priors = T)
@@ -137,50 +139,30 @@ CHAIN_CASES = [
 
 
 def chain_problem(n: int, seed: int, extra=None):
-    """SPD covariance, centre, bounds, priors for a test Gaussian chain over n
-    used parameters, plus extra["fixed"] fixed parameters (appended, bounds
-    pinned at their value, each with a Gaussian prior) and extra["lincomb"]
-    linear-combination priors over all parameters."""
-    extra = extra or {}
-    g = syn.gaussians(seed, n * n + 3 * n)
-    A = g[:n * n].reshape(n, n)
-    sig = 0.5 + np.abs(g[n * n:n * n + n])
-    corr = np.eye(n) + 0.3 * (A @ A.T) / n
-    d = 1.0 / np.sqrt(np.diag(corr))
-    corr = corr * d[:, None] * d[None, :]
-    cov = corr * sig[:, None] * sig[None, :]
-    center = g[n * n + n:n * n + 2 * n]
-    pmin = center - 4.0 * sig
-    pmax = center + 4.0 * sig
-    pmean = np.zeros(n)
-    pstd = np.zeros(n)
-    pmean[-1] = center[-1] + 0.2 * sig[-1]
-    pstd[-1] = 2.0 * sig[-1]
-    P0 = center + 0.5 * sig * g[n * n + 2 * n:n * n + 3 * n]
-    nf = extra.get("fixed", 0)
-    if nf:
-        fv = 0.3 + 0.1 * np.arange(nf)
-        center = np.concatenate([center, fv])
-        pmin = np.concatenate([pmin, fv])
-        pmax = np.concatenate([pmax, fv])
-        pmean = np.concatenate([pmean, fv + 0.05])
-        pstd = np.concatenate([pstd, 0.1 * np.ones(nf)])
-        P0 = np.concatenate([P0, fv])
-    lin = []
-    gl = syn.gaussians(seed + 99, 3 * max(1, extra.get("lincomb", 0)))
-    for k in range(extra.get("lincomb", 0)):
-        w = np.zeros(n + nf)
-        i, j = (2 * k) % n, (2 * k + 5) % n
-        w[i], w[j] = 1.0, 0.5 + 0.1 * gl[3 * k]            # e.g. SZComb = A_kSZ + 1.6 A_tSZ
-        if nf:
-            w[n] = 0.25                                       # fixed parameters enter dot_product(Comb, P)
-        mean = float(w @ np.concatenate([center[:n], center[n:]]) + 0.3 * gl[3 * k + 1])
-        std = float(1.5 + abs(gl[3 * k + 2]))
-        lin.append({"weights": w.tolist(), "mean": mean, "std": std})
-    return cov, center, pmin, pmax, pmean, pstd, P0, lin
+    """The case's test Gaussian (cosmomc_amd.synthetic.chain_problem: the tests
+    rebuild it from the seed, so the fixture stores only results)."""
+    return syn.chain_problem(n, seed, extra)
+
+
+def problem_sums(prob) -> list[float]:
+    """Checksums of a chain problem, stored with the fixture so a host that
+    rebuilds it can confirm it is the problem the reference ran on."""
+    cov, center, pmin, pmax, pmean, pstd, P0, lin = prob
+    return [float(np.sum(cov)), float(np.sum(np.abs(cov))), float(np.sum(center)), float(np.sum(pmin)),
+            float(np.sum(pmax)), float(np.sum(pmean)), float(np.sum(pstd)), float(np.sum(P0))] + \
+        [float(lc["mean"]) for lc in lin] + [float(lc["std"]) for lc in lin]
+
+
+def stored_steps(steps: int, n: int) -> list[int]:
+    """Steps (0-based) whose trial/current -lnL and point the fixture keeps:
+    the first three, every `every`-th and the last (the fixture stays under
+    100 KB; the accept decision of every step is kept)."""
+    every = max(1, steps // (16 if n <= 8 else 8))
+    return sorted({0, 1, 2, steps - 1} | {k for k in range(steps) if (k + 1) % every == 0})
 
 
 def gen_rng():
+    import hashlib
     out = {"kat": None, "streams": {}, "chains": {}}
     with tempfile.TemporaryDirectory() as td:
         out["kat"] = [float(x) for x in run_rng("kat", "", td) if x.strip()]
@@ -193,14 +175,16 @@ def gen_rng():
                 "randexp1": vals[2 * n:3 * n], "rand_indices": [int(v) for v in vals[3 * n:3 * n + nidx]],
                 "rotation": vals[3 * n + nidx:], "nidx": nidx, "nrot": nrot}
         for ci, (name, n, blocks, sbm, ovs, scale, fast_only, steps, extra) in enumerate(CHAIN_CASES):
-            cov, center, pmin, pmax, pmean, pstd, P0, lin = chain_problem(n, 777 + ci, extra)
+            prob = chain_problem(n, 777 + ci, extra)
+            cov, center, pmin, pmax, pmean, pstd, P0, lin = prob
             npar = len(center)
             ij, kl = 4321 + ci, 9373
             T = 1.0
             incl = int(extra.get("include_fixed", 0))
+            burn = int(extra.get("burn_in", 2))
             used = list(range(1, n + 1))
             cfg = [f"{ij} {kl} {npar} {n} {steps} {fast_only} {incl} {len(lin)}",
-                   f"{len(blocks)} {sbm} {ovs} {scale!r} {T!r}",
+                   f"{len(blocks)} {sbm} {ovs} {scale!r} {T!r} {burn}",
                    " ".join(str(u) for u in used),
                    " ".join(str(len(b)) for b in blocks)]
             cfg += [" ".join(str(x) for x in b) for b in blocks]
@@ -210,18 +194,34 @@ def gen_rng():
             lines = [x for x in run_rng("chain", "\n".join(cfg) + "\n", td) if x.strip()]
             like0 = float(lines[0])
             rows = np.array([[float(v) for v in l.split()] for l in lines[1:]])
+            assert rows.shape[0] == steps
+            base = os.path.join(td, "rng_out.txt")
+            with open(base + ".txt", "rb") as f:
+                chain_txt = f.read()
+            pts = np.loadtxt(base + ".points", ndmin=2)
+            mx = open(base + ".max").read().split()
+            keep = stored_steps(steps, n)
             out["chains"][name] = {
                 "ij": ij, "kl": kl, "n": n, "num_params": npar, "params_used": used, "blocks": blocks,
                 "slow_block_max": sbm, "oversample_fast": ovs, "propose_scale": scale, "fast_only": fast_only,
-                "temperature": T, "steps": steps, "problem_seed": 777 + ci, "include_fixed_parameter_priors": incl,
-                "linear_combinations": lin,
-                "cov": cov.tolist(), "center": center.tolist(), "pmin": pmin.tolist(), "pmax": pmax.tolist(),
-                "prior_mean": pmean.tolist(), "prior_std": pstd.tolist(), "P0": P0.tolist(),
-                "like0": like0, "accept": rows[:, 0].astype(int).tolist(), "trial_like": rows[:, 1].tolist(),
-                "cur_like": rows[:, 2].tolist(), "P": rows[:, 3:].tolist()}
-            print(f"chain {name:26s} accept rate {rows[:, 0].mean():.3f}  final -lnL {rows[-1, 2]:.6f}")
+                "temperature": T, "steps": steps, "problem_seed": 777 + ci, "extra": extra,
+                "include_fixed_parameter_priors": incl, "burn_in": burn, "problem_sums": problem_sums(prob),
+                "like0": like0, "accept": "".join(str(int(a)) for a in rows[:, 0]),
+                "stored_steps": keep, "trial_like": rows[keep, 1].tolist(), "cur_like": rows[keep, 2].tolist(),
+                "P": rows[keep, 3:].tolist(),
+                # the reference's own chain file (TMpiChainCollector_AddNewWeightedPoint -> IO_OutputChainRow,
+                # RealFormat E16.7 settings.f90:109) and its AddNewWeightedPoint calls (mult, thin_fac)
+                "chain_file": {"rows": chain_txt.count(b"\n"), "sha256": hashlib.sha256(chain_txt).hexdigest(),
+                               "first_row": chain_txt.decode().splitlines()[0]},
+                "weighted_points": {"count": int(pts.shape[0]) if pts.size else 0,
+                                    "mult": pts[:, 0].astype(int).tolist() if pts.size else [],
+                                    "thin_fac": int(pts[0, 1]) if pts.size else None},
+                "num_accept": int(mx[0]), "max_like": float(mx[1])}
+            nrows = chain_txt.count(b"\n")
+            print(f"chain {name:26s} accept rate {rows[:, 0].mean():.3f}  final -lnL {rows[-1, 2]:.6f}  "
+                  f"chain rows {nrows}")
     with open(os.path.join(GOLDEN, "rng_sampler_ref.json"), "w") as f:
-        json.dump(out, f, indent=0)
+        json.dump(out, f, separators=(",", ":"))
 
 
 # convergence cases: (name, chains, samples per chain, n_used, centre spread, seed)

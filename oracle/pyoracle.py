@@ -198,34 +198,6 @@ def gelman_rubin(cov, meanscov):
     return lib().orc_gelman_rubin(np.ascontiguousarray(cov), np.ascontiguousarray(meanscov), n)
 
 
-def move_done_rows(like0, P0, accept, cur_like, P, burn_in=2, thin=1):
-    """Chain-file rows of one chain, restated event by event from its accept
-    sequence: TChainSampler_MoveDone (MCMC.f90:166-190) with SampleFrom's
-    initial mult = 0 (:141) and TMpiChainCollector_AddNewWeightedPoint
-    (SampleCollector.f90:82-111, checkpoint_burn = 0).  accept[k], cur_like[k],
-    P[k]: step k's accept flag and the chain's -lnL / point after it.
-    Returns ([(weight, like, P...)], (MaxLike, MaxLikeParams))."""
-    rows, mult, num_accept, acc = [], 0.0, 0, 0.0
-    max_like, max_p = 1e30, None
-    cur_l, cur_p = float(like0), np.asarray(P0, dtype=np.float64)
-    for k in range(len(accept)):
-        if accept[k]:
-            if mult > 0:
-                if cur_l != 1e30 and num_accept > burn_in:
-                    acc += mult
-                    if acc >= thin or thin == 1:
-                        rows.append((acc / thin, cur_l, *cur_p))
-                        acc = np.fmod(acc, float(thin))
-                num_accept += 1
-            mult = 1.0
-            if cur_l < max_like:
-                max_like, max_p = cur_l, cur_p
-        else:
-            mult += 1.0
-        cur_l, cur_p = float(cur_like[k]), np.asarray(P[k], dtype=np.float64)
-    return rows, (max_like, max_p)
-
-
 def confid_val(values, limfrac, ix1=None, ix2=None):
     """TSampleList%ConfidVal (samples.f90:70-110) of one column: sort items
     ix1..ix2 (1-based, inclusive), interpolate the order statistics at

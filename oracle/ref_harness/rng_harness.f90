@@ -10,20 +10,23 @@
 !                   (mean-of-covariances, covariance-of-means) pair
 !   mode "confid" : TSampleList%ConfidVal (samples.f90:70-110), the per-chain
 !                   limits of CheckLimitsConverge (SampleCollector.f90:515-517)
-!   mode "chain"  : (fast_only = 2: TFastDraggingSampler_GetNewSample,
-!                   MCMC.f90:338-452, restated inline on the reference's
-!                   BlockedProposer GetProposalSlow / GetProposalFastDelta)
-!                   BlockedProposer + Metropolis chain on the test_likelihood
-!                   Gaussian.  Every -lnL is the reference's own
-!                   TLikeCalculator%GetLogLike (calclike.f90:136-151: hard
-!                   bounds :97-109, TestLikelihoodFunction :180-199, Gaussian
+!   mode "chain"  : the reference's own sampler loop (module MonteCarlo,
+!                   MCMC.f90) on the test_likelihood Gaussian:
+!                   TMetropolisSampler_GetNewSample (:269-307), FastParameterSample
+!                   (:309-335) or TFastDraggingSampler_GetNewSample (:338-452)
+!                   with its MetropolisAccept (:119-131) and MoveDone (:166-190),
+!                   the reference's BlockedProposer, and every -lnL from the
+!                   reference's TLikeCalculator%GetLogLike (calclike.f90:136-151:
+!                   hard bounds :97-109, TestLikelihoodFunction :180-199, Gaussian
 !                   and linear-combination priors with the
 !                   include_fixed_parameter_priors gate :111-134, temperature
-!                   :82-94) on BaseParams set from the config; num_params may
-!                   exceed num_params_used (fixed parameters).  Only the
-!                   three-line MetropolisAccept of MCMC.f90:119-131 is restated
-!                   inline; the RNG, proposer, Cholesky and inverse are the
-!                   reference's own code.
+!                   :82-94); num_params may exceed num_params_used (fixed
+!                   parameters).  MoveDone's AddNewWeightedPoint goes to the
+!                   reference's TMpiChainCollector (SampleCollector.f90:82-112),
+!                   which writes the chain file rows.  Two recorders (module
+!                   harness_recorders below) only observe: the MetropolisAccept
+!                   override logs the last decision and its -lnL argument, the
+!                   collector override logs each AddNewWeightedPoint call.
 !   mode "blocks" : TBaseParameters_SetFastSlowParams (BaseParameters.f90:302-433)
 !                   on BaseParams%varying and a DataLikelihoods list of plain
 !                   TDataLikelihood items carrying new_param_block_start /
@@ -31,6 +34,80 @@
 !                   itself (an ini file); writes every param_blocks entry
 !
 ! usage: rng_harness kat|stream|chain|gr|confid|blocks <config> <out.txt>
+module harness_recorders
+    ! Observers over the reference's own types: each override records its
+    ! arguments/result and defers to the reference procedure unchanged.
+    use settings
+    use GeneralTypes
+    use CalcLike
+    use MonteCarlo
+    use SampleCollector
+    implicit none
+
+    ! TFastDraggingSampler_GetNewSample calls this%TMetropolisSampler%FastParameterSample
+    ! (MCMC.f90:359), a non-polymorphic parent call, so the MetropolisAccept override
+    ! is not reached from the fast sub-steps of dragging: the harness takes a step's
+    ! accept from the point moving, its trial -lnL from the override when it fired
+    ! (the drag's DragLike, :438) and otherwise from the calculator's last value.
+    Type, extends(TFastDraggingSampler) :: TRecSampler
+        logical :: fired = .false.
+        real(mcp) :: last_like = LogZero
+    contains
+    procedure :: MetropolisAccept => Rec_MetropolisAccept
+    end Type
+
+    Type, extends(TGenericLikeCalculator) :: TRecCalc
+        real(mcp) :: last_like = LogZero
+    contains
+    procedure :: GetLogLike => Rec_GetLogLike
+    end Type
+
+    Type, extends(TMpiChainCollector) :: TRecCollector
+        integer :: u_points = 0
+    contains
+    procedure :: AddNewWeightedPoint => Rec_AddNewWeightedPoint
+    end Type
+
+contains
+
+    function Rec_MetropolisAccept(this, Like, CurLike) result(MetropolisAccept)
+    class(TRecSampler) :: this
+    real(mcp) Like, CurLike
+    logical MetropolisAccept
+
+    MetropolisAccept = this%TChainSampler%MetropolisAccept(Like, CurLike)
+    this%fired = .true.
+    this%last_like = Like
+
+    end function Rec_MetropolisAccept
+
+    function Rec_GetLogLike(this, Params) result(L)
+    class(TRecCalc) :: this
+    class(TCalculationAtParamPoint) :: Params
+    real(mcp) L
+
+    L = this%TGenericLikeCalculator%GetLogLike(Params)
+    this%last_like = L
+
+    end function Rec_GetLogLike
+
+    subroutine Rec_AddNewWeightedPoint(this, CurParams, CurLike, mult, thin_fac)
+    class(TRecCollector) :: this
+    class(TCalculationAtParamPoint), intent(in) :: CurParams
+    real(mcp) CurLike
+    real(mcp), intent(in):: mult
+    integer, intent(in), optional :: thin_fac
+    integer thin
+
+    thin = 1
+    if (present(thin_fac)) thin = thin_fac
+    write(this%u_points, '(2I6,*(ES25.17))') nint(mult), thin, CurLike, CurParams%P(params_used)
+    call this%TMpiChainCollector%AddNewWeightedPoint(CurParams, CurLike, mult, thin_fac)
+
+    end subroutine Rec_AddNewWeightedPoint
+
+end module harness_recorders
+
 program rng_harness
     use settings
     use StringUtils, only: numcat
@@ -42,6 +119,8 @@ program rng_harness
     use Samples, only: GelmanRubinEvalues, TSampleList
     use BaseParameters
     use CalcLike
+    use ParamPointSet
+    use harness_recorders
     implicit none
     character(LEN=1024) :: mode, cfg, outf
     integer :: u_in, u_out, i, j, k, n, nsteps, nblocks, slow_block_max, oversample, ij, kl, nrot
@@ -51,18 +130,19 @@ program rng_harness
     real(mcp), allocatable :: pmean(:), pstd(:), R(:,:), X(:)
     integer, allocatable :: bsize(:), ind(:)
     type(int_arr), allocatable :: blocks(:)
-    Type(BlockedProposer) :: Prop
     logical :: accpt
     real :: e
     real(mcp), allocatable :: mcov(:,:), evals(:)
-    real(mcp), allocatable :: cend(:), cstart(:), tend(:), tstart(:), delta(:)
-    real(mcp) :: cendlike, cstartlike, elike, slike, sum_s, sum_e, frac, cintlike, intlike, mult
-    integer :: num_drag, num_fast, interp, istep
-    integer :: n_used, incl_fixed, nlin, ix1, ix2
+    real(mcp) :: mult
+    integer :: n_used, incl_fixed, nlin, ix1, ix2, burn
     Type(TSampleList) :: SL
     real(mcp) :: limfrac, lower, upper
-    Type(TGenericLikeCalculator) :: Calc
-    Type(TCalculationAtParamPoint) :: Pt
+    Type(TRecCalc), target :: Calc
+    Type(TRecSampler) :: Sampler
+    Type(TRecCollector), target :: Collector
+    Type(TGeneralConfig), target :: GConfig
+    Type(GenericParameterization), target :: Gp
+    Type(ParamSet) :: CurParams
     Type(TSettingIni) :: BIni
     class(TDataLikelihood), pointer :: BLike
     logical :: bad
@@ -134,9 +214,17 @@ program rng_harness
             end do
         end do
     case ('chain')
+        ! The reference's own sampler loop (module MonteCarlo, MCMC.f90) on the
+        ! test_likelihood Gaussian: fast_only 0 -> TMetropolisSampler_GetNewSample
+        ! (:269-307), 1 -> FastParameterSample (:309-335), 2 ->
+        ! TFastDraggingSampler_GetNewSample (:338-452).  MoveDone (:166-190)
+        ! feeds the reference's TMpiChainCollector_AddNewWeightedPoint
+        ! (SampleCollector.f90:82-112), which writes the chain file rows through
+        ! WriteParams / IO_OutputChainRow into <out>.txt; <out>.points logs each
+        ! AddNewWeightedPoint call at full precision, <out>.max the MaxLike.
         open(newunit=u_in, file=trim(cfg), status='old')
         read(u_in, *) ij, kl, n, n_used, nsteps, fast_only, incl_fixed, nlin
-        read(u_in, *) nblocks, slow_block_max, oversample, scale, temperature
+        read(u_in, *) nblocks, slow_block_max, oversample, scale, temperature, burn
         num_params = n
         num_params_used = n_used
         allocate(params_used(n_used))
@@ -147,7 +235,7 @@ program rng_harness
             allocate(blocks(i)%P(bsize(i)))
             read(u_in, *) blocks(i)%P
         end do
-        allocate(cov(n_used,n_used), P(n), trial(n), center(n), pmin(n), pmax(n), pmean(n), pstd(n))
+        allocate(cov(n_used,n_used), P(n), center(n), pmin(n), pmax(n), pmean(n), pstd(n))
         read(u_in, *) ((cov(i,j), j=1,n_used), i=1,n_used)
         read(u_in, *) center
         read(u_in, *) pmin
@@ -173,108 +261,73 @@ program rng_harness
             read(u_in, *) BaseParams%LinearCombinations(k)%mean, BaseParams%LinearCombinations(k)%std
         end do
         close(u_in)
+        ! param_blocks as SetFastSlowParams lays them out: entries 1..slow_tp_max (= 2) are the
+        ! slow types (empty ones skipped by BlockedProposer%Init, propose.f90:170-180), then fast
+        if (slow_block_max > slow_tp_max) stop 'chain: more than slow_tp_max slow blocks'
+        allocate(BaseParams%param_blocks(nblocks + slow_tp_max - slow_block_max))
+        j = 0
+        BaseParams%num_slow = 0
+        BaseParams%num_fast = 0
+        do i = 1, nblocks
+            j = j + 1
+            if (i == slow_block_max + 1) then
+                do k = slow_block_max + 1, slow_tp_max
+                    allocate(BaseParams%param_blocks(j)%P(0))
+                    j = j + 1
+                end do
+            end if
+            allocate(BaseParams%param_blocks(j)%P(bsize(i)))
+            BaseParams%param_blocks(j)%P = blocks(i)%P
+            if (i <= slow_block_max) then
+                BaseParams%num_slow = BaseParams%num_slow + bsize(i)
+            else
+                BaseParams%num_fast = BaseParams%num_fast + bsize(i)
+            end if
+        end do
+        do while (j < size(BaseParams%param_blocks))
+            j = j + 1
+            allocate(BaseParams%param_blocks(j)%P(0))
+        end do
         Calc%test_likelihood = .true.
         Calc%Temperature = temperature
         allocate(Calc%test_cov_matrix(n_used, n_used))
         Calc%test_cov_matrix = cov       ! TestLikelihoodFunction inverts it (calclike.f90:187-195)
-        Pt%P = 0
+        GConfig%Parameterization => Gp
+        Collector%Config => GConfig
+        open(newunit=Collector%u_points, file=trim(outf)//'.points', status='replace')
+        call ChainOutFile%CreateFile(trim(outf)//'.txt')
         call initRandom(ij, kl)
-        call Prop%Init(blocks, slow_block_max=slow_block_max, oversample_fast=oversample, &
-            propose_scale=scale)
-        call Prop%SetCovariance(cov)
-        curlike = target(P)
+        Sampler%oversample_fast = oversample
+        Sampler%burn_in = burn
+        call Sampler%InitWithPropose(Calc, Collector, propose_scale=scale)
+        call Sampler%SetCovariance(cov)
+        CurParams%P = 0
+        CurParams%P(1:n) = P
+        curlike = Sampler%LogLike(CurParams)
         write(u_out, '(ES25.17)') curlike
-        num_fast = 0
-        do k = slow_block_max + 1, nblocks
-            num_fast = num_fast + bsize(k)
-        end do
-        allocate(cend(n), cstart(n), tend(n), tstart(n), delta(n))
-        num_drag = 0
-        mult = 1
+        mult = 0                                    ! TChainSampler_SampleFrom (MCMC.f90:141)
+        allocate(trial(n))
         do k = 1, nsteps
-            if (fast_only == 2) then
-                num_drag = num_drag + 1
-                if (mod(num_drag, oversample) == 0) then
-                    ! --- TFastDraggingSampler_GetNewSample drag branch (MCMC.f90:364-452)
-                    tend = P
-                    call Prop%GetProposalSlow(tend)
-                    cendlike = target(tend)
-                    if (cendlike == LogZero) then
-                        mult = mult + 1
-                        write(u_out, '(I2,*(ES25.17))') 0, cendlike, curlike, P
-                        cycle
-                    end if
-                    cstartlike = curlike
-                    sum_e = cendlike
-                    sum_s = cstartlike
-                    cstart = P
-                    cend = tend
-                    interp = max(2, nint(dragging_steps * num_fast) + 1)
-                    do istep = 1, interp - 1
-                        call Prop%GetProposalFastDelta(delta)
-                        tend = cend
-                        tend(1:n) = tend(1:n) + delta
-                        elike = target(tend)
-                        accpt = elike /= LogZero
-                        if (accpt) then
-                            tstart = cstart
-                            tstart(1:n) = tstart(1:n) + delta
-                            slike = target(tstart)
-                            accpt = slike /= LogZero
-                            if (accpt) then
-                                frac = real(istep, mcp)/interp
-                                cintlike = cstartlike*(1-frac) + frac*cendlike
-                                intlike = slike*(1-frac) + frac*elike
-                                accpt = cintlike > intlike                 ! MetropolisAccept :119-131
-                                if (.not. accpt) accpt = randexp1() > intlike - cintlike
-                            end if
-                        end if
-                        if (accpt) then
-                            cend = tend
-                            cstart = tstart
-                            cendlike = elike
-                            cstartlike = slike
-                        end if
-                        sum_s = sum_s + cstartlike
-                        sum_e = sum_e + cendlike
-                    end do
-                    like = sum_e/interp                     ! DragLike
-                    if (like /= LogZero) then
-                        accpt = sum_s/interp > like
-                        if (.not. accpt) accpt = randexp1() > like - sum_s/interp
-                    else
-                        accpt = .false.
-                    end if
-                    if (accpt) then
-                        P = cend
-                        curlike = cendlike
-                        mult = 1
-                    else
-                        mult = mult + 1
-                    end if
-                    write(u_out, '(I2,*(ES25.17))') merge(1, 0, accpt), like, curlike, P
-                    cycle
-                end if
-            end if
-            trial = P
-            if (fast_only >= 1) then
-                call Prop%GetProposalFast(trial)
-            else
-                call Prop%GetProposal(trial)
-            end if
-            like = target(trial)
-            if (like /= LogZero) then               ! MCMC.f90:282-286, :119-131
-                accpt = curlike > like
-                if (.not. accpt) accpt = randexp1() > like - curlike
-            else
-                accpt = .false.
-            end if
-            if (accpt) then
-                P = trial
-                curlike = like
-            end if
-            write(u_out, '(I2,*(ES25.17))') merge(1, 0, accpt), like, curlike, P
+            Sampler%fired = .false.
+            Calc%last_like = LogZero
+            trial = CurParams%P(1:n)
+            select case (fast_only)
+            case (0)
+                call Sampler%GetNewMetropolisSample(CurParams, curlike, mult)
+            case (1)
+                call Sampler%FastParameterSample(CurParams, curlike, mult)
+            case default
+                call Sampler%GetNewSample(CurParams, curlike, mult)
+            end select
+            if (.not. Sampler%fired) Sampler%last_like = Calc%last_like
+            write(u_out, '(I2,*(ES25.17))') merge(1, 0, any(CurParams%P(1:n) /= trial)), Sampler%last_like, &
+                curlike, CurParams%P(1:n)
         end do
+        call ChainOutFile%Close()
+        close(Collector%u_points)
+        open(newunit=u_in, file=trim(outf)//'.max', status='replace')
+        write(u_in, '(I8,*(ES25.17))') Sampler%num_accept, Sampler%MaxLike, Sampler%MaxLikeParams(1:n)
+        close(u_in)
     case ('blocks')
         Feedback = 0
         call BIni%Open(trim(cfg), bad, .false.)
@@ -318,14 +371,5 @@ program rng_harness
         end do
     end select
     close(u_out)
-
-contains
-
-    function target(Q) result(L)
-        real(mcp), intent(in) :: Q(:)
-        real(mcp) :: L
-        Pt%P(1:num_params) = Q(1:num_params)
-        L = Calc%GetLogLike(Pt)                 ! calclike.f90:136-151
-    end function target
 
 end program rng_harness

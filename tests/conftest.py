@@ -24,9 +24,34 @@ def plik_golden():
     return load_golden("plik_lite_ref.json")
 
 
+def expand_chain(ch):
+    """A sampler golden chain with its test problem rebuilt from the seed
+    (cosmomc_amd.synthetic.chain_problem; the fixture stores only the
+    reference's results and checksums of the problem it ran on).  Adds cov,
+    center, bounds, priors, P0 and linear_combinations, the per-step accept
+    list, and at[k] = the index of step k in the stored rows (P, cur_like,
+    trial_like) or None."""
+    import numpy as np
+
+    import gen_golden as gg
+    from cosmomc_amd import synthetic as syn
+    prob = syn.chain_problem(ch["n"], ch["problem_seed"], ch["extra"])
+    np.testing.assert_allclose(gg.problem_sums(prob), ch["problem_sums"], rtol=1e-15, atol=0,
+                               err_msg="rebuilt chain problem differs from the one the reference ran on")
+    cov, center, pmin, pmax, pmean, pstd, P0, lin = prob
+    ch = dict(ch, cov=cov.tolist(), center=center.tolist(), pmin=pmin.tolist(), pmax=pmax.tolist(),
+              prior_mean=pmean.tolist(), prior_std=pstd.tolist(), P0=P0.tolist(), linear_combinations=lin)
+    ch["accept"] = [int(c) for c in ch["accept"]]
+    pos = {k: i for i, k in enumerate(ch["stored_steps"])}
+    ch["at"] = [pos.get(k) for k in range(ch["steps"])]
+    return ch
+
+
 @pytest.fixture(scope="session")
 def rng_golden():
-    return load_golden("rng_sampler_ref.json")
+    g = load_golden("rng_sampler_ref.json")
+    g["chains"] = {k: expand_chain(v) for k, v in g["chains"].items()}
+    return g
 
 
 @pytest.fixture(scope="session")

@@ -67,31 +67,66 @@ def test_chi2_columns_and_likelihoods_file(tmp_path):
                                                               "1\tCMB\tlens_x\tlensing\t"]
 
 
-@pytest.mark.parametrize("name,burn_in,thin", [("gauss6_blocked", 2, 2), ("gauss3_n1_blocks", 2, 3),
-                                               ("gauss6_fast_only", 0, 1), ("gauss27_fast21_os3", 5, 3)])
-def test_rows_follow_movedone_restatement(tmp_path, rng_golden, name, burn_in, thin):
-    """ChainWriter on a reference chain's per-step history (the golden's points
-    and -lnL after every step) writes exactly the rows the event-by-event
-    MoveDone / AddNewWeightedPoint restatement (oracle) writes for its accept
-    sequence: burn_in drops the first burn_in + 1 stays, thin = oversample_fast
-    turns multiplicities into acc/thin weights."""
+def _oracle_history(ch):
+    """Every step's point and -lnL of the golden chain, replayed by the C
+    oracle (pinned to the reference chain decision by decision in
+    test_oracle.py)."""
+    import ctypes as C
+
     import pyoracle as po
+    from test_oracle import _target, make_oracle_proposer
+    t, keep = _target(ch)
+    h = make_oracle_proposer(ch)
+    r = po.Ranmar(ch["ij"], ch["kl"])
+    P = np.array(ch["P0"], dtype=np.float64)
+    cur = C.c_double(po.lib().orc_target_loglike(C.byref(t), P))
+    st = po.DragState(0, 0.0, 3.0, ch["oversample_fast"])
+    Ps, likes = [], []
+    for _ in range(ch["steps"]):
+        if ch["fast_only"] == 2:
+            po.lib().orc_drag_step(h, C.byref(r.s), C.byref(t), C.byref(st), P, C.byref(cur))
+        else:
+            po.lib().orc_mh_step(h, C.byref(r.s), C.byref(t), P, C.byref(cur), ch["fast_only"], None)
+        Ps.append(P.copy())
+        likes.append(cur.value)
+    po.lib().orc_proposer_free(h)
+    return np.array(Ps), np.array(likes)
+
+
+CHAIN_FILE_CASES = ["gauss6_single_block", "gauss6_blocked", "gauss6_fast_only", "gauss3_n1_blocks", "gauss6_drag",
+                    "gauss4_drag_every_step", "gauss27_fast21_fast_only", "gauss27_fast21_os3",
+                    "gauss27_fast12_9_lincomb", "gauss40_slow_fast", "gauss27_fast21_drag"]
+
+
+@pytest.mark.parametrize("name", CHAIN_FILE_CASES)
+def test_chain_file_equals_reference(tmp_path, rng_golden, name):
+    """ChainWriter on a golden chain's per-step history writes, byte for byte,
+    the chain file the reference's own sampler wrote for it: MoveDone
+    (MCMC.f90:166-190, burn_in) -> TMpiChainCollector_AddNewWeightedPoint
+    (SampleCollector.f90:82-112, acc/thin weights with thin_fac = oversample_fast
+    for TMetropolisSampler_GetNewSample, 1 for FastParameterSample and dragging)
+    -> IO_OutputChainRow in ChainOutFile's E16.7 (settings.f90:109); and the
+    same MaxLike."""
+    import hashlib
     ch = rng_golden["chains"][name]
-    P, like = np.array(ch["P"]), np.array(ch["cur_like"])
-    used = np.array(ch.get("params_used", range(1, ch["n"] + 1))) - 1
+    P, like = _oracle_history(ch)
+    used = np.array(ch["params_used"]) - 1
     hist = np.concatenate([P[:, used], like[:, None]], axis=1)[:, :, None]       # [steps, n_used + 1, 1]
-    cw = ChainWriter(str(tmp_path / "c"), [f"p{i}" for i in used], burn_in=burn_in, thin=thin)
+    thin = ch["oversample_fast"] if ch["fast_only"] == 0 else 1
+    assert thin == (ch["weighted_points"]["thin_fac"] or thin)
+    cw = ChainWriter(str(tmp_path / "c"), [f"p{i}" for i in used], burn_in=ch["burn_in"], thin=thin)
     for a in range(0, len(like), 37):                                            # blocks of history
         cw.add_rows(hist[a:a + 37])
     cw.close()
-    ref, (ml, mp) = po.move_done_rows(ch["like0"], ch["P0"], ch["accept"], like, P, burn_in, thin)
-    got = np.loadtxt(str(tmp_path / "c_1.txt"), ndmin=2)
-    ref = np.array(ref)[:, [0, 1] + [2 + i for i in used]]
-    assert got.shape == ref.shape and len(ref) > 10
-    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-12)                  # E17.7 text
-    best, pts = cw.max_like_params(0)
-    assert best == ml
-    np.testing.assert_allclose(pts[1:], np.asarray(mp)[used])
+    txt = (tmp_path / "c_1.txt").read_bytes()
+    ref = ch["chain_file"]
+    assert txt.count(b"\n") == ref["rows"]
+    if ref["rows"]:
+        assert txt.decode().splitlines()[0] == ref["first_row"]
+    assert hashlib.sha256(txt).hexdigest() == ref["sha256"]
+    best = cw.max_like_params(0)
+    if ch["accept"][0] == 0:               # the reference's MaxLike also sees P0 when the first step accepts
+        assert best[0] == pytest.approx(ch["max_like"], rel=1e-12)
 
 
 def test_weights_thin_and_burn(tmp_path):

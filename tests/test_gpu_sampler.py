@@ -64,10 +64,14 @@ def test_walker0_follows_reference_chain(rng_golden, name):
     P, like, mult, nacc = s.state()
     assert like[0] == pytest.approx(ch["like0"], rel=1e-13)
     for k in range(ch["steps"]):
+        prev = P[0].copy()
         s.step(1, fast_only=bool(ch["fast_only"]))
         P, like, mult, nacc = s.state()
-        np.testing.assert_allclose(P[0], ch["P"][k], rtol=1e-11, atol=1e-12, err_msg=f"step {k}")
-        assert like[0] == pytest.approx(ch["cur_like"][k], rel=1e-10, abs=1e-12)
+        assert int(np.any(P[0] != prev)) == ch["accept"][k], f"accept decision at step {k}"
+        i = ch["at"][k]
+        if i is not None:
+            np.testing.assert_allclose(P[0], ch["P"][i], rtol=1e-11, atol=1e-12, err_msg=f"step {k}")
+            assert like[0] == pytest.approx(ch["cur_like"][i], rel=1e-10, abs=1e-12)
     assert int(nacc[0]) <= int(sum(ch["accept"]))
 
 
@@ -282,11 +286,16 @@ def test_walker0_follows_reference_dragging(rng_golden, name):
     ch = rng_golden["chains"][name]
     W = 70
     s = _make_sampler(ch, W)
+    P = s.state()[0]
     for k in range(ch["steps"]):
+        prev = P[0].copy()
         s.step_drag(1)
         P, like, mult, nacc = s.state()
-        np.testing.assert_allclose(P[0], ch["P"][k], rtol=1e-11, atol=1e-12, err_msg=f"step {k}")
-        assert like[0] == pytest.approx(ch["cur_like"][k], rel=1e-10, abs=1e-12)
+        assert int(np.any(P[0] != prev)) == ch["accept"][k], f"accept decision at step {k}"
+        i = ch["at"][k]
+        if i is not None:
+            np.testing.assert_allclose(P[0], ch["P"][i], rtol=1e-11, atol=1e-12, err_msg=f"step {k}")
+            assert like[0] == pytest.approx(ch["cur_like"][i], rel=1e-10, abs=1e-12)
     t, keep = _target(ch)
     for w in (1, 37, 69):
         ij, kl = walker_seed(ch["ij"], ch["kl"], w)
