@@ -32,16 +32,19 @@ VERSION = 1
 
 
 def write_checkpoint(root: str, sampler, propose_cov, chains=None, exchange=None, collector: dict | None = None,
-                     history: bool = True) -> str:
+                     history: bool = True, chain_collector=None) -> str:
     """Write ``root.chk`` atomically.  ``propose_cov``: the proposal covariance
     in force (n_used x n_used); ``collector``: any extra JSON-able run state
-    (sample counters, MaxLike, burn-in flags ...)."""
+    (sample counters, MaxLike, burn-in flags ...); ``chain_collector``: a
+    converge.ChainCollector whose host state is saved beside the device
+    Samples lists of the image."""
     image = sampler.save_state()
     meta = {"W": sampler.W, "np": sampler.np, "params_used": list(sampler.params_used),
             "propose_cov": np.asarray(propose_cov, dtype=np.float64).tolist(),
             "collector": collector or {},
             "flukecheck": bool(exchange.flukecheck) if exchange is not None else False,
-            "chains": chains.checkpoint_state(sampler.W) if chains is not None else None}
+            "chains": chains.checkpoint_state(sampler.W) if chains is not None else None,
+            "chain_collector": chain_collector.checkpoint_state() if chain_collector is not None else None}
     hist = b""
     if history and getattr(sampler, "_hist_cap", 0):
         count = sampler.history_count()
@@ -63,9 +66,12 @@ def write_checkpoint(root: str, sampler, propose_cov, chains=None, exchange=None
     return root + ".chk"
 
 
-def read_checkpoint(root: str, sampler, chains=None, exchange=None, theory_fn=None) -> dict:
+def read_checkpoint(root: str, sampler, chains=None, exchange=None, theory_fn=None, chain_collector=None) -> dict:
     """Resume ``sampler`` (same configuration and likelihoods as the run that
     wrote the file) from ``root.chk``; returns the ``collector`` dict.
+    chain_collector: a converge.ChainCollector built on ``sampler`` for the
+    resumed run before this call (the image carries its device Samples lists
+    and load_state checks the capacity); its host state is restored.
     theory_fn: when the run moved slow parameters (step_theory / step_drag),
     the theory at the restored points is recomputed with it
     (BatchedMCMC.refresh_theory); without it stepping fails loudly."""
@@ -106,6 +112,10 @@ def read_checkpoint(root: str, sampler, chains=None, exchange=None, theory_fn=No
         chains.restore(meta["chains"], sampler.W)
     if exchange is not None:
         exchange.flukecheck = meta["flukecheck"]
+    if chain_collector is not None:
+        if meta.get("chain_collector") is None:
+            raise ValueError(f"{root}.chk holds no ChainCollector state")
+        chain_collector.restore(meta["chain_collector"])
     if theory_fn is not None:
         sampler.refresh_theory(theory_fn)
     return meta["collector"]

@@ -191,7 +191,7 @@ class ChainCollector:
 
     def __init__(self, sampler, settings: CollectorSettings | None = None, num_slow: int = 0, num_fast: int = 0,
                  dragging: bool = False, oversample_fast: int = 1, output_thin: int | None = None, group=None,
-                 sample_capacity: int | None = None, thin_limit: int = 500000, root: str | None = None):
+                 sample_capacity: int | None = None, thin_limit: int | None = None, root: str | None = None):
         self.s = sampler
         self.settings = settings or CollectorSettings()
         self.n = len(sampler.params_used)
@@ -200,9 +200,12 @@ class ChainCollector:
         self.oversample_fast = max(1, oversample_fast)
         self.output_thin = output_thin if output_thin is not None else (1 if dragging else self.oversample_fast)
         self.group = group
-        self.thin_limit = thin_limit
         self.root = root
         cap = sample_capacity or getattr(sampler, "_hist_cap", 0)
+        # Samples%Thin(2) once a list passes the reference's 500000 (SampleCollector.f90:300-304), or half
+        # the list capacity when that is smaller, so a long run thins and goes on instead of overflowing.
+        # The items are history steps: the ring must still hold the second half of each list's window.
+        self.thin_limit = min(500000, max(1, cap // 2)) if thin_limit is None else thin_limit
         sampler.collector_enable(cap)
         self.cap = cap
         self.min_update = self.settings.MPI_Min_Sample_Update
@@ -224,6 +227,28 @@ class ChainCollector:
         import torch.distributed as dist
         self._world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self._rank = dist.get_rank(group) if self._world > 1 else 0
+
+    _STATE = ("next_step", "burn0", "all_burn", "waiting", "done", "count0", "min_count", "update_freq",
+              "min_update")
+
+    def checkpoint_state(self) -> dict:
+        """The host side of the collector a resume needs (the Samples lists
+        themselves are in the sampler's device image): the next history step
+        to add, walker 0's burn-in and trigger state, all_burn, the update
+        frequency and MPI_Min_Sample_Update in force and flukecheck -- the
+        pieces TMpiChainCollector_SaveState writes (SampleCollector.f90:139-151)."""
+        st = {k: getattr(self, k) for k in self._STATE}
+        st["flukecheck"] = bool(self.exchange.flukecheck)
+        st["cap"] = self.cap
+        return st
+
+    def restore(self, state: dict):
+        """Undo checkpoint_state (TMpiChainCollector_ReadState, :153-172)."""
+        if int(state.get("cap", self.cap)) != self.cap:
+            raise ValueError(f"checkpointed collector capacity {state['cap']} != {self.cap}")
+        for k in self._STATE:
+            setattr(self, k, type(getattr(self, k))(state[k]))
+        self.exchange.flukecheck = bool(state["flukecheck"])
 
     # -- cross-rank reductions of the per-walker collector state
     def _reduce(self, burned, total, count0, mincount):

@@ -225,18 +225,33 @@ int cmbl_clik_compute_batch(cmbl_t *h, int W, const int *clik_lmax, const double
         if (W <= 0) return;
         if (!clik_lmax || !cl_and_pars || !lnlike) cmamd::fail(CMBL_ERR_ARG, "cmbl_clik_compute_batch: bad arguments");
         const ClikWs c = clik_ws_layout(*h->like, W, clik_lmax);
-        if (!workspace) {
-            h->clik_ws.grow(c.bytes);
-            workspace = h->clik_ws.p;
+        const hipStream_t st = (hipStream_t)stream;
+        auto run = [&](void *ws) {
+            double *dl = static_cast<double *>(ws);
+            double *mlnl = dl + (size_t)c.ldw * W;
+            void *lws = mlnl + W;
+            cmamd::launch_clik_to_dl(cl_and_pars, ld, c.lm, dl, c.ldf, c.ldw, c.lmax_out, W, st);
+            // nuisance parameters follow the C_l blocks (cliklike.f90:157-163)
+            h->like->loglike_batch(W, dl, c.ldf, c.ldw, cl_and_pars + c.ncl, ld, mlnl, lws, st);
+            // lnlike = -(-lnL): clik_compute returns +lnL (cliklike.f90:166), negated on device
+            cmamd::launch_negate(mlnl, lnlike, W, st);
+        };
+        if (workspace) {
+            run(workspace);
+            return;
         }
-        double *dl = static_cast<double *>(workspace);
-        double *mlnl = dl + (size_t)c.ldw * W;
-        void *lws = mlnl + W;
-        cmamd::launch_clik_to_dl(cl_and_pars, ld, c.lm, dl, c.ldf, c.ldw, c.lmax_out, W, (hipStream_t)stream);
-        // nuisance parameters follow the C_l blocks (cliklike.f90:157-163)
-        h->like->loglike_batch(W, dl, c.ldf, c.ldw, cl_and_pars + c.ncl, ld, mlnl, lws, (hipStream_t)stream);
-        // lnlike = -(-lnL): clik_compute returns +lnL (cliklike.f90:166), negated on device
-        cmamd::launch_negate(mlnl, lnlike, W, (hipStream_t)stream);
+        // the handle's scratch: one host call at a time, and on the device after
+        // every earlier call's kernels on whatever stream they ran
+        std::lock_guard<std::mutex> lock(h->clik_mu);
+        if (h->clik_ev) {
+            if (h->clik_ws.bytes < c.bytes) HIP_CHECK(hipEventSynchronize(h->clik_ev));   // grow frees it
+            HIP_CHECK(hipStreamWaitEvent(st, h->clik_ev, 0));
+        } else {
+            HIP_CHECK(hipEventCreateWithFlags(&h->clik_ev, hipEventDisableTiming));
+        }
+        h->clik_ws.grow(c.bytes);
+        run(h->clik_ws.p);
+        HIP_CHECK(hipEventRecord(h->clik_ev, st));
     });
 }
 

@@ -265,6 +265,9 @@ void sampler_collector_enable(cmbs *s, int samp_capacity) {
     if (samp_capacity <= 0) fail(CMBL_ERR_ARG, "sample capacity must be positive");
     const size_t ld = s->W;
     auto &c = s->coll;
+    // already enabled at this capacity: keep the lists (a collector built after
+    // cmbs_load_state must not wipe the restored ones)
+    if (c.enabled && c.cap == samp_capacity) return;
     c.cap = samp_capacity;
     c.samp.alloc((size_t)samp_capacity * ld * 4);
     c.state.alloc((size_t)(5 + s->n_used) * ld * 4);     // start, count, snum, thin, burn, pchg[n]

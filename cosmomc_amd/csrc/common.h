@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/cosmomc_amd.h"
+#include "smallgauss.h"
 
 namespace cmamd {
 
@@ -161,10 +162,16 @@ std::string load_paramnames(const std::string &path, int *count);
 // for the kernel that consumes it: -lnL of walker w is the fixed-order combine
 // of quadform.h (qf_group_sum / qf_tree) over the partials of walker tile
 // w / 64 at lane w % 64, + addend[w] when addend is not null.
+// kind 1 (small gaussian CMBlikes, smallgauss.h): -lnL is the chi^2 the
+// consumer forms from the window stage's partial rows ([rows][W]) with the
+// likelihood's SmallGaussDev tables and the calibration in nuis.
 struct QFDeferred {
-    const double *partial = nullptr;   // [tiles][n_items][64]
+    int kind = 0;
+    const double *partial = nullptr;   // kind 0: [tiles][n_items][64]; kind 1: partial rows [rows][W]
     int n_items = 0;
     const double *addend = nullptr;
+    const double *nuis = nullptr;      // kind 1: the nuisance vectors the evaluation used
+    long long ld_nuis = 0;
 };
 
 // Window stage of a likelihood: its first kernel contracts every walker's
@@ -215,6 +222,12 @@ struct Like {
     // sampler's next mh_kernel performs (QFDeferred).  ws must stay untouched
     // until then.
     virtual bool deferred_capable() const { return false; }
+    // a small gaussian likelihood whose whole chi^2 the consumer can form
+    // (QFDeferred kind 1): its tables, or false
+    virtual bool deferred_small(SmallGaussDev &sg) const {
+        (void)sg;
+        return false;
+    }
     virtual QFDeferred loglike_batch_deferred(int W, const double *dl, long long ld_field, long long ld_walker,
                                               const double *nuis, long long ld_nuis, void *ws, hipStream_t stream) {
         (void)W, (void)dl, (void)ld_field, (void)ld_walker, (void)nuis, (void)ld_nuis, (void)ws, (void)stream;
@@ -242,6 +255,10 @@ struct Like {
         (void)starts;
         return false;
     }
+    // The segmentation in force (opaque) and its restore, so a caller whose
+    // resegment came to nothing can put the handle back as it found it.
+    virtual std::map<int, std::vector<int>> window_segments() const { return {}; }
+    virtual void window_set_segments(const std::map<int, std::vector<int>> &segs) { (void)segs; }
     // internal workspace for ws == nullptr
     DevBuf own_ws;
     // sticky CMBL_STATUS_* bits set by the kernels (cmbl_status)
@@ -281,9 +298,17 @@ struct cmbl {
     void *pin = nullptr;
     size_t pin_bytes = 0;
     hipStream_t host_stream = nullptr;
-    // cmbl_clik_compute_batch scratch when the caller passes no workspace
+    // cmbl_clik_compute_batch scratch when the caller passes no workspace: calls
+    // that share it are serialised by clik_mu and ordered on the device by
+    // clik_ev (recorded on the stream of the last call that used it)
+    std::mutex clik_mu;
     cmamd::DevBuf clik_ws;
+    hipEvent_t clik_ev = nullptr;
     ~cmbl() {
+        if (clik_ev) {
+            (void)hipEventSynchronize(clik_ev);
+            (void)hipEventDestroy(clik_ev);
+        }
         if (pin) (void)hipHostFree(pin);
         if (host_stream) (void)hipStreamDestroy(host_stream);
     }

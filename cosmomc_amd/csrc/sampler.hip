@@ -523,7 +523,10 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     double *vc = lk + (size_t)nlk * NB;                          // [max_blk][NB]
     double *tq = vc + (size_t)c.max_blk * NB;                    // [tq_rows][NB] test-Gaussian row sums / block
     double *dq = tq + (size_t)c.tq_rows * NB;                    // [def_cap][QF_GROUPS + 1][NB] deferred combines
-    double *td = dq + (size_t)c.def_cap * (QF_GROUPS + 1) * NB;  // [ntd rounded to 32]
+    double *sgt = dq + (size_t)c.def_cap * (QF_GROUPS + 1) * NB; // [sg.ntask][NB] small-gaussian task sums
+    double *sgx = sgt + (size_t)(c.sg_cap ? c.sg.ntask : 0) * NB; // [sg.nX][NB] its bigX
+    double *sgz = sgx + (size_t)(c.sg_cap ? c.sg.nX : 0) * NB;    // [sg.nX][NB] x_i (M x)_i
+    double *td = sgz + (size_t)(c.sg_cap ? c.sg.nX : 0) * NB;     // [ntd rounded to 32]
     int *si = reinterpret_cast<int *>(td + ((ntd + 31) & ~31));  // [ni_st][NB]
     int *it = si + (size_t)ni_st * NB;                           // [all_n][NB] when stage_cyc
     int *ti = it + (size_t)(c.stage_cyc ? c.all_n : 0) * NB;     // [n_int rounded to 64]
@@ -565,9 +568,27 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
             if (wave == MH_WAVES - 1) row[(size_t)QF_GROUPS * NB + lane] = (c.def_add[d] && act) ? c.def_add[d][w] : 0.0;
         }
     }
+    // the deferred small gaussian: its partial rows summed in tasks, one task per wave at a time
+    double sg_cal = 1.0;
+    if (ACCEPT && c.n_sg) {
+        sg_tasks<NB, MH_WAVES>(c.sg, c.sg_partial, c.W, w, act, wave, lane, sgt);
+        if (wave == 0 && act && c.sg.log_cal_prior > 0 && c.sg.cal_index >= 0)
+            sg_cal = c.sg_nuis[(size_t)w * c.sg_ld_nuis + c.sg.cal_index];
+    }
     STAMP(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (ACCEPT && c.n_sg) {   // then its elements and rows over the waves, the sum on wave 0 (smallgauss.h's order)
+        sg_elems<NB, MH_WAVES>(c.sg, wave, lane, sgt, sgx);
+        __syncthreads();
+        sg_rows<NB, MH_WAVES>(c.sg, c.sg.M, wave, lane, sgx, sgz);
+        __syncthreads();
+        if (wave == 0 && act) {
+            const double v = sg_final<NB>(c.sg, lane, sgz, sg_cal);
+            lk[(size_t)c.sg_like * NB + lane] = v;
+            const_cast<double *>(c.like_terms)[(size_t)c.sg_like * W + w] = v;
+        }
+    }
     if (ACCEPT && c.n_def && wave == 0 && act) {   // finish them in quadform.h's fixed order
         for (int d = 0; d < MAXDEF; d++) {
             if (d >= c.n_def) break;
@@ -1287,7 +1308,8 @@ static size_t mh_lds_bytes(const cmbs *s) {
     const int nd_st = d.stage_R ? d.rows.ND : d.rows.ND - d.rows.RR;
     const int ni_st = d.stage_cyc ? d.rows.NI : d.rows.CYC;
     const int ntd = d.stage_cov ? d.tl.n_dbl : d.tl.covinv;
-    return (size_t)(nd_st + MAXLIKE + d.max_blk + d.tq_rows + d.def_cap * (QF_GROUPS + 1)) * NB * 8 +
+    return (size_t)(nd_st + MAXLIKE + d.max_blk + d.tq_rows + d.def_cap * (QF_GROUPS + 1) +
+                    (d.sg_cap ? d.sg.ntask + 2 * d.sg.nX : 0)) * NB * 8 +
            (size_t)((ntd + 31) & ~31) * 8 +
            (size_t)(ni_st + (d.stage_cyc ? d.all_n : 0)) * NB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 + 64;
 }
@@ -1301,9 +1323,15 @@ static void set_mh_lds(cmbs *s) {
     const size_t cap = 160 * 1024;
     d.stage_R = d.stage_cyc = d.stage_cov = 1;
     d.tq_rows = d.test_like ? s->n_used : 1;   // a row per test-Gaussian row, or one (the proposal's block)
-    d.def_cap = (int)s->defer_likes.size();
+    d.def_cap = 0;
+    d.sg_cap = 0;
+    for (int i : s->defer_likes) {
+        if (s->likes[i].like->like->deferred_capable()) d.def_cap++;
+        else d.sg_cap = 1;
+    }
     if (mh_lds_bytes(s) > cap) {               // the deferred combines go first: the likelihoods combine in-launch
         d.def_cap = 0;
+        d.sg_cap = 0;
         s->defer_likes.clear();
     }
     if (mh_lds_bytes(s) > cap) d.stage_R = 0;
@@ -1643,10 +1671,19 @@ static void setup_fusion(cmbs *s) {
                 if (hi < lo) continue;
                 starts[kv.first] = bin_safe_cuts(kv.second, lo & ~1, hi);
             }
-            if (!C.like->like->window_resegment(starts) || !C.like->like->window_stage(sc)) continue;
+            // the handle may be shared (standalone calls, other samplers): its
+            // segmentation changes only if the fused pass is kept
+            const auto saved = C.like->like->window_segments();
+            if (!C.like->like->window_resegment(starts) || !C.like->like->window_stage(sc)) {
+                C.like->like->window_set_segments(saved);
+                continue;
+            }
             s->tp_why = std::max(s->tp_why, 6);
             std::unique_ptr<TheoryPass> tp(new TheoryPass());
-            if (!tp->build({sp, sc})) continue;
+            if (!tp->build({sp, sc})) {
+                C.like->like->window_set_segments(saved);
+                continue;
+            }
             s->tpass = std::move(tp);
             s->tp_like[0] = i;
             s->tp_like[1] = j;
@@ -1709,11 +1746,25 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, const int *nuisance_indices, 
     set_change_mask(s);
     // likelihoods whose quadratic-form combine the accepting mh_kernel can take
     // over (dense evaluation only: the sparse ones write compacted slots)
+    // and the one small gaussian likelihood whose whole chi^2 it can form
     s->defer_likes.clear();
-    for (int i = 0; i < (int)s->likes.size() && (int)s->defer_likes.size() < MAXDEF; i++) {
+    int n_qf = 0;
+    bool have_sg = false;
+    for (int i = 0; i < (int)s->likes.size(); i++) {
         bool sparse = false;
         for (int q : s->sparse_likes) sparse |= q == i;
-        if (!sparse && s->likes[i].like->like->deferred_capable()) s->defer_likes.push_back(i);
+        if (sparse) continue;
+        Like &L = *s->likes[i].like->like;
+        SmallGaussDev sg{};
+        if (L.deferred_capable() && n_qf < MAXDEF) {
+            s->defer_likes.push_back(i);
+            n_qf++;
+        } else if (!have_sg && L.deferred_small(sg)) {
+            s->defer_likes.push_back(i);
+            s->dc.sg = sg;
+            s->dc.sg_like = i;
+            have_sg = true;
+        }
     }
     for (int i = 0; i < MAXLIKE; i++) s->like_ws[i].release();
     set_mh_lds(s);
@@ -1774,6 +1825,14 @@ static bool is_deferred(const cmbs *s, size_t i) {
 }
 
 static void record_deferred(cmbs *s, size_t i, const QFDeferred &d) {
+    if (d.kind == 1) {
+        if ((int)i != s->dc.sg_like || s->pending_sg) fail(CMBL_ERR_ARG, "internal: unexpected small-gaussian deferral");
+        s->pending_sg = 1;
+        s->dc.sg_partial = d.partial;
+        s->dc.sg_nuis = d.nuis;
+        s->dc.sg_ld_nuis = d.ld_nuis;
+        return;
+    }
     const int p = s->pending_def++;
     s->dc.def_like[p] = (int)i;
     s->dc.def_items[p] = d.n_items;
@@ -1942,9 +2001,12 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
     const size_t lds = s->mh_lds;
     DevCfg dc = s->dc;
     dc.mask_on = masked ? 1 : 0;
-    if (s->pending_def && !accept) fail(CMBL_ERR_ARG, "internal: deferred likelihoods without an accepting step");
+    if ((s->pending_def || s->pending_sg) && !accept)
+        fail(CMBL_ERR_ARG, "internal: deferred likelihoods without an accepting step");
     dc.n_def = s->pending_def;
+    dc.n_sg = s->pending_sg;
     s->pending_def = 0;
+    s->pending_sg = 0;
     timed_launch("mh_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
         if (accept && propose)
             hipExtLaunchKernelGGL(mh_kernel<true, true>, g, b, lds, stream, e0, e1, 0, dc, fast_only, row.p, row.t, blk0);
@@ -2205,10 +2267,12 @@ void sampler_step_theory(cmbs *s, int n_steps, cmbs_theory_fn fn, void *user, hi
 }
 
 // After a resume: the theory at every walker's current point (rows P) from the
-// caller's theory function, copied into each likelihood's walker theory rows;
-// the restored CurLike / terms are then checked against the likelihoods
-// re-evaluated there (the reference recomputes theory at the restart point
-// too, GeneralSetup.f90:123-131).
+// caller's theory function, copied into each likelihood's walker theory rows
+// (the reference recomputes theory at the restart point too,
+// GeneralSetup.f90:123-131).  The restored CurLike and per-likelihood terms are
+// kept as saved, not re-evaluated: theory_fn must reproduce the theory the run
+// had at those points (under a change mask, unchanged likelihoods keep their
+// saved terms).
 __global__ void copy_theory_rows(int W, const double *src, long long src_ld, double *dst, long long dst_ld, long long n)
 {
     const int w = blockIdx.y;
@@ -2457,3 +2521,5 @@ extern "C" int cmamd_debug_stamps(unsigned long long *host) {
 // number of work items of the sampler's fused window pass (0: none); for tests
 // (without one: minus the last set-up check passed)
 extern "C" int cmamd_debug_fused(const cmbs *s) { return !s ? 0 : s->tpass ? s->tpass->n_items() : -s->tp_why; }
+// test hook: the likelihoods the accepting mh_kernel finishes (split-K combines + 100 x small gaussian)
+extern "C" int cmamd_debug_deferred(const cmbs *s) { return !s ? 0 : s->dc.def_cap + 100 * s->dc.sg_cap; }

@@ -106,7 +106,9 @@ int  cmbl_clik_compute_batch(cmbl_t *h, int W, const int *clik_lmax,
                              const double *cl_and_pars, long long ld,
                              double *lnlike, void *workspace, void *stream);
 /* Device workspace bytes cmbl_clik_compute_batch needs for W walkers
- * (workspace NULL: the handle's own, grown on demand; asynchronous either way). */
+ * (workspace NULL: the handle's own, grown on demand; such calls are serialised
+ * on the host and ordered on the device after the previous one, whatever its
+ * stream; asynchronous either way). */
 size_t cmbl_clik_workspace_size(const cmbl_t *h, int W);
 
 /* Sticky numerical status of a handle, set on device by the likelihood
@@ -229,7 +231,9 @@ int  cmbs_step_theory(cmbs_t *s, int n_steps, cmbs_theory_fn theory_fn, void *us
  * called once with the current points P [num_params][ld] and fills every
  * trial-theory buffer (cmbs_set_trial_theory), which is then copied into the
  * walkers' theory rows.  The reference likewise recomputes the theory at the
- * restart point (GeneralSetup.f90:123-131). */
+ * restart point (GeneralSetup.f90:123-131).  CurLike and the per-likelihood
+ * terms stay as saved (not re-evaluated): theory_fn must reproduce the theory
+ * the run had at those points. */
 int  cmbs_refresh_theory(cmbs_t *s, cmbs_theory_fn theory_fn, void *user, void *stream);
 
 /* Execution tuning (no reference counterpart; results are unchanged): split the

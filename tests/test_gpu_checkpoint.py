@@ -251,3 +251,64 @@ def test_resume_slow_steps_refreshes_theory(tmp_path):
     b.step_theory(20, theory_fn=fn_b)
     _same_state(a, b)
     assert torch.equal(th_a, th_b)
+
+
+def test_resume_with_chain_collector(tmp_path):
+    """A run with the convergence collector (ChainCollector: per-walker
+    Samples lists on device, walker-0 triggers, burn-in and update frequency
+    on the host) checkpointed between exchanges and resumed in a fresh
+    sampler + collector makes the same exchanges -- same R-1 and proposal
+    covariance, same collector lists -- as the run that never stopped."""
+    from cosmomc_amd.checkpoint import read_checkpoint, write_checkpoint
+    from cosmomc_amd.converge import ChainCollector, CollectorSettings
+    from cosmomc_amd.sampler import BatchedMCMC
+    n, W, cap = 3, 96, 4000
+    rng = np.random.default_rng(8)
+    A = rng.standard_normal((n, n))
+    cov = A @ A.T / n + np.eye(n)
+    start = rng.standard_normal((W, n))
+
+    def make():
+        s = BatchedMCMC(W, n, [1, 2, 3], [[1, 2], [3]], 1, -30 * np.ones(n), 30 * np.ones(n), seed_ij=71,
+                        seed_kl=72)
+        s.set_covariance(cov)
+        s.set_test_gaussian(cov, np.zeros(n))
+        s.enable_history(cap)
+        c = ChainCollector(s, CollectorSettings(MPI_R_Stop=0.01, covariance_is_diagonal=True), num_slow=2,
+                           num_fast=1, sample_capacity=cap)
+        return s, c
+
+    def run(s, c, blocks, out, prop):
+        for _ in range(blocks):
+            s.step(c.next_block())
+            r = c.process()
+            if r is not None:
+                out.append((r.R, r.propose_cov.copy()))
+                if r.update_proposal:
+                    s.set_covariance(r.propose_cov)
+                    prop = r.propose_cov
+        return prop
+
+    a, ca = make()
+    a.set_start(start)
+    full = []
+    run(a, ca, 60, full, cov)
+    assert len(full) >= 4, "too few exchanges for the test to mean much"
+
+    b, cb = make()
+    b.set_start(start)
+    part = []
+    prop = run(b, cb, 25, part, cov)
+    assert 0 < len(part) < len(full)
+    root = str(tmp_path / "coll")
+    write_checkpoint(root, b, prop, chain_collector=cb)        # with the proposal in force
+    c_, cc = make()                               # fresh sampler and collector, as a restarted job
+    read_checkpoint(root, c_, chain_collector=cc)
+    run(c_, cc, 35, part, prop)
+    assert len(part) == len(full)
+    for (r1, p1), (r2, p2) in zip(full, part):
+        assert r1 == r2
+        np.testing.assert_array_equal(p1, p2)
+    for x, y in zip(a.collector_state(), c_.collector_state()):
+        np.testing.assert_array_equal(x, y)
+    _same_state(a, c_)
