@@ -31,7 +31,6 @@
 #include <sstream>
 
 #include "quadform.h"
-#include "smallgauss.h"
 
 namespace cmamd {
 
@@ -783,45 +782,95 @@ __global__ __launch_bounds__(256) void cmbl_reduce_kernel(CLDev c, const double 
 
 // Small gaussian likelihoods (nX <= 64, e.g. lensing 9, SPT-SZ 47): binned
 // spectra, bigX = C - Chat and chi^2 = bigX^T C^-1 bigX in one kernel
-// (CMBlikes.f90:1183-1225), in smallgauss.h's order (the sampler's mh_kernel
-// forms the same chi^2 in its fast steps).  Workgroup = SMALL_WT walkers x
-// 256 / SMALL_WT thread groups.  The partial rows of every element are cut into
-// tasks of <= 8 rows (host); groups take tasks round-robin with all loads of a
-// task in flight.  The inverse covariance and the calibration are loaded
-// beside the partials.
+// (CMBlikes.f90:1183-1225; Matrix_QuadForm as row sums y = M x, then x.y).
+// Workgroup = 8 walkers x 32 thread groups.  The partial rows of every
+// element are cut into tasks of <= 8 rows (host); groups take tasks
+// round-robin with all loads of a task in flight, then combine them per
+// element in task order (deterministic), then split the rows of M.  Every
+// table load is issued at the start, beside the others: the partial loads
+// wait on one table level (the task's rows), nothing after them on any.
 struct SmallTask { int first, count; };      // rows e_*_rows[first .. first+count) (host side)
 struct SmallDev {
     int ntask;
-    const int *trow;                         // [ntask][SG_ROWS]: each task's partial rows, -1 padded
+    const int *trow;                         // [ntask][8]: each task's partial rows, -1 padded
     const int *e_main_t, *e_corr_t;          // [nE+1] task ranges per element
 };
 
 template <int WT>
-__global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(SmallGaussDev sg, const int *__restrict__ wcount,
-                                                              const double *__restrict__ partial,
+__global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev sd, const double *__restrict__ partial,
                                                               const double *__restrict__ nuis, long long ld_nuis,
-                                                              double *__restrict__ out, int W)
+                                                              const double *__restrict__ M, double *__restrict__ out,
+                                                              int W)
 {
     constexpr int NG = 256 / WT;             // thread groups of WT walkers
-    __shared__ double tp[SMALL_MAXTASK * WT];
-    __shared__ double xs[SMALL_NX * WT];
-    __shared__ double zs[SMALL_NX * WT];
+    __shared__ double tp[SMALL_MAXTASK][WT];
+    __shared__ double xs[SMALL_NX][WT];
+    __shared__ double red[NG][WT];
     __shared__ double Msh[SMALL_NX * SMALL_NX];
     const int wl = threadIdx.x % WT, g = threadIdx.x / WT;
     const int w = blockIdx.x * WT + wl;
-    const int Wc = live_walkers(wcount, W);
+    const int Wc = live_walkers(c.wcount, W);
     if (blockIdx.x * WT >= Wc) return;
-    for (int i = threadIdx.x; i < sg.nX * sg.nX; i += 256) Msh[i] = sg.M[i];   // in flight with the partial loads
+    for (int i = threadIdx.x; i < c.nX * c.nX; i += 256) Msh[i] = M[i];   // in flight with the partial loads
     const bool act = w < Wc;
-    const bool calp = sg.log_cal_prior > 0 && sg.cal_index >= 0;
-    const double cal = (g == 0 && act && calp) ? nuis[(long long)w * ld_nuis + sg.cal_index] : 1.0;   // likewise
-    sg_tasks<WT, NG>(sg, partial, W, w, act, g, wl, tp);
+    const bool calp = c.log_cal_prior > 0 && c.cal_index >= 0;
+    const double cal = (g == 0 && act && calp) ? nuis[(long long)w * ld_nuis + c.cal_index] : 1.0;   // likewise
+    struct Elem { int ix, m0, m1, c0, c1; double mc, cc, fc, ch; };
+    auto elem = [&](int e) {   // element e's table entries
+        Elem q{c.e_to_x[e], sd.e_main_t[e], sd.e_main_t[e + 1], 0, 0, c.e_main_const[e], 0.0, 0.0, c.chat[e]};
+        if (c.has_corr) {
+            q.c0 = sd.e_corr_t[e];
+            q.c1 = sd.e_corr_t[e + 1];
+            q.cc = c.e_corr_const[e];
+            q.fc = c.fidcorr[e];
+        }
+        return q;
+    };
+    Elem e0{-1, 0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0};
+    if (g < c.nE) e0 = elem(g);   // this group's first element, in flight with the partials
+    for (int t = g; t < sd.ntask; t += NG) {
+        const int4 ra = *reinterpret_cast<const int4 *>(sd.trow + 8 * t);
+        const int4 rb = *reinterpret_cast<const int4 *>(sd.trow + 8 * t + 4);
+        const int r[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = (act && r[u] >= 0) ? partial[(long long)r[u] * W + w] : 0.0;
+        double s = 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) s += v[u];
+        tp[t][wl] = s;
+    }
     __syncthreads();
-    sg_elems<WT, NG>(sg, g, wl, tp, xs);
+    for (int e = g; e < c.nE; e += NG) {
+        const Elem q = e == g ? e0 : elem(e);
+        if (q.ix < 0) continue;
+        double s = q.mc;
+        for (int t = q.m0; t < q.m1; t++) s += tp[t][wl];
+        if (c.has_corr) {
+            double cs = q.cc;
+            for (int t = q.c0; t < q.c1; t++) cs += tp[t][wl];
+            s = s + (cs - q.fc);
+        }
+        xs[q.ix][wl] = s - q.ch;
+    }
     __syncthreads();
-    sg_rows<WT, NG>(sg, Msh, g, wl, xs, zs);
+    double part = 0.0;
+    for (int i = g; i < c.nX; i += NG) {
+        double y = 0.0;
+        for (int j = 0; j < c.nX; j++) y += Msh[i * c.nX + j] * xs[j][wl];
+        part += xs[i][wl] * y;
+    }
+    red[g][wl] = part;
     __syncthreads();
-    if (g == 0 && act) out[w] = sg_final<WT>(sg, wl, zs, cal);
+    if (g == 0 && act) {
+        double chisq = 0.0;
+        for (int k = 0; k < NG; k++) chisq += red[k][wl];
+        if (calp) {
+            const double t = log(cal) / c.log_cal_prior;
+            chisq = chisq + t * t;
+        }
+        out[w] = chisq / 2;
+    }
 }
 
 // ---------------------------------------------------------------- HL
@@ -2240,8 +2289,7 @@ struct CMBLikes final : Like {
                             bool defer) override {
         if (W <= 0) return QFDeferred{};
         if (n_nuis > 0 && !nuis) fail(CMBL_ERR_ARG, "%s needs its %d nuisance parameters", name.c_str(), n_nuis);
-        if (defer && !deferred_capable() && !small_gauss)
-            fail(CMBL_ERR_UNSUPPORTED, "%s: no deferred evaluation", name.c_str());
+        if (defer && !deferred_capable()) fail(CMBL_ERR_UNSUPPORTED, "%s: no deferred evaluation", name.c_str());
         dev.wcount = nullptr;
         hl.wcount = nullptr;
         const double *nu = nuis ? nuis : reinterpret_cast<const double *>(ws);   // never read when n_nuis == 0
@@ -2269,20 +2317,9 @@ struct CMBLikes final : Like {
 
     // the quadratic-form datasets (HL and large gaussian) can leave the combine to the sampler
     bool deferred_capable() const override { return approx != 3 && !small_gauss; }
-    // the small gaussian ones their whole chi^2 (smallgauss.h)
-    SmallGaussDev small_dev() const {
-        return SmallGaussDev{dev.nE, dev.nX, sdev.ntask, dev.has_corr, dev.cal_index, dev.log_cal_prior, sdev.trow,
-                             sdev.e_main_t, sdev.e_corr_t, dev.e_to_x, dev.e_main_const, dev.e_corr_const,
-                             dev.fidcorr, dev.chat, d_invcov.as<double>()};
-    }
-    bool deferred_small(SmallGaussDev &sg) const override {
-        if (!small_gauss) return false;
-        sg = small_dev();
-        return true;
-    }
     QFDeferred loglike_batch_deferred(int W, const double *dl, long long ld_field, long long ld_walker,
                                       const double *nuis, long long ld_nuis, void *ws, hipStream_t stream) override {
-        if (!deferred_capable() && !small_gauss) fail(CMBL_ERR_UNSUPPORTED, "%s: no deferred evaluation", name.c_str());
+        if (!deferred_capable()) fail(CMBL_ERR_UNSUPPORTED, "%s: no deferred evaluation", name.c_str());
         if (!ws) fail(CMBL_ERR_ARG, "deferred evaluation needs a caller workspace");
         return run(W, dl, ld_field, ld_walker, nuis, ld_nuis, nullptr, ws, stream, nullptr, true);
     }
@@ -2383,20 +2420,11 @@ struct CMBLikes final : Like {
         double *addend = reinterpret_cast<double *>(base + o.add);
         const bool use_add = log_cal_prior > 0 && cal_index >= 0;
         const int tiles = (W + 63) / 64;
-        if (small_gauss && defer) {   // the consumer forms the chi^2 from the partial rows
-            QFDeferred d;
-            d.kind = 1;
-            d.partial = partial;
-            d.nuis = nu;
-            d.ld_nuis = ld_nuis;
-            return d;
-        }
         if (small_gauss) {
-            const SmallGaussDev sgdev = small_dev();
             timed_launch("cmbl_gauss_small_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
 #define CMBL_SMALL(T)                                                                                             \
-    hipExtLaunchKernelGGL(cmbl_gauss_small_kernel<T>, dim3((W + T - 1) / T), dim3(256), 0, stream, e0, e1, 0, sgdev, \
-                          (const int *)wcount, (const double *)partial, nu, ld_nuis, out, W)
+    hipExtLaunchKernelGGL(cmbl_gauss_small_kernel<T>, dim3((W + T - 1) / T), dim3(256), 0, stream, e0, e1, 0, dev, \
+                          sdev, (const double *)partial, nu, ld_nuis, d_invcov.as<double>(), out, W)
                 CMBL_SMALL(SMALL_WT);
 #undef CMBL_SMALL
             });

@@ -15,7 +15,6 @@
 #include <vector>
 
 #include "../../include/cosmomc_amd.h"
-#include "smallgauss.h"
 
 namespace cmamd {
 
@@ -162,16 +161,10 @@ std::string load_paramnames(const std::string &path, int *count);
 // for the kernel that consumes it: -lnL of walker w is the fixed-order combine
 // of quadform.h (qf_group_sum / qf_tree) over the partials of walker tile
 // w / 64 at lane w % 64, + addend[w] when addend is not null.
-// kind 1 (small gaussian CMBlikes, smallgauss.h): -lnL is the chi^2 the
-// consumer forms from the window stage's partial rows ([rows][W]) with the
-// likelihood's SmallGaussDev tables and the calibration in nuis.
 struct QFDeferred {
-    int kind = 0;
-    const double *partial = nullptr;   // kind 0: [tiles][n_items][64]; kind 1: partial rows [rows][W]
+    const double *partial = nullptr;   // [tiles][n_items][64]
     int n_items = 0;
     const double *addend = nullptr;
-    const double *nuis = nullptr;      // kind 1: the nuisance vectors the evaluation used
-    long long ld_nuis = 0;
 };
 
 // Window stage of a likelihood: its first kernel contracts every walker's
@@ -222,12 +215,6 @@ struct Like {
     // sampler's next mh_kernel performs (QFDeferred).  ws must stay untouched
     // until then.
     virtual bool deferred_capable() const { return false; }
-    // a small gaussian likelihood whose whole chi^2 the consumer can form
-    // (QFDeferred kind 1): its tables, or false
-    virtual bool deferred_small(SmallGaussDev &sg) const {
-        (void)sg;
-        return false;
-    }
     virtual QFDeferred loglike_batch_deferred(int W, const double *dl, long long ld_field, long long ld_walker,
                                               const double *nuis, long long ld_nuis, void *ws, hipStream_t stream) {
         (void)W, (void)dl, (void)ld_field, (void)ld_walker, (void)nuis, (void)ld_nuis, (void)ws, (void)stream;

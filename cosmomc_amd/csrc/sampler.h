@@ -83,16 +83,6 @@ struct DevCfg {
     int def_like[MAXDEF], def_items[MAXDEF];
     const double *def_part[MAXDEF];         // [tiles][def_items][64]
     const double *def_add[MAXDEF];          // [W] or null
-    // a deferred small gaussian likelihood (QFDeferred kind 1): the accepting
-    // mh_kernel forms its whole chi^2 from the partial rows (smallgauss.h) with
-    // its 16 waves, beside the state image's LDS-DMA
-    int sg_cap;                             // LDS room for it (0/1)
-    int n_sg;                               // this launch: finish it (set per launch)
-    int sg_like;
-    SmallGaussDev sg;
-    const double *sg_partial;               // [rows][W]
-    const double *sg_nuis;                  // the trial's nuisance vectors [W][ld]
-    long long sg_ld_nuis;
 };
 
 struct LikeSlot {
@@ -157,7 +147,6 @@ struct cmbs {
     std::vector<int> defer_likes;
     cmamd::DevBuf like_ws[cmamd::MAXLIKE];
     int pending_def = 0;
-    int pending_sg = 0;
     // fused window pass (theorypass.h): plik_lite and a CMBlikes dataset that
     // read one theory buffer run their window stages as one pass; each then
     // continues from its own workspace (like_ws)

@@ -30,13 +30,20 @@ namespace cmamd {
 static constexpr double LOGZERO = CMBL_LOGZERO;
 static constexpr int MAXP = 64;        // max parameters per chain
 static constexpr int MAXBLK = 32;      // max block size
-static constexpr int NB = 64;          // walkers per mh_kernel block (one wavefront of chain logic)
-#ifndef CMAMD_MH_WAVES
-#define CMAMD_MH_WAVES 16
-#endif
-static constexpr int MH_WAVES = CMAMD_MH_WAVES;   // waves per mh_kernel block sharing the state staging (measured 4 / 8 / 12 / 16: 12.0 / 11.1 / 11.2 / 10.8 us, W = 1024)
+static constexpr int NB = 64;          // walker tile of the history / collector kernels (one wavefront)
+// mh_kernel: MB walkers per block (lanes 0..MB-1 of wave 0 run their chain
+// logic) and MH_THREADS threads, i.e. NV = MH_THREADS / MB groups of MB threads
+// for the staging, the deferred combines and the multi-group products.  With
+// 16-walker blocks a W = 1024 step spreads over 64 CUs instead of 16: each
+// block stages a quarter of the state image (round 3: 64-walker blocks, 16
+// waves, 12.9 us).
+static constexpr int MB = 16;
+static constexpr int MH_THREADS = 256;
+static constexpr int NV = MH_THREADS / MB;
+static_assert(NV == QF_GROUPS, "one group per split-K group sum");
+static_assert(64 % MB == 0, "blocks tile the 64-walker rows of the split-K partials");
 
-// strided per-walker column view (LDS: stride NB; HBM: stride W)
+// strided per-walker column view (LDS: stride MB; HBM: stride W)
 template <class T> struct Col {
     T *p;
     int s;
@@ -358,7 +365,7 @@ __device__ inline double test_row(const DevCfg &c, const Tabs &t, const Q &q, in
     return s;
 }
 
-// trows (stride NB), when given, holds test_row(i) for every i, computed by
+// trows (stride MB), when given, holds test_row(i) for every i, computed by
 // the other waves of mh_kernel: the same sums in the same order
 template <class Q, class L>
 __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const L &likes,
@@ -386,7 +393,7 @@ __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const 
         const int n = c.n_used;
         double d = 0.0;
         for (int i = 0; i < n; i++) {
-            const double s = trows ? trows[(size_t)i * NB] : test_row(c, t, q, i);
+            const double s = trows ? trows[(size_t)i * MB] : test_row(c, t, q, i);
             d += (q[t.params_used[i]] - t.center[t.params_used[i]]) * s;
         }
         main = d / 2.0;
@@ -444,26 +451,35 @@ __device__ unsigned long long g_stamps[64][16];
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void gbl_void_t;
 
-// LDS-DMA (global_load_lds_dwordx4): rows [r0, r0+n) (n even) of a [rows][ld]
-// double array, columns wb..wb+63, into LDS rows [d0, d0+n) of [row][NB].
-// One wave instruction moves two 512-byte rows; nothing passes through VGPRs,
-// so every piece of the walker state is in flight at once.
+// LDS-DMA (global_load_lds_dwordx4): rows [r0, r0+n) of a [rows][ld] double
+// array, columns wb..wb+MB-1, into LDS rows [d0, d0+n) of [row][MB].  One wave
+// instruction moves 1 KB (64 lanes x 16 bytes), i.e. 1024 / (8 MB) rows, and
+// nothing passes through VGPRs, so every piece of the walker state is in
+// flight at once.  Lanes past the last row are off.
 __device__ inline void dma_rows_f64(double *dst, int d0, const double *src, int r0, int n, size_t ld, int wb,
                                     int lane, int wave = 0, int nw = 1)
 {
-    for (int r = 2 * wave; r < n; r += 2 * nw) {
-        const double *g = src + (size_t)(r0 + r + (lane >> 5)) * ld + wb + 2 * (lane & 31);
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)g, (lds_void_t *)(dst + (size_t)(d0 + r) * NB), 16, 0, 0);
+    constexpr int LPR = MB / 2, RPI = 64 / LPR;   // lanes per row, rows per instruction
+    for (int r = RPI * wave; r < n; r += RPI * nw) {
+        const int rr = r + lane / LPR;
+        if (rr < n) {
+            const double *g = src + (size_t)(r0 + rr) * ld + wb + 2 * (lane % LPR);
+            __builtin_amdgcn_global_load_lds((gbl_void_t *)g, (lds_void_t *)(dst + (size_t)(d0 + r) * MB), 16, 0, 0);
+        }
     }
 }
 
-// same for int rows (n multiple of 4): one instruction moves four 256-byte rows
+// same for int rows
 __device__ inline void dma_rows_i32(int *dst, const int *src, int n, size_t ld, int wb, int lane, int wave = 0,
                                     int nw = 1)
 {
-    for (int r = 4 * wave; r < n; r += 4 * nw) {
-        const int *g = src + (size_t)(r + (lane >> 4)) * ld + wb + 4 * (lane & 15);
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)g, (lds_void_t *)(dst + (size_t)r * NB), 16, 0, 0);
+    constexpr int LPR = MB / 4, RPI = 64 / LPR;
+    for (int r = RPI * wave; r < n; r += RPI * nw) {
+        const int rr = r + lane / LPR;
+        if (rr < n) {
+            const int *g = src + (size_t)rr * ld + wb + 4 * (lane % LPR);
+            __builtin_amdgcn_global_load_lds((gbl_void_t *)g, (lds_void_t *)(dst + (size_t)r * MB), 16, 0, 0);
+        }
     }
 }
 
@@ -477,11 +493,12 @@ __device__ inline void dma_words(void *dst, const void *src, int n, int lane, in
     }
 }
 
+// write-back: group v of nv (MB threads each, lane = walker) stores rows r0 + v, r0 + v + nv, ...
 template <class T>
-__device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size_t ld, int w, int lane, int wave = 0,
-                          int nw = 1)
+__device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size_t ld, int w, int lane, int v = 0,
+                          int nv = 1)
 {
-    for (int r = r0 + wave; r < r1; r += nw) dst[(size_t)r * ld + w] = src[(size_t)(src_r0 + r - r0) * NB + lane];
+    for (int r = r0 + v; r < r1; r += nv) dst[(size_t)r * ld + w] = src[(size_t)(src_r0 + r - r0) * MB + lane];
 }
 
 // changeMask of the trial (TheoryLike_GetLogLikeMain, calclike.f90:302-306):
@@ -502,14 +519,15 @@ __device__ inline void write_like_flags(const DevCfg &c, const QT &trial, const 
 // One launch per Metropolis step boundary: accept/reject the pending trial
 // (MetropolisAccept MCMC.f90:119-131 + MoveDone :166-190), then propose the
 // next trial (GetProposal / GetProposalFast) and scatter its nuisance
-// parameters for the likelihood kernels.  One wavefront per 64 walkers.
+// parameters for the likelihood kernels.  MB walkers per block.
 template <bool ACCEPT, bool PROPOSE>
-__global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_only, double *hist_row, double *hist_terms, int blk0)
+__global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only, double *hist_row, double *hist_terms, int blk0)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Rows &R = c.rows;
-    const int lane = threadIdx.x & (NB - 1), wave = threadIdx.x / NB;
-    const int wb = (blk0 + blockIdx.x) * NB;
+    const int lane = threadIdx.x % MB, grp = threadIdx.x / MB;    // walker in block, thread group
+    const int wl64 = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = MH_THREADS / 64;
+    const int wb = (blk0 + blockIdx.x) * MB;
     const int w = wb + lane;
     const bool act = w < c.W;
     const size_t W = c.ld;
@@ -518,85 +536,63 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     const int nd_st = c.stage_R ? R.ND : R.ND - R.RR;           // staged double rows
     const int ni_st = c.stage_cyc ? R.NI : R.CYC;                // staged int rows
     const int ntd = c.stage_cov ? c.tl.n_dbl : c.tl.covinv;      // staged double-table words
-    double *sd = lds;                                            // [nd_st][NB]
-    double *lk = sd + (size_t)nd_st * NB;                        // [nlk][NB]
-    double *vc = lk + (size_t)nlk * NB;                          // [max_blk][NB]
-    double *tq = vc + (size_t)c.max_blk * NB;                    // [tq_rows][NB] test-Gaussian row sums / block
-    double *dq = tq + (size_t)c.tq_rows * NB;                    // [def_cap][QF_GROUPS + 1][NB] deferred combines
-    double *sgt = dq + (size_t)c.def_cap * (QF_GROUPS + 1) * NB; // [sg.ntask][NB] small-gaussian task sums
-    double *sgx = sgt + (size_t)(c.sg_cap ? c.sg.ntask : 0) * NB; // [sg.nX][NB] its bigX
-    double *sgz = sgx + (size_t)(c.sg_cap ? c.sg.nX : 0) * NB;    // [sg.nX][NB] x_i (M x)_i
-    double *td = sgz + (size_t)(c.sg_cap ? c.sg.nX : 0) * NB;     // [ntd rounded to 32]
-    int *si = reinterpret_cast<int *>(td + ((ntd + 31) & ~31));  // [ni_st][NB]
-    int *it = si + (size_t)ni_st * NB;                           // [all_n][NB] when stage_cyc
-    int *ti = it + (size_t)(c.stage_cyc ? c.all_n : 0) * NB;     // [n_int rounded to 64]
+    double *sd = lds;                                            // [nd_st][MB]
+    double *lk = sd + (size_t)nd_st * MB;                        // [nlk][MB]
+    double *vc = lk + (size_t)nlk * MB;                          // [max_blk][MB]
+    double *tq = vc + (size_t)c.max_blk * MB;                    // [tq_rows][MB] test-Gaussian row sums / block
+    double *dq = tq + (size_t)c.tq_rows * MB;                    // [def_cap][QF_GROUPS + 1][MB] deferred combines
+    double *td = dq + (size_t)c.def_cap * (QF_GROUPS + 1) * MB;  // [ntd rounded to 32]
+    int *si = reinterpret_cast<int *>(td + ((ntd + 31) & ~31));  // [ni_st][MB]
+    int *it = si + (size_t)ni_st * MB;                           // [all_n][MB] when stage_cyc
+    int *ti = it + (size_t)(c.stage_cyc ? c.all_n : 0) * MB;     // [n_int rounded to 64]
     const bool skipR = !c.stage_R;
     // staged double row index of global row r (rotation rows dropped when not staged)
 #define SROW(r) ((skipR && (r) >= R.R) ? (r) - R.RR : (r))
 
     STAMP(0);
-    // all MH_WAVES waves issue the LDS-DMA of the state image (row pairs
-    // interleaved across waves); wave 0 alone runs the chain logic; all waves
-    // write the image back
+    // every wave issues the LDS-DMA of the state image; lanes 0..MB-1 of wave
+    // 0 alone run the chain logic; every thread group writes the image back
     const int rEnd = R.R + R.RR;
     if (skipR) {
-        dma_rows_f64(sd, 0, c.sd, 0, R.R, W, wb, lane, wave, MH_WAVES);
-        dma_rows_f64(sd, R.R, c.sd, rEnd, R.ND - rEnd, W, wb, lane, wave, MH_WAVES);
+        dma_rows_f64(sd, 0, c.sd, 0, R.R, W, wb, wl64, wave, nwave);
+        dma_rows_f64(sd, R.R, c.sd, rEnd, R.ND - rEnd, W, wb, wl64, wave, nwave);
     } else {
-        dma_rows_f64(sd, 0, c.sd, 0, R.ND, W, wb, lane, wave, MH_WAVES);
+        dma_rows_f64(sd, 0, c.sd, 0, R.ND, W, wb, wl64, wave, nwave);
     }
-    dma_rows_f64(lk, 0, c.like_terms, 0, nlk, W, wb, lane, wave, MH_WAVES);
-    dma_rows_i32(si, c.si, ni_st, W, wb, lane, wave, MH_WAVES);
-    dma_words(td, c.tab_d, 2 * ntd, lane, wave, MH_WAVES);
-    dma_words(ti, c.tab_i, c.tl.n_int, lane, wave, MH_WAVES);
+    dma_rows_f64(lk, 0, c.like_terms, 0, nlk, W, wb, wl64, wave, nwave);
+    dma_rows_i32(si, c.si, ni_st, W, wb, wl64, wave, nwave);
+    dma_words(td, c.tab_d, 2 * ntd, wl64, wave, nwave);
+    dma_words(ti, c.tab_i, c.tl.n_int, wl64, wave, nwave);
     // per-likelihood terms of the current point, for the history (rejected walkers keep theirs)
     double ct[MAXLIKE];
-    if (ACCEPT && hist_terms && wave == 0 && act) {
+    if (ACCEPT && hist_terms && grp == 0 && act) {
 #pragma unroll
         for (int l = 0; l < MAXLIKE; l++)
             if (l < c.n_like) ct[l] = c.cur_terms[(size_t)l * W + w];
     }
     // deferred split-K combines: the 16 group sums of this walker tile's
     // partials, one group per wave, loaded beside the state image
-    if (ACCEPT && c.n_def) {
-        const int tile = wb / NB;
+    if (ACCEPT && c.n_def) {   // group g sums split-K group g of this block's walkers (columns wb % 64 + lane of the tile)
+        const int tile = wb / QF_TILE, col = wb % QF_TILE + lane;
         for (int d = 0; d < MAXDEF; d++) {
             if (d >= c.n_def) break;
             const double *tp = c.def_part[d] + (size_t)tile * c.def_items[d] * QF_TILE;
-            double *row = dq + (size_t)d * (QF_GROUPS + 1) * NB;
-            for (int g = wave; g < QF_GROUPS; g += MH_WAVES) row[(size_t)g * NB + lane] = qf_group_sum(tp, c.def_items[d], g, lane);
-            if (wave == MH_WAVES - 1) row[(size_t)QF_GROUPS * NB + lane] = (c.def_add[d] && act) ? c.def_add[d][w] : 0.0;
+            double *row = dq + (size_t)d * (QF_GROUPS + 1) * MB;
+            row[(size_t)grp * MB + lane] = qf_group_sum(tp, c.def_items[d], grp, col);
+            if (grp == NV - 1) row[(size_t)QF_GROUPS * MB + lane] = (c.def_add[d] && act) ? c.def_add[d][w] : 0.0;
         }
-    }
-    // the deferred small gaussian: its partial rows summed in tasks, one task per wave at a time
-    double sg_cal = 1.0;
-    if (ACCEPT && c.n_sg) {
-        sg_tasks<NB, MH_WAVES>(c.sg, c.sg_partial, c.W, w, act, wave, lane, sgt);
-        if (wave == 0 && act && c.sg.log_cal_prior > 0 && c.sg.cal_index >= 0)
-            sg_cal = c.sg_nuis[(size_t)w * c.sg_ld_nuis + c.sg.cal_index];
     }
     STAMP(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (ACCEPT && c.n_sg) {   // then its elements and rows over the waves, the sum on wave 0 (smallgauss.h's order)
-        sg_elems<NB, MH_WAVES>(c.sg, wave, lane, sgt, sgx);
-        __syncthreads();
-        sg_rows<NB, MH_WAVES>(c.sg, c.sg.M, wave, lane, sgx, sgz);
-        __syncthreads();
-        if (wave == 0 && act) {
-            const double v = sg_final<NB>(c.sg, lane, sgz, sg_cal);
-            lk[(size_t)c.sg_like * NB + lane] = v;
-            const_cast<double *>(c.like_terms)[(size_t)c.sg_like * W + w] = v;
-        }
-    }
-    if (ACCEPT && c.n_def && wave == 0 && act) {   // finish them in quadform.h's fixed order
+    if (ACCEPT && c.n_def && grp == 0 && act) {   // finish them in quadform.h's fixed order
         for (int d = 0; d < MAXDEF; d++) {
             if (d >= c.n_def) break;
-            const double *row = dq + (size_t)d * (QF_GROUPS + 1) * NB;
-            double v = qf_tree(row + lane, NB);
-            if (c.def_add[d]) v = v + row[(size_t)QF_GROUPS * NB + lane];
+            const double *row = dq + (size_t)d * (QF_GROUPS + 1) * MB;
+            double v = qf_tree(row + lane, MB);
+            if (c.def_add[d]) v = v + row[(size_t)QF_GROUPS * MB + lane];
             const int l = c.def_like[d];
-            lk[(size_t)l * NB + lane] = v;
+            lk[(size_t)l * MB + lane] = v;
             const_cast<double *>(c.like_terms)[(size_t)l * W + w] = v;
         }
     }
@@ -608,34 +604,34 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     if (par_test) {
         if (act) {
             const Tabs t0 = make_tabs(c, ti, td, c.stage_cov ? td : c.tab_d);
-            const Col<double> q{sd + (size_t)SROW(R.T) * NB + lane, NB};
-            for (int i = wave; i < c.n_used; i += MH_WAVES) tq[(size_t)i * NB + lane] = test_row(c, t0, q, i);
+            const Col<double> q{sd + (size_t)SROW(R.T) * MB + lane, MB};
+            for (int i = grp; i < c.n_used; i += NV) tq[(size_t)i * MB + lane] = test_row(c, t0, q, i);
         }
         __syncthreads();
     }
     STAMP(2);
-    if (wave == 0 && act) {
+    if (grp == 0 && act) {
 
     const Tabs t = make_tabs(c, ti, td, c.stage_cov ? td : c.tab_d);
     Walker k;
-    k.r.u = Col<double>{sd + (size_t)R.U * NB + lane, NB};
-    k.r.c = sd[(size_t)R.C * NB + lane];
-    k.r.gset = sd[(size_t)R.G * NB + lane];
-    k.r.i97 = si[(size_t)R.I97 * NB + lane];
-    k.r.j97 = si[(size_t)R.J97 * NB + lane];
-    k.r.iset = si[(size_t)R.ISET * NB + lane];
-    k.R = c.stage_R ? Col<double>{sd + (size_t)R.R * NB + lane, NB} : Col<double>{c.sd + (size_t)R.R * W + w, c.ld};
-    k.P = Col<double>{sd + (size_t)SROW(R.P) * NB + lane, NB};
-    k.trial = Col<double>{sd + (size_t)SROW(R.T) * NB + lane, NB};
-    k.vec = Col<double>{vc + lane, NB};
-    k.cyc = c.stage_cyc ? Col<int>{si + (size_t)R.CYC * NB + lane, NB} : Col<int>{c.si + (size_t)R.CYC * W + w, c.ld};
-    k.cyclp = Col<int>{si + (size_t)R.CYCLP * NB + lane, NB};
-    k.blklp = Col<int>{si + (size_t)R.BLKLP * NB + lane, NB};
-    k.itmp = c.stage_cyc ? Col<int>{it + lane, NB} : Col<int>{c.itmp_g + w, c.ld};
-    k.fast_ix = si[(size_t)R.FASTIX * NB + lane];
-    double &cur = sd[(size_t)SROW(R.L) * NB + lane];
-    double &mult = sd[(size_t)SROW(R.M) * NB + lane];
-    int &nacc = si[(size_t)R.NACC * NB + lane];
+    k.r.u = Col<double>{sd + (size_t)R.U * MB + lane, MB};
+    k.r.c = sd[(size_t)R.C * MB + lane];
+    k.r.gset = sd[(size_t)R.G * MB + lane];
+    k.r.i97 = si[(size_t)R.I97 * MB + lane];
+    k.r.j97 = si[(size_t)R.J97 * MB + lane];
+    k.r.iset = si[(size_t)R.ISET * MB + lane];
+    k.R = c.stage_R ? Col<double>{sd + (size_t)R.R * MB + lane, MB} : Col<double>{c.sd + (size_t)R.R * W + w, c.ld};
+    k.P = Col<double>{sd + (size_t)SROW(R.P) * MB + lane, MB};
+    k.trial = Col<double>{sd + (size_t)SROW(R.T) * MB + lane, MB};
+    k.vec = Col<double>{vc + lane, MB};
+    k.cyc = c.stage_cyc ? Col<int>{si + (size_t)R.CYC * MB + lane, MB} : Col<int>{c.si + (size_t)R.CYC * W + w, c.ld};
+    k.cyclp = Col<int>{si + (size_t)R.CYCLP * MB + lane, MB};
+    k.blklp = Col<int>{si + (size_t)R.BLKLP * MB + lane, MB};
+    k.itmp = c.stage_cyc ? Col<int>{it + lane, MB} : Col<int>{c.itmp_g + w, c.ld};
+    k.fast_ix = si[(size_t)R.FASTIX * MB + lane];
+    double &cur = sd[(size_t)SROW(R.L) * MB + lane];
+    double &mult = sd[(size_t)SROW(R.M) * MB + lane];
+    int &nacc = si[(size_t)R.NACC * MB + lane];
 
     if (ACCEPT) {
         if (c.mask_on) {   // unchanged likelihoods keep the current point's term (calclike.f90:377-384)
@@ -644,12 +640,12 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
                 double v;
                 if (f == 0) v = c.cur_terms[(size_t)l * W + w];
                 else if (c.like_out[l]) v = c.like_out[l][f - 1];        // sparse: compacted slot
-                else v = lk[(size_t)l * NB + lane];
-                lk[(size_t)l * NB + lane] = v;
+                else v = lk[(size_t)l * MB + lane];
+                lk[(size_t)l * MB + lane] = v;
             }
         }
         STAMP(8);
-        const double like = target_like(c, t, k.trial, Col<double>{lk + lane, NB}, par_test ? tq + lane : nullptr);
+        const double like = target_like(c, t, k.trial, Col<double>{lk + lane, MB}, par_test ? tq + lane : nullptr);
         STAMP(9);
         bool acc = false;
         if (like != LOGZERO) {
@@ -672,14 +668,14 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
 #pragma unroll
             for (int l = 0; l < MAXLIKE; l++)
                 if (l < c.n_like) {
-                    ct[l] = lk[(size_t)l * NB + lane];
+                    ct[l] = lk[(size_t)l * MB + lane];
                     c.cur_terms[(size_t)l * W + w] = ct[l];
                 }
         } else {
             mult += 1.0;
         }
         STAMP(11);
-        si[(size_t)R.ACCF * NB + lane] = acc ? 1 : 0;
+        si[(size_t)R.ACCF * MB + lane] = acc ? 1 : 0;
         if (hist_row) {
             for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = k.P[t.params_used[i]];
             hist_row[(size_t)c.n_used * c.W + w] = cur;
@@ -704,7 +700,7 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
         k.defer_rot = c.rot_defer;
         if (fast_only) proposal_fast(c, t, k);
         else proposal(c, t, k);
-        si[(size_t)R.PROT * NB + lane] = k.pend_rot + 1;             // rot_kernel finishes this walker
+        si[(size_t)R.PROT * MB + lane] = k.pend_rot + 1;             // rot_kernel finishes this walker
         if (k.pend_rot >= 0) {
             if (par_map) tq[lane] = -1.0;
         } else if (par_map) tq[lane] = (double)k.pend_b;             // the block, for the mapping waves
@@ -716,12 +712,12 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
         }
     }
     STAMP(4);
-    sd[(size_t)R.C * NB + lane] = k.r.c;
-    sd[(size_t)R.G * NB + lane] = k.r.gset;
-    si[(size_t)R.I97 * NB + lane] = k.r.i97;
-    si[(size_t)R.J97 * NB + lane] = k.r.j97;
-    si[(size_t)R.ISET * NB + lane] = k.r.iset;
-    si[(size_t)R.FASTIX * NB + lane] = k.fast_ix;
+    sd[(size_t)R.C * MB + lane] = k.r.c;
+    sd[(size_t)R.G * MB + lane] = k.r.gset;
+    si[(size_t)R.I97 * MB + lane] = k.r.i97;
+    si[(size_t)R.J97 * MB + lane] = k.r.j97;
+    si[(size_t)R.ISET * MB + lane] = k.r.iset;
+    si[(size_t)R.FASTIX * MB + lane] = k.fast_ix;
     }
     if (par_map) {   // UpdateParams' mapping product, rows spread over the waves (one thread per row, same order)
         __syncthreads();
@@ -731,23 +727,23 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
             const int n = t.blk_n[b], nc = t.blk_nchanged[b];
             const double *M = t.mapping + t.blk_map_off[b];
             const int *chg = t.changed + t.blk_changed_off[b];
-            double *trial = sd + (size_t)SROW(R.T) * NB + lane;
+            double *trial = sd + (size_t)SROW(R.T) * MB + lane;
             const double *vec = vc + lane;
-            for (int j = wave; j < nc; j += MH_WAVES) {
+            for (int j = grp; j < nc; j += NV) {
                 double s = 0.0;
-                for (int q = 0; q < n; q++) s += M[j * n + q] * vec[(size_t)q * NB];
-                trial[(size_t)chg[j] * NB] += s;
+                for (int q = 0; q < n; q++) s += M[j * n + q] * vec[(size_t)q * MB];
+                trial[(size_t)chg[j] * MB] += s;
             }
         }
         __syncthreads();
         STAMP(12);
-        if (wave == 0 && act && si[(size_t)R.PROT * NB + lane] == 0) {
-            const double *trial = sd + (size_t)SROW(R.T) * NB + lane;
+        if (grp == 0 && act && si[(size_t)R.PROT * MB + lane] == 0) {
+            const double *trial = sd + (size_t)SROW(R.T) * MB + lane;
             for (int l = 0; l < c.n_like; l++)
                 for (int q = 0; q < c.like_nn[l]; q++)
-                    c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = trial[(size_t)ti[c.like_nidx[l] + q] * NB];
+                    c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = trial[(size_t)ti[c.like_nidx[l] + q] * MB];
             if (c.mask_on)
-                write_like_flags(c, Col<const double>{trial, NB}, Col<const double>{sd + (size_t)SROW(R.P) * NB + lane, NB},
+                write_like_flags(c, Col<const double>{trial, MB}, Col<const double>{sd + (size_t)SROW(R.P) * MB + lane, MB},
                                  w);
         }
     }
@@ -755,12 +751,12 @@ __global__ __launch_bounds__(NB * MH_WAVES) void mh_kernel(DevCfg c, int fast_on
     STAMP(13);
     if (!act) return;
     if (skipR) {
-        stage_out(c.sd, sd, 0, 0, R.R, W, w, lane, wave, MH_WAVES);
-        stage_out(c.sd, sd, R.R, rEnd, R.ND, W, w, lane, wave, MH_WAVES);
+        stage_out(c.sd, sd, 0, 0, R.R, W, w, lane, grp, NV);
+        stage_out(c.sd, sd, R.R, rEnd, R.ND, W, w, lane, grp, NV);
     } else {
-        stage_out(c.sd, sd, 0, 0, R.ND, W, w, lane, wave, MH_WAVES);
+        stage_out(c.sd, sd, 0, 0, R.ND, W, w, lane, grp, NV);
     }
-    stage_out(c.si, si, 0, 0, ni_st, W, w, lane, wave, MH_WAVES);
+    stage_out(c.si, si, 0, 0, ni_st, W, w, lane, grp, NV);
     STAMP(5);
 #ifdef CMAMD_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1308,10 +1304,9 @@ static size_t mh_lds_bytes(const cmbs *s) {
     const int nd_st = d.stage_R ? d.rows.ND : d.rows.ND - d.rows.RR;
     const int ni_st = d.stage_cyc ? d.rows.NI : d.rows.CYC;
     const int ntd = d.stage_cov ? d.tl.n_dbl : d.tl.covinv;
-    return (size_t)(nd_st + MAXLIKE + d.max_blk + d.tq_rows + d.def_cap * (QF_GROUPS + 1) +
-                    (d.sg_cap ? d.sg.ntask + 2 * d.sg.nX : 0)) * NB * 8 +
+    return (size_t)(nd_st + MAXLIKE + d.max_blk + d.tq_rows + d.def_cap * (QF_GROUPS + 1)) * MB * 8 +
            (size_t)((ntd + 31) & ~31) * 8 +
-           (size_t)(ni_st + (d.stage_cyc ? d.all_n : 0)) * NB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 + 64;
+           (size_t)(ni_st + (d.stage_cyc ? d.all_n : 0)) * MB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 + 64;
 }
 
 static void set_mh_lds(cmbs *s) {
@@ -1323,15 +1318,9 @@ static void set_mh_lds(cmbs *s) {
     const size_t cap = 160 * 1024;
     d.stage_R = d.stage_cyc = d.stage_cov = 1;
     d.tq_rows = d.test_like ? s->n_used : 1;   // a row per test-Gaussian row, or one (the proposal's block)
-    d.def_cap = 0;
-    d.sg_cap = 0;
-    for (int i : s->defer_likes) {
-        if (s->likes[i].like->like->deferred_capable()) d.def_cap++;
-        else d.sg_cap = 1;
-    }
+    d.def_cap = (int)s->defer_likes.size();
     if (mh_lds_bytes(s) > cap) {               // the deferred combines go first: the likelihoods combine in-launch
         d.def_cap = 0;
-        d.sg_cap = 0;
         s->defer_likes.clear();
     }
     if (mh_lds_bytes(s) > cap) d.stage_R = 0;
@@ -1608,7 +1597,7 @@ static void set_change_mask(cmbs *s);
 
 // Segment starts (absolute l, even) about TP_MAXL apart over [lo, hi] at which
 // none of the bins [b.first, b.second] is split.
-static std::vector<int> bin_safe_cuts(const std::vector<std::pair<int, int>> &bins, int lo, int hi) {
+static std::vector<int> bin_safe_cuts(const std::vector<std::pair<int, int>> &bins, int lo, int hi, int L) {
     auto valid = [&](int c) {
         if (c % 2 != 0) return false;
         for (auto &b : bins)
@@ -1617,11 +1606,11 @@ static std::vector<int> bin_safe_cuts(const std::vector<std::pair<int, int>> &bi
     };
     std::vector<int> cuts;
     int pos = lo;
-    while (pos + TP_MAXL <= hi) {
+    while (pos + L <= hi) {
         int c = -1;
-        for (int x = pos + TP_MAXL; x > pos && c < 0; x--)
+        for (int x = pos + L; x > pos && c < 0; x--)
             if (valid(x)) c = x;
-        for (int x = pos + TP_MAXL + 1; x <= hi && c < 0; x++)
+        for (int x = pos + L + 1; x <= hi && c < 0; x++)
             if (valid(x)) c = x;
         if (c < 0) break;
         cuts.push_back(c);
@@ -1669,7 +1658,7 @@ static void setup_fusion(cmbs *s) {
                         hi = std::max(hi, c.hi);
                     }
                 if (hi < lo) continue;
-                starts[kv.first] = bin_safe_cuts(kv.second, lo & ~1, hi);
+                starts[kv.first] = bin_safe_cuts(kv.second, lo & ~1, hi, TP_MAXL);
             }
             // the handle may be shared (standalone calls, other samplers): its
             // segmentation changes only if the fused pass is kept
@@ -1746,25 +1735,11 @@ void sampler_add_likelihood(cmbs *s, cmbl_t *like, const int *nuisance_indices, 
     set_change_mask(s);
     // likelihoods whose quadratic-form combine the accepting mh_kernel can take
     // over (dense evaluation only: the sparse ones write compacted slots)
-    // and the one small gaussian likelihood whose whole chi^2 it can form
     s->defer_likes.clear();
-    int n_qf = 0;
-    bool have_sg = false;
-    for (int i = 0; i < (int)s->likes.size(); i++) {
+    for (int i = 0; i < (int)s->likes.size() && (int)s->defer_likes.size() < MAXDEF; i++) {
         bool sparse = false;
         for (int q : s->sparse_likes) sparse |= q == i;
-        if (sparse) continue;
-        Like &L = *s->likes[i].like->like;
-        SmallGaussDev sg{};
-        if (L.deferred_capable() && n_qf < MAXDEF) {
-            s->defer_likes.push_back(i);
-            n_qf++;
-        } else if (!have_sg && L.deferred_small(sg)) {
-            s->defer_likes.push_back(i);
-            s->dc.sg = sg;
-            s->dc.sg_like = i;
-            have_sg = true;
-        }
+        if (!sparse && s->likes[i].like->like->deferred_capable()) s->defer_likes.push_back(i);
     }
     for (int i = 0; i < MAXLIKE; i++) s->like_ws[i].release();
     set_mh_lds(s);
@@ -1825,14 +1800,6 @@ static bool is_deferred(const cmbs *s, size_t i) {
 }
 
 static void record_deferred(cmbs *s, size_t i, const QFDeferred &d) {
-    if (d.kind == 1) {
-        if ((int)i != s->dc.sg_like || s->pending_sg) fail(CMBL_ERR_ARG, "internal: unexpected small-gaussian deferral");
-        s->pending_sg = 1;
-        s->dc.sg_partial = d.partial;
-        s->dc.sg_nuis = d.nuis;
-        s->dc.sg_ld_nuis = d.ld_nuis;
-        return;
-    }
     const int p = s->pending_def++;
     s->dc.def_like[p] = (int)i;
     s->dc.def_items[p] = d.n_items;
@@ -1996,17 +1963,14 @@ static HistRow next_hist(cmbs *s) {
 
 static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const HistRow &row, hipStream_t stream,
                       int g0, int g1, bool masked = false) {
-    const dim3 g((g1 - g0 + NB - 1) / NB), b(NB * MH_WAVES);
-    const int blk0 = g0 / NB;
+    const dim3 g((g1 - g0 + MB - 1) / MB), b(MH_THREADS);
+    const int blk0 = g0 / MB;
     const size_t lds = s->mh_lds;
     DevCfg dc = s->dc;
     dc.mask_on = masked ? 1 : 0;
-    if ((s->pending_def || s->pending_sg) && !accept)
-        fail(CMBL_ERR_ARG, "internal: deferred likelihoods without an accepting step");
+    if (s->pending_def && !accept) fail(CMBL_ERR_ARG, "internal: deferred likelihoods without an accepting step");
     dc.n_def = s->pending_def;
-    dc.n_sg = s->pending_sg;
     s->pending_def = 0;
-    s->pending_sg = 0;
     timed_launch("mh_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
         if (accept && propose)
             hipExtLaunchKernelGGL(mh_kernel<true, true>, g, b, lds, stream, e0, e1, 0, dc, fast_only, row.p, row.t, blk0);
@@ -2521,5 +2485,3 @@ extern "C" int cmamd_debug_stamps(unsigned long long *host) {
 // number of work items of the sampler's fused window pass (0: none); for tests
 // (without one: minus the last set-up check passed)
 extern "C" int cmamd_debug_fused(const cmbs *s) { return !s ? 0 : s->tpass ? s->tpass->n_items() : -s->tp_why; }
-// test hook: the likelihoods the accepting mh_kernel finishes (split-K combines + 100 x small gaussian)
-extern "C" int cmamd_debug_deferred(const cmbs *s) { return !s ? 0 : s->dc.def_cap + 100 * s->dc.sg_cap; }

@@ -704,43 +704,3 @@ def test_dragging_fused_plik_lensing(cmbl_golden, refdata, tmp_path):
         assert terms[1, w] == pytest.approx(ol.loglike(th[w], P[w, 1:2]), rel=1e-10)
         ref = terms[0, w] + terms[1, w] + 0.5 * ((P[w, 1] - 1.0) / 0.0025) ** 2
         assert lk[w] == pytest.approx(ref, rel=1e-12)
-
-
-@pytest.mark.parametrize("case,W", [("lensing_consext8", 200), ("sptsz_aberration_calprior", 70)])
-def test_deferred_small_gaussian_bitwise(cmbl_golden, refdata, case, W):
-    """In fast steps a small gaussian CMBlikes likelihood (Planck lensing, 9
-    bandpowers; SPT-SZ, 47) leaves its whole chi^2 to the accepting mh_kernel
-    (QFDeferred kind 1, smallgauss.h); the terms it forms are bit-identical to
-    cmbl_loglike_batch's cmbl_gauss_small_kernel at the same points."""
-    import os
-
-    from cosmomc_amd import _native as N
-    from cosmomc_amd.likelihood import NativeCMBLikelihood
-    from cosmomc_amd.sampler import BatchedMCMC
-    c = cmbl_golden["cases"][case]
-    like = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
-    nn = len(like.nuisance_names)
-    like.nuisance_indices = list(range(2, 2 + nn))
-    steps = 8
-    lmax = max(like.lmax_needed(), 2508)
-    th = syn.walker_theory(W, seed=9, n_fields=10, lmax=lmax, ld_field=lmax + 4)
-    dl = torch.tensor(th, device="cuda")
-    npar = 1 + nn
-    P0 = np.array([0.0222] + [1.0] * nn)
-    pmin, pmax = P0.copy(), P0.copy()
-    pmin[1], pmax[1] = P0[1] * 0.9, P0[1] * 1.1
-    s = BatchedMCMC(W, npar, [2], [[1]], 0, pmin, pmax, seed_ij=59, seed_kl=70)
-    s.set_covariance(np.array([[(0.002 * P0[1]) ** 2]]))
-    s.add_likelihood(like, dl)
-    assert N.lib().cmamd_debug_deferred(s._h) >= 100
-    s.enable_history(steps)
-    s.set_start(np.tile(P0, (W, 1)))
-    s.step(steps, fast_only=True)
-    hist = s.history_host(0, steps)
-    terms = s.history_terms(0, steps)
-    assert len(set(hist[:, 0, :].ravel())) > W, "the calibration never moved"
-    for k in (0, steps // 2, steps - 1):
-        nu = np.tile(P0[1:], (W, 1))
-        nu[:, 0] = hist[k, 0, :]
-        ref = like.loglike_batch(dl, torch.tensor(nu, device="cuda")).cpu().numpy()
-        assert np.array_equal(terms[k, 0], ref), np.abs(terms[k, 0] - ref).max()
