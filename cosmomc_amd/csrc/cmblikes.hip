@@ -962,29 +962,23 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
         for (int rr = 0; rr < M - 1; rr++) {
             const int p = on ? hl_partner<M>(rr, r) : r;
             HL_STAMP(t0);
-            if (on) {
-#pragma unroll
-                for (int k = 0; k < M; k++) {
-                    S.rows[grp][0][r][k] = G[k];
-                    S.rows[grp][1][r][k] = V[k];
-                }
-                S.dg[grp][r] = nrm;
-            }
-            __syncthreads();
+            // the partner's column and norm by lane permutes (ds_bpermute: no LDS
+            // banks, no barrier; the same values the row buffers carried)
+            const int src = on ? grp * M + p : lane;
             HL_STAMP(t1);
 #ifdef CMAMD_STAMPS
             unsigned long long t2 = 0;
 #endif
             double Gp[M], Vp[M];
 #pragma unroll
-            for (int k = 0; k < M; k++) {        // every load in flight together
-                Gp[k] = on ? S.rows[grp][0][p][k] : 0.0;
-                Vp[k] = on ? S.rows[grp][1][p][k] : 0.0;
+            for (int k = 0; k < M; k++) {        // every permute in flight together
+                Gp[k] = __shfl(G[k], src);
+                Vp[k] = __shfl(V[k], src);
             }
+            const double np_ = __shfl(nrm, src);
             if (on) {
                 const bool low = r < p;
-                const double np = S.dg[grp][p];
-                const double all = low ? nrm : np, ahh = low ? np : nrm;
+                const double all = low ? nrm : np_, ahh = low ? np_ : nrm;
                 double alh = 0.0;
 #pragma unroll
                 for (int k = 0; k < M; k++) alh = fma(low ? G[k] : Gp[k], low ? Gp[k] : G[k], alh);
@@ -1019,7 +1013,6 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
                     }
                 }
             }
-            __syncthreads();                           // partners' columns read: the next round may write
 #ifdef CMAMD_STAMPS
             {
                 const unsigned long long t3 = __builtin_amdgcn_s_memtime();

@@ -367,14 +367,17 @@ __device__ inline double test_row(const DevCfg &c, const Tabs &t, const Q &q, in
 
 // trows (stride MB), when given, holds test_row(i) for every i, computed by
 // the other waves of mh_kernel: the same sums in the same order
+// zrows / oobv (stride MB), when given, hold every parameter's squared prior z
+// (0 where there is no prior) and the bounds verdict of q, formed by the other
+// thread groups: the same terms, summed here in the same order
 template <class Q, class L>
 __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const L &likes,
-                              const double *trows = nullptr)
+                              const double *trows = nullptr, const double *zrows = nullptr, const int *oobv = nullptr)
 {
     // the parameter loops load RCH entries at a time (all in flight together;
     // the chain wave would otherwise wait out one LDS round trip per entry)
-    bool oob = false;
-    for (int i0 = 0; i0 < c.np; i0 += RCH) {                         // GetLogLikeBounds :97-109
+    bool oob = oobv ? *oobv != 0 : false;
+    for (int i0 = 0; !oobv && i0 < c.np; i0 += RCH) {                // GetLogLikeBounds :97-109
         double qv[RCH], hi[RCH], lo[RCH];
 #pragma unroll
         for (int u = 0; u < RCH; u++) {
@@ -406,7 +409,15 @@ __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const 
     double like = main / c.temperature;
     if (c.has_priors) {                                              // GetLogPriors :111-134
         double pri = 0.0;
-        for (int i0 = 0; i0 < c.np; i0 += RCH) {   // std already 0 where the varying/include_fixed gate (:119) is off
+        for (int i0 = 0; zrows && i0 < c.np; i0 += RCH) {
+            double zv[RCH];
+#pragma unroll
+            for (int u = 0; u < RCH; u++) zv[u] = zrows[(size_t)(i0 + u < c.np ? i0 + u : 0) * MB];
+#pragma unroll
+            for (int u = 0; u < RCH; u++)
+                if (i0 + u < c.np) pri += zv[u];
+        }
+        for (int i0 = 0; !zrows && i0 < c.np; i0 += RCH) {   // std already 0 where the varying/include_fixed gate (:119) is off
             double qv[RCH], mu[RCH], sd[RCH];
 #pragma unroll
             for (int u = 0; u < RCH; u++) {
@@ -493,12 +504,17 @@ __device__ inline void dma_words(void *dst, const void *src, int n, int lane, in
     }
 }
 
-// write-back: group v of nv (MB threads each, lane = walker) stores rows r0 + v, r0 + v + nv, ...
+// write-back of LDS rows [row][MB] (src rows src_r0 + (r - r0)) to HBM rows r
+// in [r0, r1), columns wb .. wb+MB-1: 16 bytes per thread (MB = 16 doubles is 8
+// threads a row, 16 ints 4 threads), all threads of the block, rows round-robin
 template <class T>
-__device__ void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size_t ld, int w, int lane, int v = 0,
-                          int nv = 1)
+__device__ inline void stage_out(T *dst, const T *src, int src_r0, int r0, int r1, size_t ld, int wb)
 {
-    for (int r = r0 + v; r < r1; r += nv) dst[(size_t)r * ld + w] = src[(size_t)(src_r0 + r - r0) * MB + lane];
+    constexpr int PER = 16 / sizeof(T), TPR = MB / PER, RPB = MH_THREADS / TPR;   // per thread, threads per row, rows per pass
+    const int tr = threadIdx.x / TPR, col = (threadIdx.x % TPR) * PER;
+    for (int r = r0 + tr; r < r1; r += RPB)
+        *reinterpret_cast<uint4 *>(dst + (size_t)r * ld + wb + col) =
+            *reinterpret_cast<const uint4 *>(src + (size_t)(src_r0 + r - r0) * MB + col);
 }
 
 // changeMask of the trial (TheoryLike_GetLogLikeMain, calclike.f90:302-306):
@@ -545,6 +561,9 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
     int *si = reinterpret_cast<int *>(td + ((ntd + 31) & ~31));  // [ni_st][MB]
     int *it = si + (size_t)ni_st * MB;                           // [all_n][MB] when stage_cyc
     int *ti = it + (size_t)(c.stage_cyc ? c.all_n : 0) * MB;     // [n_int rounded to 64]
+    int *oobw = ti + ((c.tl.n_int + 63) & ~63);                  // [MB] trial out of bounds (par_prior)
+    double *zz = reinterpret_cast<double *>(oobw + MB);          // [np][MB] the trial's squared prior z (par_prior)
+    if (threadIdx.x < MB) oobw[threadIdx.x] = 0;
     const bool skipR = !c.stage_R;
     // staged double row index of global row r (rotation rows dropped when not staged)
 #define SROW(r) ((skipR && (r) >= R.R) ? (r) - R.RR : (r))
@@ -601,11 +620,29 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
     // by the chain wave
     const bool par_test = ACCEPT && c.test_like && c.n_used >= 4 && c.tq_rows >= c.n_used;
     const bool par_map = PROPOSE && c.max_blk >= 4 && c.tq_rows >= 1;
-    if (par_test) {
+    // the trial's bounds check and squared Gaussian-prior z of every parameter,
+    // spread over the thread groups (the chain thread then only sums them in order)
+    const bool par_prior = ACCEPT;
+    if (par_test || par_prior) {
         if (act) {
             const Tabs t0 = make_tabs(c, ti, td, c.stage_cov ? td : c.tab_d);
             const Col<double> q{sd + (size_t)SROW(R.T) * MB + lane, MB};
-            for (int i = grp; i < c.n_used; i += NV) tq[(size_t)i * MB + lane] = test_row(c, t0, q, i);
+            if (par_test)
+                for (int i = grp; i < c.n_used; i += NV) tq[(size_t)i * MB + lane] = test_row(c, t0, q, i);
+            if (par_prior) {
+                int oob = 0;
+                for (int i = grp; i < c.np; i += NV) {
+                    const double qv = q[i];
+                    if (qv > t0.pmax[i] || qv < t0.pmin[i]) oob = 1;   // GetLogLikeBounds :97-109
+                    double z2 = 0.0;
+                    if (c.has_priors && t0.pstd[i] != 0.0) {           // GetLogPriors :111-124
+                        const double z = (qv - t0.pmean[i]) / t0.pstd[i];
+                        z2 = z * z;
+                    }
+                    zz[(size_t)i * MB + lane] = z2;
+                }
+                if (oob) atomicOr(&oobw[lane], 1);
+            }
         }
         __syncthreads();
     }
@@ -645,7 +682,8 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
             }
         }
         STAMP(8);
-        const double like = target_like(c, t, k.trial, Col<double>{lk + lane, MB}, par_test ? tq + lane : nullptr);
+        const double like = target_like(c, t, k.trial, Col<double>{lk + lane, MB}, par_test ? tq + lane : nullptr,
+                                        par_prior ? zz + lane : nullptr, par_prior ? oobw + lane : nullptr);
         STAMP(9);
         bool acc = false;
         if (like != LOGZERO) {
@@ -749,14 +787,15 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
     }
     __syncthreads();
     STAMP(13);
-    if (!act) return;
+    // write back the image (rows of walkers past W are padding of the ld-wide
+    // rows: written back unchanged)
     if (skipR) {
-        stage_out(c.sd, sd, 0, 0, R.R, W, w, lane, grp, NV);
-        stage_out(c.sd, sd, R.R, rEnd, R.ND, W, w, lane, grp, NV);
+        stage_out(c.sd, sd, 0, 0, R.R, W, wb);
+        stage_out(c.sd, sd, R.R, rEnd, R.ND, W, wb);
     } else {
-        stage_out(c.sd, sd, 0, 0, R.ND, W, w, lane, grp, NV);
+        stage_out(c.sd, sd, 0, 0, R.ND, W, wb);
     }
-    stage_out(c.si, si, 0, 0, ni_st, W, w, lane, grp, NV);
+    stage_out(c.si, si, 0, 0, ni_st, W, wb);
     STAMP(5);
 #ifdef CMAMD_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1306,7 +1345,8 @@ static size_t mh_lds_bytes(const cmbs *s) {
     const int ntd = d.stage_cov ? d.tl.n_dbl : d.tl.covinv;
     return (size_t)(nd_st + MAXLIKE + d.max_blk + d.tq_rows + d.def_cap * (QF_GROUPS + 1)) * MB * 8 +
            (size_t)((ntd + 31) & ~31) * 8 +
-           (size_t)(ni_st + (d.stage_cyc ? d.all_n : 0)) * MB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 + 64;
+           (size_t)(ni_st + (d.stage_cyc ? d.all_n : 0)) * MB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 +
+           MB * 4 + (size_t)d.np * MB * 8 + 64;
 }
 
 static void set_mh_lds(cmbs *s) {
