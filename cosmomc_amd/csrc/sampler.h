@@ -49,6 +49,10 @@ struct DevCfg {
     double propose_scale, temperature;
     int has_priors, test_like, n_lin;
     int rot_defer;          // mh_kernel leaves new rotations of blocks >= ROT_DEFER_MIN to rot_kernel
+    int *rot_list;          // [ld] walkers whose rotation is pending, listed per 64-walker-aligned range from its start
+    int *rot_cnt;           // [ld / 64][2] list lengths; a proposing launch appends to rot_par, zeroes the other
+    int rot_par;            // set per launch
+    int rot_serial;         // debug: every rotation by rot_kernel's serial path
     Rows rows;
     TabLayout tl;
     const int *tab_i;       // [tl.n_int] (allocation padded to a multiple of 64 words)
@@ -99,6 +103,9 @@ struct cmbs {
     int W = 0, np = 0, n_used = 0;
     std::vector<int> params_used;
     std::string last_error;
+    cmamd::DevBuf rot;                  // rotation lists + counters (DevCfg::rot_list / rot_cnt)
+    std::vector<int> rot_par;
+    bool no_stage_R = false;            // debug: keep the rotation rows in HBM (cmamd_debug_stage_R)           // per 64-walker range: the counter the next proposing launch appends to
     cmamd::DevBuf tab_i, tab_d, sd, si, like_terms, cur_terms, ws, hist, hist_terms, mom, itmp_g;
     cmamd::DevBuf nuis_bufs[cmamd::MAXLIKE];
     std::vector<int> h_tab_i;

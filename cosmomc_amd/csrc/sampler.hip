@@ -564,6 +564,10 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
     int *oobw = ti + ((c.tl.n_int + 63) & ~63);                  // [MB] trial out of bounds (par_prior)
     double *zz = reinterpret_cast<double *>(oobw + MB);          // [np][MB] the trial's squared prior z (par_prior)
     if (threadIdx.x < MB) oobw[threadIdx.x] = 0;
+    // the rotation list of this walker range: this launch appends to counter
+    // rot_par; the other one (read by the previous step's rot_kernel) restarts
+    if (PROPOSE && c.rot_defer && blockIdx.x == 0 && threadIdx.x == 0)
+        c.rot_cnt[2 * (blk0 * MB / 64) + (c.rot_par ^ 1)] = 0;
     const bool skipR = !c.stage_R;
     // staged double row index of global row r (rotation rows dropped when not staged)
 #define SROW(r) ((skipR && (r) >= R.R) ? (r) - R.RR : (r))
@@ -740,6 +744,8 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
         else proposal(c, t, k);
         si[(size_t)R.PROT * MB + lane] = k.pend_rot + 1;             // rot_kernel finishes this walker
         if (k.pend_rot >= 0) {
+            const int slot = atomicAdd(c.rot_cnt + 2 * (blk0 * MB / 64) + c.rot_par, 1);
+            c.rot_list[blk0 * MB + slot] = w;
             if (par_map) tq[lane] = -1.0;
         } else if (par_map) tq[lane] = (double)k.pend_b;             // the block, for the mapping waves
         else {
@@ -807,12 +813,31 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
 // ------------------------------------------------------- deferred rotations
 // A new random rotation of a block of ROT_DEFER_MIN or more parameters
 // (RotMatrix propose.f90:88-102 -> RandRotationD RandUtils.f90:133-153) is too
-// big for one lane: mh_kernel stops that walker's proposal at the rotation
-// (Rows::PROT) and this kernel, one wave per walker, finishes it.  Lane q owns
-// column q of the new R in registers; lane 0 draws the Gaussians, and every
-// sum of the modified Gram-Schmidt is formed from the lanes' products in q
-// order (readlane broadcasts), as rot_matrix does, so R is bit-identical.  Then the rest of ProposeVec
-// (proposal_tail), the nuisance scatter and the change-mask flags.
+// big for the chain lane: mh_kernel stops that walker's proposal at the
+// rotation (Rows::PROT), appends the walker to the step's rotation list, and
+// rot_kernel, one wave per listed walker, finishes it.
+//
+// The Gaussians.  RANMAR's lagged-Fibonacci part is x_m = x_{m-97} - x_{m-33}
+// mod 1 (RandUtils.f90:350-374), an integer recurrence mod 2^24 in units of
+// 2^-24, and its carry c_m = c - (m+1) cd mod cm has a closed form, so the 64
+// lanes make 64 uniforms per round (lanes 33..63 substitute x_{m-33} =
+// x_{m-130} - x_{m-66}).  The lanes then take Gaussian1's polar pairs
+// (uniforms 2p, 2p+1, RandUtils.f90:156-178) 32 at a time, and the accepted
+// pairs are placed by a ballot prefix in stream order (v2 fac, then the saved
+// deviate v1 fac).  Nothing is committed until the rotation is done; then the
+// state advances by exactly the uniforms the consumed Gaussians used (ring,
+// i97/j97, c, iset, gset): bit-identical to drawing them one at a time.
+//
+// Gram-Schmidt.  Lane j owns row j's vec in registers.  Row i is final once
+// its projections on rows 0..i-1 are done, so the rows advance in lockstep:
+// at iteration i lane i takes its norm (below 1e-3 row i is redrawn and the
+// later rows restart on the shifted Gaussians) and publishes R(i,:) in LDS,
+// then every lane j > i projects onto it.  Every sum runs over q in order, as
+// the reference's sum() and rot_matrix do, so R is bit-identical.  A rotation
+// whose Gaussians would overflow the LDS buffers (many redraws) is redone by
+// the serial path (lane 0 draws, the lanes project with readlane sums), which
+// is also the debug reference (DevCfg::rot_serial).
+
 // sum of x over lanes 0..n-1 in lane order, formed identically on every lane
 // from v_readlane broadcasts (no LDS round trip, no divergent lane-0 section)
 __device__ __forceinline__ double lane_sum_ordered(double x, int n)
@@ -830,80 +855,340 @@ __device__ __forceinline__ double lane_sum_ordered(double x, int n)
     return s;
 }
 
+__device__ __forceinline__ double readlane_f64(double x, int q)
+{
+    const long long bits = __double_as_longlong(x);
+    const unsigned l = (unsigned)__builtin_amdgcn_readlane((int)bits, q);
+    const long long h = __builtin_amdgcn_readlane((int)(bits >> 32), q);
+    return __longlong_as_double((h << 32) | l);
+}
+
+// LDS written by some lanes of a wave and read by others (the wave's LDS
+// operations complete in order; this keeps the compiler from moving them)
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+static constexpr int ROT_WAVES = 4;                        // walkers per rot_kernel workgroup
+static constexpr int ROT_GC = MAXBLK * (MAXBLK + 4);       // Gaussians a parallel rotation may use
+static constexpr int ROT_GA = ROT_GC + 64;                 // + one round's overshoot
+static constexpr int ROT_UC = 1536;                        // uniforms (a multiple of 64)
+
+struct RotLds {
+    double g[ROT_GA];             // the Gaussian stream from the rotation's start (g[0] = gset if iset)
+    double rm[MAXBLK * MAXBLK];   // R(i, q) at rm[i * MAXBLK + q]
+    double u[98];                 // RANMAR u(1:97) as doubles (the state rows' form)
+    double gs[MAXBLK];            // serial path: one attempt's Gaussians
+    int x[ROT_UC];                // lagged-Fibonacci values x_m (units of 2^-24)
+    int o[ROT_UC];                // uniforms x_m - c_m (units of 2^-24)
+    int pi[ROT_GA / 2];           // pair index of the r-th accepted pair
+    int ui[100];                  // u(1:97) in units of 2^-24
+};
+
+struct RotGen {
+    int i97, j97, C0;             // RANMAR pointers and carry (units of 2^-24) at the start
+    int off;                      // 1 when the start state holds a saved deviate (iset)
+    int m = 0, p = 0, nr = 0;     // uniforms made, pairs taken, pairs accepted
+    int cbase;                    // carry before this round's first call: C0 - m cd mod cm
+    int ck;                       // this lane's (lane + 1) cd mod cm
+};
+
+__device__ __forceinline__ int mod97(int v) { return v >= 97 ? v - 97 : v; }   // v in [0, 194)
+
+__device__ __forceinline__ int rot_x(const RotLds &L, const RotGen &G, int p)
+{   // x_p; p in [-97, -1] is the start ring: u(i97 - 1 - p mod 97)
+    return p >= 0 ? L.x[p] : L.ui[mod97(G.i97 - 1 - p)];
+}
+
+__device__ __forceinline__ int sub24(int a, int b) { const int d = a - b; return d < 0 ? d + (1 << 24) : d; }
+
+static constexpr int RM_P = 16777213, RM_CD = 7654321;     // cm and cd in units of 2^-24
+
+__device__ void rot_round(RotLds &L, RotGen &G, int lane)
+{   // 64 uniforms, then the 32 polar pairs they hold
+    const int m = G.m + lane;
+    const int b = lane < 33 ? rot_x(L, G, m - 33) : sub24(rot_x(L, G, m - 130), rot_x(L, G, m - 66));
+    const int x = sub24(rot_x(L, G, m - 97), b);
+    int cm = G.cbase - G.ck;                 // c after call m: C0 - (m + 1) cd mod cm
+    if (cm < 0) cm += RM_P;
+    L.x[m] = x;
+    L.o[m] = sub24(x, cm);
+    G.m += 64;
+    G.cbase -= (64 * RM_CD) % RM_P;
+    if (G.cbase < 0) G.cbase += RM_P;
+    wave_sync();
+    const int p = G.p + lane;
+    bool acc = false;
+    double v1 = 0.0, v2 = 0.0, rr = 0.0;
+    if (lane < 32) {
+        v1 = 2.0 * ((double)L.o[2 * p] * (1.0 / 16777216.0)) - 1.0;
+        v2 = 2.0 * ((double)L.o[2 * p + 1] * (1.0 / 16777216.0)) - 1.0;
+        rr = v1 * v1 + v2 * v2;
+        acc = rr < 1.0;
+    }
+    const unsigned long long mask = __ballot(acc);
+    if (acc) {
+        const int r = G.nr + __popcll(mask & ((1ull << lane) - 1ull));
+        const double fac = sqrt(-2.0 * log(rr) / rr);
+        L.g[G.off + 2 * r] = v2 * fac;
+        L.g[G.off + 2 * r + 1] = v1 * fac;
+        L.pi[r] = p;
+    }
+    G.nr += __popcll(mask);
+    G.p += 32;
+    wave_sync();
+}
+
+__device__ __forceinline__ bool rot_fill(RotLds &L, RotGen &G, int need, int lane)
+{
+    if (need > ROT_GC) return false;
+    while (G.off + 2 * G.nr < need) {
+        if (G.m + 64 > ROT_UC) return false;
+        rot_round(L, G, lane);
+    }
+    return true;
+}
+
+// advance the RANMAR / Gaussian1 state past the first T Gaussians of the stream
+__device__ void rot_commit(RotLds &L, const RotGen &G, int T, Rng &r, int lane)
+{
+    const int t = T - G.off;
+    int K = 0;
+    if (t > 0) {
+        const int q = (t - 1) / 2;            // the pair that gave the last Gaussian
+        K = 2 * (L.pi[q] + 1);
+        r.iset = t & 1;
+        r.gset = L.g[G.off + 2 * q + 1];
+    } else {
+        r.iset = 0;
+    }
+    for (int s = lane; s < 97; s += 64) {    // ring slot s (u(s+1)) last written by call m = i97-1-s mod 97 (+97k)
+        const int r0 = mod97(G.i97 - 1 - s + 97);
+        if (K - 1 >= r0) L.ui[s] = L.x[r0 + 97 * ((K - 1 - r0) / 97)];
+        L.u[s] = (double)L.ui[s] * (1.0 / 16777216.0);
+    }
+    r.i97 = (G.i97 - 1 - K % 97 + 97) % 97 + 1;
+    r.j97 = (G.j97 - 1 - K % 97 + 97) % 97 + 1;
+    int cm = G.C0 - (int)((long long)K * RM_CD % RM_P);
+    if (cm < 0) cm += RM_P;
+    r.c = (double)cm * (1.0 / 16777216.0);
+    wave_sync();
+}
+
 #ifdef CMAMD_STAMPS
-__device__ unsigned long long g_rot_ticks[3];     // block 0: total, Gaussian draws, Gram-Schmidt + norms
+__device__ unsigned long long g_rot_ticks[3];     // first listed walker: total, Gaussian draws, Gram-Schmidt
+#define RTICK(v) (v) = __builtin_amdgcn_s_memtime()
+#else
+#define RTICK(v) ((void)0)
 #endif
 
-__global__ __launch_bounds__(64) void rot_kernel(DevCfg c, int w0)
+// One lockstep Gram-Schmidt pass over rows start..n-1 (row j from the n
+// Gaussians at g[gbase + (j - start) n]); NQ = n rounded up to 8.  The
+// padding columns q in [n, NQ) hold +0.0 in vec and in R, so every product
+// there is +0.0 and the sums (which start at +0.0) are bit-identical to sums
+// over q < n, with no selects.  Lane i publishes its raw vec and the lanes
+// divide one element each.  Returns the row that needs a redraw, or -1.
+template <int NQ>
+__device__ int rot_gs_pass(RotLds &L, int n, int start, int gbase, int lane)
 {
-    const int w = w0 + blockIdx.x, lane = threadIdx.x;
-    if (w >= c.W) return;
-    const size_t ld = c.ld;
-    const Rows &R = c.rows;
-    const int pend = c.si[(size_t)R.PROT * ld + w];
-    if (pend == 0) return;                              // block-uniform
-    const int b = pend - 1;
-    __shared__ double u_s[97], g[MAXBLK], vec_s[MAXBLK];
-    const Tabs t = make_tabs(c, c.tab_i, c.tab_d, c.tab_d);
-    const int n = t.blk_n[b], off = t.blk_R_off[b];
-    for (int i = lane; i < 97; i += 64) u_s[i] = c.sd[(size_t)(R.U + i) * ld + w];
-    Walker k;
-    k.r.u = Col<double>{u_s, 1};
-    k.r.c = c.sd[(size_t)R.C * ld + w];
-    k.r.gset = c.sd[(size_t)R.G * ld + w];
-    k.r.i97 = c.si[(size_t)R.I97 * ld + w];
-    k.r.j97 = c.si[(size_t)R.J97 * ld + w];
-    k.r.iset = c.si[(size_t)R.ISET * ld + w];
-    __syncthreads();
+    double v[NQ];
+    if (lane >= start && lane < n) {
+        const double *gv = L.g + gbase + (lane - start) * n;    // within g: gbase + n^2 + NQ <= ROT_GA
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            const double x = gv[q];
+            v[q] = q < n ? x : 0.0;
+        }
+    }
+    for (int i = 0; i < n; i++) {
+        if (i >= start) {
+            double norm = 0.0;
+            if (lane == i)
+#pragma unroll
+                for (int q = 0; q < NQ; q++) norm += v[q] * v[q];
+            norm = readlane_f64(norm, i);
+            if (!(norm > 1e-3)) return i;     // RandRotationD :143: draw row i again
+            double *ri = L.rm + i * MAXBLK;
+            if (lane == i)
+#pragma unroll
+                for (int q = 0; q < NQ; q += 2) *reinterpret_cast<double2 *>(ri + q) = make_double2(v[q], v[q + 1]);
+            wave_sync();
+            if (lane < NQ) {                  // R(i, q) = vec(q) / sqrt(norm), lane q
+                const double x = ri[lane];
+                ri[lane] = lane < n ? x / sqrt(norm) : 0.0;
+            }
+            wave_sync();
+        }
+        if (lane > i && lane < n) {           // vec = vec - sum(vec*R(i,:))*R(i,:)
+            const double *ri = L.rm + i * MAXBLK;
+            double rv[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; q += 2) {
+                const double2 t = *reinterpret_cast<const double2 *>(ri + q);
+                rv[q] = t.x;
+                rv[q + 1] = t.y;
+            }
+            double s = 0.0;
+#pragma unroll
+            for (int q = 0; q < NQ; q++) s += v[q] * rv[q];
+#pragma unroll
+            for (int q = 0; q < NQ; q++) v[q] = v[q] - s * rv[q];
+        }
+    }
+    return -1;
+}
+
+// the parallel rotation into L.rm; false (state untouched) when the buffers overflow
+__device__ bool rot_parallel(RotLds &L, Rng &r, int n, int lane, unsigned long long *tk)
+{
+    RotGen G;
+    G.i97 = r.i97;
+    G.j97 = r.j97;
+    G.C0 = (int)(r.c * 16777216.0);
+    G.off = r.iset ? 1 : 0;
+    G.cbase = G.C0;
+    G.ck = (lane + 1) * RM_CD % RM_P;                      // < 64 cd < 2^31
+    if ((G.i97 - G.j97 + 97) % 97 != 64) return false;     // not RMARIN's pointer pair: serial path
+    for (int s = lane; s < 97; s += 64) L.ui[s] = (int)(L.u[s] * 16777216.0);
+    if (lane == 0 && G.off) L.g[0] = r.gset;
+    wave_sync();
+    int start = 0, gbase = 0;
+    (void)tk;
+    for (;;) {                                // one pass per redraw
+#ifdef CMAMD_STAMPS
+        unsigned long long t0, t1;
+        RTICK(t0);
+#endif
+        if (!rot_fill(L, G, gbase + (n - start) * n, lane)) return false;
+#ifdef CMAMD_STAMPS
+        RTICK(t1);
+        tk[1] += t1 - t0;
+#endif
+        const int fail = n <= 8    ? rot_gs_pass<8>(L, n, start, gbase, lane)
+                         : n <= 16 ? rot_gs_pass<16>(L, n, start, gbase, lane)
+                         : n <= 24 ? rot_gs_pass<24>(L, n, start, gbase, lane)
+                                   : rot_gs_pass<32>(L, n, start, gbase, lane);
+        static_assert(MAXBLK == 32, "rot_gs_pass widths");
+#ifdef CMAMD_STAMPS
+        RTICK(t0);
+        tk[2] += t0 - t1;
+#endif
+        if (fail < 0) {
+            rot_commit(L, G, gbase + (n - start) * n, r, lane);
+            return true;
+        }
+        gbase += (fail - start) * n + n;
+        start = fail;
+    }
+}
+
+// the serial rotation into L.rm: lane 0 draws each attempt's Gaussians, lane q
+// holds column q of R, every sum is formed in q order from readlane broadcasts
+__device__ void rot_serial(RotLds &L, Rng &r, int n, int lane)
+{
     double rcol[MAXBLK];
 #pragma unroll
     for (int i = 0; i < MAXBLK; i++) rcol[i] = 0.0;
-#ifdef CMAMD_STAMPS
-    unsigned long long t_start = __builtin_amdgcn_s_memtime(), t_g = 0, t_m = 0, t0;
-#endif
     for (int j = 0; j < n; j++) {
         double v, norm;
         for (;;) {
-#ifdef CMAMD_STAMPS
-            t0 = __builtin_amdgcn_s_memtime();
-#endif
             if (lane == 0)
-                for (int q = 0; q < n; q++) g[q] = gaussian1(k.r);
-            __syncthreads();
-#ifdef CMAMD_STAMPS
-            t_g += __builtin_amdgcn_s_memtime() - t0;
-            t0 = __builtin_amdgcn_s_memtime();
-#endif
-            v = lane < n ? g[lane] : 0.0;
+                for (int q = 0; q < n; q++) L.gs[q] = gaussian1(r);
+            wave_sync();
+            v = lane < n ? L.gs[lane] : 0.0;
 #pragma unroll
             for (int i = 0; i < MAXBLK; i++) {
-                if (i < j) {                            // vec = vec - sum(vec*R(i,:))*R(i,:)
+                if (i < j) {
                     const double s = lane_sum_ordered(v * rcol[i], n);
                     v = v - s * rcol[i];
                 }
             }
             norm = lane_sum_ordered(v * v, n);
-#ifdef CMAMD_STAMPS
-            t_m += __builtin_amdgcn_s_memtime() - t0;
-#endif
+            wave_sync();
             if (norm > 1e-3) break;
         }
         const double rv = v / sqrt(norm);
 #pragma unroll
         for (int i = 0; i < MAXBLK; i++)
             if (i == j) rcol[i] = rv;
+        if (lane < n) L.rm[j * MAXBLK + lane] = rv;
     }
-    if (lane < n)
-#pragma unroll
-        for (int i = 0; i < MAXBLK; i++)
-            if (i < n) c.sd[(size_t)(R.R + off + i * n + lane) * ld + w] = rcol[i];
-    if (lane == 0) {   // R(:, 1) is lane 0's own column: the tail reads its own stores
-        k.R = Col<double>{c.sd + (size_t)R.R * ld + w, (int)ld};
-        k.trial = Col<double>{c.sd + (size_t)R.T * ld + w, (int)ld};
-        k.P = Col<double>{c.sd + (size_t)R.P * ld + w, (int)ld};
-        k.vec = Col<double>{vec_s, 1};
+    // lane 0's RNG state is the walker's: broadcast it
+    r.c = readlane_f64(r.c, 0);
+    r.gset = readlane_f64(r.gset, 0);
+    r.i97 = __builtin_amdgcn_readlane(r.i97, 0);
+    r.j97 = __builtin_amdgcn_readlane(r.j97, 0);
+    r.iset = __builtin_amdgcn_readlane(r.iset, 0);
+    wave_sync();
+}
+
+__global__ __launch_bounds__(64 * ROT_WAVES) void rot_kernel(DevCfg c, int g0)
+{
+    extern __shared__ __attribute__((aligned(16))) double rot_lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int idx = blockIdx.x * ROT_WAVES + wave;
+    if (idx >= c.rot_cnt[2 * (g0 / 64) + c.rot_par]) return;   // wave-uniform
+    const int w = c.rot_list[g0 + idx];
+    const size_t ld = c.ld;
+    const Rows &R = c.rows;
+    const int b = c.si[(size_t)R.PROT * ld + w] - 1;
+    RotLds &L = reinterpret_cast<RotLds *>(rot_lds)[wave];
+    const Tabs t = make_tabs(c, c.tab_i, c.tab_d, c.tab_d);
+    const int n = t.blk_n[b], off = t.blk_R_off[b];
+    for (int i = lane; i < 97; i += 64) L.u[i] = c.sd[(size_t)(R.U + i) * ld + w];
+    Walker k;
+    k.r.u = Col<double>{L.u, 1};
+    k.r.c = c.sd[(size_t)R.C * ld + w];
+    k.r.gset = c.sd[(size_t)R.G * ld + w];
+    k.r.i97 = c.si[(size_t)R.I97 * ld + w];
+    k.r.j97 = c.si[(size_t)R.J97 * ld + w];
+    k.r.iset = c.si[(size_t)R.ISET * ld + w];
+    wave_sync();
+    unsigned long long tk[3] = {0, 0, 0};
+#ifdef CMAMD_STAMPS
+    RTICK(tk[0]);
+#endif
+    if (c.rot_serial || !rot_parallel(L, k.r, n, lane, tk)) rot_serial(L, k.r, n, lane);
+#ifdef CMAMD_STAMPS
+    if (idx == 0 && lane == 0) {
+        g_rot_ticks[0] = __builtin_amdgcn_s_memtime() - tk[0];
+        g_rot_ticks[1] = tk[1];
+        g_rot_ticks[2] = tk[2];
+    }
+#endif
+    // R(i, q) (rm, row stride MAXBLK) -> the state rows and a packed copy (row stride n) in g
+    for (int e = lane; e < n * n; e += 64) {
+        const double x = L.rm[(e / n) * MAXBLK + e % n];
+        c.sd[(size_t)(R.R + off + e) * ld + w] = x;
+        L.g[e] = x;
+    }
+    wave_sync();
+    k.trial = Col<double>{c.sd + (size_t)R.T * ld + w, (int)ld};
+    k.P = Col<double>{c.sd + (size_t)R.P * ld + w, (int)ld};
+    if (lane == 0) {   // the rest of ProposeVec on column 1 of the packed copy of R, up to UpdateParams
+        k.R = Col<double>{L.g - off, 1};
+        k.vec = Col<double>{L.gs, 1};
         k.blklp = Col<int>{c.si + (size_t)R.BLKLP * ld + w, (int)ld};
+        k.defer = 1;
         proposal_tail(c, t, k, b, 0);
+    }
+    wave_sync();
+    {   // UpdateParams (propose.f90:142-149): one lane per changed parameter, each sum in q order
+        const int nc = t.blk_nchanged[b];
+        const double *M = t.mapping + t.blk_map_off[b];
+        const int *chg = t.changed + t.blk_changed_off[b];
+        for (int j = lane; j < nc; j += 64) {
+            double s = 0.0;
+            for (int q = 0; q < n; q++) s += M[j * n + q] * L.gs[q];
+            k.trial[chg[j]] += s;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the trial row's stores, before lane 0 reads it
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
         for (int l = 0; l < c.n_like; l++)
             for (int q = 0; q < c.like_nn[l]; q++)
                 c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = k.trial[t.ti[c.like_nidx[l] + q]];
@@ -915,15 +1200,8 @@ __global__ __launch_bounds__(64) void rot_kernel(DevCfg c, int w0)
         c.si[(size_t)R.ISET * ld + w] = k.r.iset;
         c.si[(size_t)R.PROT * ld + w] = 0;
     }
-    __syncthreads();
-    for (int i = lane; i < 97; i += 64) c.sd[(size_t)(R.U + i) * ld + w] = u_s[i];
-#ifdef CMAMD_STAMPS
-    if (w == 0 && lane == 0) {
-        g_rot_ticks[0] = __builtin_amdgcn_s_memtime() - t_start;
-        g_rot_ticks[1] = t_g;
-        g_rot_ticks[2] = t_m;
-    }
-#endif
+    wave_sync();
+    for (int i = lane; i < 97; i += 64) c.sd[(size_t)(R.U + i) * ld + w] = L.u[i];
 }
 
 #ifdef CMAMD_STAMPS
@@ -1356,7 +1634,8 @@ static void set_mh_lds(cmbs *s) {
     // multi-wave scratch rows stay in HBM and are read in place.
     DevCfg &d = s->dc;
     const size_t cap = 160 * 1024;
-    d.stage_R = d.stage_cyc = d.stage_cov = 1;
+    d.stage_R = s->no_stage_R ? 0 : 1;
+    d.stage_cyc = d.stage_cov = 1;
     d.tq_rows = d.test_like ? s->n_used : 1;   // a row per test-Gaussian row, or one (the proposal's block)
     d.def_cap = (int)s->defer_likes.size();
     if (mh_lds_bytes(s) > cap) {               // the deferred combines go first: the likelihoods combine in-launch
@@ -1541,6 +1820,14 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     HIP_CHECK(hipMemset(s->si.p, 0, (size_t)R.NI * d.ld * 4));
     d.sd = s->sd.as<double>();
     d.si = s->si.as<int>();
+    // rotation lists: walker indices [ld] + two counters per 64-walker range
+    s->rot.alloc((size_t)(d.ld + 2 * (d.ld / 64)) * 4);
+    HIP_CHECK(hipMemset(s->rot.p, 0, (size_t)(d.ld + 2 * (d.ld / 64)) * 4));
+    d.rot_list = s->rot.as<int>();
+    d.rot_cnt = d.rot_list + d.ld;
+    s->rot_par.assign(d.ld / 64, 0);
+    HIP_CHECK(hipFuncSetAttribute((const void *)rot_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(ROT_WAVES * sizeof(RotLds))));
 
     set_mh_lds(s);
 
@@ -2009,6 +2296,10 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
     DevCfg dc = s->dc;
     dc.mask_on = masked ? 1 : 0;
     if (s->pending_def && !accept) fail(CMBL_ERR_ARG, "internal: deferred likelihoods without an accepting step");
+    if (propose && dc.rot_defer) {   // alternate the two rotation-list counters of this walker range
+        dc.rot_par = s->rot_par[g0 / 64];
+        s->rot_par[g0 / 64] ^= 1;
+    }
     dc.n_def = s->pending_def;
     s->pending_def = 0;
     timed_launch("mh_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
@@ -2022,7 +2313,8 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
     if (propose && dc.rot_defer) {   // the walkers whose proposal waits on a new rotation
         HIP_CHECK(hipGetLastError());
         timed_launch("rot_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(rot_kernel, dim3(g1 - g0), dim3(64), 0, stream, e0, e1, 0, dc, g0);
+            hipExtLaunchKernelGGL(rot_kernel, dim3((g1 - g0 + ROT_WAVES - 1) / ROT_WAVES), dim3(64 * ROT_WAVES),
+                                  ROT_WAVES * sizeof(RotLds), stream, e0, e1, 0, dc, g0);
         });
     }
     HIP_CHECK(hipGetLastError());
@@ -2524,4 +2816,15 @@ extern "C" int cmamd_debug_stamps(unsigned long long *host) {
 
 // number of work items of the sampler's fused window pass (0: none); for tests
 // (without one: minus the last set-up check passed)
+extern "C" int cmamd_debug_rot_serial(cmbs *s, int on) {   // rotations by the serial reference path
+    if (!s) return -1;
+    s->dc.rot_serial = on ? 1 : 0;
+    return 0;
+}
+extern "C" int cmamd_debug_stage_R(cmbs *s, int on) {     // rotation rows staged in mh_kernel's LDS image
+    if (!s) return -1;
+    s->no_stage_R = !on;
+    cmamd::set_mh_lds(s);
+    return 0;
+}
 extern "C" int cmamd_debug_fused(const cmbs *s) { return !s ? 0 : s->tpass ? s->tpass->n_items() : -s->tp_why; }

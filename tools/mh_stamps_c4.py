@@ -37,16 +37,16 @@ rows = []
 for step in range(44):
     smp.step(2, fast_only=True)        # one accept+propose launch (the stamped one) per call
     torch.cuda.synchronize()
-    st = np.zeros((64, 8), dtype=np.uint64)
+    st = np.zeros((64, 16), dtype=np.uint64)
     assert N.lib().cmamd_debug_stamps(st.ctypes.data_as(C.c_void_p)) == 0
-    d = np.diff(st[:W // 64, :7].astype(np.int64), axis=1)
+    d = np.diff(st[:W // 16, :7].astype(np.int64), axis=1)   # 16-walker blocks
     rows.append(np.median(d, axis=0))
 rows = np.array(rows)
 rt = np.zeros(3, dtype=np.uint64)
 fn = N.lib().cmamd_debug_rot_ticks
 fn.argtypes = [C.c_void_p]
 assert fn(rt.ctypes.data) == 0
-print(f"rot_kernel walker 0, last rotation: total {rt[0]} ticks, Gaussian draws {rt[1]}, Gram-Schmidt {rt[2]}")
+print(f"rot_kernel first listed walker, last rotation: total {rt[0]} ticks, Gaussian draws {rt[1]}, Gram-Schmidt {rt[2]}")
 names = ["dma issue", "dma wait", "accept", "propose", "wb issue", "drain"]
 print("step  " + " ".join(f"{x:>10s}" for x in names))
 for i, r in enumerate(rows):
