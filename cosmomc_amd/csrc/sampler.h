@@ -52,7 +52,7 @@ struct DevCfg {
     int *rot_list;          // [ld] walkers whose rotation is pending, listed per 64-walker-aligned range from its start
     int *rot_cnt;           // [ld / 64][2] list lengths; a proposing launch appends to rot_par, zeroes the other
     int rot_par;            // set per launch
-    int rot_serial;         // debug: every rotation by rot_kernel's serial path
+    int rot_serial;         // debug: 1 every rotation by the serial path, 2 parallel without speculative lanes
     Rows rows;
     TabLayout tl;
     const int *tab_i;       // [tl.n_int] (allocation padded to a multiple of 64 words)
@@ -104,8 +104,11 @@ struct cmbs {
     std::vector<int> params_used;
     std::string last_error;
     cmamd::DevBuf rot;                  // rotation lists + counters (DevCfg::rot_list / rot_cnt)
-    std::vector<int> rot_par;
-    bool no_stage_R = false;            // debug: keep the rotation rows in HBM (cmamd_debug_stage_R)           // per 64-walker range: the counter the next proposing launch appends to
+    std::vector<int> rot_par;           // per 64-walker range: the counter the next proposing launch appends to
+    std::vector<int> rot_lp;            // per 64-walker range: the single fast block's loop index mod n, or -1 (rot_may_pend)
+    bool rot_fast_any = false;          // some fast block is wide enough to defer its rotations
+    int rot_fast_n = 0;                 // width of the only fast block when it is deferred, else 0
+    bool no_stage_R = false;            // debug: keep the rotation rows in HBM (cmamd_debug_stage_R)
     cmamd::DevBuf tab_i, tab_d, sd, si, like_terms, cur_terms, ws, hist, hist_terms, mom, itmp_g;
     cmamd::DevBuf nuis_bufs[cmamd::MAXLIKE];
     std::vector<int> h_tab_i;

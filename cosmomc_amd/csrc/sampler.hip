@@ -872,9 +872,9 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-static constexpr int ROT_WAVES = 4;                        // walkers per rot_kernel workgroup
-static constexpr int ROT_GC = MAXBLK * (MAXBLK + 4);       // Gaussians a parallel rotation may use
-static constexpr int ROT_GA = ROT_GC + 64;                 // + one round's overshoot
+static constexpr int ROT_WAVES = 4;                        // walkers per rot_kernel workgroup (a wave each)
+static constexpr int ROT_GC = MAXBLK * (MAXBLK + 4);       // Gaussians a parallel rotation may use (>= n (n + ROT_SPEC))
+static constexpr int ROT_GA = ROT_GC + 128;                // + one pair round's overshoot
 static constexpr int ROT_UC = 1536;                        // uniforms (a multiple of 64)
 
 struct RotLds {
@@ -907,8 +907,8 @@ __device__ __forceinline__ int sub24(int a, int b) { const int d = a - b; return
 
 static constexpr int RM_P = 16777213, RM_CD = 7654321;     // cm and cd in units of 2^-24
 
-__device__ void rot_round(RotLds &L, RotGen &G, int lane)
-{   // 64 uniforms, then the 32 polar pairs they hold
+__device__ void rot_uniforms(RotLds &L, RotGen &G, int lane)
+{   // 64 uniforms
     const int m = G.m + lane;
     const int b = lane < 33 ? rot_x(L, G, m - 33) : sub24(rot_x(L, G, m - 130), rot_x(L, G, m - 66));
     const int x = sub24(rot_x(L, G, m - 97), b);
@@ -920,10 +920,14 @@ __device__ void rot_round(RotLds &L, RotGen &G, int lane)
     G.cbase -= (64 * RM_CD) % RM_P;
     if (G.cbase < 0) G.cbase += RM_P;
     wave_sync();
+}
+
+__device__ void rot_pairs(RotLds &L, RotGen &G, int lane)
+{   // up to 64 polar pairs of the uniforms made so far
     const int p = G.p + lane;
     bool acc = false;
     double v1 = 0.0, v2 = 0.0, rr = 0.0;
-    if (lane < 32) {
+    if (2 * p < G.m) {
         v1 = 2.0 * ((double)L.o[2 * p] * (1.0 / 16777216.0)) - 1.0;
         v2 = 2.0 * ((double)L.o[2 * p + 1] * (1.0 / 16777216.0)) - 1.0;
         rr = v1 * v1 + v2 * v2;
@@ -938,16 +942,26 @@ __device__ void rot_round(RotLds &L, RotGen &G, int lane)
         L.pi[r] = p;
     }
     G.nr += __popcll(mask);
-    G.p += 32;
+    G.p = min(G.p + 64, G.m / 2);
     wave_sync();
 }
 
+// Gaussians g[0, need): the uniforms for about 1.3 pairs per missing
+// accepted pair go first (their rounds are short), then the pairs 64 at a time
 __device__ __forceinline__ bool rot_fill(RotLds &L, RotGen &G, int need, int lane)
 {
     if (need > ROT_GC) return false;
     while (G.off + 2 * G.nr < need) {
-        if (G.m + 64 > ROT_UC) return false;
-        rot_round(L, G, lane);
+        const int short_pairs = (need - G.off - 2 * G.nr + 1) / 2;
+        int want = 2 * (G.p + short_pairs + short_pairs / 3 + 8);
+        want = min(ROT_UC, (want + 63) & ~63);
+        if (want <= G.m) {
+            if (2 * G.p < G.m) want = G.m;        // pairs left to take
+            else if (G.m + 64 <= ROT_UC) want = G.m + 64;
+            else return false;                    // the uniform buffer is spent
+        }
+        while (G.m < want) rot_uniforms(L, G, lane);
+        while (2 * G.p < G.m && G.off + 2 * G.nr < need) rot_pairs(L, G, lane);
     }
     return true;
 }
@@ -985,18 +999,25 @@ __device__ unsigned long long g_rot_ticks[3];     // first listed walker: total,
 #define RTICK(v) ((void)0)
 #endif
 
+static constexpr int ROT_SPEC = 2;   // idle lanes n, n+1 carry the last row's next two attempts
+
 // One lockstep Gram-Schmidt pass over rows start..n-1 (row j from the n
 // Gaussians at g[gbase + (j - start) n]); NQ = n rounded up to 8.  The
 // padding columns q in [n, NQ) hold +0.0 in vec and in R, so every product
 // there is +0.0 and the sums (which start at +0.0) are bit-identical to sums
 // over q < n, with no selects.  Lane i publishes its raw vec and the lanes
-// divide one element each.  Returns the row that needs a redraw, or -1.
+// divide one element each.  A redraw is most likely for the last row (its
+// residual has one degree of freedom: P(norm <= 1e-3) = 2.5 %), so lanes n and
+// n+1 project the Gaussians that follow as that row's second and third
+// attempts and stand in when it fails.  Returns -1 and the last row's extra
+// attempts in *extra, or the row to redraw and its failed attempts in *extra.
 template <int NQ>
-__device__ int rot_gs_pass(RotLds &L, int n, int start, int gbase, int lane)
+__device__ int rot_gs_pass(RotLds &L, int n, int start, int gbase, int lane, int spec, int *extra)
 {
-    double v[NQ];
-    if (lane >= start && lane < n) {
-        const double *gv = L.g + gbase + (lane - start) * n;    // within g: gbase + n^2 + NQ <= ROT_GA
+    const int top = n + spec;
+    double v[NQ], pp[NQ];
+    if (lane >= start && lane < top) {
+        const double *gv = L.g + gbase + (lane - start) * n;   // within g: the fill covered (top - start) n
 #pragma unroll
         for (int q = 0; q < NQ; q++) {
             const double x = gv[q];
@@ -1005,24 +1026,44 @@ __device__ int rot_gs_pass(RotLds &L, int n, int start, int gbase, int lane)
     }
     for (int i = 0; i < n; i++) {
         if (i >= start) {
+            const bool last = i == n - 1;
             double norm = 0.0;
-            if (lane == i)
+            if (lane == i || (last && lane >= n && lane < top)) {
 #pragma unroll
-                for (int q = 0; q < NQ; q++) norm += v[q] * v[q];
-            norm = readlane_f64(norm, i);
-            if (!(norm > 1e-3)) return i;     // RandRotationD :143: draw row i again
+                for (int q = 0; q < NQ; q++) pp[q] = v[q] * v[q];
+#pragma unroll
+                for (int q = 0; q < NQ; q++) norm += pp[q];
+            }
+            int src = i, a = 0;
+            double nv = readlane_f64(norm, i);
+            if (!(nv > 1e-3)) {               // RandRotationD :143: draw row i again
+                if (!last) {
+                    *extra = 1;
+                    return i;
+                }
+                for (a = 1; a <= spec; a++) {
+                    nv = readlane_f64(norm, n - 1 + a);
+                    if (nv > 1e-3) break;
+                }
+                if (a > spec) {
+                    *extra = 1 + spec;
+                    return i;
+                }
+                src = n - 1 + a;
+            }
+            *extra = a;
             double *ri = L.rm + i * MAXBLK;
-            if (lane == i)
+            if (lane == src)
 #pragma unroll
                 for (int q = 0; q < NQ; q += 2) *reinterpret_cast<double2 *>(ri + q) = make_double2(v[q], v[q + 1]);
             wave_sync();
             if (lane < NQ) {                  // R(i, q) = vec(q) / sqrt(norm), lane q
                 const double x = ri[lane];
-                ri[lane] = lane < n ? x / sqrt(norm) : 0.0;
+                ri[lane] = lane < n ? x / sqrt(nv) : 0.0;
             }
             wave_sync();
         }
-        if (lane > i && lane < n) {           // vec = vec - sum(vec*R(i,:))*R(i,:)
+        if (i < n - 1 && lane > i && lane < top) {   // vec = vec - sum(vec*R(i,:))*R(i,:)
             const double *ri = L.rm + i * MAXBLK;
             double rv[NQ];
 #pragma unroll
@@ -1031,18 +1072,22 @@ __device__ int rot_gs_pass(RotLds &L, int n, int start, int gbase, int lane)
                 rv[q] = t.x;
                 rv[q + 1] = t.y;
             }
+#pragma unroll
+            for (int q = 0; q < NQ; q++) pp[q] = v[q] * rv[q];
             double s = 0.0;
 #pragma unroll
-            for (int q = 0; q < NQ; q++) s += v[q] * rv[q];
+            for (int q = 0; q < NQ; q++) s += pp[q];
 #pragma unroll
-            for (int q = 0; q < NQ; q++) v[q] = v[q] - s * rv[q];
+            for (int q = 0; q < NQ; q++) pp[q] = s * rv[q];
+#pragma unroll
+            for (int q = 0; q < NQ; q++) v[q] = v[q] - pp[q];
         }
     }
     return -1;
 }
 
 // the parallel rotation into L.rm; false (state untouched) when the buffers overflow
-__device__ bool rot_parallel(RotLds &L, Rng &r, int n, int lane, unsigned long long *tk)
+__device__ bool rot_parallel(RotLds &L, Rng &r, int n, int lane, int spec, unsigned long long *tk)
 {
     RotGen G;
     G.i97 = r.i97;
@@ -1062,25 +1107,26 @@ __device__ bool rot_parallel(RotLds &L, Rng &r, int n, int lane, unsigned long l
         unsigned long long t0, t1;
         RTICK(t0);
 #endif
-        if (!rot_fill(L, G, gbase + (n - start) * n, lane)) return false;
+        if (!rot_fill(L, G, gbase + (n - start + spec) * n, lane)) return false;
 #ifdef CMAMD_STAMPS
         RTICK(t1);
         tk[1] += t1 - t0;
 #endif
-        const int fail = n <= 8    ? rot_gs_pass<8>(L, n, start, gbase, lane)
-                         : n <= 16 ? rot_gs_pass<16>(L, n, start, gbase, lane)
-                         : n <= 24 ? rot_gs_pass<24>(L, n, start, gbase, lane)
-                                   : rot_gs_pass<32>(L, n, start, gbase, lane);
+        int extra = 0;
+        const int fail = n <= 8    ? rot_gs_pass<8>(L, n, start, gbase, lane, spec, &extra)
+                         : n <= 16 ? rot_gs_pass<16>(L, n, start, gbase, lane, spec, &extra)
+                         : n <= 24 ? rot_gs_pass<24>(L, n, start, gbase, lane, spec, &extra)
+                                   : rot_gs_pass<32>(L, n, start, gbase, lane, spec, &extra);
         static_assert(MAXBLK == 32, "rot_gs_pass widths");
 #ifdef CMAMD_STAMPS
         RTICK(t0);
         tk[2] += t0 - t1;
 #endif
         if (fail < 0) {
-            rot_commit(L, G, gbase + (n - start) * n, r, lane);
+            rot_commit(L, G, gbase + (n - start + extra) * n, r, lane);
             return true;
         }
-        gbase += (fail - start) * n + n;
+        gbase += (fail - start + extra) * n;
         start = fail;
     }
 }
@@ -1125,17 +1171,12 @@ __device__ void rot_serial(RotLds &L, Rng &r, int n, int lane)
     wave_sync();
 }
 
-__global__ __launch_bounds__(64 * ROT_WAVES) void rot_kernel(DevCfg c, int g0)
+// One wave: walker w's pending rotation, then the rest of its proposal.
+__device__ void rot_walker(const DevCfg &c, int w, int lane, RotLds &L, bool stamp)
 {
-    extern __shared__ __attribute__((aligned(16))) double rot_lds[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int idx = blockIdx.x * ROT_WAVES + wave;
-    if (idx >= c.rot_cnt[2 * (g0 / 64) + c.rot_par]) return;   // wave-uniform
-    const int w = c.rot_list[g0 + idx];
     const size_t ld = c.ld;
     const Rows &R = c.rows;
     const int b = c.si[(size_t)R.PROT * ld + w] - 1;
-    RotLds &L = reinterpret_cast<RotLds *>(rot_lds)[wave];
     const Tabs t = make_tabs(c, c.tab_i, c.tab_d, c.tab_d);
     const int n = t.blk_n[b], off = t.blk_R_off[b];
     for (int i = lane; i < 97; i += 64) L.u[i] = c.sd[(size_t)(R.U + i) * ld + w];
@@ -1151,13 +1192,16 @@ __global__ __launch_bounds__(64 * ROT_WAVES) void rot_kernel(DevCfg c, int g0)
 #ifdef CMAMD_STAMPS
     RTICK(tk[0]);
 #endif
-    if (c.rot_serial || !rot_parallel(L, k.r, n, lane, tk)) rot_serial(L, k.r, n, lane);
+    if (c.rot_serial == 1 || !rot_parallel(L, k.r, n, lane, c.rot_serial == 2 ? 0 : ROT_SPEC, tk))
+        rot_serial(L, k.r, n, lane);
 #ifdef CMAMD_STAMPS
-    if (idx == 0 && lane == 0) {
+    if (stamp && lane == 0) {
         g_rot_ticks[0] = __builtin_amdgcn_s_memtime() - tk[0];
         g_rot_ticks[1] = tk[1];
         g_rot_ticks[2] = tk[2];
     }
+#else
+    (void)stamp;
 #endif
     // R(i, q) (rm, row stride MAXBLK) -> the state rows and a packed copy (row stride n) in g
     for (int e = lane; e < n * n; e += 64) {
@@ -1202,6 +1246,16 @@ __global__ __launch_bounds__(64 * ROT_WAVES) void rot_kernel(DevCfg c, int g0)
     }
     wave_sync();
     for (int i = lane; i < 97; i += 64) c.sd[(size_t)(R.U + i) * ld + w] = L.u[i];
+}
+
+// One wave per listed walker (the launch's list counter is wave-uniform).
+__global__ __launch_bounds__(64 * ROT_WAVES) void rot_kernel(DevCfg c, int g0)
+{
+    extern __shared__ __attribute__((aligned(16))) double rot_lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int idx = blockIdx.x * ROT_WAVES + wave;
+    if (idx >= c.rot_cnt[2 * (g0 / 64) + c.rot_par]) return;
+    rot_walker(c, c.rot_list[g0 + idx], lane, reinterpret_cast<RotLds *>(rot_lds)[wave], idx == 0);
 }
 
 #ifdef CMAMD_STAMPS
@@ -1826,6 +1880,17 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     d.rot_list = s->rot.as<int>();
     d.rot_cnt = d.rot_list + d.ld;
     s->rot_par.assign(d.ld / 64, 0);
+    s->rot_lp.assign(d.ld / 64, 0);                   // every loop index starts at 0
+    {   // the fast blocks: any deferred?  a single one (its width)?
+        std::vector<int> fb;
+        for (int q = s->slow_n; q < s->all_n; q++) {
+            const int b = s->proposer_for_index[q] - 1;
+            if (std::find(fb.begin(), fb.end(), b) == fb.end()) fb.push_back(b);
+        }
+        s->rot_fast_any = false;
+        for (int b : fb) s->rot_fast_any = s->rot_fast_any || s->blk_n[b] >= ROT_DEFER_MIN;
+        s->rot_fast_n = (fb.size() == 1 && s->blk_n[fb[0]] >= ROT_DEFER_MIN) ? s->blk_n[fb[0]] : 0;
+    }
     HIP_CHECK(hipFuncSetAttribute((const void *)rot_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(ROT_WAVES * sizeof(RotLds))));
 
@@ -2288,6 +2353,29 @@ static HistRow next_hist(cmbs *s) {
     return r;
 }
 
+// Whether a proposing launch over the walker range from g0 can leave a
+// rotation pending, so rot_kernel is worth launching.  Fast-only steps
+// propose only fast blocks: none of them deferred, never.  With a single fast
+// block every walker proposes in it at every fast-only step, so all of its
+// loop indices move together and the host knows them (rot_lp: proposals so
+// far mod n, or -1 once anything else has touched them: full steps, dragging,
+// a loaded state, a new walker split); a rotation is due when it is 0 mod n.
+static bool rot_may_pend(cmbs *s, int fast_only, int g0) {
+    if (!s->dc.rot_defer) return false;
+    int &lp = s->rot_lp[g0 / 64];
+    if (!fast_only) {
+        lp = -1;
+        return true;
+    }
+    if (!s->rot_fast_any) return false;
+    if (s->rot_fast_n == 0 || lp < 0) return true;
+    const bool due = lp % s->rot_fast_n == 0;
+    lp = (lp + 1) % s->rot_fast_n;
+    return due;
+}
+
+static void rot_schedule_unknown(cmbs *s) { std::fill(s->rot_lp.begin(), s->rot_lp.end(), -1); }
+
 static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const HistRow &row, hipStream_t stream,
                       int g0, int g1, bool masked = false) {
     const dim3 g((g1 - g0 + MB - 1) / MB), b(MH_THREADS);
@@ -2296,7 +2384,8 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
     DevCfg dc = s->dc;
     dc.mask_on = masked ? 1 : 0;
     if (s->pending_def && !accept) fail(CMBL_ERR_ARG, "internal: deferred likelihoods without an accepting step");
-    if (propose && dc.rot_defer) {   // alternate the two rotation-list counters of this walker range
+    const bool rot = propose && rot_may_pend(s, fast_only, g0);
+    if (rot) {                       // alternate the two rotation-list counters of this walker range
         dc.rot_par = s->rot_par[g0 / 64];
         s->rot_par[g0 / 64] ^= 1;
     }
@@ -2310,7 +2399,7 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
         else
             hipExtLaunchKernelGGL(mh_kernel<false, true>, g, b, lds, stream, e0, e1, 0, dc, fast_only, row.p, row.t, blk0);
     });
-    if (propose && dc.rot_defer) {   // the walkers whose proposal waits on a new rotation
+    if (rot) {                       // the walkers whose proposal waits on a new rotation
         HIP_CHECK(hipGetLastError());
         timed_launch("rot_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
             hipExtLaunchKernelGGL(rot_kernel, dim3((g1 - g0 + ROT_WAVES - 1) / ROT_WAVES), dim3(64 * ROT_WAVES),
@@ -2433,6 +2522,7 @@ static void eval_likes_drag(cmbs *s, int set, hipStream_t stream) {
 
 void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_fn fn, void *user,
                        hipStream_t stream) {
+    rot_schedule_unknown(s);           // the drag proposals move the blocks' loop indices
     if (!s->started) fail(CMBL_ERR_ARG, "cmbs_set_start must be called before cmbs_step_drag");
     check_theory_fresh(s);
     if (n_steps <= 0) return;
@@ -2597,6 +2687,11 @@ void sampler_refresh_theory(cmbs *s, cmbs_theory_fn fn, void *user, hipStream_t 
 }
 
 void sampler_set_groups(cmbs *s, int n_groups) {
+    {   // the groups step together: a common known loop index carries over to the new split
+        const int v = s->rot_lp.empty() ? -1 : s->rot_lp[0];
+        const bool same = std::all_of(s->rot_lp.begin(), s->rot_lp.end(), [v](int x) { return x == v; });
+        std::fill(s->rot_lp.begin(), s->rot_lp.end(), same ? v : -1);
+    }
     const int nblk = (s->W + NB - 1) / NB;
     if (n_groups < 1 || n_groups > MAXGROUPS) fail(CMBL_ERR_ARG, "n_groups must be in 1..%d", MAXGROUPS);
     if (n_groups > nblk) n_groups = nblk;
@@ -2776,6 +2871,7 @@ void sampler_save_state(cmbs *s, void *buf, size_t bytes) {
 }
 
 void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
+    rot_schedule_unknown(s);
     if (bytes < sizeof(StateHeader)) fail(CMBL_ERR_ARG, "state image too short");
     StateHeader h;
     std::memcpy(&h, buf, sizeof h);
@@ -2816,9 +2912,9 @@ extern "C" int cmamd_debug_stamps(unsigned long long *host) {
 
 // number of work items of the sampler's fused window pass (0: none); for tests
 // (without one: minus the last set-up check passed)
-extern "C" int cmamd_debug_rot_serial(cmbs *s, int on) {   // rotations by the serial reference path
+extern "C" int cmamd_debug_rot_serial(cmbs *s, int mode) {   // 1: rotations by the serial path; 2: parallel, no speculative lanes
     if (!s) return -1;
-    s->dc.rot_serial = on ? 1 : 0;
+    s->dc.rot_serial = mode;
     return 0;
 }
 extern "C" int cmamd_debug_stage_R(cmbs *s, int on) {     // rotation rows staged in mh_kernel's LDS image

@@ -714,7 +714,9 @@ def test_parallel_rotations_match_serial(blocks, W, groups):
     points and likelihoods -- bit-identical to the serial path (lane 0 draws
     one Gaussian at a time), over several rotations per walker, including the
     redraws of rows whose norm falls below 1e-3 (about 2.5 % of the 21-d
-    rotations) and blocks of 8 (ROT_DEFER_MIN) to 32 (MAXBLK) parameters."""
+    rotations: taken by the spare lanes' attempts, or, in debug mode 2, by
+    restarting the pass) and blocks of 8 (ROT_DEFER_MIN) to 32 (MAXBLK)
+    parameters."""
     from cosmomc_amd import _native as N
     from cosmomc_amd.sampler import BatchedMCMC
     n = sum(blocks)
@@ -731,7 +733,7 @@ def test_parallel_rotations_match_serial(blocks, W, groups):
     steps = 3 * max(blocks) + 2
     start = np.tile(P0, (W, 1)) + 0.1 * rng.standard_normal((W, n)) * width
     images = []
-    for serial in (0, 1):
+    for serial in (0, 1, 2):
         s = BatchedMCMC(W, n, used, split, 0, P0 - 20 * width, P0 + 20 * width, propose_scale=2.4,
                         seed_ij=4004, seed_kl=9373)
         s.set_covariance(np.diag(width ** 2))
@@ -744,7 +746,8 @@ def test_parallel_rotations_match_serial(blocks, W, groups):
             s.step(1, fast_only=True)
         images.append((s.save_state(), s.state()))
         s.close()
-    (a, sa), (b, sb) = images
+    (a, sa), (b, sb), (c, sc) = images
     np.testing.assert_array_equal(sa[0], sb[0])
     np.testing.assert_array_equal(sa[1], sb[1])
     assert a == b
+    assert c == b          # mode 2: a last-row redraw restarts the pass instead of using the spare lanes
