@@ -878,6 +878,8 @@ struct HLDev {
     int n, m, nb, ncl, ncl_used, nX, Np;
     const double *chat;     // [nb][n][n]
     const double *cfhalf;   // [nb][n][n]
+    const double *u0;       // [nb][n][n] eigenvectors (columns) of C_fid: the first eigensolve's starting basis
+    const double *v0;       // [nb][n][n] eigenvectors of C_fid^-1/2 Chat C_fid^-1/2: the second's
     const int *cl_use;
     int *status;            // sticky CMBL_STATUS_* bits (cmbl_status)
     const int *wcount;      // live walkers (CLDev::wcount)
@@ -915,7 +917,18 @@ __device__ inline int hl_partner(int rr, int r) {   // round-robin pairing of ro
     return ((2 * rr - r) % (M - 1) + (M - 1)) % (M - 1);
 }
 
-static constexpr int HL_MAX_SWEEPS = 40;   // as DSYEV's own iteration limit, a cap that fails loudly
+static constexpr int HL_MAX_SWEEPS = 40;
+// a sweep in which no pair was further from orthogonal than cos = 1e-6 is the
+// last (its own rotations leave every pair near cos 1e-12: -lnL moves by
+// ~1e-14 relative against the reference's DSYEV, tools/hl_margin.py)
+#ifndef CMAMD_HL_SWEEP_COS2
+#define CMAMD_HL_SWEEP_COS2 1e-12
+#endif
+static constexpr double HL_SWEEP_COS2 = CMAMD_HL_SWEEP_COS2;
+#ifndef CMAMD_HL_VFREE
+#define CMAMD_HL_VFREE 1
+#endif
+static constexpr bool HL_VFREE = CMAMD_HL_VFREE;   // as DSYEV's own iteration limit, a cap that fails loudly
 
 // One-sided (Hestenes) cyclic Jacobi of the group's symmetric M x M matrix C:
 // lane r owns column r of G (initially C's column r, i.e. its row r) and
@@ -938,15 +951,21 @@ static constexpr int HL_MAX_SWEEPS = 40;   // as DSYEV's own iteration limit, a 
 // separate check sweep).
 // Returns true on lanes whose pair still needed rotating in sweep
 // HL_MAX_SWEEPS (the caller fails that problem: NaN and a status bit).
-template <int M>
+// VF (V-free): the matrices here are symmetric positive definite (C, and
+// C^-1/2 Chat C^-1/2), so G = C V = U Sigma with U = V: eigenvalue r is the
+// norm of column r and eigenvector r that column normalised, and V need not
+// be carried -- each round exchanges and rotates one column instead of two
+// (the exchange is the round's cost: lane permutes through the LDS crossbar).
+template <int M, bool VF = false>
 __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int grp, int r, int lane, int which,
                            double &lam)
 {
     (void)which;
     (void)lane;
     const bool on = grp < HLRowsLds<M>::G;        // lanes past G*M idle
+    if (!VF)
 #pragma unroll
-    for (int k = 0; k < M; k++) V[k] = (k == r) ? 1.0 : 0.0;
+        for (int k = 0; k < M; k++) V[k] = (k == r) ? 1.0 : 0.0;
     bool failed = false;
 #ifdef CMAMD_STAMPS
     unsigned long long ph0 = 0, ph1 = 0, ph2 = 0, nround = 0;
@@ -973,7 +992,7 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
 #pragma unroll
             for (int k = 0; k < M; k++) {        // every permute in flight together
                 Gp[k] = __shfl(G[k], src);
-                Vp[k] = __shfl(V[k], src);
+                if (!VF) Vp[k] = __shfl(V[k], src);
             }
             const double np_ = __shfl(nrm, src);
             if (on) {
@@ -983,9 +1002,9 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
 #pragma unroll
                 for (int k = 0; k < M; k++) alh = fma(low ? G[k] : Gp[k], low ? Gp[k] : G[k], alh);
                 if (alh != 0.0 && alh * alh > 1e-30 * (all * ahh)) {
-                    // cos^2 > 1e-18: columns this far from orthogonal need another sweep;
-                    // below it this sweep's rotation leaves them at ~1e-18 (quadratic convergence)
-                    big = big || alh * alh > 1e-18 * (all * ahh);
+                    // cos^2 > HL_SWEEP_COS2: columns this far from orthogonal need another
+                    // sweep; below it this sweep's rotation leaves them near cos^2 squared
+                    big = big || alh * alh > HL_SWEEP_COS2 * (all * ahh);
                     const double d = ahh - all, e = 2.0 * alh;
                     const double den = fabs(d) + sqrt(d * d + e * e);
                     double q = __builtin_amdgcn_rcp(den);           // reciprocal + two Newton steps
@@ -1000,14 +1019,14 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
 #pragma unroll
                         for (int k = 0; k < M; k++) {
                             G[k] = fma(-s, Gp[k], c * G[k]);
-                            V[k] = fma(-s, Vp[k], c * V[k]);
+                            if (!VF) V[k] = fma(-s, Vp[k], c * V[k]);
                         }
                         nrm = fma(-t, alh, all);
                     } else {
 #pragma unroll
                         for (int k = 0; k < M; k++) {
                             G[k] = fma(s, Gp[k], c * G[k]);
-                            V[k] = fma(s, Vp[k], c * V[k]);
+                            if (!VF) V[k] = fma(s, Vp[k], c * V[k]);
                         }
                         nrm = fma(t, alh, ahh);
                     }
@@ -1042,6 +1061,16 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
         atomicAdd(&g_hl_phase[3], nround);
     }
 #endif
+    if (VF) {
+        double n2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; k++) n2 = fma(G[k], G[k], n2);
+        const double sg = sqrt(n2);
+#pragma unroll
+        for (int k = 0; k < M; k++) V[k] = n2 > 0.0 ? G[k] / sg : (k == r ? 1.0 : 0.0);
+        lam = sg;
+        return failed;
+    }
     double l = 0.0;
 #pragma unroll
     for (int k = 0; k < M; k++) l = fma(V[k], G[k], l);
@@ -1077,9 +1106,54 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
         }
         A[j] = v;
     }
+    // Warm start: the solve runs on B0^T A B0, with B0 the eigenvectors of
+    // the fiducial's matrix (host, per bin), which is nearly diagonal for
+    // walkers near the fiducial, and maps its eigenvectors back (V <- B0 V).
+    // Lane r holds row r of A (= column r); B0 rows go to row buffer 1.
+    auto to_basis = [&](const double *B0) {
+        if (on)
+#pragma unroll
+            for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = (row_ok && k < n) ? B0[r * n + k] : (k == r ? 1.0 : 0.0);
+        __syncthreads();
+        double T[M];
+#pragma unroll
+        for (int j = 0; j < M; j++) {             // T = A B0, row r
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < M; k++) s += A[k] * S.rows[grp][1][k][j];
+            T[j] = s;
+        }
+        if (on)
+#pragma unroll
+            for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = T[k];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < M; j++) {             // B0^T T, row r
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < M; k++) s += S.rows[grp][1][k][r] * S.rows[grp][0][k][j];
+            A[j] = s;
+        }
+        __syncthreads();
+    };
+    auto from_basis = [&]() {                     // V <- B0 V (column r), B0 still in row buffer 1
+        double U[M];
+#pragma unroll
+        for (int i = 0; i < M; i++) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < M; k++) s += S.rows[grp][1][i][k] * V[k];
+            U[i] = s;
+        }
+#pragma unroll
+        for (int i = 0; i < M; i++) V[i] = U[i];
+        __syncthreads();
+    };
     // (1) C = U diag U^T (lane r: eigenvector r, i.e. column r of U)
     double dgr;
-    bool unconverged = hl_ojacobi<M>(A, V, S, grp, r, lane, 0, dgr);
+    if (h.u0) to_basis(h.u0 + (long long)b * n * n);
+    bool unconverged = hl_ojacobi<M, HL_VFREE>(A, V, S, grp, r, lane, 0, dgr);
+    if (h.u0) from_basis();
     if (on) {
         S.dg[grp][r] = dgr;
 #pragma unroll
@@ -1153,7 +1227,9 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     __syncthreads();
     // (4) Rot = V diag V^T; g(x) = sign(x - 1) sqrt(2 max(0, x - ln x - 1))  (:892-894)
     double x;
-    unconverged = hl_ojacobi<M>(A, V, S, grp, r, lane, 1, x) || unconverged;
+    if (h.v0) to_basis(h.v0 + (long long)b * n * n);
+    unconverged = hl_ojacobi<M, HL_VFREE>(A, V, S, grp, r, lane, 1, x) || unconverged;
+    if (h.v0) from_basis();
     __syncthreads();                               // the solve's last reads of the row buffers
     if (on) {
         const double g = sqrt(2 * fmax(0.0, x - log(x) - 1));
@@ -1409,7 +1485,7 @@ struct CMBLikes final : Like {
     CLDev dev{};
     HLDev hl{};
     DevBuf d_pairs, d_items, d_wts, d_wdir, d_sumoff, d_sumcols, d_sumconst, d_corroff, d_corrcols, d_corrconst,
-        d_etox, d_fidcorr, d_noise, d_chat, d_cluse, d_bkmaps, d_bpnu, d_bpR, d_bpdnu, d_hlchat, d_hlcf;
+        d_etox, d_fidcorr, d_noise, d_chat, d_cluse, d_bkmaps, d_bpnu, d_bpR, d_bpdnu, d_hlchat, d_hlcf, d_hlu0, d_hlv0;
     int max_field = 0, n_part_rows = 0;
     bool items_even = true, small_gauss = false;
     bool use_group = false;      // BK foregrounds: grouped-pair window kernel
@@ -2179,6 +2255,37 @@ struct CMBLikes final : Like {
         up(d_cluse, cl_use.data(), cl_use.size() * 4);
         up(d_hlchat, chatM.data(), chatM.size() * 8);
         up(d_hlcf, cfh.data(), cfh.size() * 8);
+        if (approx == 1) {   // the HL eigensolves' starting bases (cmbl_hl_rows_kernel warm start)
+            const int n = nmaps;
+            std::vector<double> u0((size_t)nb * n * n), v0((size_t)nb * n * n);
+            for (int b = 0; b < nb; b++) {
+                std::vector<double> cf(cfh.begin() + (size_t)b * n * n, cfh.begin() + (size_t)(b + 1) * n * n);
+                std::vector<double> ev, U, cm = cf, R((size_t)n * n, 0.0), V;
+                sym_eigen(cf, n, ev, U);                       // C_fid^1/2 and C_fid share eigenvectors
+                bool ok = true;
+                for (double e : ev) ok = ok && e > 0.0;
+                if (ok) {
+                    sym_power(cm, n, -1.0);                    // C_fid^-1/2
+                    const double *ch = &chatM[(size_t)b * n * n];
+                    std::vector<double> T((size_t)n * n, 0.0);
+                    for (int i = 0; i < n; i++)
+                        for (int j = 0; j < n; j++)
+                            for (int k = 0; k < n; k++) T[i * n + j] += ch[i * n + k] * cm[k * n + j];
+                    for (int i = 0; i < n; i++)
+                        for (int j = 0; j < n; j++)
+                            for (int k = 0; k < n; k++) R[i * n + j] += cm[i * n + k] * T[k * n + j];
+                    sym_eigen(R, n, ev, V);
+                } else {
+                    U.assign((size_t)n * n, 0.0);
+                    for (int i = 0; i < n; i++) U[i * n + i] = 1.0;
+                    V = U;
+                }
+                std::copy(U.begin(), U.end(), u0.begin() + (size_t)b * n * n);
+                std::copy(V.begin(), V.end(), v0.begin() + (size_t)b * n * n);
+            }
+            up(d_hlu0, u0.data(), u0.size() * 8);
+            up(d_hlv0, v0.data(), v0.size() * 8);
+        }
         if (bk) {
             up(d_bkmaps, bkm.data(), bkm.size() * sizeof(BKMap));
             up(d_bpnu, bnu.data(), bnu.size() * 8);
@@ -2226,6 +2333,11 @@ struct CMBLikes final : Like {
         hl.Np = qf.Np;
         hl.chat = d_hlchat.as<double>();
         hl.cfhalf = d_hlcf.as<double>();
+        {
+            static const int ws = getenv("CMAMD_HL_WARM") ? atoi(getenv("CMAMD_HL_WARM")) : 3;   // bit 0: first solve, 1: second
+            hl.u0 = (approx == 1 && (ws & 1)) ? d_hlu0.as<double>() : nullptr;
+            hl.v0 = (approx == 1 && (ws & 2)) ? d_hlv0.as<double>() : nullptr;
+        }
         hl.cl_use = d_cluse.as<int>();
         hl.status = status_word();
     }
