@@ -596,7 +596,7 @@ def pmc_traffic(kernel, W):
         return None, None
     symbols = {"plik_quadform_ksplit": ("quadform_ksplit<false>", "quadform_ksplit"),   # profiler label -> kernel
                "cmbl_window_kernel": ("cmbl_window_direct",),
-               "theory_window_kernel": ("theory_window_kernel<2>", "theory_window_kernel<4>",
+               "theory_window_kernel": ("theory_window_vec<2, 0>", "theory_window_kernel<2>", "theory_window_kernel<4>",
                                         "theory_window_kernel")}.get(kernel, (kernel,))
     t = next((d["per_launch"][k] for k in symbols if k in d["per_launch"]), None)
     if not t:
