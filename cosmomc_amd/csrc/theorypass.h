@@ -5,6 +5,8 @@
 // run as one pass, each walker's rows leave HBM once instead of twice.
 #pragma once
 
+#include <map>
+
 #include "common.h"
 
 namespace cmamd {
@@ -36,6 +38,7 @@ static constexpr int TP_MAXSTEP = 16;   // 32-l steps per work item (the active-
 
 struct TPItem {           // one workgroup's l range of one theory field, with <= 64 columns
     int field, l0, l1, nch, ncol, cdesc;
+    int nst;              // 32-l steps: ceil((l1 - l0 + 1) / 32) (<= 2 nch)
     int nsb;              // 16-slot MFMA blocks in use (slots are reused: TheoryPass::build)
     int soff;             // first of its steps in TPDev::emit / cmap
     long long woff;       // weights [nch][nsb][16 slots][TP_CHUNK], zero padded
@@ -61,10 +64,13 @@ class TheoryPass {
   public:
     // pack the stages' columns into work items (no column split between two);
     // false when some l range needs more than TP_MAXCOL columns
-    bool build(const std::vector<WinStage> &stages);
+    // cuts (optional): per field the l at which items start (after the first);
+    // the columns are grouped by them instead of greedily by TP_MAXL
+    bool build(const std::vector<WinStage> &stages, const std::map<int, std::vector<int>> *cuts = nullptr);
     void launch(const double *dl, long long ld_field, long long ld_walker, const TPOut *outs, int W,
                 hipStream_t stream);
     int n_items() const { return (int)items.size(); }
+    const TPItem &item(int k) const { return items[k]; }
     int n_stages() const { return nstage; }
 
   private:

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_kernel(TPD
     const int wl = min(w, W - 1);
     const double *Df = dl + (long long)wl * ld_walker + (long long)it.field * ld_field;
     const int ncb = it.nsb;
-    const int nstep = it.nch * NSUB;
+    const int nstep = it.nst;
     double t[LPL], tn[LPL], tnn[LPL], a[LPL];
     auto load_t = [&](int st, double *dst) {
         const int lb = it.l0 + st * STEP + 2 * kq;
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev 
     const double *Df = dl + (long long)wl * ld_walker + (long long)it.field * ld_field;
     const int lcap = ((int)ld_field - 2) & ~1;
     const int ncb = it.nsb;
-    const int nstep = it.nch * NSUB;
+    const int nstep = it.nst;
     double tA[LPL], tB[LPL], tC[LPL], a[LPL];
     auto load_t = [&](int st, double *dst) {  // raw rows, addresses clamped into the row
         const int lb = it.l0 + st * STEP + 2 * kq;
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev 
 
 // ------------------------------------------------------------------ host side
 
-bool TheoryPass::build(const std::vector<WinStage> &stages) {
+bool TheoryPass::build(const std::vector<WinStage> &stages, const std::map<int, std::vector<int>> *cuts) {
     if (stages.empty() || stages.size() > (size_t)TP_MAXOUT) return false;
     struct C { int lo, hi, stage, col; };
     std::map<int, std::vector<C>> byf;
@@ -506,6 +506,23 @@ bool TheoryPass::build(const std::vector<WinStage> &stages) {
         std::vector<std::vector<C>> groups;
         std::vector<C> cur;
         int a = 0, bnd = -1;
+        const std::vector<int> *fcv = nullptr;
+        if (cuts) {
+            const auto fc = cuts->find(kv.first);
+            if (fc != cuts->end()) fcv = &fc->second;
+        }
+        if (fcv) {   // the given cuts: column x goes to the interval of x.lo
+            const std::vector<int> &cv = *fcv;
+            std::vector<std::vector<C>> byc(cv.size() + 1);
+            for (const C &x : v) {
+                const size_t k = std::upper_bound(cv.begin(), cv.end(), x.lo) - cv.begin();
+                if (k < cv.size() && x.hi >= cv[k]) return false;   // a column across a cut
+                byc[k].push_back(x);
+            }
+            for (auto &g : byc)
+                if (!g.empty()) groups.push_back(g);
+            v.clear();
+        }
         for (const C &x : v) {
             // a column that overlaps the group joins it; otherwise it starts a
             // new group once the group would pass TP_MAXL l or TP_MAXCOL columns
@@ -545,7 +562,8 @@ bool TheoryPass::build(const std::vector<WinStage> &stages) {
             it.l0 = lo & ~1;                      // even: 16-byte theory loads
             it.l1 = hi;
             it.nch = (it.l1 - it.l0 + TP_CHUNK) / TP_CHUNK;
-            if (it.nch * (TP_CHUNK / 32) > TP_MAXSTEP) {
+            it.nst = (it.l1 - it.l0 + 32) / 32;
+            if (it.nst > TP_MAXSTEP || (int)g.size() > TP_MAXCOL) {
                 fprintf(stderr, "theorypass: field %d [%d, %d] longer than %d l\n", kv.first, it.l0, it.l1,
                         TP_MAXSTEP * 32);
                 return false;
@@ -553,7 +571,7 @@ bool TheoryPass::build(const std::vector<WinStage> &stages) {
             it.ncol = (int)g.size();
             it.cdesc = (int)cols.size();
             it.woff = (long long)w.size();
-            const int nstep = it.nch * (TP_CHUNK / 32);
+            const int nstep = it.nst;
             // steps of each column, and its slot: the lowest slot whose previous
             // column ended before this one's first step (g: wide ones first, then by l)
             std::vector<int> s0(g.size()), s1(g.size()), slot(g.size());
@@ -586,7 +604,8 @@ bool TheoryPass::build(const std::vector<WinStage> &stages) {
                     for (int sl = 16 * cb; sl < 16 * cb + 16; sl++)
                         for (int k = 0; k < TP_CHUNK; k++) {
                             const int l = it.l0 + ch * TP_CHUNK + k;
-                            const int q = sm[(size_t)((ch * TP_CHUNK + k) / 32) * TP_MAXCOL + sl];
+                            const int stk = (ch * TP_CHUNK + k) / 32;   // steps past nstep: padding
+                            const int q = stk < nstep ? sm[(size_t)stk * TP_MAXCOL + sl] : 255;
                             double x = 0.0;
                             if (q != 255) {
                                 const WinCol &wc = stages[g[q].stage].cols[g[q].col];
@@ -642,7 +661,7 @@ void TheoryPass::plan_units(int tiles) {
     const int ni = (int)items.size();
     std::vector<double> cost(ni);
     for (int i = 0; i < ni; i++)
-        cost[i] = __builtin_popcountll(items[i].act) + 1.1 * items[i].nch * (TP_CHUNK / 32);
+        cost[i] = __builtin_popcountll(items[i].act) + 1.1 * items[i].nst;
     std::vector<int> ord(ni);
     for (int i = 0; i < ni; i++) ord[i] = i;
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cost[a] > cost[b]; });
