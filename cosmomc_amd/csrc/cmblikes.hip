@@ -2333,11 +2333,8 @@ struct CMBLikes final : Like {
         hl.Np = qf.Np;
         hl.chat = d_hlchat.as<double>();
         hl.cfhalf = d_hlcf.as<double>();
-        {
-            static const int ws = getenv("CMAMD_HL_WARM") ? atoi(getenv("CMAMD_HL_WARM")) : 3;   // bit 0: first solve, 1: second
-            hl.u0 = (approx == 1 && (ws & 1)) ? d_hlu0.as<double>() : nullptr;
-            hl.v0 = (approx == 1 && (ws & 2)) ? d_hlv0.as<double>() : nullptr;
-        }
+        hl.u0 = approx == 1 ? d_hlu0.as<double>() : nullptr;   // the warm-started eigensolves' bases
+        hl.v0 = approx == 1 ? d_hlv0.as<double>() : nullptr;
         hl.cl_use = d_cluse.as<int>();
         hl.status = status_word();
     }

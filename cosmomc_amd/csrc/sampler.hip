@@ -2011,31 +2011,6 @@ static std::vector<int> bin_safe_cuts(const std::vector<std::pair<int, int>> &bi
     return cuts;
 }
 
-// Item starts over [lo, hi] for items of as equal length as the bins allow:
-// n = round(len / L) items, cut at the even l nearest the ideal positions
-// lo + k len / n at which no bin is split.
-static std::vector<int> balanced_cuts(const std::vector<std::pair<int, int>> &bins, int lo, int hi, int L) {
-    auto valid = [&](int c) {
-        if (c % 2 != 0) return false;
-        for (auto &b : bins)
-            if (b.first < c && c <= b.second) return false;
-        return true;
-    };
-    const int len = hi - lo + 1;
-    const int n = std::max(1, (int)std::lround((double)len / L));
-    std::vector<int> cuts;
-    for (int k = 1; k < n; k++) {
-        const int ideal = lo + (int)std::lround((double)k * len / n);
-        int c = -1;
-        for (int d = 0; d < L / 2 && c < 0; d++) {
-            if (ideal - d > lo && valid(ideal - d) && (cuts.empty() || ideal - d > cuts.back())) c = ideal - d;
-            else if (ideal + d < hi && valid(ideal + d)) c = ideal + d;
-        }
-        if (c > (cuts.empty() ? lo : cuts.back())) cuts.push_back(c);
-    }
-    return cuts;
-}
-
 // Fused window pass: a plik_lite likelihood (window stage kind 1) and a
 // CMBlikes likelihood (kind 0) evaluated densely on the same theory buffer.
 // The CMBlikes windows are re-segmented at l where no plik bin is split, so
@@ -2066,34 +2041,16 @@ static void setup_fusion(cmbs *s) {
             s->tp_why = std::max(s->tp_why, 5);
             std::map<int, std::vector<std::pair<int, int>>> bins;
             for (auto &c : sp.cols) bins[c.field].push_back({c.lo, c.hi});
-            std::map<int, std::vector<int>> starts, cuts;
-            static const int balanced = getenv("CMAMD_TP_BALANCE") ? atoi(getenv("CMAMD_TP_BALANCE")) : 0;   // measured neutral (21.6 vs 21.3 us)
-            if (balanced) {   // every field's l range in items of (nearly) equal length, about TP_MAXL
-                std::map<int, std::pair<int, int>> span;
-                for (const WinStage *st : {&sp, &sc})
-                    for (auto &c : st->cols) {
-                        auto it = span.find(c.field);
-                        if (it == span.end()) span[c.field] = {c.lo, c.hi};
-                        else it->second = {std::min(it->second.first, c.lo), std::max(it->second.second, c.hi)};
+            std::map<int, std::vector<int>> starts;
+            for (auto &kv : bins) {
+                int lo = 1 << 30, hi = -1;
+                for (auto &c : sc.cols)
+                    if (c.field == kv.first) {
+                        lo = std::min(lo, c.lo);
+                        hi = std::max(hi, c.hi);
                     }
-                for (auto &kv : span)
-                    cuts[kv.first] = balanced_cuts(bins[kv.first], kv.second.first & ~1, kv.second.second, TP_MAXL);
-                for (auto &kv : cuts) {   // the CMBlikes windows split at the same l
-                    bool has = false;
-                    for (auto &c : sc.cols) has = has || c.field == kv.first;
-                    if (has) starts[kv.first] = kv.second;
-                }
-            } else {
-                for (auto &kv : bins) {
-                    int lo = 1 << 30, hi = -1;
-                    for (auto &c : sc.cols)
-                        if (c.field == kv.first) {
-                            lo = std::min(lo, c.lo);
-                            hi = std::max(hi, c.hi);
-                        }
-                    if (hi < lo) continue;
-                    starts[kv.first] = bin_safe_cuts(kv.second, lo & ~1, hi, TP_MAXL);
-                }
+                if (hi < lo) continue;
+                starts[kv.first] = bin_safe_cuts(kv.second, lo & ~1, hi, TP_MAXL);
             }
             // the handle may be shared (standalone calls, other samplers): its
             // segmentation changes only if the fused pass is kept
@@ -2104,7 +2061,7 @@ static void setup_fusion(cmbs *s) {
             }
             s->tp_why = std::max(s->tp_why, 6);
             std::unique_ptr<TheoryPass> tp(new TheoryPass());
-            if (!tp->build({sp, sc}, balanced ? &cuts : nullptr) && !(balanced && tp->build({sp, sc}))) {
+            if (!tp->build({sp, sc})) {
                 C.like->like->window_set_segments(saved);
                 continue;
             }

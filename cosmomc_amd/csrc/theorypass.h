@@ -64,9 +64,7 @@ class TheoryPass {
   public:
     // pack the stages' columns into work items (no column split between two);
     // false when some l range needs more than TP_MAXCOL columns
-    // cuts (optional): per field the l at which items start (after the first);
-    // the columns are grouped by them instead of greedily by TP_MAXL
-    bool build(const std::vector<WinStage> &stages, const std::map<int, std::vector<int>> *cuts = nullptr);
+    bool build(const std::vector<WinStage> &stages);
     void launch(const double *dl, long long ld_field, long long ld_walker, const TPOut *outs, int W,
                 hipStream_t stream);
     int n_items() const { return (int)items.size(); }

@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_kernel(TPD
 // compiler then counts the loads in flight exactly, and a step waits only for
 // its own data instead of draining the prefetch (vmcnt(0)) at the weight
 // store, which held every step to a full memory latency.
-template <int NB, int ABL = 0>
+template <int NB>
 __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev c, const double *__restrict__ dl, long long ld_field,
                                                          long long ld_walker, int W)
 {
@@ -383,16 +383,13 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev 
                 double *out = o1 ? c.out[1].out : c.out[0].out;
                 if ((o1 ? c.out[1].kind : c.out[0].kind) == 0)
                     out[(long long)d[r].row * W + w] = q;
-                else if (ABL & 4)   // timing only: the [W][ld] rows written bin-major
-                    out[(long long)d[r].row * W + w] = x[r] - q;
                 else
                     out[(long long)w * (o1 ? c.out[1].ld : c.out[0].ld) + d[r].row] = x[r] - q;
             }
         }
     };
-    double keep = 0.0;
     auto closes = [&](int st) {   // the columns that end at step st
-        const unsigned long long e = (ABL & 1) ? 0ull : esh[st];
+        const unsigned long long e = esh[st];
 #pragma unroll
         for (int cb = 0; cb < NB; cb++)
             if ((e >> (16 * cb)) & 0xffffull) emit(st, e, cb, acc[cb], bcc[cb]);
@@ -405,7 +402,7 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev 
 #pragma unroll
             for (int h = 0; h < 2; h++) tb[2 * q + h] = (!tail || lb + 8 * q + h <= it.l1) ? tc[2 * q + h] : 0.0;
         const int cur = st & 1;
-        const unsigned m = (ABL & 2) ? 0u : (unsigned)(it.act >> (4 * st)) & 15u;   // (ABL: timing ablations only)
+        const unsigned m = (unsigned)(it.act >> (4 * st)) & 15u;
 #pragma unroll
         for (int cb = 0; cb < NB; cb++)
             if (m & (1u << cb)) {
@@ -416,9 +413,6 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev 
                     bcc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s2 + 1], tb[s2 + 1], bcc[cb], 0, 0, 0);
                 }
             }
-        if (ABL & 2)
-#pragma unroll
-            for (int s2 = 0; s2 < LPL; s2++) keep += tb[s2];   // keep the loads live
     };
     // main steps: weights of st + 1 and theory of st + 2 in flight; step s
     // lives in buffer s mod 3 (A, B, C)
@@ -454,11 +448,6 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev 
         case 1: tail(tB, tC); break;
         default: tail(tC, tA); break;
     }
-    if (ABL) {   // timing ablations: consume what the dropped stages would have
-#pragma unroll
-        for (int cb = 0; cb < NB; cb++) keep += acc[cb][0] + acc[cb][1] + acc[cb][2] + acc[cb][3] + bcc[cb][0] + bcc[cb][3];
-        if (keep == 1.2345e-300) c.out[0].out[w] = keep;
-    }
     TP_STAMP(2);
 #ifdef CMAMD_STAMPS
     if (threadIdx.x == 0 && b < 4096) {
@@ -480,7 +469,7 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev 
 
 // ------------------------------------------------------------------ host side
 
-bool TheoryPass::build(const std::vector<WinStage> &stages, const std::map<int, std::vector<int>> *cuts) {
+bool TheoryPass::build(const std::vector<WinStage> &stages) {
     if (stages.empty() || stages.size() > (size_t)TP_MAXOUT) return false;
     struct C { int lo, hi, stage, col; };
     std::map<int, std::vector<C>> byf;
@@ -506,23 +495,6 @@ bool TheoryPass::build(const std::vector<WinStage> &stages, const std::map<int, 
         std::vector<std::vector<C>> groups;
         std::vector<C> cur;
         int a = 0, bnd = -1;
-        const std::vector<int> *fcv = nullptr;
-        if (cuts) {
-            const auto fc = cuts->find(kv.first);
-            if (fc != cuts->end()) fcv = &fc->second;
-        }
-        if (fcv) {   // the given cuts: column x goes to the interval of x.lo
-            const std::vector<int> &cv = *fcv;
-            std::vector<std::vector<C>> byc(cv.size() + 1);
-            for (const C &x : v) {
-                const size_t k = std::upper_bound(cv.begin(), cv.end(), x.lo) - cv.begin();
-                if (k < cv.size() && x.hi >= cv[k]) return false;   // a column across a cut
-                byc[k].push_back(x);
-            }
-            for (auto &g : byc)
-                if (!g.empty()) groups.push_back(g);
-            v.clear();
-        }
         for (const C &x : v) {
             // a column that overlaps the group joins it; otherwise it starts a
             // new group once the group would pass TP_MAXL l or TP_MAXCOL columns
@@ -710,25 +682,10 @@ void TheoryPass::launch(const double *dl, long long ld_field, long long ld_walke
     const int tiles = (W + 63) / 64;
     if (tiles != unit_tiles) plan_units(tiles);
     c.units = d_units.as<int2>();
-    static const int vk = getenv("CMAMD_TP_VEC") ? atoi(getenv("CMAMD_TP_VEC")) : 1;
-    if (vec_ok && vk && max_nsb <= 2) {   // (four blocks would not fit the registers: theory_window_kernel<4>)
+    if (vec_ok && max_nsb <= 2) {   // (four blocks would not fit the registers: theory_window_kernel<4>)
         timed_launch("theory_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            static const int abl = getenv("CMAMD_TP_ABL") ? atoi(getenv("CMAMD_TP_ABL")) : 0;   // timing ablations
-            if (abl == 1)
-                hipExtLaunchKernelGGL((theory_window_vec<2, 1>), dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl,
-                                      ld_field, ld_walker, W);
-            else if (abl == 2)
-                hipExtLaunchKernelGGL((theory_window_vec<2, 2>), dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl,
-                                      ld_field, ld_walker, W);
-            else if (abl == 3)
-                hipExtLaunchKernelGGL((theory_window_vec<2, 3>), dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl,
-                                      ld_field, ld_walker, W);
-            else if (abl == 4)
-                hipExtLaunchKernelGGL((theory_window_vec<2, 4>), dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl,
-                                      ld_field, ld_walker, W);
-            else
-                hipExtLaunchKernelGGL(theory_window_vec<2>, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl, ld_field,
-                                      ld_walker, W);
+            hipExtLaunchKernelGGL(theory_window_vec<2>, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl, ld_field,
+                                  ld_walker, W);
         });
         HIP_CHECK(hipGetLastError());
         return;
