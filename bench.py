@@ -216,7 +216,7 @@ def kernel_profile(smp, steps):
     more fast steps (HIP events on the launch stream)."""
     import torch
     from cosmomc_amd import _native as N
-    names = ("plik_bin_delta", "plik_quadform_ksplit", "mh_kernel", "rot_kernel", "cmbl_bk_prologue", "cmbl_window_kernel",
+    names = ("plik_bin_delta", "plik_quadform_ksplit", "plik_quadform_corun", "mh_kernel", "rot_kernel", "cmbl_bk_prologue", "cmbl_window_kernel",
              "cmbl_reduce_kernel", "cmbl_hl_kernel", "cmbl_quadform", "cmbl_gauss_small_kernel")
     N.profile_reset()
     N.profile_enable(True)
@@ -691,7 +691,8 @@ def main():
         smp.step(args.steps, fast_only=True)
         torch.cuda.synchronize()
         N.profile_enable(False)
-        kern = {k: N.profile_read(k) for k in ("theory_window_kernel", "plik_bin_delta", "plik_quadform_ksplit", "mh_kernel",
+        kern = {k: N.profile_read(k) for k in ("theory_window_kernel", "plik_bin_delta", "plik_quadform_ksplit",
+                                                "plik_quadform_corun", "mh_kernel",
                                                 "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_gauss_small_kernel",
                                                 "cmbl_quadform")}
         kern = {k: v for k, v in kern.items() if v[1]}

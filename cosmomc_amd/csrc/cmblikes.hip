@@ -31,6 +31,7 @@
 #include <sstream>
 
 #include "quadform.h"
+#include "smallgauss.h"
 
 namespace cmamd {
 
@@ -44,9 +45,6 @@ static constexpr int WK_CHUNK = 64;             // l per chunk
 #endif
 static constexpr int WK_NCH = CMAMD_WK_NCH;     // chunks per work item
 static constexpr int WK_TS = WK_CHUNK + 2;      // LDS row stride of the spectrum tile (doubles)
-static constexpr int SMALL_NX = 64;
-static constexpr int SMALL_WT = 4;          // walkers per workgroup (measured: 7.1 / 8.0 / 9.8 / 13.9 us for 4 / 2 / 8 / 16)
-static constexpr int SMALL_MAXTASK = 256;   // tasks per dataset
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
@@ -780,15 +778,9 @@ __global__ __launch_bounds__(256) void cmbl_reduce_kernel(CLDev c, const double 
     }
 }
 
-// Small gaussian likelihoods (nX <= 64, e.g. lensing 9, SPT-SZ 47): binned
-// spectra, bigX = C - Chat and chi^2 = bigX^T C^-1 bigX in one kernel
-// (CMBlikes.f90:1183-1225; Matrix_QuadForm as row sums y = M x, then x.y).
-// Workgroup = 8 walkers x 32 thread groups.  The partial rows of every
-// element are cut into tasks of <= 8 rows (host); groups take tasks
-// round-robin with all loads of a task in flight, then combine them per
-// element in task order (deterministic), then split the rows of M.  Every
-// table load is issued at the start, beside the others: the partial loads
-// wait on one table level (the task's rows), nothing after them on any.
+// Small gaussian likelihoods (nX <= 64, e.g. lensing 9, SPT-SZ 47): the
+// whole chi^2 in one kernel (smallgauss.h).  The host cuts the partial rows of
+// every element into tasks of <= 8 rows.
 struct SmallTask { int first, count; };      // rows e_*_rows[first .. first+count) (host side)
 struct SmallDev {
     int ntask;
@@ -797,80 +789,10 @@ struct SmallDev {
 };
 
 template <int WT>
-__global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(CLDev c, SmallDev sd, const double *__restrict__ partial,
-                                                              const double *__restrict__ nuis, long long ld_nuis,
-                                                              const double *__restrict__ M, double *__restrict__ out,
-                                                              int W)
+__global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(SmallGaussLaunch a)
 {
-    constexpr int NG = 256 / WT;             // thread groups of WT walkers
-    __shared__ double tp[SMALL_MAXTASK][WT];
-    __shared__ double xs[SMALL_NX][WT];
-    __shared__ double red[NG][WT];
-    __shared__ double Msh[SMALL_NX * SMALL_NX];
-    const int wl = threadIdx.x % WT, g = threadIdx.x / WT;
-    const int w = blockIdx.x * WT + wl;
-    const int Wc = live_walkers(c.wcount, W);
-    if (blockIdx.x * WT >= Wc) return;
-    for (int i = threadIdx.x; i < c.nX * c.nX; i += 256) Msh[i] = M[i];   // in flight with the partial loads
-    const bool act = w < Wc;
-    const bool calp = c.log_cal_prior > 0 && c.cal_index >= 0;
-    const double cal = (g == 0 && act && calp) ? nuis[(long long)w * ld_nuis + c.cal_index] : 1.0;   // likewise
-    struct Elem { int ix, m0, m1, c0, c1; double mc, cc, fc, ch; };
-    auto elem = [&](int e) {   // element e's table entries
-        Elem q{c.e_to_x[e], sd.e_main_t[e], sd.e_main_t[e + 1], 0, 0, c.e_main_const[e], 0.0, 0.0, c.chat[e]};
-        if (c.has_corr) {
-            q.c0 = sd.e_corr_t[e];
-            q.c1 = sd.e_corr_t[e + 1];
-            q.cc = c.e_corr_const[e];
-            q.fc = c.fidcorr[e];
-        }
-        return q;
-    };
-    Elem e0{-1, 0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0};
-    if (g < c.nE) e0 = elem(g);   // this group's first element, in flight with the partials
-    for (int t = g; t < sd.ntask; t += NG) {
-        const int4 ra = *reinterpret_cast<const int4 *>(sd.trow + 8 * t);
-        const int4 rb = *reinterpret_cast<const int4 *>(sd.trow + 8 * t + 4);
-        const int r[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = (act && r[u] >= 0) ? partial[(long long)r[u] * W + w] : 0.0;
-        double s = 0.0;
-#pragma unroll
-        for (int u = 0; u < 8; u++) s += v[u];
-        tp[t][wl] = s;
-    }
-    __syncthreads();
-    for (int e = g; e < c.nE; e += NG) {
-        const Elem q = e == g ? e0 : elem(e);
-        if (q.ix < 0) continue;
-        double s = q.mc;
-        for (int t = q.m0; t < q.m1; t++) s += tp[t][wl];
-        if (c.has_corr) {
-            double cs = q.cc;
-            for (int t = q.c0; t < q.c1; t++) cs += tp[t][wl];
-            s = s + (cs - q.fc);
-        }
-        xs[q.ix][wl] = s - q.ch;
-    }
-    __syncthreads();
-    double part = 0.0;
-    for (int i = g; i < c.nX; i += NG) {
-        double y = 0.0;
-        for (int j = 0; j < c.nX; j++) y += Msh[i * c.nX + j] * xs[j][wl];
-        part += xs[i][wl] * y;
-    }
-    red[g][wl] = part;
-    __syncthreads();
-    if (g == 0 && act) {
-        double chisq = 0.0;
-        for (int k = 0; k < NG; k++) chisq += red[k][wl];
-        if (calp) {
-            const double t = log(cal) / c.log_cal_prior;
-            chisq = chisq + t * t;
-        }
-        out[w] = chisq / 2;
-    }
+    __shared__ double lds[small_gauss_lds_doubles<WT>()];
+    small_gauss_body<WT>(a, lds, blockIdx.x);
 }
 
 // ---------------------------------------------------------------- HL
@@ -2388,7 +2310,8 @@ struct CMBLikes final : Like {
         return reinterpret_cast<double *>(static_cast<char *>(ws) + layout(W).part);
     }
     QFDeferred after_window(int W, const double *nuis, long long ld_nuis, double *out, void *ws, hipStream_t stream,
-                            bool defer) override {
+                            bool defer, const SmallGaussLaunch *co = nullptr) override {
+        if (co) fail(CMBL_ERR_ARG, "internal: %s carries no co-run", name.c_str());
         if (W <= 0) return QFDeferred{};
         if (n_nuis > 0 && !nuis) fail(CMBL_ERR_ARG, "%s needs its %d nuisance parameters", name.c_str(), n_nuis);
         if (defer && !deferred_capable()) fail(CMBL_ERR_UNSUPPORTED, "%s: no deferred evaluation", name.c_str());
@@ -2396,6 +2319,17 @@ struct CMBLikes final : Like {
         hl.wcount = nullptr;
         const double *nu = nuis ? nuis : reinterpret_cast<const double *>(ws);   // never read when n_nuis == 0
         return post_window(W, nu, ld_nuis, out, ws, stream, nullptr, defer);
+    }
+    // the small chi^2 as a co-run of another likelihood's deferred quadratic
+    // form (the after_window stage of a fused small gaussian dataset)
+    bool corun_small(SmallGaussLaunch &a, int W, const double *nuis, long long ld_nuis, double *out,
+                     void *ws) override {
+        if (!small_gauss || W <= 0 || !ws) return false;
+        if (n_nuis > 0 && !nuis) fail(CMBL_ERR_ARG, "%s needs its %d nuisance parameters", name.c_str(), n_nuis);
+        dev.wcount = nullptr;
+        hl.wcount = nullptr;
+        a = small_args(W, nuis ? nuis : reinterpret_cast<const double *>(ws), ld_nuis, out, ws);
+        return true;
     }
     bool window_resegment(const std::map<int, std::vector<int>> &starts) override {
         if (approx == 3 || bk || aberration != 0.0 || use_group || !binned) return false;
@@ -2510,6 +2444,20 @@ struct CMBLikes final : Like {
         return post_window(W, nu, ld_nuis, out, ws, stream, wcount, defer);
     }
 
+    SmallGaussLaunch small_args(int W, const double *nu, long long ld_nuis, double *out, void *ws) const {
+        SmallGaussLaunch a{};
+        a.d = SmallGaussDev{dev.nE,        dev.nX,         dev.has_corr,       dev.cal_index, dev.log_cal_prior,
+                            dev.e_to_x,    dev.e_main_const, dev.e_corr_const, dev.fidcorr,   dev.chat,
+                            sdev.ntask,    sdev.trow,      sdev.e_main_t,      sdev.e_corr_t, dev.wcount};
+        a.partial = reinterpret_cast<const double *>(static_cast<const char *>(ws) + layout(W).part);
+        a.nuis = nu;
+        a.ld_nuis = ld_nuis;
+        a.M = d_invcov.as<double>();
+        a.out = out;
+        a.W = W;
+        return a;
+    }
+
     // the kernels after the window stage: binned spectra, then chi^2 (small
     // gaussian) or the HL transform / gaussian residuals and the quadratic form
     QFDeferred post_window(int W, const double *nu, long long ld_nuis, double *out, void *ws, hipStream_t stream,
@@ -2523,12 +2471,10 @@ struct CMBLikes final : Like {
         const bool use_add = log_cal_prior > 0 && cal_index >= 0;
         const int tiles = (W + 63) / 64;
         if (small_gauss) {
+            const SmallGaussLaunch a = small_args(W, nu, ld_nuis, out, ws);
             timed_launch("cmbl_gauss_small_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-#define CMBL_SMALL(T)                                                                                             \
-    hipExtLaunchKernelGGL(cmbl_gauss_small_kernel<T>, dim3((W + T - 1) / T), dim3(256), 0, stream, e0, e1, 0, dev, \
-                          sdev, (const double *)partial, nu, ld_nuis, d_invcov.as<double>(), out, W)
-                CMBL_SMALL(SMALL_WT);
-#undef CMBL_SMALL
+                hipExtLaunchKernelGGL(cmbl_gauss_small_kernel<SMALL_WT>, dim3((W + SMALL_WT - 1) / SMALL_WT), dim3(256),
+                                      0, stream, e0, e1, 0, a);
             });
             HIP_CHECK(hipGetLastError());
             return QFDeferred{};

@@ -167,6 +167,30 @@ struct QFDeferred {
     const double *addend = nullptr;
 };
 
+// A small gaussian CMBlikes chi^2 (smallgauss.h) as one launch's arguments:
+// its workgroups can run in cmbl_gauss_small_kernel or beside a deferred
+// quadratic form's (QuadForm::launch_deferred, Like::corun_small).
+struct SmallGaussDev {
+    int nE, nX, has_corr, cal_index;
+    double log_cal_prior;
+    const int *e_to_x;                               // [nE] index into bigX or -1
+    const double *e_main_const, *e_corr_const;       // [nE] fixed-spectrum window dots
+    const double *fidcorr, *chat;                    // [nE]
+    int ntask;
+    const int *trow;                                 // [ntask][8] partial rows per task, -1 padded
+    const int *e_main_t, *e_corr_t;                  // [nE + 1] task ranges per element
+    const int *wcount;                               // live walkers [0, *wcount), or null: all
+};
+struct SmallGaussLaunch {
+    SmallGaussDev d;
+    const double *partial;   // [rows][W] window partial rows
+    const double *nuis;      // [W][ld_nuis]
+    long long ld_nuis;
+    const double *M;         // [nX][nX] inverse covariance
+    double *out;             // [W] -lnL
+    int W;
+};
+
 // Window stage of a likelihood: its first kernel contracts every walker's
 // theory rows with fixed weights (plik_lite's binning, CMBlikes' bin windows).
 // Exposed as columns, the stages of several likelihoods that read one theory
@@ -230,10 +254,20 @@ struct Like {
         (void)ws, (void)W;
         return nullptr;
     }
+    // co: another likelihood's small chi^2 to run inside this one's deferred
+    // quadratic-form launch (only with defer, only if accepts_corun())
     virtual QFDeferred after_window(int W, const double *nuis, long long ld_nuis, double *out, void *ws,
-                                    hipStream_t stream, bool defer) {
-        (void)W, (void)nuis, (void)ld_nuis, (void)out, (void)ws, (void)stream, (void)defer;
+                                    hipStream_t stream, bool defer, const SmallGaussLaunch *co = nullptr) {
+        (void)W, (void)nuis, (void)ld_nuis, (void)out, (void)ws, (void)stream, (void)defer, (void)co;
         fail(CMBL_ERR_UNSUPPORTED, "%s: no window stage", name.c_str());
+    }
+    virtual bool accepts_corun() const { return false; }
+    // This likelihood's whole after-window stage as a small chi^2 another
+    // launch can carry (same arguments as after_window); false if it has none.
+    virtual bool corun_small(SmallGaussLaunch &a, int W, const double *nuis, long long ld_nuis, double *out,
+                             void *ws) {
+        (void)a, (void)W, (void)nuis, (void)ld_nuis, (void)out, (void)ws;
+        return false;
     }
     // Move the l boundaries at which the window stage splits its dot products
     // to the given segment starts (absolute l, per theory field), so that

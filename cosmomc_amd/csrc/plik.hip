@@ -348,11 +348,13 @@ struct PlikLite final : Like {
         (void)W;
         return qf.x_rows(ws);
     }
+    bool accepts_corun() const override { return true; }
     QFDeferred after_window(int W, const double *nuis, long long ld_nuis, double *out, void *ws, hipStream_t stream,
-                            bool defer) override {
+                            bool defer, const SmallGaussLaunch *co = nullptr) override {
         (void)nuis, (void)ld_nuis;
+        if (co && !defer) fail(CMBL_ERR_ARG, "internal: a co-run needs the deferred quadratic form");
         if (W <= 0) return QFDeferred{};
-        if (defer) return qf.launch_deferred(W, ws, nullptr, stream, "plik_quadform_ksplit");
+        if (defer) return qf.launch_deferred(W, ws, nullptr, stream, "plik_quadform_ksplit", co, "plik_quadform_corun");
         HIP_CHECK(hipMemsetAsync(qf.counters(ws, W), 0, (size_t)qf.n_counters(W) * 4, stream));
         qf.launch(W, ws, nullptr, out, stream, "plik_quadform_ksplit");
         return QFDeferred{};

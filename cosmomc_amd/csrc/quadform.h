@@ -74,7 +74,10 @@ class QuadForm {
                 const int *wcount = nullptr);
     // the same launch without the combine: the workgroups store their partials
     // and exit; the returned descriptor tells a later kernel how to finish
-    QFDeferred launch_deferred(int W, void *ws, const double *addend, hipStream_t stream, const char *prof_name);
+    // co: a small gaussian chi^2 whose workgroups run in the same launch
+    // (quadform_corun), timed as co_prof_name
+    QFDeferred launch_deferred(int W, void *ws, const double *addend, hipStream_t stream, const char *prof_name,
+                               const SmallGaussLaunch *co = nullptr, const char *co_prof_name = nullptr);
 
   private:
     static constexpr int MAXKB = 5;

@@ -5,6 +5,7 @@
 #include <functional>
 
 #include "quadform.h"
+#include "smallgauss.h"
 
 namespace cmamd {
 
@@ -66,26 +67,34 @@ __device__ __forceinline__ void dma_tile(double *lds_tile, const double *g, size
 // split-K recipe) sums them in fixed item order: deterministic results.
 // Without TICKET the partials are only stored: the consumer kernel that runs
 // next on the stream combines them (QFDeferred), with no in-launch hand-off.
-template <bool TICKET>
-__global__ __launch_bounds__(256, 2) void quadform_ksplit(
-    const double *__restrict__ Ct, int Np, const double *__restrict__ delta, int W,
-    const QFItem *__restrict__ items, int n_items, int xcd_map,
-    double *__restrict__ partial, unsigned int *__restrict__ counters, const double *__restrict__ addend,
-    double *__restrict__ out, const int *__restrict__ wcount)
-{
-    __shared__ __attribute__((aligned(16))) double smem[2 * 2 * QF_TILE * BK];   // [buf][A|B][64][BK], 64 KB
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int li = lane & 15, lk = lane >> 4;
-    QSTAMP(0);
-    // XCD-aware placement: blocks b and b+8 share an XCD; give each XCD whole
-    // walker tiles so a tile's Delta stays in one L2 (speed only)
-    int item_ix = blockIdx.x, tile = blockIdx.y;
+static constexpr int QF_LDS_DOUBLES = 2 * 2 * QF_TILE * BK;   // [buf][A|B][64][BK], 64 KB
+
+// Workgroup b of the launch (b = item + tile * n_items in launch order) ->
+// its (item, walker tile).  XCD-aware placement: blocks b and b+8 share an
+// XCD; give each XCD whole walker tiles so a tile's Delta stays in one L2
+// (speed only)
+__device__ __forceinline__ void qf_place(int b, int n_items, int xcd_map, int &item_ix, int &tile) {
     if (xcd_map) {
-        const int b = blockIdx.x + blockIdx.y * gridDim.x;
         const int x = b & 7, j = b >> 3;
         tile = x + 8 * (j / n_items);
         item_ix = j % n_items;
+    } else {
+        item_ix = b % n_items;
+        tile = b / n_items;
     }
+}
+
+template <bool TICKET>
+__device__ __forceinline__ void quadform_body(
+    double *smem, int item_ix, int tile,
+    const double *__restrict__ Ct, int Np, const double *__restrict__ delta, int W,
+    const QFItem *__restrict__ items, int n_items,
+    double *__restrict__ partial, unsigned int *__restrict__ counters, const double *__restrict__ addend,
+    double *__restrict__ out, const int *__restrict__ wcount)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    QSTAMP(0);
     const int w0 = tile * QF_TILE;
     if (wcount) {                                     // sparse evaluation: walkers [0, *wcount) live
         const int wc = *wcount;
@@ -221,6 +230,49 @@ __global__ __launch_bounds__(256, 2) void quadform_ksplit(
     QSTAMP(4);
 }
 
+template <bool TICKET>
+__global__ __launch_bounds__(256, 2) void quadform_ksplit(
+    const double *__restrict__ Ct, int Np, const double *__restrict__ delta, int W,
+    const QFItem *__restrict__ items, int n_items, int xcd_map,
+    double *__restrict__ partial, unsigned int *__restrict__ counters, const double *__restrict__ addend,
+    double *__restrict__ out, const int *__restrict__ wcount)
+{
+    __shared__ __attribute__((aligned(16))) double smem[QF_LDS_DOUBLES];
+    int item_ix, tile;
+    qf_place(blockIdx.x + blockIdx.y * gridDim.x, n_items, xcd_map, item_ix, tile);
+    quadform_body<TICKET>(smem, item_ix, tile, Ct, Np, delta, W, items, n_items, partial, counters, addend, out,
+                          wcount);
+}
+
+// The deferred quadratic form with a small gaussian chi^2 riding along: the
+// first workgroups are quadform_ksplit<false>'s in its order, the last ns run
+// smallgauss.h's body over the co-run's walkers.  One launch instead of two on
+// the sampler's critical path, and the chi^2 workgroups fill the slots the
+// quadratic form leaves free (480 of 512 at W = 1024) and those its one-block
+// items release half way (MI355X, plik_lite + lensing, W = 1024: 15.4 us
+// against 13.5 + 4.6 us for the two launches; with the chi^2 workgroups first
+// 19.8 us, with 8 walkers per chi^2 workgroup 16.5 us).  Both bodies compute
+// exactly what their own kernels do.
+template <int WT>
+__global__ __launch_bounds__(256, 2) void quadform_corun(
+    const double *__restrict__ Ct, int Np, const double *__restrict__ delta, int W,
+    const QFItem *__restrict__ items, int n_items, int xcd_map, double *__restrict__ partial,
+    SmallGaussLaunch co, int ns)
+{
+    static_assert(small_gauss_lds_doubles<WT>() <= QF_LDS_DOUBLES, "co-run LDS");
+    __shared__ __attribute__((aligned(16))) double smem[QF_LDS_DOUBLES];
+    const int nq = gridDim.x - ns;
+    const int b = blockIdx.x;
+    if (b >= nq) {
+        small_gauss_body<WT>(co, smem, b - nq);
+        return;
+    }
+    int item_ix, tile;
+    qf_place(b, n_items, xcd_map, item_ix, tile);
+    quadform_body<false>(smem, item_ix, tile, Ct, Np, delta, W, items, n_items, partial, nullptr, nullptr, nullptr,
+                         nullptr);
+}
+
 #ifdef CMAMD_STAMPS
 extern "C" int cmamd_debug_qf_stamps(unsigned long long *host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_qf_stamps), sizeof(g_qf_stamps)) == hipSuccess ? 0 : -5;
@@ -312,12 +364,21 @@ void QuadForm::launch(int W, void *ws, const double *addend, double *out, hipStr
     HIP_CHECK(hipGetLastError());
 }
 
-QFDeferred QuadForm::launch_deferred(int W, void *ws, const double *addend, hipStream_t stream, const char *prof_name) {
+QFDeferred QuadForm::launch_deferred(int W, void *ws, const double *addend, hipStream_t stream, const char *prof_name,
+                                     const SmallGaussLaunch *co, const char *co_prof_name) {
     const int tiles = wpad(W) / QF_TILE;
     const int kb = choose_kb(tiles);
     const int n_items = (int)items[kb].size();
     double *x = x_rows(ws);
     double *partial = x + (size_t)wpad(W) * Np;
+    if (co) {
+        const int ns = (co->W + SMALL_WT - 1) / SMALL_WT;
+        timed_launch(co_prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            hipExtLaunchKernelGGL(quadform_corun<SMALL_WT>, dim3(n_items * tiles + ns), dim3(256), 0, stream, e0, e1, 0,
+                                  d_ct.as<double>(), Np, (const double *)x, W, d_items[kb].as<QFItem>(), n_items,
+                                  (int)(tiles % 8 == 0), partial, *co, ns);
+        });
+    } else
     timed_launch(prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
         hipExtLaunchKernelGGL(quadform_ksplit<false>, dim3(n_items, tiles), dim3(256), 0, stream, e0, e1, 0,
                               d_ct.as<double>(), Np, (const double *)x, W, d_items[kb].as<QFItem>(), n_items,

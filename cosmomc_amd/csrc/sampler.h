@@ -163,6 +163,7 @@ struct cmbs {
     std::unique_ptr<cmamd::TheoryPass> tpass;
     int tp_like[2] = {-1, -1};               // [0] plik_lite (Delta rows), [1] CMBlikes (partial rows)
     cmamd::WinStage tp_stage[2];
+    bool no_corun = false;                   // debug: the fused pass's tails as separate launches
     int tp_why = 0;                          // set-up progress when no pass was built (debug)
     ~cmbs() {
         for (auto &st : streams)

@@ -2224,13 +2224,43 @@ static void launch_tpass(cmbs *s, hipStream_t stream) {
     launch_tpass(s, stream, P.dl, P.ld_field, P.ld_walker, s->dc.like_nuis);
 }
 
+// The fused pass's two tails as one launch: when one fused likelihood is
+// deferred and its quadratic form carries co-runs (plik_lite) and the other's
+// whole after-window stage is a small chi^2 (Planck lensing), the chi^2's
+// workgroups run in the quadratic form's launch (quadform_corun) and its term
+// lands in its like_terms row as before.  The carrier and the carried index
+// for this step, or -1, -1.
+struct Corun {
+    int carrier = -1, carried = -1;
+    SmallGaussLaunch a{};
+};
+
+static Corun plan_corun(cmbs *s, bool defer) {
+    Corun c;
+    if (!defer || !s->tpass || s->no_corun) return c;
+    for (int k = 0; k < 2; k++) {
+        const int h = s->tp_like[k], o = s->tp_like[1 - k];
+        Like &H = *s->likes[h].like->like;
+        Like &O = *s->likes[o].like->like;
+        if (!is_deferred(s, h) || !H.accepts_corun()) continue;
+        if (O.corun_small(c.a, s->W, s->dc.like_nuis[o], O.n_nuis, s->like_terms.as<double>() + o * (size_t)s->dc.ld,
+                          s->like_ws[o].p)) {
+            c.carrier = h;
+            c.carried = o;
+            return c;
+        }
+    }
+    return c;
+}
+
 // the rest of a fused likelihood after the pass: deferred or into its like_terms row
-static void eval_after_window(cmbs *s, size_t i, bool defer, hipStream_t stream) {
+static void eval_after_window(cmbs *s, size_t i, bool defer, hipStream_t stream, const Corun &co) {
+    if ((int)i == co.carried) return;   // inside the carrier's launch
     Like &L = *s->likes[i].like->like;
     const bool d = defer && is_deferred(s, i);
     const QFDeferred q = L.after_window(s->W, s->dc.like_nuis[i], L.n_nuis,
                                         d ? nullptr : s->like_terms.as<double>() + i * (size_t)s->dc.ld,
-                                        s->like_ws[i].p, stream, d);
+                                        s->like_ws[i].p, stream, d, (int)i == co.carrier ? &co.a : nullptr);
     if (d) record_deferred(s, i, q);
 }
 
@@ -2258,6 +2288,7 @@ static void eval_likes_masked(cmbs *s, hipStream_t stream, bool defer = false) {
     hipLaunchKernelGGL(like_compact_kernel, dim3(ns), dim3(1024), 0, stream, s->dc, ss, cnt);
     HIP_CHECK(hipGetLastError());
     if (s->tpass) launch_tpass(s, stream);   // the fused likelihoods are dense (setup_fusion)
+    const Corun co = plan_corun(s, defer);
     for (size_t i = 0; i < s->likes.size(); i++) {
         auto &l = s->likes[i];
         const int nn = l.like->like->n_nuis;
@@ -2266,7 +2297,7 @@ static void eval_likes_masked(cmbs *s, hipStream_t stream, bool defer = false) {
             if (ss.like[q] == (int)i) b = q;
         if (b < 0) {
             if (fused(s, i)) {
-                eval_after_window(s, i, defer, stream);
+                eval_after_window(s, i, defer, stream, co);
                 continue;
             }
             if (defer && eval_deferred(s, i, s->dc.like_nuis[i], stream)) continue;
@@ -2308,13 +2339,15 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
         gather = false;
         launch_tpass(s, stream);
     }
+    const Corun co = fuse ? plan_corun(s, defer) : Corun{};
     // the likelihoods run in order on the caller's stream: side by side on forked
     // streams the memory-bound likelihood kernels slow each other more than they
     // overlap (MI355X, W = 1024, plik_lite + lensing: 77.1 vs 71.9 us/step; the
     // binning kernel alone 12.5 -> 26.2 us next to the lensing windows).  Even
     // the fused pass's two tails (quadratic form and the lensing chi^2, 13.6 and
     // 7.1 us) lose: with the chi^2 on a side stream forked and joined by events
-    // the step took 87.5 instead of 63.3 us (round 2)
+    // the step took 87.5 instead of 63.3 us (round 2).  They share one launch
+    // instead (plan_corun): 15.4 us against 13.5 + 4.6 (round 3)
     for (size_t i = 0; i < nl; i++) {
         hipStream_t st = stream;
         auto &l = s->likes[i];
@@ -2327,7 +2360,7 @@ static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1,
             HIP_CHECK(hipGetLastError());
         }
         if (fuse && fused(s, i)) {
-            eval_after_window(s, i, defer, st);
+            eval_after_window(s, i, defer, st, co);
             continue;
         }
         if (defer && eval_deferred(s, i, nb, st)) continue;
@@ -2932,5 +2965,10 @@ extern "C" int cmamd_debug_tp_items(const cmbs *s, int *out, int cap) {   // (fi
         for (int q = 0; q < 6; q++) out[6 * k + q] = v[q];
     }
     return s->tpass->n_items();
+}
+extern "C" int cmamd_debug_corun(cmbs *s, int on) {     // the lensing chi^2 inside plik's quadratic-form launch
+    if (!s) return -1;
+    s->no_corun = !on;
+    return 0;
 }
 extern "C" int cmamd_debug_fused(const cmbs *s) { return !s ? 0 : s->tpass ? s->tpass->n_items() : -s->tp_why; }

@@ -1,0 +1,107 @@
+// Small gaussian CMBlikes chi^2 (nX <= 64 bandpowers, e.g. Planck lensing 9,
+// SPT-SZ 47): binned spectra, bigX = C - Chat and chi^2 = bigX^T C^-1 bigX in
+// one workgroup body (CMBlikes.f90:1183-1225; Matrix_QuadForm as row sums
+// y = M x, then x.y).  Shared by cmbl_gauss_small_kernel (cmblikes.hip) and by
+// the deferred quadratic form's launch (quadform.hip, quadform_corun), where
+// its workgroups run beside the quadratic form's instead of in a launch of
+// their own.  The arguments are SmallGaussLaunch (common.h).
+//
+// Workgroup = WT walkers x 256 / WT thread groups.  The partial rows of every
+// element are cut into tasks of <= 8 rows (host); groups take tasks
+// round-robin with all loads of a task in flight, then combine them per
+// element in task order (deterministic), then split the rows of M.  Every
+// table load is issued at the start, beside the others: the partial loads
+// wait on one table level (the task's rows), nothing after them on any.
+#pragma once
+
+#include "common.h"
+
+namespace cmamd {
+
+static constexpr int SMALL_NX = 64;
+static constexpr int SMALL_WT = 4;          // walkers per workgroup (measured: 7.1 / 8.0 / 9.8 / 13.9 us for 4 / 2 / 8 / 16)
+static constexpr int SMALL_MAXTASK = 256;   // tasks per dataset
+
+// LDS of one workgroup body: tp[SMALL_MAXTASK][WT], xs[SMALL_NX][WT],
+// red[256 / WT][WT], M[SMALL_NX][SMALL_NX]
+template <int WT> constexpr int small_gauss_lds_doubles() {
+    return SMALL_MAXTASK * WT + SMALL_NX * WT + 256 + SMALL_NX * SMALL_NX;
+}
+
+template <int WT>
+__device__ __forceinline__ void small_gauss_body(const SmallGaussLaunch &a, double *lds, int blk)
+{
+    constexpr int NG = 256 / WT;             // thread groups of WT walkers
+    double *tp = lds;                        // [SMALL_MAXTASK][WT]
+    double *xs = tp + SMALL_MAXTASK * WT;    // [SMALL_NX][WT]
+    double *red = xs + SMALL_NX * WT;        // [NG][WT]
+    double *Msh = red + NG * WT;             // [nX][nX]
+    const SmallGaussDev &c = a.d;
+    const int W = a.W;
+    const int wl = threadIdx.x % WT, g = threadIdx.x / WT;
+    const int w = blk * WT + wl;
+    const int Wc = c.wcount ? min(W, *c.wcount) : W;
+    if (blk * WT >= Wc) return;
+    for (int i = threadIdx.x; i < c.nX * c.nX; i += 256) Msh[i] = a.M[i];   // in flight with the partial loads
+    const bool act = w < Wc;
+    const bool calp = c.log_cal_prior > 0 && c.cal_index >= 0;
+    const double cal = (g == 0 && act && calp) ? a.nuis[(long long)w * a.ld_nuis + c.cal_index] : 1.0;   // likewise
+    struct Elem { int ix, m0, m1, c0, c1; double mc, cc, fc, ch; };
+    auto elem = [&](int e) {   // element e's table entries
+        Elem q{c.e_to_x[e], c.e_main_t[e], c.e_main_t[e + 1], 0, 0, c.e_main_const[e], 0.0, 0.0, c.chat[e]};
+        if (c.has_corr) {
+            q.c0 = c.e_corr_t[e];
+            q.c1 = c.e_corr_t[e + 1];
+            q.cc = c.e_corr_const[e];
+            q.fc = c.fidcorr[e];
+        }
+        return q;
+    };
+    Elem e0{-1, 0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0};
+    if (g < c.nE) e0 = elem(g);   // this group's first element, in flight with the partials
+    for (int t = g; t < c.ntask; t += NG) {
+        const int4 ra = *reinterpret_cast<const int4 *>(c.trow + 8 * t);
+        const int4 rb = *reinterpret_cast<const int4 *>(c.trow + 8 * t + 4);
+        const int r[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = (act && r[u] >= 0) ? a.partial[(long long)r[u] * W + w] : 0.0;
+        double s = 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) s += v[u];
+        tp[t * WT + wl] = s;
+    }
+    __syncthreads();
+    for (int e = g; e < c.nE; e += NG) {
+        const Elem q = e == g ? e0 : elem(e);
+        if (q.ix < 0) continue;
+        double s = q.mc;
+        for (int t = q.m0; t < q.m1; t++) s += tp[t * WT + wl];
+        if (c.has_corr) {
+            double cs = q.cc;
+            for (int t = q.c0; t < q.c1; t++) cs += tp[t * WT + wl];
+            s = s + (cs - q.fc);
+        }
+        xs[q.ix * WT + wl] = s - q.ch;
+    }
+    __syncthreads();
+    double part = 0.0;
+    for (int i = g; i < c.nX; i += NG) {
+        double y = 0.0;
+        for (int j = 0; j < c.nX; j++) y += Msh[i * c.nX + j] * xs[j * WT + wl];
+        part += xs[i * WT + wl] * y;
+    }
+    red[g * WT + wl] = part;
+    __syncthreads();
+    if (g == 0 && act) {
+        double chisq = 0.0;
+        for (int k = 0; k < NG; k++) chisq += red[k * WT + wl];
+        if (calp) {
+            const double t = log(cal) / c.log_cal_prior;
+            chisq = chisq + t * t;
+        }
+        a.out[w] = chisq / 2;
+    }
+}
+
+}  // namespace cmamd
