@@ -216,8 +216,9 @@ def kernel_profile(smp, steps):
     more fast steps (HIP events on the launch stream)."""
     import torch
     from cosmomc_amd import _native as N
-    names = ("plik_bin_delta", "plik_quadform_ksplit", "plik_quadform_corun", "mh_kernel", "rot_kernel", "cmbl_bk_prologue", "cmbl_window_kernel",
-             "cmbl_reduce_kernel", "cmbl_hl_kernel", "cmbl_quadform", "cmbl_gauss_small_kernel")
+    names = ("plik_bin_delta", "plik_quadform_ksplit", "plik_quadform_corun", "mh_kernel", "mh_pass_kernel",
+             "rot_kernel", "cmbl_bk_prologue", "cmbl_window_kernel", "cmbl_reduce_kernel",
+             "cmbl_hl_kernel", "cmbl_quadform", "cmbl_gauss_small_kernel")
     N.profile_reset()
     N.profile_enable(True)
     smp.step(steps, fast_only=True)
@@ -597,7 +598,8 @@ def pmc_traffic(kernel, W):
     symbols = {"plik_quadform_ksplit": ("quadform_ksplit<false>", "quadform_ksplit"),   # profiler label -> kernel
                "cmbl_window_kernel": ("cmbl_window_direct",),
                "theory_window_kernel": ("theory_window_vec<2, 0>", "theory_window_kernel<2>", "theory_window_kernel<4>",
-                                        "theory_window_kernel")}.get(kernel, (kernel,))
+                                        "theory_window_kernel"),
+               "mh_pass_kernel": ("mh_pass_kernel<true>", "mh_pass_kernel")}.get(kernel, (kernel,))
     t = next((d["per_launch"][k] for k in symbols if k in d["per_launch"]), None)
     if not t:
         return None, None
@@ -692,7 +694,7 @@ def main():
         torch.cuda.synchronize()
         N.profile_enable(False)
         kern = {k: N.profile_read(k) for k in ("theory_window_kernel", "plik_bin_delta", "plik_quadform_ksplit",
-                                                "plik_quadform_corun", "mh_kernel",
+                                                "plik_quadform_corun", "mh_kernel", "mh_pass_kernel",
                                                 "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_gauss_small_kernel",
                                                 "cmbl_quadform")}
         kern = {k: v for k, v in kern.items() if v[1]}
@@ -723,7 +725,11 @@ def main():
             ach = W * BYTES_BIN / (avg_ms[dom] * 1e-3) / 1e9
         elif dom == "cmbl_window_kernel":
             ach = (W * lens_bytes[0] + lens_bytes[1]) / (avg_ms[dom] * 1e-3) / 1e9
-        elif dom == "theory_window_kernel":   # + plik's Delta rows written (the lensing partial rows not counted)
+        elif dom in ("theory_window_kernel", "mh_pass_kernel"):
+            # the fused pass's bytes: theory rows + weights + plik's Delta rows written (the lensing partial
+            # rows not counted); for mh_pass_kernel (the pipelined steps: the pass with the Metropolis
+            # workgroups in one launch) the Metropolis state traffic is not counted either, and the pass
+            # reads its own sums back once (L2) to apply the calibrations: also not counted
             ach = (W * (fused_bytes[0] + 8 * N_B) + fused_bytes[1]) / (avg_ms[dom] * 1e-3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": (ach / PEAK_HBM_GBS) if ach else None, "traffic": None}

@@ -87,6 +87,13 @@ struct DevCfg {
     int def_like[MAXDEF], def_items[MAXDEF];
     const double *def_part[MAXDEF];         // [tiles][def_items][64]
     const double *def_add[MAXDEF];          // [W] or null
+    // pipelined fast steps (mh_pass_kernel): a proposing launch publishes the
+    // fused pass's two stage calibrations of every walker's trial and counts
+    // its workgroups done per 64-walker tile (TPDev::tilecnt)
+    int pub_on;                             // set per launch
+    int pub_pcal[2];                        // the stages' calibration parameters (0-based, -1: none)
+    double *calbuf;                         // [2][ld]
+    unsigned *tilecnt;                      // [ld / 64]
 };
 
 struct LikeSlot {
@@ -164,6 +171,13 @@ struct cmbs {
     int tp_like[2] = {-1, -1};               // [0] plik_lite (Delta rows), [1] CMBlikes (partial rows)
     cmamd::WinStage tp_stage[2];
     bool no_corun = false;                   // debug: the fused pass's tails as separate launches
+    // pipelined fast steps: the fused pass of step k runs in the launch of
+    // the mh_kernel proposing it (sampler_step, mh_pass_kernel)
+    bool no_pipe = false;                    // debug: off
+    cmamd::DevBuf pipe_cal, pipe_cnt;        // DevCfg::calbuf, tilecnt
+    size_t pipe_lds = 0;                     // mh_pass_kernel's LDS
+    unsigned pipe_epoch = 0;                 // proposing pipelined launches so far
+    int pipe_ready = 0;                      // set up for this W (0: not yet)
     int tp_why = 0;                          // set-up progress when no pass was built (debug)
     ~cmbs() {
         for (auto &st : streams)

@@ -24,6 +24,19 @@
 
 #include "quadform.h"
 #include "sampler.h"
+#ifdef CMAMD_STAMPS
+// mh_pass_kernel block timeline (tools/pipe_stamps.py): s_memrealtime at the
+// start, [pass] streaming done / wait done, end; [3] the block's role
+namespace cmamd {
+__device__ unsigned long long g_pipe_stamps[2048][5];
+}
+#define TP_PIPE_STAMP(i)                                                                        \
+    do {                                                                                        \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                         \
+        if (threadIdx.x == 0 && blockIdx.x < 2048) cmamd::g_pipe_stamps[blockIdx.x][i] = t_;    \
+    } while (0)
+#endif
+#include "theorypass_body.h"
 
 namespace cmamd {
 
@@ -537,13 +550,13 @@ __device__ inline void write_like_flags(const DevCfg &c, const QT &trial, const 
 // next trial (GetProposal / GetProposalFast) and scatter its nuisance
 // parameters for the likelihood kernels.  MB walkers per block.
 template <bool ACCEPT, bool PROPOSE>
-__global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only, double *hist_row, double *hist_terms, int blk0)
+__device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *hist_row, double *hist_terms, int blk0,
+                                        double *lds, int bx)
 {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
     const Rows &R = c.rows;
     const int lane = threadIdx.x % MB, grp = threadIdx.x / MB;    // walker in block, thread group
     const int wl64 = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = MH_THREADS / 64;
-    const int wb = (blk0 + blockIdx.x) * MB;
+    const int wb = (blk0 + bx) * MB;
     const int w = wb + lane;
     const bool act = w < c.W;
     const size_t W = c.ld;
@@ -566,7 +579,7 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
     if (threadIdx.x < MB) oobw[threadIdx.x] = 0;
     // the rotation list of this walker range: this launch appends to counter
     // rot_par; the other one (read by the previous step's rot_kernel) restarts
-    if (PROPOSE && c.rot_defer && blockIdx.x == 0 && threadIdx.x == 0)
+    if (PROPOSE && c.rot_defer && bx == 0 && threadIdx.x == 0)
         c.rot_cnt[2 * (blk0 * MB / 64) + (c.rot_par ^ 1)] = 0;
     const bool skipR = !c.stage_R;
     // staged double row index of global row r (rotation rows dropped when not staged)
@@ -793,6 +806,18 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
     }
     __syncthreads();
     STAMP(13);
+    if (PROPOSE && c.pub_on) {   // the fused pass in this launch waits for these (tp_vec_body<.., true>)
+        if (threadIdx.x < MB && act)
+            for (int k = 0; k < 2; k++) {
+                const int pc = c.pub_pcal[k];
+                const double v = pc >= 0 ? sd[(size_t)(SROW(R.T) + pc) * MB + lane] : 1.0;
+                __hip_atomic_store(c.calbuf + (size_t)k * W + w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_fetch_add(c.tilecnt + wb / 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // write back the image (rows of walkers past W are padding of the ld-wide
     // rows: written back unchanged)
     if (skipR) {
@@ -808,6 +833,46 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
     STAMP(6);
 #endif
 #undef SROW
+}
+
+template <bool ACCEPT, bool PROPOSE>
+__global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only, double *hist_row, double *hist_terms, int blk0)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, blk0, lds, blockIdx.x);
+}
+
+// A proposing mh_kernel and the fused window pass of the step it proposes in
+// one launch (the pipelined fast steps of sampler_step): the first nmh
+// workgroups are mh_kernel's (walker blocks 0 .. nmh - 1, the pad up to a
+// multiple of 8 idle so the pass's blocks keep their XCDs), the rest run the
+// pass (tp_vec_body<2, true>), which needs the new trial calibrations only for
+// its last phase and waits for its tile's Metropolis workgroups there.  Those
+// are dispatched first and wait on nothing, so the wait always ends.  The
+// latency-bound Metropolis blocks (64 CUs at W = 1024) overlap the HBM-bound
+// pass instead of preceding it.
+template <bool ACCEPT>
+__global__ __launch_bounds__(MH_THREADS, 3) void mh_pass_kernel(DevCfg c, int fast_only, double *hist_row,
+                                                                double *hist_terms, int nmh, int nmh_pad, TPDev tp,
+                                                                const double *dl, long long ld_field,
+                                                                long long ld_walker)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int b = blockIdx.x;
+    TP_PIPE_STAMP(0);
+    if (b < nmh_pad) {
+        if (b < nmh) mh_body<ACCEPT, true>(c, fast_only, hist_row, hist_terms, 0, lds, b);
+        TP_PIPE_STAMP(3);
+#ifdef CMAMD_STAMPS
+        if (threadIdx.x == 0 && b < 2048) cmamd::g_pipe_stamps[b][4] = 1;
+#endif
+        return;
+    }
+    tp_vec_body<2, true>(tp, dl, ld_field, ld_walker, c.W, reinterpret_cast<char *>(lds), b - nmh_pad);
+    TP_PIPE_STAMP(3);
+#ifdef CMAMD_STAMPS
+    if (threadIdx.x == 0 && b < 2048) cmamd::g_pipe_stamps[b][4] = 2;
+#endif
 }
 
 // ------------------------------------------------------- deferred rotations
@@ -1707,6 +1772,11 @@ static void set_mh_lds(cmbs *s) {
         d.itmp_g = s->itmp_g.as<int>();
     }
     const int lds = (int)s->mh_lds;
+    s->pipe_lds = std::max(s->mh_lds, (size_t)tp_vec_lds_bytes<2, true>());
+    HIP_CHECK(hipFuncSetAttribute((const void *)mh_pass_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)s->pipe_lds));
+    HIP_CHECK(hipFuncSetAttribute((const void *)mh_pass_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)s->pipe_lds));
     HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -2018,6 +2088,7 @@ static std::vector<int> bin_safe_cuts(const std::vector<std::pair<int, int>> &bi
 static void setup_fusion(cmbs *s) {
     s->tpass.reset();
     s->tp_like[0] = s->tp_like[1] = -1;
+    s->pipe_ready = 0;
     const int nl = (int)s->likes.size();
     auto sparse = [&](int i) {
         for (int q : s->sparse_likes)
@@ -2322,12 +2393,14 @@ static void eval_likes_masked(cmbs *s, hipStream_t stream, bool defer = false) {
 // likelihood terms of walkers [g0, g1) at their trial points
 // defer: the accepting mh_kernel launched next finishes the deferrable
 // likelihoods (all walkers, one group)
-static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1, void *ws, bool defer = false) {
+// pass_done: the fused pass already ran (the pipelined steps' mh_pass_kernel)
+static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1, void *ws, bool defer = false,
+                       bool pass_done = false) {
     const int Wg = g1 - g0;
     if (defer && (g0 != 0 || g1 != s->W)) fail(CMBL_ERR_ARG, "internal: deferred evaluation of a walker group");
     const size_t nl = s->likes.size();
     const bool fuse = s->tpass && g0 == 0 && g1 == s->W;
-    if (fuse) {   // every nuisance slice first: the pass reads both likelihoods'
+    if (fuse && !pass_done) {   // every nuisance slice first: the pass reads both likelihoods'
         if (gather)
             for (size_t i = 0; i < nl; i++) {
                 const int nn = s->likes[i].like->like->n_nuis;
@@ -2409,8 +2482,47 @@ static bool rot_may_pend(cmbs *s, int fast_only, int g0) {
 
 static void rot_schedule_unknown(cmbs *s) { std::fill(s->rot_lp.begin(), s->rot_lp.end(), -1); }
 
+// The pipelined fast steps (sampler_step).  The fused window pass of step k
+// runs in the launch of the mh_kernel that proposes step k (mh_pass_kernel):
+// its blocks stream the theory while the Metropolis blocks work, store raw
+// sums, and apply the new calibrations once their tile's Metropolis blocks
+// have published them (tp_vec_body<2, true>).  Step k's tails (plik's
+// deferred quadratic form with the lensing chi^2) follow as before.  Every
+// step's pass still reads the theory once; the Metropolis blocks (64 CUs at
+// W = 1024) now overlap the HBM-bound pass instead of following it.
+// The pass's workgroups hold back this long (10 ns ticks of s_memrealtime)
+// at the start of the launch: the Metropolis workgroups' loads go ahead of the
+// pass's streaming, and those workgroups, whose end the pass waits for, end
+// sooner (block stamps, tools/pipe_stamps.py: Metropolis ends 18.2-23.6 us
+// without it, 16.1-22.4 with 2 us; mh_pass_kernel 27.1 / 24.2 / 25.3 / 26.1 us
+// for 0 / 2 / 3 / 4 us, MI355X, W = 1024)
+static constexpr int PIPE_DELAY = 200;
+
+static TPOut pass_out(cmbs *s, int k) {
+    const int i = s->tp_like[k];
+    const WinStage &st = s->tp_stage[k];
+    Like &L = *s->likes[i].like->like;
+    return TPOut{st.kind, st.cal_index, st.ld, 0, L.window_out(s->like_ws[i].p, s->W), st.X, s->dc.like_nuis[i],
+                 (long long)std::max(1, L.n_nuis)};
+}
+
+// Whether this run of fast steps can be pipelined: the fused pass takes its
+// vectorised form and every walker proposes in one launch (one group, no
+// change mask, no rotations left to rot_kernel).
+static bool pipe_setup(cmbs *s, int fast_only) {
+    if (s->no_pipe || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on || s->dc.rot_defer) return false;
+    const LikeSlot &P = s->likes[s->tp_like[0]];
+    if (!s->tpass->vec_ok(P.dl, P.ld_field, P.ld_walker)) return false;
+    if (s->pipe_ready == s->W) return true;
+    s->pipe_cal.alloc((size_t)2 * s->dc.ld * 8);
+    s->pipe_cnt.alloc((size_t)(s->dc.ld / 64 + 1) * 4);   // zeroed
+    s->pipe_epoch = 0;
+    s->pipe_ready = s->W;
+    return true;
+}
+
 static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const HistRow &row, hipStream_t stream,
-                      int g0, int g1, bool masked = false) {
+                      int g0, int g1, bool masked = false, bool pipe = false) {
     const dim3 g((g1 - g0 + MB - 1) / MB), b(MH_THREADS);
     const int blk0 = g0 / MB;
     const size_t lds = s->mh_lds;
@@ -2424,6 +2536,38 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
     }
     dc.n_def = s->pending_def;
     s->pending_def = 0;
+    dc.pub_on = 0;
+    if (pipe) {   // mh_pass_kernel: this launch proposes the step whose pass rides along
+        if (!propose || g0 != 0 || g1 != s->W || rot) fail(CMBL_ERR_ARG, "internal: pipelined step launch");
+        dc.pub_on = 1;
+        for (int k = 0; k < 2; k++) {
+            const WinStage &st = s->tp_stage[k];
+            dc.pub_pcal[k] = st.cal_index >= 0 ? s->likes[s->tp_like[k]].nidx[st.cal_index] : -1;
+        }
+        dc.calbuf = s->pipe_cal.as<double>();
+        dc.tilecnt = s->pipe_cnt.as<unsigned>();
+        const int nmh = (int)g.x, nmh_pad = (nmh + 7) / 8 * 8;
+        const TPOut o[2] = {pass_out(s, 0), pass_out(s, 1)};
+        TPDev tp = s->tpass->dev_args(o, s->W);
+        tp.tilecnt = dc.tilecnt;
+        tp.epoch = ++s->pipe_epoch;
+        tp.mblk = MB;
+        tp.calbuf = dc.calbuf;
+        tp.cal_ld = dc.ld;
+        tp.delay = PIPE_DELAY;
+        const LikeSlot &P = s->likes[s->tp_like[0]];
+        const dim3 gp(nmh_pad + s->tpass->n_blocks());
+        timed_launch("mh_pass_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            if (accept)
+                hipExtLaunchKernelGGL(mh_pass_kernel<true>, gp, b, s->pipe_lds, stream, e0, e1, 0, dc, fast_only, row.p,
+                                      row.t, nmh, nmh_pad, tp, P.dl, P.ld_field, P.ld_walker);
+            else
+                hipExtLaunchKernelGGL(mh_pass_kernel<false>, gp, b, s->pipe_lds, stream, e0, e1, 0, dc, fast_only,
+                                      row.p, row.t, nmh, nmh_pad, tp, P.dl, P.ld_field, P.ld_walker);
+        });
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
     timed_launch("mh_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
         if (accept && propose)
             hipExtLaunchKernelGGL(mh_kernel<true, true>, g, b, lds, stream, e0, e1, 0, dc, fast_only, row.p, row.t, blk0);
@@ -2473,6 +2617,16 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (n_steps <= 0) return;
     // propose(1) | likes | accept(1)+propose(2) | likes | ... | likes | accept(n)
     const int G = s->n_groups;
+    if (G == 1 && pipe_setup(s, fast_only)) {
+        // pipelined: propose(1) + pass(1) | tails(1) | accept(1) + propose(2) + pass(2) |
+        // tails(2) | ... | tails(n) | accept(n)
+        for (int k = 0; k < n_steps; k++) {
+            launch_mh(s, k > 0, true, fast_only, k > 0 ? next_hist(s) : HistRow{}, stream, 0, s->W, false, true);
+            eval_likes(s, stream, false, 0, s->W, s->ws.p, true, true);
+        }
+        launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W, false);
+        return;
+    }
     if (G == 1) {
         const bool m = s->mask_on;
         launch_mh(s, false, true, fast_only, HistRow{}, stream, 0, s->W, m);
@@ -2938,6 +3092,10 @@ void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
 }  // namespace cmamd
 
 #ifdef CMAMD_STAMPS
+extern "C" int cmamd_debug_pipe_stamps(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_pipe_stamps), sizeof(cmamd::g_pipe_stamps)) == hipSuccess ? 0
+                                                                                                                 : -5;
+}
 extern "C" int cmamd_debug_stamps(unsigned long long *host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_stamps), sizeof(cmamd::g_stamps)) == hipSuccess ? 0 : -5;
 }
@@ -2965,6 +3123,11 @@ extern "C" int cmamd_debug_tp_items(const cmbs *s, int *out, int cap) {   // (fi
         for (int q = 0; q < 6; q++) out[6 * k + q] = v[q];
     }
     return s->tpass->n_items();
+}
+extern "C" int cmamd_debug_pipeline(cmbs *s, int on) {   // pipelined fast steps (sampler_step)
+    if (!s) return -1;
+    s->no_pipe = !on;
+    return 0;
 }
 extern "C" int cmamd_debug_corun(cmbs *s, int on) {     // the lensing chi^2 inside plik's quadratic-form launch
     if (!s) return -1;

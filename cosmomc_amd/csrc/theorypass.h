@@ -58,6 +58,16 @@ struct TPDev {
     const unsigned char *cmap;        // per item step, [64] slots: the item's column index (255: none)
     int nitem;
     TPOut out[TP_MAXOUT];
+    // pipelined form (tp_vec_body<.., true>, the sampler's mh_pass_kernel):
+    // the step's calibrations come from the Metropolis workgroups of the same
+    // launch, which publish them per walker and count themselves done per
+    // 64-walker tile
+    const unsigned *tilecnt;   // [tiles] Metropolis workgroups done, cumulative over launches
+    unsigned epoch;            // launches so far, this one included
+    int mblk;                  // walkers per Metropolis workgroup
+    const double *calbuf;      // [TP_MAXOUT][cal_ld] each stage's calibration of walker w
+    long long cal_ld;
+    int delay;                 // 10 ns ticks the pass holds back at the start
 };
 
 class TheoryPass {
@@ -67,6 +77,13 @@ class TheoryPass {
     bool build(const std::vector<WinStage> &stages);
     void launch(const double *dl, long long ld_field, long long ld_walker, const TPOut *outs, int W,
                 hipStream_t stream);
+    // The vectorised kernel applies (16-byte aligned rows, at most two MFMA
+    // blocks per item): the form the sampler's pipelined steps run
+    bool vec_ok(const double *dl, long long ld_field, long long ld_walker) const;
+    // its arguments and block count for W walkers (theorypass_body.h)
+    TPDev dev_args(const TPOut *outs, int W);
+    int n_blocks() const { return nblk; }
+
     int n_items() const { return (int)items.size(); }
     const TPItem &item(int k) const { return items[k]; }
     int n_stages() const { return nstage; }

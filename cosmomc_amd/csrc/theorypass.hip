@@ -39,6 +39,7 @@ namespace cmamd {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 #ifdef CMAMD_STAMPS
+#define CMAMD_TP_STAMPS
 // per block of the last launch: s_memtime at start, after the prologue, after
 // the step loop, at the end; HW_ID, XCC_ID and the item (tools/tp_stamps.py)
 __device__ unsigned long long g_tp_stamps[4096][10];
@@ -50,6 +51,12 @@ __device__ unsigned long long g_tp_stamps[4096][10];
 #else
 #define TP_STAMP(i) ((void)0)
 #endif
+
+}  // namespace cmamd
+
+#include "theorypass_body.h"
+
+namespace cmamd {
 
 // NB: the most 16-slot blocks any item uses.  With slot reuse the headline
 // items need at most two, and four accumulators fit three waves per SIMD
@@ -249,222 +256,13 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_kernel(TPD
 #endif
 }
 
-// The same pass when every theory row is 16-byte aligned (the sampler's
-// case), written so that each step's loads are unconditional straight-line
-// code: the theory rows two steps ahead (addresses clamped into the row, l
-// past the item read as 0), the weight tiles of every block two steps ahead
-// in registers (blocks past the item's own read its neighbour's weights or
-// the padding: stored, never used), and the last two steps peeled off.  The
-// compiler then counts the loads in flight exactly, and a step waits only for
-// its own data instead of draining the prefetch (vmcnt(0)) at the weight
-// store, which held every step to a full memory latency.
+// The vectorised pass (theorypass_body.h) as a kernel of its own
 template <int NB>
-__global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev c, const double *__restrict__ dl, long long ld_field,
-                                                         long long ld_walker, int W)
+__global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev c, const double *__restrict__ dl,
+                                                                         long long ld_field, long long ld_walker, int W)
 {
-    constexpr int LPL = 8, STEP = 4 * LPL, NSUB = TP_CHUNK / STEP, WROW = STEP + 2;
-    __shared__ __attribute__((aligned(16))) double wsh[2 * NB * 16 * WROW];   // [buf][col block][col][l]
-    __shared__ TPCol csh[TP_MAXCOL];
-    __shared__ double xsh[TP_MAXCOL];
-    __shared__ unsigned long long esh[TP_MAXSTEP];
-    __shared__ unsigned char msh[TP_MAXSTEP * TP_MAXCOL];
-    const int b = blockIdx.x;
-    const int2 unit = c.units[b];
-    const int item = unit.x, tile = unit.y;
-    if (item < 0) return;
-    TP_STAMP(0);
-#ifdef CMAMD_STAMPS
-    const unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();
-#endif
-    const TPItem it = c.items[item];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int li = lane & 15, kq = lane >> 4;
-    const int w = tile * 64 + wave * 16 + li;
-    const int wl = min(w, W - 1);
-    const double *Df = dl + (long long)wl * ld_walker + (long long)it.field * ld_field;
-    const int lcap = ((int)ld_field - 2) & ~1;
-    const int ncb = it.nsb;
-    const int nstep = it.nst;
-    double tA[LPL], tB[LPL], tC[LPL], a[LPL];
-    auto load_t = [&](int st, double *dst) {  // raw rows, addresses clamped into the row
-        const int lb = it.l0 + st * STEP + 2 * kq;
-#pragma unroll
-        for (int q = 0; q < LPL / 2; q++) {
-            const double2 v = *reinterpret_cast<const double2 *>(Df + min(lb + 8 * q, lcap));
-            dst[2 * q] = v.x;
-            dst[2 * q + 1] = v.y;
-        }
-    };
-    const int wc = tid >> 4, wp = 2 * (tid & 15);
-    double2 wr0{}, wr1{}, wr2{}, wr3{};      // named registers: an array here lands in scratch
-    auto fetch_w = [&](int st) {
-        const int ch = st / NSUB, sub = st % NSUB;
-        const double *base = c.w + it.woff + (long long)ch * ncb * 16 * TP_CHUNK + sub * STEP + wc * TP_CHUNK + wp;
-        wr0 = *reinterpret_cast<const double2 *>(base);
-        wr1 = *reinterpret_cast<const double2 *>(base + 16 * TP_CHUNK);
-        if constexpr (NB > 2) {
-            wr2 = *reinterpret_cast<const double2 *>(base + 2 * 16 * TP_CHUNK);
-            wr3 = *reinterpret_cast<const double2 *>(base + 3 * 16 * TP_CHUNK);
-        }
-    };
-    auto store_w = [&](int buf) {
-        double *d = wsh + (buf * NB * 16 + wc) * WROW + wp;
-        *reinterpret_cast<double2 *>(d) = wr0;
-        *reinterpret_cast<double2 *>(d + 16 * WROW) = wr1;
-        if constexpr (NB > 2) {
-            *reinterpret_cast<double2 *>(d + 2 * 16 * WROW) = wr2;
-            *reinterpret_cast<double2 *>(d + 3 * 16 * WROW) = wr3;
-        }
-    };
-    auto read_w = [&](int buf, int cb) {
-        const double *src = wsh + ((buf * NB + cb) * 16 + li) * WROW + 2 * kq;
-#pragma unroll
-        for (int q = 0; q < LPL / 2; q++) {
-            const double2 v = *reinterpret_cast<const double2 *>(src + 8 * q);
-            a[2 * q] = v.x;
-            a[2 * q + 1] = v.y;
-        }
-    };
-    f64x4 acc[NB], bcc[NB];
-#pragma unroll
-    for (int cb = 0; cb < NB; cb++) acc[cb] = bcc[cb] = f64x4{0.0, 0.0, 0.0, 0.0};
-    // prologue: theory steps 0, 1; weights of step 0 into LDS, of step 1 in registers
-    load_t(0, tA);
-    load_t(1, tB);                       // nstep >= 2: an item is whole 64-l chunks
-    fetch_w(0);
-    if (tid < it.ncol) {
-        const TPCol d = c.cols[it.cdesc + tid];
-        csh[tid] = d;
-        const int kind = d.out ? c.out[1].kind : c.out[0].kind;
-        const double *X = d.out ? c.out[1].X : c.out[0].X;
-        xsh[tid] = kind == 1 ? X[d.row] : 0.0;
-    }
-    if (tid < nstep) esh[tid] = c.emit[it.soff + tid];
-    for (int q = tid; q < nstep * (TP_MAXCOL / 4); q += 256)
-        reinterpret_cast<unsigned int *>(msh)[q] =
-            reinterpret_cast<const unsigned int *>(c.cmap + (long long)it.soff * TP_MAXCOL)[q];
-    double c2[TP_MAXOUT];
-#pragma unroll
-    for (int o = 0; o < TP_MAXOUT; o++) {
-        const int ci = o ? c.out[1].cal_index : c.out[0].cal_index;
-        const double *nu = o ? c.out[1].nuis : c.out[0].nuis;
-        const long long ldn = o ? c.out[1].ld_nuis : c.out[0].ld_nuis;
-        double cl = 1.0;
-        if (ci >= 0 && nu) cl = nu[(long long)wl * ldn + ci];
-        c2[o] = cl * cl;
-    }
-    store_w(0);
-    __syncthreads();
-    TP_STAMP(1);
-    auto emit = [&](int st, unsigned long long e, int cb, f64x4 &a0, f64x4 &b0) {
-        int col[4];
-        bool on[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int slot = 16 * cb + kq + 4 * r;
-            on[r] = (e >> slot) & 1ull;
-            col[r] = msh[st * TP_MAXCOL + slot] & (TP_MAXCOL - 1);   // 255 (no column) -> any: not stored
-        }
-        TPCol d[4];
-        double x[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            d[r] = csh[col[r]];
-            x[r] = xsh[col[r]];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const double v = a0[r] + b0[r];
-            a0[r] = on[r] ? 0.0 : a0[r];
-            b0[r] = on[r] ? 0.0 : b0[r];
-            const bool o1 = d[r].out != 0;
-            const double q = d[r].cal ? v / (o1 ? c2[1] : c2[0]) : v;
-            if (on[r] && w < W) {
-                double *out = o1 ? c.out[1].out : c.out[0].out;
-                if ((o1 ? c.out[1].kind : c.out[0].kind) == 0)
-                    out[(long long)d[r].row * W + w] = q;
-                else
-                    out[(long long)w * (o1 ? c.out[1].ld : c.out[0].ld) + d[r].row] = x[r] - q;
-            }
-        }
-    };
-    auto closes = [&](int st) {   // the columns that end at step st
-        const unsigned long long e = esh[st];
-#pragma unroll
-        for (int cb = 0; cb < NB; cb++)
-            if ((e >> (16 * cb)) & 0xffffull) emit(st, e, cb, acc[cb], bcc[cb]);
-    };
-    auto compute = [&](int st, const double *tc, bool tail) {
-        double tb[LPL];
-        const int lb = it.l0 + st * STEP + 2 * kq;
-#pragma unroll
-        for (int q = 0; q < LPL / 2; q++)
-#pragma unroll
-            for (int h = 0; h < 2; h++) tb[2 * q + h] = (!tail || lb + 8 * q + h <= it.l1) ? tc[2 * q + h] : 0.0;
-        const int cur = st & 1;
-        const unsigned m = (unsigned)(it.act >> (4 * st)) & 15u;
-#pragma unroll
-        for (int cb = 0; cb < NB; cb++)
-            if (m & (1u << cb)) {
-                read_w(cur, cb);
-#pragma unroll
-                for (int s2 = 0; s2 < LPL; s2 += 2) {
-                    acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s2], tb[s2], acc[cb], 0, 0, 0);
-                    bcc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s2 + 1], tb[s2 + 1], bcc[cb], 0, 0, 0);
-                }
-            }
-    };
-    // main steps: weights of st + 1 and theory of st + 2 in flight; step s
-    // lives in buffer s mod 3 (A, B, C)
-    auto step = [&](int st, const double *tc, double *tl) {
-        fetch_w(st + 1);
-        load_t(st + 2, tl);
-        compute(st, tc, false);
-        closes(st);
-        store_w((st & 1) ^ 1);
-        __syncthreads();
-    };
-    int st = 0;
-    while (st + 2 < nstep) {
-        step(st, tA, tC);
-        if (++st + 2 >= nstep) break;
-        step(st, tB, tA);
-        if (++st + 2 >= nstep) break;
-        step(st, tC, tB);
-        ++st;
-    }
-    // the last two steps: nothing more to load
-    auto tail = [&](const double *t0, const double *t1) {
-        fetch_w(st + 1);
-        compute(st, t0, true);
-        store_w((st & 1) ^ 1);
-        __syncthreads();
-        closes(st);
-        compute(st + 1, t1, true);
-        closes(st + 1);
-    };
-    switch (st % 3) {
-        case 0: tail(tA, tB); break;
-        case 1: tail(tB, tC); break;
-        default: tail(tC, tA); break;
-    }
-    TP_STAMP(2);
-#ifdef CMAMD_STAMPS
-    if (threadIdx.x == 0 && b < 4096) {
-        g_tp_stamps[b][4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-        g_tp_stamps[b][5] = __builtin_amdgcn_s_getreg((3 << 11) | 20);
-        g_tp_stamps[b][6] = item;
-        g_tp_stamps[b][7] = (unsigned long long)nstep * 1000 + __builtin_popcountll(it.act);
-    }
-#endif
-    TP_STAMP(3);
-#ifdef CMAMD_STAMPS
-    const unsigned long long rt1_ = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0 && b < 4096) {
-        g_tp_stamps[b][8] = rt0_;
-        g_tp_stamps[b][9] = rt1_;
-    }
-#endif
+    __shared__ __attribute__((aligned(16))) char lds[tp_vec_lds_bytes<NB>()];
+    tp_vec_body<NB, false>(c, dl, ld_field, ld_walker, W, lds, blockIdx.x);
 }
 
 // ------------------------------------------------------------------ host side
@@ -667,9 +465,12 @@ void TheoryPass::plan_units(int tiles) {
     unit_tiles = tiles;
 }
 
-void TheoryPass::launch(const double *dl, long long ld_field, long long ld_walker, const TPOut *outs, int W,
-                        hipStream_t stream) {
-    if (W <= 0 || items.empty()) return;
+bool TheoryPass::vec_ok(const double *dl, long long ld_field, long long ld_walker) const {
+    // (four blocks would not fit the registers: theory_window_kernel<4>)
+    return ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0 && max_nsb <= 2;
+}
+
+TPDev TheoryPass::dev_args(const TPOut *outs, int W) {
     TPDev c{};
     c.items = d_items.as<TPItem>();
     c.cols = d_cols.as<TPCol>();
@@ -678,11 +479,19 @@ void TheoryPass::launch(const double *dl, long long ld_field, long long ld_walke
     c.cmap = d_cmap.as<unsigned char>();
     c.nitem = (int)items.size();
     for (int s = 0; s < nstage; s++) c.out[s] = outs[s];
-    const int vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0;
     const int tiles = (W + 63) / 64;
     if (tiles != unit_tiles) plan_units(tiles);
     c.units = d_units.as<int2>();
-    if (vec_ok && max_nsb <= 2) {   // (four blocks would not fit the registers: theory_window_kernel<4>)
+    return c;
+}
+
+void TheoryPass::launch(const double *dl, long long ld_field, long long ld_walker, const TPOut *outs, int W,
+                        hipStream_t stream) {
+    if (W <= 0 || items.empty()) return;
+    const TPDev c = dev_args(outs, W);
+    const int vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0;
+    const int tiles = (W + 63) / 64;
+    if (this->vec_ok(dl, ld_field, ld_walker)) {
         timed_launch("theory_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
             hipExtLaunchKernelGGL(theory_window_vec<2>, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, c, dl, ld_field,
                                   ld_walker, W);

@@ -699,6 +699,54 @@ def test_corun_tails_bitwise(cmbl_golden, refdata, tmp_path, W):
     assert np.array_equal(out[0][1], out[1][1])
 
 
+@pytest.mark.parametrize("W", [1, 100, 1024])
+def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
+    """Pipelined fast steps (sampler_step): the fused pass of step k runs in
+    the launch of the mh_kernel proposing step k, stores raw sums, and applies
+    the trial calibrations once its tile's Metropolis workgroups have published
+    them (mh_pass_kernel).  Chains, CurLike and both likelihood terms are
+    bit-identical to the unpipelined steps, over step() calls of 1, 2 and 5
+    steps, and the terms equal each likelihood's own loglike_batch at the
+    recorded points."""
+    import os
+
+    from cosmomc_amd import _native as N
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    c = cmbl_golden["cases"]["lensing_consext8"]
+    data = syn.make_plik_lite(12345)
+    th = syn.walker_theory(W, seed=11, n_fields=10, ld_field=2512)
+    dl = torch.tensor(th, device="cuda")
+    calls = (1, 2, 5)
+    steps = sum(calls)
+    out = []
+    for pipe in (1, 0):
+        plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+        lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
+        plik.nuisance_indices = [2]
+        lens.nuisance_indices = [2]
+        s = BatchedMCMC(W, 3, [2], [[1]], 0, [0.0222, 0.9, 3.05], [0.0222, 1.1, 3.05], [0.0, 1.0, 0.0],
+                        [0.0, 0.0025, 0.0], seed_ij=61, seed_kl=72)
+        s.set_covariance(np.array([[0.002 ** 2]]))
+        s.add_likelihood(plik, dl)
+        s.add_likelihood(lens, dl)
+        assert N.lib().cmamd_debug_fused(s._h) > 0
+        assert N.lib().cmamd_debug_pipeline(s._h, pipe) == 0
+        s.enable_history(steps)
+        s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
+        for n in calls:
+            s.step(n, fast_only=True)
+        out.append((s.history_host(0, steps), s.history_terms(0, steps)))
+        if pipe:
+            for k in (0, steps - 1):
+                cal = out[0][0][k, 0, :].copy()
+                nu = torch.tensor(cal, device="cuda").reshape(-1, 1)
+                np.testing.assert_allclose(out[0][1][k, 0], plik.loglike_batch(dl, nu).cpu().numpy(), rtol=1e-12)
+                np.testing.assert_allclose(out[0][1][k, 1], lens.loglike_batch(dl, nu).cpu().numpy(), rtol=1e-12)
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
+
+
 def test_dragging_fused_plik_lensing(cmbl_golden, refdata, tmp_path):
     """Dragging with plik_lite + lensing on one theory buffer (the fused
     window pass at both the start and the end-point theories): every walker's
