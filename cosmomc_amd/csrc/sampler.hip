@@ -2554,6 +2554,7 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
         tp.mblk = MB;
         tp.calbuf = dc.calbuf;
         tp.cal_ld = dc.ld;
+        for (int k = 0; k < 2; k++) tp.status[k] = s->likes[s->tp_like[k]].like->like->status_word();
         tp.delay = PIPE_DELAY;
         const LikeSlot &P = s->likes[s->tp_like[0]];
         const dim3 gp(nmh_pad + s->tpass->n_blocks());

@@ -68,6 +68,7 @@ struct TPDev {
     const double *calbuf;      // [TP_MAXOUT][cal_ld] each stage's calibration of walker w
     long long cal_ld;
     int delay;                 // 10 ns ticks the pass holds back at the start
+    int *status[TP_MAXOUT];    // the stages' sticky status words (CMBL_STATUS_PIPE_WAIT)
 };
 
 class TheoryPass {

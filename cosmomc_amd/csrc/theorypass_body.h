@@ -241,10 +241,14 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
         TP_PIPE_STAMP(1);
         if (tid == 0) {    // this tile's Metropolis workgroups of this launch (bounded wait)
             const unsigned need = c.epoch * (unsigned)((min(64, W - tile * 64) + c.mblk - 1) / c.mblk);
-            for (long it2 = 0; it2 < (1l << 26); it2++) {
+            long it2 = 0;
+            for (; it2 < (1l << 26); it2++) {
                 if (__hip_atomic_load(c.tilecnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
                 __builtin_amdgcn_s_sleep(2);
             }
+            if (it2 == (1l << 26))   // gave up (a safety net: the wait ends by construction)
+                for (int o = 0; o < TP_MAXOUT; o++)
+                    if (c.status[o]) atomicOr(c.status[o], CMBL_STATUS_PIPE_WAIT);
         }
         __syncthreads();   // the wait, and every wave's sums in lsum
         TP_PIPE_STAMP(2);

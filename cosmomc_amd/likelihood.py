@@ -118,7 +118,9 @@ class NativeCMBLikelihood(DataLikelihood):
     def status(self, clear: bool = True) -> int:
         """Sticky numerical status bits of the handle (cmbl_status; synchronises):
         CMBL_STATUS_HL_NOCONV = 1 when an HL eigensolve hit its sweep cap since
-        the last clear (that walker's -lnL is NaN)."""
+        the last clear (that walker's -lnL is NaN); CMBL_STATUS_PIPE_WAIT = 2 when
+        a sampler's pipelined fast step gave up waiting for its walkers' trial
+        calibrations (a safety net; its terms are not to be trusted)."""
         f = C.c_int()
         N.check(N.lib().cmbl_status(self._h, C.byref(f), int(clear)), self._h)
         return f.value

@@ -116,10 +116,15 @@ size_t cmbl_clik_workspace_size(const cmbl_t *h, int W);
  *   CMBL_STATUS_HL_NOCONV  an HL eigensolve (CMBLikes_Transform, CMBlikes.f90:
  *                          861-914) did not converge in 40 Jacobi sweeps; the
  *                          reference's LAPACK call would stop the run
+ *   CMBL_STATUS_PIPE_WAIT  a sampler's pipelined fast step (cmbs_step) gave up
+ *                          waiting for its walkers' trial calibrations, so its
+ *                          terms are not to be trusted (a safety net: the wait
+ *                          ends by construction)
  * cmbl_status synchronises the device, writes the bits accumulated since the
  * last clear to *flags and clears them when clear != 0.  The host entry
  * (cmbl_loglike_batch_host) checks them itself and returns CMBL_ERR_NUMERIC. */
 #define CMBL_STATUS_HL_NOCONV 1
+#define CMBL_STATUS_PIPE_WAIT 2
 int  cmbl_status(cmbl_t *h, int *flags, int clear);
 
 /* Per-kernel device timing (HIP events around every library launch; off by

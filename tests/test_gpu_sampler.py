@@ -737,6 +737,7 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
         for n in calls:
             s.step(n, fast_only=True)
         out.append((s.history_host(0, steps), s.history_terms(0, steps)))
+        assert plik.status() == 0 and lens.status() == 0   # no CMBL_STATUS_PIPE_WAIT
         if pipe:
             for k in (0, steps - 1):
                 cal = out[0][0][k, 0, :].copy()
