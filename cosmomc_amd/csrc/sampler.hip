@@ -2495,7 +2495,8 @@ static void rot_schedule_unknown(cmbs *s) { std::fill(s->rot_lp.begin(), s->rot_
 // pass's streaming, and those workgroups, whose end the pass waits for, end
 // sooner (block stamps, tools/pipe_stamps.py: Metropolis ends 18.2-23.6 us
 // without it, 16.1-22.4 with 2 us; mh_pass_kernel 27.1 / 24.2 / 25.3 / 26.1 us
-// for 0 / 2 / 3 / 4 us, MI355X, W = 1024)
+// for 0 / 2 / 3 / 4 us, MI355X, W = 1024; 1 / 1.5 / 2.5 us: 27.0-27.5 /
+// 24.6-24.7 / 24.8 against 24.1-24.5)
 static constexpr int PIPE_DELAY = 200;
 
 static TPOut pass_out(cmbs *s, int k) {
