@@ -88,12 +88,13 @@ struct DevCfg {
     const double *def_part[MAXDEF];         // [tiles][def_items][64]
     const double *def_add[MAXDEF];          // [W] or null
     // pipelined fast steps (mh_pass_kernel): a proposing launch publishes the
-    // fused pass's two stage calibrations of every walker's trial and counts
-    // its workgroups done per 64-walker tile (TPDev::tilecnt)
+    // fused pass's two stage calibrations of every walker's trial into calbuf
+    // (this launch's half) and resets the other half to PIPE_UNSET for the
+    // next launch; the pass polls for its walkers' values
     int pub_on;                             // set per launch
     int pub_pcal[2];                        // the stages' calibration parameters (0-based, -1: none)
-    double *calbuf;                         // [2][ld]
-    unsigned *tilecnt;                      // [ld / 64]
+    double *calbuf;                         // [2 stages][ld], this launch's half
+    double *calbuf_next;                    // the next launch's half
 };
 
 struct LikeSlot {
@@ -174,9 +175,9 @@ struct cmbs {
     // pipelined fast steps: the fused pass of step k runs in the launch of
     // the mh_kernel proposing it (sampler_step, mh_pass_kernel)
     bool no_pipe = false;                    // debug: off
-    cmamd::DevBuf pipe_cal, pipe_cnt;        // DevCfg::calbuf, tilecnt
+    cmamd::DevBuf pipe_cal;                  // [2 halves][2 stages][ld] (DevCfg::calbuf)
     size_t pipe_lds = 0;                     // mh_pass_kernel's LDS
-    unsigned pipe_epoch = 0;                 // proposing pipelined launches so far
+    unsigned pipe_epoch = 0;                 // proposing pipelined launches so far (its parity: the half)
     int pipe_ready = 0;                      // set up for this W (0: not yet)
     int tp_why = 0;                          // set-up progress when no pass was built (debug)
     ~cmbs() {

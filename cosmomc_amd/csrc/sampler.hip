@@ -806,18 +806,14 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     }
     __syncthreads();
     STAMP(13);
-    if (PROPOSE && c.pub_on) {   // the fused pass in this launch waits for these (tp_vec_body<.., true>)
-        if (threadIdx.x < MB && act)
-            for (int k = 0; k < 2; k++) {
-                const int pc = c.pub_pcal[k];
-                const double v = pc >= 0 ? sd[(size_t)(SROW(R.T) + pc) * MB + lane] : 1.0;
-                __hip_atomic_store(c.calbuf + (size_t)k * W + w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_fetch_add(c.tilecnt + wb / 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (PROPOSE && c.pub_on && threadIdx.x < MB && act)   // the fused pass in this launch polls for these
+        for (int k = 0; k < 2; k++) {
+            const int pc = c.pub_pcal[k];
+            const double v = pc >= 0 ? sd[(size_t)(SROW(R.T) + pc) * MB + lane] : 1.0;
+            __hip_atomic_store(c.calbuf + (size_t)k * W + w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(c.calbuf_next + (size_t)k * W + w, __longlong_as_double((long long)TP_PIPE_UNSET),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // read by the next launch only
+        }
     // write back the image (rows of walkers past W are padding of the ld-wide
     // rows: written back unchanged)
     if (skipR) {
@@ -2515,8 +2511,11 @@ static bool pipe_setup(cmbs *s, int fast_only) {
     const LikeSlot &P = s->likes[s->tp_like[0]];
     if (!s->tpass->vec_ok(P.dl, P.ld_field, P.ld_walker)) return false;
     if (s->pipe_ready == s->W) return true;
-    s->pipe_cal.alloc((size_t)2 * s->dc.ld * 8);
-    s->pipe_cnt.alloc((size_t)(s->dc.ld / 64 + 1) * 4);   // zeroed
+    {   // both halves unset: the first launch publishes into half 1, resets half 0
+        const std::vector<unsigned long long> unset((size_t)4 * s->dc.ld, TP_PIPE_UNSET);
+        s->pipe_cal.alloc(unset.size() * 8);
+        s->pipe_cal.upload(unset.data(), unset.size() * 8);
+    }
     s->pipe_epoch = 0;
     s->pipe_ready = s->W;
     return true;
@@ -2545,14 +2544,12 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
             const WinStage &st = s->tp_stage[k];
             dc.pub_pcal[k] = st.cal_index >= 0 ? s->likes[s->tp_like[k]].nidx[st.cal_index] : -1;
         }
-        dc.calbuf = s->pipe_cal.as<double>();
-        dc.tilecnt = s->pipe_cnt.as<unsigned>();
+        const unsigned e = ++s->pipe_epoch;   // this launch's half e % 2; it resets the other for the next
+        dc.calbuf = s->pipe_cal.as<double>() + (size_t)(e % 2) * 2 * dc.ld;
+        dc.calbuf_next = s->pipe_cal.as<double>() + (size_t)((e + 1) % 2) * 2 * dc.ld;
         const int nmh = (int)g.x, nmh_pad = (nmh + 7) / 8 * 8;
         const TPOut o[2] = {pass_out(s, 0), pass_out(s, 1)};
         TPDev tp = s->tpass->dev_args(o, s->W);
-        tp.tilecnt = dc.tilecnt;
-        tp.epoch = ++s->pipe_epoch;
-        tp.mblk = MB;
         tp.calbuf = dc.calbuf;
         tp.cal_ld = dc.ld;
         for (int k = 0; k < 2; k++) tp.status[k] = s->likes[s->tp_like[k]].like->like->status_word();

@@ -34,7 +34,10 @@ struct TPOut {            // a stage's output for one launch
     long long ld_nuis;
 };
 
-static constexpr int TP_MAXSTEP = 16;   // 32-l steps per work item (the active-block mask)
+static constexpr int TP_MAXSTEP = 16;
+// a calibration slot not yet published in this launch (a NaN payload no
+// calibration takes; compared by bits)
+static constexpr unsigned long long TP_PIPE_UNSET = 0x7ff4c0ffee0dd00dull;   // 32-l steps per work item (the active-block mask)
 
 struct TPItem {           // one workgroup's l range of one theory field, with <= 64 columns
     int field, l0, l1, nch, ncol, cdesc;
@@ -60,11 +63,7 @@ struct TPDev {
     TPOut out[TP_MAXOUT];
     // pipelined form (tp_vec_body<.., true>, the sampler's mh_pass_kernel):
     // the step's calibrations come from the Metropolis workgroups of the same
-    // launch, which publish them per walker and count themselves done per
-    // 64-walker tile
-    const unsigned *tilecnt;   // [tiles] Metropolis workgroups done, cumulative over launches
-    unsigned epoch;            // launches so far, this one included
-    int mblk;                  // walkers per Metropolis workgroup
+    // launch, which publish them per walker over TP_PIPE_UNSET
     const double *calbuf;      // [TP_MAXOUT][cal_ld] each stage's calibration of walker w
     long long cal_ld;
     int delay;                 // 10 ns ticks the pass holds back at the start

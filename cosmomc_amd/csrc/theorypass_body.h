@@ -36,9 +36,10 @@ template <int NB, bool PIPE = false> constexpr int tp_vec_lds_bytes() {
 // PIPE (the sampler's pipelined steps, mh_pass_kernel): the calibrations of
 // the step are being proposed by the Metropolis workgroups of the same
 // launch, so every column's sum is kept in LDS as it comes out of the MFMAs;
-// once the block's walker tile has its calibrations (TPDev::tilecnt) the block
-// applies them with the emit's own operations (v / cal^2, X - v / cal^2: the
-// same bits as the unpipelined pass) and stores the outputs.
+// after its last step each thread polls its walker's published calibrations
+// (TPDev::calbuf, TP_PIPE_UNSET until published), applies them with the
+// emit's own operations (v / cal^2, X - v / cal^2: the same bits as the
+// unpipelined pass) and stores the outputs.
 template <int NB, bool PIPE>
 __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__restrict__ dl, long long ld_field,
                                             long long ld_walker, int W, char *lds, int b)
@@ -239,29 +240,26 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
     }
     if constexpr (PIPE) {
         TP_PIPE_STAMP(1);
-        if (tid == 0) {    // this tile's Metropolis workgroups of this launch (bounded wait)
-            const unsigned need = c.epoch * (unsigned)((min(64, W - tile * 64) + c.mblk - 1) / c.mblk);
-            long it2 = 0;
-            for (; it2 < (1l << 26); it2++) {
-                if (__hip_atomic_load(c.tilecnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-            if (it2 == (1l << 26))   // gave up (a safety net: the wait ends by construction)
-                for (int o = 0; o < TP_MAXOUT; o++)
-                    if (c.status[o]) atomicOr(c.status[o], CMBL_STATUS_PIPE_WAIT);
-        }
-        __syncthreads();   // the wait, and every wave's sums in lsum
-        TP_PIPE_STAMP(2);
-        // thread: walker tid % 64 of the tile, columns tid / 64, + 4, ...
+        __syncthreads();   // every wave's sums in lsum
+        // thread: walker tid % 64 of the tile, columns tid / 64, + 4, ...; it
+        // polls its walker's two published calibrations (bounded)
         const int wl2 = tid & 63, wv = tile * 64 + wl2;
         if (wv < W) {
             double c2p[TP_MAXOUT];
 #pragma unroll
             for (int o = 0; o < TP_MAXOUT; o++) {
-                const double cl = __hip_atomic_load(c.calbuf + o * c.cal_ld + wv, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
+                double cl = 0.0;
+                long it2 = 0;
+                for (; it2 < (1l << 24); it2++) {
+                    cl = __hip_atomic_load(c.calbuf + o * c.cal_ld + wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((unsigned long long)__double_as_longlong(cl) != TP_PIPE_UNSET) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (it2 == (1l << 24) && c.status[o])   // gave up (a safety net: the wait ends by construction)
+                    atomicOr(c.status[o], CMBL_STATUS_PIPE_WAIT);
                 c2p[o] = cl * cl;
             }
+            TP_PIPE_STAMP(2);
             for (int col = tid >> 6; col < it.ncol; col += 4) {
                 const TPCol d = csh[col];
                 const bool o1 = d.out != 0;
