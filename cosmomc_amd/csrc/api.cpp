@@ -1,6 +1,7 @@
 // C ABI of libcosmomc_amd.so (include/cosmomc_amd.h).  Every entry point
 // catches internal errors and turns them into codes + messages.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "sampler.h"
@@ -270,6 +271,10 @@ int cmbs_create(const cmbs_config_t *cfg, cmbs_t **out, char *errbuf, size_t err
     if (!cfg || !out) return CMBL_ERR_ARG;
     *out = nullptr;
     std::unique_ptr<cmbs> s(new cmbs);
+    if (const char *e = std::getenv("CMAMD_PIPE")) {   // fast-step schedule for A/B runs (cmamd_debug_pipeline)
+        const int m = std::atoi(e);
+        if (m >= 0 && m <= 2) s->pipe_mode = m;
+    }
     int rc = guarded(&err, [&] { cmamd::sampler_create(s.get(), cfg); });
     if (rc) {
         put_err(errbuf, errlen, err.c_str());

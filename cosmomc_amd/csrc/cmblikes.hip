@@ -888,6 +888,12 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
     if (!VF)
 #pragma unroll
         for (int k = 0; k < M; k++) V[k] = (k == r) ? 1.0 : 0.0;
+    if (VF) {   // the input matrix (row r = column r), for the eigenvalues' signs after the solve
+        if (on)
+#pragma unroll
+            for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = G[k];
+        __syncthreads();
+    }
     bool failed = false;
 #ifdef CMAMD_STAMPS
     unsigned long long ph0 = 0, ph1 = 0, ph2 = 0, nround = 0;
@@ -990,7 +996,25 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
         const double sg = sqrt(n2);
 #pragma unroll
         for (int k = 0; k < M; k++) V[k] = n2 > 0.0 ? G[k] / sg : (k == r ? 1.0 : 0.0);
-        lam = sg;
+        // |g_r| is |lambda_r| and g_r / |g_r| is sign(lambda_r) u_r, so the norm alone
+        // loses the sign of an eigenvalue of a matrix that is not positive definite
+        // (a trial theory C can be): lambda_r = (A v)_i / v_i at the largest |v_i|,
+        // so a negative eigenvalue stays negative and its sqrt / log give NaN, as the
+        // reference's DSYEV eigenvalues do (CMBlikes.f90:877-894)
+        int im = 0;
+        double vm = V[0];
+#pragma unroll
+        for (int k = 1; k < M; k++)
+            if (fabs(V[k]) > fabs(vm)) {
+                im = k;
+                vm = V[k];
+            }
+        double d = 0.0;
+        if (on)
+#pragma unroll
+            for (int k = 0; k < M; k++) d = fma(S.rows[grp][0][im][k], V[k], d);
+        __syncthreads();   // the callers reuse the row buffers
+        lam = (d * vm < 0.0) ? -sg : sg;
         return failed;
     }
     double l = 0.0;
@@ -1154,7 +1178,10 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     if (h.v0) from_basis();
     __syncthreads();                               // the solve's last reads of the row buffers
     if (on) {
-        const double g = sqrt(2 * fmax(0.0, x - log(x) - 1));
+        // a NaN argument (x < 0 or NaN: a C that is not positive definite) stays NaN:
+        // fmax(0, NaN) would make it 0 and the point's chi^2 finite
+        const double arg = x - log(x) - 1;
+        const double g = arg == arg ? sqrt(2 * fmax(0.0, arg)) : arg;
         S.dg[grp][r] = (x - 1 >= 0) ? g : -g;
 #pragma unroll
         for (int k = 0; k < M; k++) S.rows[grp][0][k][r] = V[k];     // V rows, from its columns

@@ -167,6 +167,19 @@ struct QFDeferred {
     const double *addend = nullptr;
 };
 
+// A deferred quadratic form whose operand rows a later launch forms itself from
+// a window pass's raw sums (the sampler's split pipelined steps, steptail.hip):
+// Delta[w][k] = X[k] - S[w][k] / cal_w^2, every row calibrated.
+struct QFItem;
+struct QFSource {
+    const double *Ct = nullptr;   // [Np][Np] C^-1 with halved diagonal blocks
+    int Np = 0, xcd_map = 0;
+    const QFItem *items = nullptr;
+    int n_items = 0;
+    double *partial = nullptr;    // [tiles][n_items][64]
+    const double *X = nullptr;    // [Np] data vector, zero padded
+};
+
 // A small gaussian CMBlikes chi^2 (smallgauss.h) as one launch's arguments:
 // its workgroups can run in cmbl_gauss_small_kernel or beside a deferred
 // quadratic form's (QuadForm::launch_deferred, Like::corun_small).
@@ -189,6 +202,12 @@ struct SmallGaussLaunch {
     const double *M;         // [nX][nX] inverse covariance
     double *out;             // [W] -lnL
     int W;
+    // the sampler's split pipelined steps (steptail.hip): partial holds the window
+    // pass's raw sums, and a row r with row_cal[r] != 0 is divided by cal^2 (cal =
+    // nuis[w * ld_nuis + stage_cal]) as it is loaded -- the operation the pass's
+    // emit would have applied before storing it
+    const unsigned char *row_cal;
+    int stage_cal;
 };
 
 // Window stage of a likelihood: its first kernel contracts every walker's
@@ -262,6 +281,12 @@ struct Like {
         fail(CMBL_ERR_UNSUPPORTED, "%s: no window stage", name.c_str());
     }
     virtual bool accepts_corun() const { return false; }
+    // The deferred quadratic form after this likelihood's window stage as a
+    // QFSource (its workspace ws for W walkers); false if it has none.
+    virtual bool qf_source(QFSource &q, int W, void *ws) {
+        (void)q, (void)W, (void)ws;
+        return false;
+    }
     // This likelihood's whole after-window stage as a small chi^2 another
     // launch can carry (same arguments as after_window); false if it has none.
     virtual bool corun_small(SmallGaussLaunch &a, int W, const double *nuis, long long ld_nuis, double *out,

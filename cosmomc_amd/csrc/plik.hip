@@ -349,6 +349,11 @@ struct PlikLite final : Like {
         return qf.x_rows(ws);
     }
     bool accepts_corun() const override { return true; }
+    bool qf_source(QFSource &q, int W, void *ws) override {
+        if (W <= 0 || !ws) return false;
+        q = qf.source(W, ws, d_X.as<double>());
+        return true;
+    }
     QFDeferred after_window(int W, const double *nuis, long long ld_nuis, double *out, void *ws, hipStream_t stream,
                             bool defer, const SmallGaussLaunch *co = nullptr) override {
         (void)nuis, (void)ld_nuis;

@@ -21,6 +21,7 @@ static constexpr int QF_TILE = 64;   // M block edge and walker tile
 struct QFItem {   // one workgroup's share: row block I x column blocks J0 .. J0+nJ-1 (all >= I)
     int I, J0, nJ, pad;
 };
+static constexpr int QF_MAXKB = 5;   // column blocks per item at most (QuadForm::choose_kb)
 
 // Split-K combine, one fixed order shared by the in-launch reducer and by a
 // deferred consumer (the sampler's mh_kernel), so both give the same bits:
@@ -79,8 +80,12 @@ class QuadForm {
     QFDeferred launch_deferred(int W, void *ws, const double *addend, hipStream_t stream, const char *prof_name,
                                const SmallGaussLaunch *co = nullptr, const char *co_prof_name = nullptr);
 
+    // the deferred launch's operands for a launch that forms the rows itself
+    // (X: the data vector the rows are X - S / cal^2 of)
+    QFSource source(int W, void *ws, const double *X);
+
   private:
-    static constexpr int MAXKB = 5;
+    static constexpr int MAXKB = QF_MAXKB;
     int nblk = 0;
     DevBuf d_ct;
     DevBuf d_items[MAXKB + 1];

@@ -2,6 +2,7 @@
 #pragma once
 
 #include "common.h"
+#include "steptail.h"
 #include "theorypass.h"
 
 namespace cmamd {
@@ -174,11 +175,20 @@ struct cmbs {
     bool no_corun = false;                   // debug: the fused pass's tails as separate launches
     // pipelined fast steps: the fused pass of step k runs in the launch of
     // the mh_kernel proposing it (sampler_step, mh_pass_kernel)
-    bool no_pipe = false;                    // debug: off
     cmamd::DevBuf pipe_cal;                  // [2 halves][2 stages][ld] (DevCfg::calbuf)
     size_t pipe_lds = 0;                     // mh_pass_kernel's LDS
     unsigned pipe_epoch = 0;                 // proposing pipelined launches so far (its parity: the half)
     int pipe_ready = 0;                      // set up for this W (0: not yet)
+    // split pipelined fast steps (pipe_mode 2, sampler_step): the fused pass of
+    // step k + 1 runs in step k's tail launch (steptail.h) and stores raw sums,
+    // which step k + 1's tails calibrate as they read them; the Metropolis
+    // kernel between two tails runs alone
+    int pipe_mode = 2;                       // 0 off, 1 mh_pass_kernel, 2 step tails (cmamd_debug_pipeline)
+    cmamd::DevBuf tail_S[2][2];              // [parity][stage] the pass's raw sums
+    cmamd::DevBuf tail_rowcal;               // the chi^2 stage's calibrated partial rows (SmallGaussLaunch::row_cal)
+    cmamd::StepTailPlan tail_plan[3];        // workgroup rows: tails + pass, tails, pass
+    int tail_ready = 0;                      // W it is set up for (0: not yet, -W: not possible)
+    int tail_qf = -1, tail_g = -1;           // the stage (0 / 1) of the quadratic form / of the chi^2
     int tp_why = 0;                          // set-up progress when no pass was built (debug)
     ~cmbs() {
         for (auto &st : streams)

@@ -24,6 +24,7 @@
 
 #include "quadform.h"
 #include "sampler.h"
+#include "smallgauss.h"
 #ifdef CMAMD_STAMPS
 // mh_pass_kernel block timeline (tools/pipe_stamps.py): s_memrealtime at the
 // start, [pass] streaming done / wait done, end; [3] the block's role
@@ -2085,6 +2086,7 @@ static void setup_fusion(cmbs *s) {
     s->tpass.reset();
     s->tp_like[0] = s->tp_like[1] = -1;
     s->pipe_ready = 0;
+    s->tail_ready = 0;
     const int nl = (int)s->likes.size();
     auto sparse = [&](int i) {
         for (int q : s->sparse_likes)
@@ -2507,7 +2509,7 @@ static TPOut pass_out(cmbs *s, int k) {
 // vectorised form and every walker proposes in one launch (one group, no
 // change mask, no rotations left to rot_kernel).
 static bool pipe_setup(cmbs *s, int fast_only) {
-    if (s->no_pipe || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on || s->dc.rot_defer) return false;
+    if (s->pipe_mode != 1 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on || s->dc.rot_defer) return false;
     const LikeSlot &P = s->likes[s->tp_like[0]];
     if (!s->tpass->vec_ok(P.dl, P.ld_field, P.ld_walker)) return false;
     if (s->pipe_ready == s->W) return true;
@@ -2607,6 +2609,105 @@ static void check_theory_fresh(const cmbs *s) {
                            "theory at the restored points with cmbs_refresh_theory before stepping");
 }
 
+// The split pipelined fast steps (steptail.h): whether this run of fast steps
+// can take them -- the fused pass's vectorised form over one walker group, no
+// change mask, no rotations left to rot_kernel, and its two stages a deferred
+// quadratic form (plik_lite: every row calibrated) and a small chi^2 another
+// launch can carry (Planck lensing).  Sets up the raw-sum buffers once per W.
+static bool tail_setup(cmbs *s, int fast_only) {
+    if (s->pipe_mode != 2 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on || s->dc.rot_defer)
+        return false;
+    {
+        const LikeSlot &P = s->likes[s->tp_like[0]];
+        if (!s->tpass->vec_ok(P.dl, P.ld_field, P.ld_walker)) return false;
+    }
+    if (s->tail_ready == s->W) return true;
+    if (s->tail_ready == -s->W) return false;
+    s->tail_ready = -s->W;
+    s->tail_qf = s->tail_g = -1;
+    for (int k = 0; k < 2; k++) {
+        const int i = s->tp_like[k];
+        Like &L = *s->likes[i].like->like;
+        const WinStage &st = s->tp_stage[k];
+        QFSource src;
+        if (st.kind == 1 && is_deferred(s, (size_t)i) && L.qf_source(src, s->W, s->like_ws[i].p)) {
+            bool all_cal = st.cal_index >= 0;
+            for (const WinCol &c : st.cols) all_cal = all_cal && c.cal;
+            if (all_cal && st.ld == src.Np) s->tail_qf = k;
+        }
+        SmallGaussLaunch g{};
+        if (st.kind == 0 && L.corun_small(g, s->W, s->dc.like_nuis[i], L.n_nuis,
+                                          s->like_terms.as<double>() + (size_t)i * s->dc.ld, s->like_ws[i].p))
+            s->tail_g = k;
+    }
+    if (s->tail_qf < 0 || s->tail_g < 0 || s->tail_qf == s->tail_g) return false;
+    const size_t Wp = (size_t)QuadForm::wpad(s->W);
+    int rows = 0;
+    for (const WinCol &c : s->tp_stage[s->tail_g].cols) rows = std::max(rows, c.row + 1);
+    const size_t bytes[2] = {Wp * (size_t)s->tp_stage[s->tail_qf].ld * 8, (size_t)rows * s->W * 8};
+    for (int p = 0; p < 2; p++)
+        for (int k = 0; k < 2; k++) {
+            const size_t b = bytes[k == s->tail_qf ? 0 : 1];
+            s->tail_S[p][k].alloc(b);
+            HIP_CHECK(hipMemset(s->tail_S[p][k].p, 0, b));   // padding rows / columns stay 0
+        }
+    std::vector<unsigned char> rc((size_t)rows + 16, 0);
+    for (const WinCol &c : s->tp_stage[s->tail_g].cols) rc[c.row] = c.cal ? 1 : 0;
+    s->tail_rowcal.alloc(rc.size());
+    s->tail_rowcal.upload(rc.data(), rc.size());
+    s->tail_ready = s->W;
+    return true;
+}
+
+// One step tail: the quadratic form and the chi^2 of the step whose raw sums
+// are in half rd (rd < 0: none), and the pass storing the next step's raw sums
+// into half wr (wr < 0: none).
+static void launch_tail(cmbs *s, hipStream_t stream, int rd, int wr) {
+    StepTail t;
+    const int W = s->W;
+    t.W = W;
+    if (rd >= 0) {
+        const int qi = s->tp_like[s->tail_qf], gi = s->tp_like[s->tail_g];
+        Like &Q = *s->likes[qi].like->like;
+        Like &G = *s->likes[gi].like->like;
+        if (!Q.qf_source(t.q.src, W, s->like_ws[qi].p)) fail(CMBL_ERR_ARG, "internal: step tail quadratic form");
+        t.q.S = s->tail_S[rd][s->tail_qf].as<double>();
+        t.q.nuis = s->dc.like_nuis[qi];
+        t.q.ld_nuis = std::max(1, Q.n_nuis);
+        t.q.cal_index = s->tp_stage[s->tail_qf].cal_index;
+        t.q.W = W;
+        t.nq = t.q.src.n_items * (QuadForm::wpad(W) / QF_TILE);
+        if (!G.corun_small(t.g, W, s->dc.like_nuis[gi], G.n_nuis, s->like_terms.as<double>() + (size_t)gi * s->dc.ld,
+                           s->like_ws[gi].p))
+            fail(CMBL_ERR_ARG, "internal: step tail chi^2");
+        t.g.partial = s->tail_S[rd][s->tail_g].as<double>();
+        t.g.row_cal = s->tail_rowcal.as<unsigned char>();
+        t.g.stage_cal = s->tp_stage[s->tail_g].cal_index;
+        t.ng = (W + SMALL_WT - 1) / SMALL_WT;
+    }
+    if (wr >= 0) {
+        TPOut o[2];
+        for (int k = 0; k < 2; k++) {
+            const int i = s->tp_like[k];
+            const WinStage &st = s->tp_stage[k];
+            Like &L = *s->likes[i].like->like;
+            o[k] = TPOut{st.kind, st.cal_index, st.ld, 0, s->tail_S[wr][k].as<double>(), st.X, s->dc.like_nuis[i],
+                         (long long)std::max(1, L.n_nuis)};
+        }
+        t.tp = s->tpass->dev_args(o, W);
+        const LikeSlot &P = s->likes[s->tp_like[0]];
+        t.dl = P.dl;
+        t.ld_field = P.ld_field;
+        t.ld_walker = P.ld_walker;
+        t.np = s->tpass->n_blocks();
+    }
+    const int v = rd >= 0 ? (wr >= 0 ? 0 : 1) : 2;
+    static const char *names[3] = {"step_tail_kernel", "step_tail_last", "step_tail_pass"};
+    launch_step_tail(t, s->tail_plan[v], stream, names[v]);
+    if (rd >= 0) record_deferred(s, (size_t)s->tp_like[s->tail_qf],
+                                 QFDeferred{t.q.src.partial, t.q.src.n_items, nullptr});
+}
+
 void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (!s->started) fail(CMBL_ERR_ARG, "cmbs_set_start must be called before cmbs_step");
     check_theory_fresh(s);
@@ -2616,6 +2717,17 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (n_steps <= 0) return;
     // propose(1) | likes | accept(1)+propose(2) | likes | ... | likes | accept(n)
     const int G = s->n_groups;
+    if (G == 1 && tail_setup(s, fast_only)) {
+        // split pipelined: pass(1) | mh(propose 1) | tails(1) + pass(2) | mh(accept 1 + propose 2) |
+        // tails(2) + pass(3) | ... | tails(n) | mh(accept n)
+        launch_tail(s, stream, -1, 0);
+        for (int k = 0; k < n_steps; k++) {
+            launch_mh(s, k > 0, true, fast_only, k > 0 ? next_hist(s) : HistRow{}, stream, 0, s->W, false);
+            launch_tail(s, stream, k % 2, k + 1 < n_steps ? (k + 1) % 2 : -1);
+        }
+        launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W, false);
+        return;
+    }
     if (G == 1 && pipe_setup(s, fast_only)) {
         // pipelined: propose(1) + pass(1) | tails(1) | accept(1) + propose(2) + pass(2) |
         // tails(2) | ... | tails(n) | accept(n)
@@ -3123,9 +3235,9 @@ extern "C" int cmamd_debug_tp_items(const cmbs *s, int *out, int cap) {   // (fi
     }
     return s->tpass->n_items();
 }
-extern "C" int cmamd_debug_pipeline(cmbs *s, int on) {   // pipelined fast steps (sampler_step)
-    if (!s) return -1;
-    s->no_pipe = !on;
+extern "C" int cmamd_debug_pipeline(cmbs *s, int mode) {   // fast-step schedule (sampler_step): 0 unpipelined,
+    if (!s || mode < 0 || mode > 2) return -1;              // 1 mh_pass_kernel, 2 step tails
+    s->pipe_mode = mode;
     return 0;
 }
 extern "C" int cmamd_debug_corun(cmbs *s, int on) {     // the lensing chi^2 inside plik's quadratic-form launch
@@ -3133,4 +3245,5 @@ extern "C" int cmamd_debug_corun(cmbs *s, int on) {     // the lensing chi^2 ins
     s->no_corun = !on;
     return 0;
 }
+extern "C" int cmamd_debug_tail(const cmbs *s) { return s ? s->tail_ready : 0; }   // W of the step tails' set-up
 extern "C" int cmamd_debug_fused(const cmbs *s) { return !s ? 0 : s->tpass ? s->tpass->n_items() : -s->tp_why; }

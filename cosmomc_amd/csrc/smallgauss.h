@@ -27,8 +27,14 @@ static constexpr int SMALL_MAXTASK = 256;   // tasks per dataset
 template <int WT> constexpr int small_gauss_lds_doubles() {
     return SMALL_MAXTASK * WT + SMALL_NX * WT + 256 + SMALL_NX * SMALL_NX;
 }
+// the same for an nX-bandpower dataset (M takes nX^2 doubles)
+template <int WT> constexpr int small_gauss_lds_doubles(int nX) {
+    return SMALL_MAXTASK * WT + SMALL_NX * WT + 256 + nX * nX;
+}
 
-template <int WT>
+// RAWCAL: partial rows are raw window sums; rows flagged in a.row_cal are
+// divided by the walker's cal^2 as they are loaded (SmallGaussLaunch)
+template <int WT, bool RAWCAL = false>
 __device__ __forceinline__ void small_gauss_body(const SmallGaussLaunch &a, double *lds, int blk)
 {
     constexpr int NG = 256 / WT;             // thread groups of WT walkers
@@ -46,6 +52,11 @@ __device__ __forceinline__ void small_gauss_body(const SmallGaussLaunch &a, doub
     const bool act = w < Wc;
     const bool calp = c.log_cal_prior > 0 && c.cal_index >= 0;
     const double cal = (g == 0 && act && calp) ? a.nuis[(long long)w * a.ld_nuis + c.cal_index] : 1.0;   // likewise
+    double c2 = 1.0;   // RAWCAL: the stage calibration's square, as the pass's emit forms it
+    if (RAWCAL && act && a.stage_cal >= 0) {
+        const double cl = a.nuis[(long long)w * a.ld_nuis + a.stage_cal];
+        c2 = cl * cl;
+    }
     struct Elem { int ix, m0, m1, c0, c1; double mc, cc, fc, ch; };
     auto elem = [&](int e) {   // element e's table entries
         Elem q{c.e_to_x[e], c.e_main_t[e], c.e_main_t[e + 1], 0, 0, c.e_main_const[e], 0.0, 0.0, c.chat[e]};
@@ -66,6 +77,10 @@ __device__ __forceinline__ void small_gauss_body(const SmallGaussLaunch &a, doub
         double v[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) v[u] = (act && r[u] >= 0) ? a.partial[(long long)r[u] * W + w] : 0.0;
+        if (RAWCAL)
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (r[u] >= 0 && a.row_cal[r[u]]) v[u] = v[u] / c2;
         double s = 0.0;
 #pragma unroll
         for (int u = 0; u < 8; u++) s += v[u];

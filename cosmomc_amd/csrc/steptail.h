@@ -1,0 +1,54 @@
+// The step tail of the sampler's split pipelined fast steps (sampler_step):
+// one launch that runs, side by side,
+//   * plik_lite's deferred quadratic form of step k, its operand rows formed
+//     in registers from the raw bin sums of step k and the walkers' step-k
+//     calibrations (Delta = X - S / cal^2, the pass's own emit operations),
+//   * the small gaussian chi^2 of the fused CMBlikes dataset (Planck lensing)
+//     of step k, its raw partial rows calibrated as they are loaded, and
+//   * the fused window pass over every walker's theory for step k + 1, which
+//     stores raw sums (no calibration: those of step k + 1 are not proposed
+//     yet) into the other half of a two-half buffer.
+// The pass is HBM-bound and the quadratic form MFMA / L2-bound, so they share
+// the CUs instead of following each other; and since the raw sums need no
+// calibration, no workgroup waits on another inside the launch (the
+// Metropolis kernel that proposes step k + 1 runs alone, between two tails).
+#pragma once
+
+#include "common.h"
+#include "theorypass.h"
+
+namespace cmamd {
+
+struct QFSArgs {             // the quadratic form from raw sums (QFSource + the step's rows)
+    QFSource src;
+    const double *S;         // [Wp][Np] raw bin sums (padding rows and columns zero)
+    const double *nuis;      // [W][ld_nuis] the walkers' step-k nuisance values
+    long long ld_nuis;
+    int cal_index;           // cal in nuis (-1: none)
+    int W;
+};
+
+struct StepTail {
+    QFSArgs q;
+    int nq = 0;              // quadratic-form workgroups (n_items x tiles), 0: none
+    SmallGaussLaunch g{};
+    int ng = 0;              // chi^2 workgroups, 0: none
+    TPDev tp{};              // the raw pass (tp.out[*].out: the raw-sum buffers it writes)
+    const double *dl = nullptr;
+    long long ld_field = 0, ld_walker = 0;
+    int np = 0;              // pass workgroups (TheoryPass::n_blocks), 0: none
+    int W = 0;
+};
+
+// the launch's workgroup rows for its role counts (owned by the caller)
+struct StepTailPlan {
+    DevBuf d_rows;
+    int key[3] = {-1, -1, -1};
+    int nrows = 0;
+};
+
+// The launch (its LDS: at most step_tail_lds_bytes()); prof_name for timed_launch.
+void launch_step_tail(const StepTail &t, StepTailPlan &plan, hipStream_t stream, const char *prof_name);
+size_t step_tail_lds_bytes();
+
+}  // namespace cmamd

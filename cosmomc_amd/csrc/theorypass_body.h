@@ -40,10 +40,18 @@ template <int NB, bool PIPE = false> constexpr int tp_vec_lds_bytes() {
 // (TPDev::calbuf, TP_PIPE_UNSET until published), applies them with the
 // emit's own operations (v / cal^2, X - v / cal^2: the same bits as the
 // unpipelined pass) and stores the outputs.
-template <int NB, bool PIPE>
+//
+// RAW (the sampler's split pipelined steps, steptail.hip): no calibration at
+// all -- every column's sum v is stored as it comes out of the MFMAs, at the
+// index its stage's output would take (out is then the stage's raw-sum buffer);
+// the consumers apply the calibrations of the step that reads them with the
+// emit's own operations (X - v / cal^2 in the quadratic form's operand, v /
+// cal^2 in the small chi^2's partial rows), so the results are the same bits.
+template <int NB, bool PIPE, bool RAW = false>
 __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__restrict__ dl, long long ld_field,
                                             long long ld_walker, int W, char *lds, int b)
 {
+    static_assert(!(PIPE && RAW), "one output mode");
     constexpr int LPL = 8, STEP = 4 * LPL, NSUB = TP_CHUNK / STEP, WROW = STEP + 2;
     double *wsh = reinterpret_cast<double *>(lds);                                   // [buf][col block][col][l]
     TPCol *csh = reinterpret_cast<TPCol *>(wsh + 2 * NB * 16 * WROW);               // [TP_MAXCOL]
@@ -123,14 +131,14 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
         csh[tid] = d;
         const int kind = d.out ? c.out[1].kind : c.out[0].kind;
         const double *X = d.out ? c.out[1].X : c.out[0].X;
-        xsh[tid] = kind == 1 ? X[d.row] : 0.0;
+        xsh[tid] = (kind == 1 && !RAW) ? X[d.row] : 0.0;
     }
     if (tid < nstep) esh[tid] = c.emit[it.soff + tid];
     for (int q = tid; q < nstep * (TP_MAXCOL / 4); q += 256)
         reinterpret_cast<unsigned int *>(msh)[q] =
             reinterpret_cast<const unsigned int *>(c.cmap + (long long)it.soff * TP_MAXCOL)[q];
     double c2[TP_MAXOUT] = {1.0, 1.0};
-    if (!PIPE) {
+    if (!PIPE && !RAW) {
 #pragma unroll
         for (int o = 0; o < TP_MAXOUT; o++) {
             const int ci = o ? c.out[1].cal_index : c.out[0].cal_index;
@@ -166,7 +174,7 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
             a0[r] = on[r] ? 0.0 : a0[r];
             b0[r] = on[r] ? 0.0 : b0[r];
             const bool o1 = d[r].out != 0;
-            const double q = (!PIPE && d[r].cal) ? v / (o1 ? c2[1] : c2[0]) : v;
+            const double q = (!PIPE && !RAW && d[r].cal) ? v / (o1 ? c2[1] : c2[0]) : v;
             if (PIPE) {
                 if (on[r]) lsum[col[r] * 64 + wave * 16 + li] = v;
             } else if (on[r] && w < W) {
@@ -174,7 +182,7 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
                 if ((o1 ? c.out[1].kind : c.out[0].kind) == 0)
                     out[(long long)d[r].row * W + w] = q;
                 else
-                    out[(long long)w * (o1 ? c.out[1].ld : c.out[0].ld) + d[r].row] = PIPE ? q : x[r] - q;
+                    out[(long long)w * (o1 ? c.out[1].ld : c.out[0].ld) + d[r].row] = RAW ? v : x[r] - q;
             }
         }
     };

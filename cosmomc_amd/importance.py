@@ -218,7 +218,8 @@ class ImportanceSampler:
 
     def run(self, in_path: str, out_root: str | None = None) -> ImportanceResult:
         """Importance-sample the chain file ``in_path``; writes out_root.txt
-        (GetDist rows, E17.7) when out_root is given."""
+        (GetDist rows through the reference's ChainOutFile format, E16.7,
+        settings.f90:109 / ImportanceSampling.f90:221) when out_root is given."""
         mult0, like, P = self.read(in_path)
         cut = getattr(self.evaluate, "prior_cut", None)
         if self.s.redo_likelihoods and cut is not None:
@@ -269,5 +270,5 @@ class ImportanceSampler:
                 os.makedirs(d, exist_ok=True)
             with open(out_root + ".txt", "w") as f:
                 for mult, tl, pu in r.rows:
-                    f.write("".join(fortran_e(v) for v in [mult, tl, *pu]) + "\n")
+                    f.write("".join(fortran_e(v, 16) for v in [mult, tl, *pu]) + "\n")
         return r

@@ -123,3 +123,28 @@ def test_hl_every_kernel_width(cmbl_golden, refdata, nmaps):
     got = like.loglike_batch(torch.tensor(th, device="cuda"), torch.tensor(nu, device="cuda")).cpu().numpy()
     ref = np.array([o.loglike(th[w], nu[w]) for w in range(W)])
     np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-8)
+
+
+@pytest.mark.parametrize("case", ["bkplanck_3map_bins1to5", "bk15_B_12maps"])
+def test_hl_non_positive_definite_theory_is_nan(cmbl_golden, refdata, case):
+    """A trial theory whose binned C is not positive definite (here a strongly
+    negative BB spectrum): the reference's CMBLikes_Transform takes sqrt / log
+    of DSYEV's negative eigenvalues (CMBlikes.f90:877-894) and the point gets
+    NaN, which the Metropolis test rejects.  The V-free eigensolver recovers the
+    eigenvalues' signs, so such walkers give NaN too, and the walkers beside
+    them in the launch keep the oracle's value."""
+    c = cmbl_golden["cases"][case]
+    like = _open(refdata, c)
+    o = co.CMBLikesOracle(os.path.join(refdata, c["dataset"]), c["overrides"], c["tag"])
+    W = 6
+    th = syn.walker_theory(W, seed=77, lmax=c["lmax"])
+    bad = [0, 3, 4]
+    for w in bad:
+        th[w, 5, :] = -1000.0 * np.abs(th[w, 5, :]) - 1.0      # BB << 0: C has a negative eigenvalue
+    base = np.array(c["nuis"])
+    nu = base[np.arange(W) % len(base)]
+    got = like.loglike_batch(torch.tensor(th, device="cuda"), torch.tensor(nu, device="cuda")).cpu().numpy()
+    assert np.all(np.isnan(got[bad])), got
+    good = [w for w in range(W) if w not in bad]
+    ref = np.array([o.loglike(th[w], nu[w]) for w in good])
+    np.testing.assert_allclose(got[good], ref, rtol=1e-9, atol=1e-8)

@@ -701,15 +701,21 @@ def test_corun_tails_bitwise(cmbl_golden, refdata, tmp_path, W):
 
 @pytest.mark.parametrize("W", [1, 100, 1024])
 def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
-    """Pipelined fast steps (sampler_step): the fused pass of step k runs in
-    the launch of the mh_kernel proposing step k, stores raw sums, and applies
-    the trial calibrations once its tile's Metropolis workgroups have published
-    them (mh_pass_kernel).  Chains, CurLike and both likelihood terms are
-    bit-identical to the unpipelined steps, over step() calls of 1, 2 and 5
-    steps, and the terms equal each likelihood's own loglike_batch at the
-    recorded points."""
+    """The fast-step schedules give the same bits.  Mode 2 (the default, the
+    split pipelined steps): the fused pass of step k + 1 runs in step k's tail
+    launch and stores raw sums, which step k + 1's quadratic form and lensing
+    chi^2 calibrate as they read them (steptail.hip), with the proposing
+    Metropolis kernel alone in between.  Mode 1: the pass of step k in the
+    launch of the mh_kernel proposing it (mh_pass_kernel).  Mode 0: the
+    unpipelined schedule.  Chains, CurLike and both likelihood terms are
+    bit-identical over step() calls of 1, 2 and 5 steps.  The headline path is
+    pinned to the oracles directly: at the first and last recorded steps the
+    terms of walkers 0, W/2 - 1 and W - 1 equal pyoracle.PlikLite's and
+    CMBLikesOracle's -lnL at the recorded calibrations (rel 1e-9), and every
+    walker's equals each likelihood's own loglike_batch (rtol 1e-12)."""
     import os
 
+    import cmblikes_oracle as co
     from cosmomc_amd import _native as N
     from cosmomc_amd.likelihood import NativeCMBLikelihood
     from cosmomc_amd.sampler import BatchedMCMC
@@ -720,7 +726,7 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
     calls = (1, 2, 5)
     steps = sum(calls)
     out = []
-    for pipe in (1, 0):
+    for mode in (2, 1, 0):
         plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
         lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
         plik.nuisance_indices = [2]
@@ -731,21 +737,30 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
         s.add_likelihood(plik, dl)
         s.add_likelihood(lens, dl)
         assert N.lib().cmamd_debug_fused(s._h) > 0
-        assert N.lib().cmamd_debug_pipeline(s._h, pipe) == 0
+        assert N.lib().cmamd_debug_pipeline(s._h, mode) == 0
         s.enable_history(steps)
         s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
         for n in calls:
             s.step(n, fast_only=True)
+        if mode == 2:
+            assert N.lib().cmamd_debug_tail(s._h) == W        # the step tails ran
         out.append((s.history_host(0, steps), s.history_terms(0, steps)))
-        assert plik.status() == 0 and lens.status() == 0   # no CMBL_STATUS_PIPE_WAIT
-        if pipe:
+        assert plik.status() == 0 and lens.status() == 0
+        if mode == 2:
+            po_plik = po.PlikLite(data)
+            o_lens = co.CMBLikesOracle(os.path.join(refdata, c["dataset"]), c["overrides"], c["tag"])
             for k in (0, steps - 1):
                 cal = out[0][0][k, 0, :].copy()
                 nu = torch.tensor(cal, device="cuda").reshape(-1, 1)
                 np.testing.assert_allclose(out[0][1][k, 0], plik.loglike_batch(dl, nu).cpu().numpy(), rtol=1e-12)
                 np.testing.assert_allclose(out[0][1][k, 1], lens.loglike_batch(dl, nu).cpu().numpy(), rtol=1e-12)
-    assert np.array_equal(out[0][0], out[1][0])
-    assert np.array_equal(out[0][1], out[1][1])
+                for w in sorted({0, max(0, W // 2 - 1), W - 1}):
+                    assert out[0][1][k, 0, w] == pytest.approx(po_plik.loglike(th[w, :3], cal[w]), rel=1e-9)
+                    assert out[0][1][k, 1, w] == pytest.approx(o_lens.loglike(th[w], cal[w:w + 1]), rel=1e-9)
+        s.close()
+    for o in out[1:]:
+        assert np.array_equal(out[0][0], o[0])
+        assert np.array_equal(out[0][1], o[1])
 
 
 def test_dragging_fused_plik_lensing(cmbl_golden, refdata, tmp_path):

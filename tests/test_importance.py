@@ -92,6 +92,14 @@ def test_weights_and_rows(tmp_path):
     assert r.mult_ratio == pytest.approx(w.sum())
     assert r.weight_min == 0.0
     assert r.effective_samples == pytest.approx((chain[:, 0] * w).sum() / (chain[:, 0] * w).max())
+    # rows go through the reference's ChainOutFile format, E16.7 (settings.f90:109,
+    # ImportanceSampling.f90:221 -> WriteParams), byte for byte as the chain writer's
+    from cosmomc_amd.chains import fortran_e
+    with open(tmp_path / "post.txt") as f:
+        lines = f.read().splitlines()
+    for line, (m, t, pu) in zip(lines, r.rows):
+        assert line == "".join(fortran_e(v, 16) for v in [m, t, *pu])
+        assert len(line) == 16 * (2 + len(pu))
 
 
 def test_skip_thin_and_fraction(tmp_path):
