@@ -273,7 +273,7 @@ int cmbs_create(const cmbs_config_t *cfg, cmbs_t **out, char *errbuf, size_t err
     std::unique_ptr<cmbs> s(new cmbs);
     if (const char *e = std::getenv("CMAMD_PIPE")) {   // fast-step schedule for A/B runs (cmamd_debug_pipeline)
         const int m = std::atoi(e);
-        if (m >= 0 && m <= 2) s->pipe_mode = m;
+        if (m >= 0 && m <= 3) s->pipe_mode = m;
     }
     int rc = guarded(&err, [&] { cmamd::sampler_create(s.get(), cfg); });
     if (rc) {
@@ -337,7 +337,10 @@ int cmbs_step_drag(cmbs_t *s, int n_steps, double dragging_steps, cmbs_theory_fn
 
 int cmbs_history_host(cmbs_t *s, int first, int count, double *out) {
     if (!s || !out || count < 0) return CMBL_ERR_ARG;
-    return guarded(&s->last_error, [&] { cmamd::sampler_history_host(s, first, count, out); });
+    return guarded(&s->last_error, [&] {
+        cmamd::sampler_check_pipe(s, true);
+        cmamd::sampler_history_host(s, first, count, out);
+    });
 }
 
 int cmbs_step_theory(cmbs_t *s, int n_steps, cmbs_theory_fn theory_fn, void *user, void *stream) {
@@ -417,14 +420,20 @@ int cmbs_state(cmbs_t *s, double **P, double **cur_like, double **mult, int **nu
 
 int cmbs_get_state_host(cmbs_t *s, double *P, double *cur_like, double *mult, int *num_accept) {
     if (!s) return CMBL_ERR_ARG;
-    return guarded(&s->last_error, [&] { cmamd::sampler_get_state_host(s, P, cur_like, mult, num_accept); });
+    return guarded(&s->last_error, [&] {
+        cmamd::sampler_check_pipe(s, true);
+        cmamd::sampler_get_state_host(s, P, cur_like, mult, num_accept);
+    });
 }
 
 size_t cmbs_state_bytes(const cmbs_t *s) { return s ? cmamd::sampler_state_bytes(s) : 0; }
 
 int cmbs_save_state(cmbs_t *s, void *buf, size_t bytes) {
     if (!s || !buf) return CMBL_ERR_ARG;
-    return guarded(&s->last_error, [&] { cmamd::sampler_save_state(s, buf, bytes); });
+    return guarded(&s->last_error, [&] {
+        cmamd::sampler_check_pipe(s, true);
+        cmamd::sampler_save_state(s, buf, bytes);
+    });
 }
 
 int cmbs_history_restore(cmbs_t *s, int first, int count, const double *in, const double *terms) {
@@ -434,7 +443,10 @@ int cmbs_history_restore(cmbs_t *s, int first, int count, const double *in, cons
 
 int cmbs_history_terms_host(cmbs_t *s, int first, int count, double *out) {
     if (!s || (count > 0 && !out)) return CMBL_ERR_ARG;
-    return guarded(&s->last_error, [&] { cmamd::sampler_history_terms_host(s, first, count, out); });
+    return guarded(&s->last_error, [&] {
+        cmamd::sampler_check_pipe(s, true);
+        cmamd::sampler_history_terms_host(s, first, count, out);
+    });
 }
 
 int cmbs_load_state(cmbs_t *s, const void *buf, size_t bytes) {

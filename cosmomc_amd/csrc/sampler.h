@@ -98,6 +98,21 @@ struct DevCfg {
     double *calbuf_next;                    // the next launch's half
 };
 
+// The unified step launch (pipe_mode 3, sampler.hip mh_step_kernel): its
+// Metropolis workgroups wait for their walker tile's quadratic-form and
+// chi^2 workgroups of the same launch, which arrive on a per-tile counter
+// after their outputs are stored write-through.  The counters only grow: a
+// tile is complete in this launch's epoch e when its count reaches e x (its
+// producers per launch).
+struct TailWait {
+    unsigned int *cnt;       // [tiles] arrivals
+    unsigned int epoch;      // launches with producers so far, this one included
+    int nq_items;            // quadratic-form workgroups per tile
+    int ng, gwt;             // chi^2 workgroups and walkers per chi^2 workgroup
+    int *status;             // CMBL_STATUS_PIPE_WAIT when a wait gives up
+    int nosignal;            // debug: the producers never arrive (the give-up test)
+};
+
 struct LikeSlot {
     cmbl_t *like;
     std::vector<int> nidx;   // nuisance_indices, 0-based
@@ -189,8 +204,24 @@ struct cmbs {
     cmamd::StepTailPlan tail_plan[3];        // workgroup rows: tails + pass, tails, pass
     int tail_ready = 0;                      // W it is set up for (0: not yet, -W: not possible)
     int tail_qf = -1, tail_g = -1;           // the stage (0 / 1) of the quadratic form / of the chi^2
+    // unified step launches (pipe_mode 3): one launch per step holds step k's
+    // tails, step k + 1's pass and the Metropolis workgroups that accept step k
+    // (waiting per tile on the tails: TailWait) and propose step k + 1
+    cmamd::DevBuf tail_cnt;                  // [tiles] TailWait::cnt
+    unsigned tail_epoch = 0;
+    cmamd::StepTailPlan uni_plan[3];         // rows: propose + pass, tails + pass + accept/propose, tails + accept
+    size_t uni_lds = 0;
+    int tail_nosignal = 0;                   // debug (cmamd_debug_tail_nosignal)
+    // a pipelined hand-off that gave up (modes 1 and 3): the device word, its
+    // pinned copy taken at the end of each step call, checked at the next
+    cmamd::DevBuf pipe_status;
+    int *pipe_status_host = nullptr;
+    hipEvent_t pipe_ev = nullptr;
+    bool pipe_ev_pending = false;
     int tp_why = 0;                          // set-up progress when no pass was built (debug)
     ~cmbs() {
+        if (pipe_status_host) (void)hipHostFree(pipe_status_host);
+        if (pipe_ev) (void)hipEventDestroy(pipe_ev);
         for (auto &st : streams)
             if (st) (void)hipStreamDestroy(st);
         for (auto &e : events)
@@ -200,6 +231,8 @@ struct cmbs {
 
 namespace cmamd {
 void sampler_set_groups(cmbs *s, int n_groups);
+// a pipelined hand-off that gave up fails here (wait: for the last step call's copy)
+void sampler_check_pipe(cmbs *s, bool wait = false);
 void sampler_chain_moments(cmbs *s, int first, int last, const double *gmean, double *out, hipStream_t stream);
 void sampler_history_host(cmbs *s, int first, int count, double *out);
 void sampler_set_trial_theory(cmbs *s, int like_index, double *dl_end, long long ld_field, long long ld_walker);

@@ -22,6 +22,7 @@
 
 #include <cstdlib>
 
+#include "qfs_body.h"
 #include "quadform.h"
 #include "sampler.h"
 #include "smallgauss.h"
@@ -550,9 +551,39 @@ __device__ inline void write_like_flags(const DevCfg &c, const QT &trial, const 
 // (MetropolisAccept MCMC.f90:119-131 + MoveDone :166-190), then propose the
 // next trial (GetProposal / GetProposalFast) and scatter its nuisance
 // parameters for the likelihood kernels.  MB walkers per block.
+// A Metropolis workgroup of the unified step launch waits here until its
+// walker tile's quadratic-form and chi^2 workgroups have arrived (TailWait),
+// then acquires their write-through outputs.  The producers are all earlier in
+// the grid and wait on nothing, so the count arrives; the wait still gives up
+// after TAIL_WAIT_TICKS (10 ns s_memrealtime ticks) and sets the status word,
+// which the next step call reports as an error (sampler_check_pipe).
+static constexpr unsigned long long TAIL_WAIT_TICKS = 5000000ull;   // 50 ms
+
+__device__ __forceinline__ void tail_wait(const TailWait &tw, int tile)
+{
+    if (threadIdx.x == 0) {
+        const int gpt = 64 / tw.gwt, g0 = tile * gpt;
+        const int gq = max(0, min(gpt, tw.ng - g0));
+        const unsigned target = tw.epoch * (unsigned)(tw.nq_items + gq);
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            const unsigned v = __hip_atomic_load(tw.cnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v >= target) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > TAIL_WAIT_TICKS) {
+                atomicOr(tw.status, CMBL_STATUS_PIPE_WAIT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// tw: the unified step launch's wait (mh_step_kernel), else null
 template <bool ACCEPT, bool PROPOSE>
 __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *hist_row, double *hist_terms, int blk0,
-                                        double *lds, int bx)
+                                        double *lds, int bx, const TailWait *tw = nullptr)
 {
     const Rows &R = c.rows;
     const int lane = threadIdx.x % MB, grp = threadIdx.x / MB;    // walker in block, thread group
@@ -596,10 +627,11 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     } else {
         dma_rows_f64(sd, 0, c.sd, 0, R.ND, W, wb, wl64, wave, nwave);
     }
-    dma_rows_f64(lk, 0, c.like_terms, 0, nlk, W, wb, wl64, wave, nwave);
     dma_rows_i32(si, c.si, ni_st, W, wb, wl64, wave, nwave);
     dma_words(td, c.tab_d, 2 * ntd, wl64, wave, nwave);
     dma_words(ti, c.tab_i, c.tl.n_int, wl64, wave, nwave);
+    if (tw) tail_wait(*tw, wb / 64);   // the trial's terms below come from this launch's producers
+    dma_rows_f64(lk, 0, c.like_terms, 0, nlk, W, wb, wl64, wave, nwave);
     // per-likelihood terms of the current point, for the history (rejected walkers keep theirs)
     double ct[MAXLIKE];
     if (ACCEPT && hist_terms && grp == 0 && act) {
@@ -870,6 +902,49 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_pass_kernel(DevCfg c, int fa
 #ifdef CMAMD_STAMPS
     if (threadIdx.x == 0 && b < 2048) cmamd::g_pipe_stamps[b][4] = 2;
 #endif
+}
+
+// The unified step launch (pipe_mode 3): one launch per fast step.  Rows of
+// workgroups (tail_rows) run step k's tails -- plik_lite's quadratic form from
+// raw sums and the lensing chi^2, which store write-through and arrive on
+// their walker tile's counter -- the window pass storing step k + 1's raw sums,
+// and last the Metropolis workgroups, which wait for their tile's arrivals
+// (tail_wait), accept step k (finishing plik's deferred combine from the
+// partials of this launch) and propose step k + 1.  The pass waits on
+// nothing; the Metropolis chain of a tile starts as soon as its tails are
+// done instead of at a kernel boundary, and overlaps the pass.
+__device__ __forceinline__ void tail_arrive(const TailWait &tw, int tile)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are done
+    __syncthreads();
+    if (threadIdx.x == 0 && !tw.nosignal)
+        __hip_atomic_fetch_add(tw.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool ACCEPT, bool PROPOSE>
+__global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fast_only, double *hist_row,
+                                                                double *hist_terms, StepTail t,
+                                                                const int2 *__restrict__ rows, TailWait tw, int nmh)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int2 rr = rows[blockIdx.x >> 3];
+    const int lb = rr.y * 8 + (blockIdx.x & 7);
+    if (rr.x == TAIL_QF) {
+        if (lb >= t.nq) return;
+        int item_ix, tile;
+        qf_place(lb, t.q.src.n_items, t.q.src.xcd_map, item_ix, tile);
+        qfs_body<true>(lds, item_ix, tile, t.q);
+        tail_arrive(tw, tile);
+    } else if (rr.x == TAIL_GAUSS) {
+        if (lb >= t.ng) return;
+        small_gauss_body<SMALL_WT, true, true>(t.g, lds, lb);
+        tail_arrive(tw, lb * SMALL_WT / 64);
+    } else if (rr.x == TAIL_PASS) {
+        if (lb < t.np)
+            tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
+    } else if (lb < nmh) {
+        mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, 0, lds, lb, ACCEPT ? &tw : nullptr);
+    }
 }
 
 // ------------------------------------------------------- deferred rotations
@@ -2505,6 +2580,44 @@ static TPOut pass_out(cmbs *s, int k) {
                  (long long)std::max(1, L.n_nuis)};
 }
 
+// The pipelined hand-offs' give-up word (modes 1 and 3): zeroed here; copied
+// to pinned memory at the end of every pipelined step call (pipe_status_post)
+// and checked at the start of the next call and by the state readbacks
+// (sampler_check_pipe), so a hand-off that gave up fails the run loudly
+// instead of leaving silently rejected trials.
+static void pipe_status_init(cmbs *s) {
+    if (!s->pipe_status.p) {
+        s->pipe_status.alloc(256);
+        HIP_CHECK(hipHostMalloc((void **)&s->pipe_status_host, 64, hipHostMallocDefault));
+        HIP_CHECK(hipEventCreateWithFlags(&s->pipe_ev, hipEventDisableTiming));
+    }
+    HIP_CHECK(hipMemset(s->pipe_status.p, 0, 256));
+    *s->pipe_status_host = 0;
+    s->pipe_ev_pending = false;
+}
+
+static void pipe_status_post(cmbs *s, hipStream_t stream) {
+    HIP_CHECK(hipMemcpyAsync(s->pipe_status_host, s->pipe_status.p, 4, hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipEventRecord(s->pipe_ev, stream));
+    s->pipe_ev_pending = true;
+}
+
+void sampler_check_pipe(cmbs *s, bool wait) {
+    if (!s->pipe_ev_pending) return;
+    if (wait) HIP_CHECK(hipEventSynchronize(s->pipe_ev));
+    const hipError_t q = hipEventQuery(s->pipe_ev);
+    if (q == hipErrorNotReady) return;   // checked at a later call
+    HIP_CHECK(q);
+    s->pipe_ev_pending = false;
+    if (*s->pipe_status_host & CMBL_STATUS_PIPE_WAIT) {
+        *s->pipe_status_host = 0;
+        s->tail_ready = 0;
+        s->pipe_ready = 0;
+        fail(CMBL_ERR_NUMERIC, "a pipelined step's in-launch hand-off gave up waiting (CMBL_STATUS_PIPE_WAIT): "
+                               "the walkers' last steps are invalid");
+    }
+}
+
 // Whether this run of fast steps can be pipelined: the fused pass takes its
 // vectorised form and every walker proposes in one launch (one group, no
 // change mask, no rotations left to rot_kernel).
@@ -2513,6 +2626,7 @@ static bool pipe_setup(cmbs *s, int fast_only) {
     const LikeSlot &P = s->likes[s->tp_like[0]];
     if (!s->tpass->vec_ok(P.dl, P.ld_field, P.ld_walker)) return false;
     if (s->pipe_ready == s->W) return true;
+    pipe_status_init(s);
     {   // both halves unset: the first launch publishes into half 1, resets half 0
         const std::vector<unsigned long long> unset((size_t)4 * s->dc.ld, TP_PIPE_UNSET);
         s->pipe_cal.alloc(unset.size() * 8);
@@ -2546,7 +2660,7 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
             const WinStage &st = s->tp_stage[k];
             dc.pub_pcal[k] = st.cal_index >= 0 ? s->likes[s->tp_like[k]].nidx[st.cal_index] : -1;
         }
-        const unsigned e = ++s->pipe_epoch;   // this launch's half e % 2; it resets the other for the next
+        const unsigned e = s->pipe_epoch + 1;   // this launch's half e % 2; it resets the other for the next
         dc.calbuf = s->pipe_cal.as<double>() + (size_t)(e % 2) * 2 * dc.ld;
         dc.calbuf_next = s->pipe_cal.as<double>() + (size_t)((e + 1) % 2) * 2 * dc.ld;
         const int nmh = (int)g.x, nmh_pad = (nmh + 7) / 8 * 8;
@@ -2554,19 +2668,25 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
         TPDev tp = s->tpass->dev_args(o, s->W);
         tp.calbuf = dc.calbuf;
         tp.cal_ld = dc.ld;
-        for (int k = 0; k < 2; k++) tp.status[k] = s->likes[s->tp_like[k]].like->like->status_word();
+        for (int k = 0; k < 2; k++) tp.status[k] = s->pipe_status.as<int>();
         tp.delay = PIPE_DELAY;
         const LikeSlot &P = s->likes[s->tp_like[0]];
         const dim3 gp(nmh_pad + s->tpass->n_blocks());
-        timed_launch("mh_pass_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            if (accept)
-                hipExtLaunchKernelGGL(mh_pass_kernel<true>, gp, b, s->pipe_lds, stream, e0, e1, 0, dc, fast_only, row.p,
-                                      row.t, nmh, nmh_pad, tp, P.dl, P.ld_field, P.ld_walker);
-            else
-                hipExtLaunchKernelGGL(mh_pass_kernel<false>, gp, b, s->pipe_lds, stream, e0, e1, 0, dc, fast_only,
-                                      row.p, row.t, nmh, nmh_pad, tp, P.dl, P.ld_field, P.ld_walker);
-        });
-        HIP_CHECK(hipGetLastError());
+        try {
+            timed_launch("mh_pass_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+                if (accept)
+                    hipExtLaunchKernelGGL(mh_pass_kernel<true>, gp, b, s->pipe_lds, stream, e0, e1, 0, dc, fast_only,
+                                          row.p, row.t, nmh, nmh_pad, tp, P.dl, P.ld_field, P.ld_walker);
+                else
+                    hipExtLaunchKernelGGL(mh_pass_kernel<false>, gp, b, s->pipe_lds, stream, e0, e1, 0, dc, fast_only,
+                                          row.p, row.t, nmh, nmh_pad, tp, P.dl, P.ld_field, P.ld_walker);
+            });
+            HIP_CHECK(hipGetLastError());
+        } catch (...) {
+            s->pipe_ready = 0;   // both halves re-uploaded as unset next time
+            throw;
+        }
+        s->pipe_epoch = e;       // only a launched step moves the halves' parity
         return;
     }
     timed_launch("mh_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
@@ -2615,7 +2735,7 @@ static void check_theory_fresh(const cmbs *s) {
 // quadratic form (plik_lite: every row calibrated) and a small chi^2 another
 // launch can carry (Planck lensing).  Sets up the raw-sum buffers once per W.
 static bool tail_setup(cmbs *s, int fast_only) {
-    if (s->pipe_mode != 2 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on || s->dc.rot_defer)
+    if (s->pipe_mode < 2 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on || s->dc.rot_defer)
         return false;
     {
         const LikeSlot &P = s->likes[s->tp_like[0]];
@@ -2655,6 +2775,25 @@ static bool tail_setup(cmbs *s, int fast_only) {
     for (const WinCol &c : s->tp_stage[s->tail_g].cols) rc[c.row] = c.cal ? 1 : 0;
     s->tail_rowcal.alloc(rc.size());
     s->tail_rowcal.upload(rc.data(), rc.size());
+    // the unified launch's arrival counters (from 0, epoch 0) and its LDS
+    const size_t tiles = Wp / QF_TILE;
+    s->tail_cnt.alloc(tiles * 4);
+    HIP_CHECK(hipMemset(s->tail_cnt.p, 0, tiles * 4));
+    s->tail_epoch = 0;
+    pipe_status_init(s);
+    {
+        const int gi = s->tp_like[s->tail_g];
+        Like &G = *s->likes[gi].like->like;
+        SmallGaussLaunch g{};
+        G.corun_small(g, s->W, s->dc.like_nuis[gi], G.n_nuis, s->like_terms.as<double>() + (size_t)gi * s->dc.ld,
+                      s->like_ws[gi].p);
+        s->uni_lds = std::max({s->mh_lds, (size_t)QFS_LDS_DOUBLES * 8, (size_t)tp_vec_lds_bytes<2, false>(),
+                               (size_t)small_gauss_lds_doubles<SMALL_WT>(g.d.nX) * 8});
+        for (const void *k : {(const void *)mh_step_kernel<false, true>, (const void *)mh_step_kernel<true, true>,
+                              (const void *)mh_step_kernel<true, false>})
+            HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->uni_lds));
+    }
+    for (auto &pl : s->uni_plan) pl.key[0] = -1;
     s->tail_ready = s->W;
     return true;
 }
@@ -2662,7 +2801,7 @@ static bool tail_setup(cmbs *s, int fast_only) {
 // One step tail: the quadratic form and the chi^2 of the step whose raw sums
 // are in half rd (rd < 0: none), and the pass storing the next step's raw sums
 // into half wr (wr < 0: none).
-static void launch_tail(cmbs *s, hipStream_t stream, int rd, int wr) {
+static StepTail make_tail(cmbs *s, int rd, int wr) {
     StepTail t;
     const int W = s->W;
     t.W = W;
@@ -2701,11 +2840,79 @@ static void launch_tail(cmbs *s, hipStream_t stream, int rd, int wr) {
         t.ld_walker = P.ld_walker;
         t.np = s->tpass->n_blocks();
     }
+    return t;
+}
+
+static void launch_tail(cmbs *s, hipStream_t stream, int rd, int wr) {
+    const StepTail t = make_tail(s, rd, wr);
     const int v = rd >= 0 ? (wr >= 0 ? 0 : 1) : 2;
     static const char *names[3] = {"step_tail_kernel", "step_tail_last", "step_tail_pass"};
     launch_step_tail(t, s->tail_plan[v], stream, names[v]);
     if (rd >= 0) record_deferred(s, (size_t)s->tp_like[s->tail_qf],
                                  QFDeferred{t.q.src.partial, t.q.src.n_items, nullptr});
+}
+
+// One unified step launch (pipe_mode 3, mh_step_kernel): the tails of the
+// step whose raw sums are in half rd (rd < 0: none), the pass into half wr
+// (wr < 0: none), and the Metropolis workgroups accepting that step (when
+// rd >= 0) and proposing the next (propose).
+static void launch_unified(cmbs *s, hipStream_t stream, bool propose, int rd, int wr, const HistRow &row,
+                           int fast_only) {
+    const bool accept = rd >= 0;
+    StepTail t = make_tail(s, rd, wr);
+    DevCfg dc = s->dc;
+    dc.mask_on = 0;
+    dc.pub_on = 0;
+    dc.n_def = 0;
+    s->pending_def = 0;
+    if (accept) {   // plik's combine from this launch's partials (QFDeferred)
+        dc.n_def = 1;
+        dc.def_like[0] = s->tp_like[s->tail_qf];
+        dc.def_items[0] = t.q.src.n_items;
+        dc.def_part[0] = t.q.src.partial;
+        dc.def_add[0] = nullptr;
+    }
+    TailWait tw{};
+    tw.cnt = s->tail_cnt.as<unsigned int>();
+    tw.epoch = s->tail_epoch + (accept ? 1u : 0u);
+    tw.nq_items = t.q.src.n_items;
+    tw.ng = t.ng;
+    tw.gwt = SMALL_WT;
+    tw.status = s->pipe_status.as<int>();
+    tw.nosignal = s->tail_nosignal;
+    const int nmh = (s->W + MB - 1) / MB;
+    const int v = accept ? (propose ? 1 : 2) : 0;
+    StepTailPlan &pl = s->uni_plan[v];
+    if (pl.key[0] != t.nq || pl.key[1] != t.ng || pl.key[2] != t.np) {
+        const std::vector<int2> rows = tail_rows(t.nq, t.ng, t.np, nmh);
+        pl.d_rows.alloc(rows.size() * sizeof(int2));
+        pl.d_rows.upload(rows.data(), rows.size() * sizeof(int2));
+        pl.nrows = (int)rows.size();
+        pl.key[0] = t.nq;
+        pl.key[1] = t.ng;
+        pl.key[2] = t.np;
+    }
+    const dim3 grid((unsigned)pl.nrows * 8), b(MH_THREADS);
+    const int2 *rows = pl.d_rows.as<int2>();
+    static const char *names[3] = {"mh_step_first", "mh_step_kernel", "mh_step_last"};
+    try {
+        timed_launch(names[v], stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            if (v == 0)
+                hipExtLaunchKernelGGL(mh_step_kernel<false, true>, grid, b, s->uni_lds, stream, e0, e1, 0, dc,
+                                      fast_only, row.p, row.t, t, rows, tw, nmh);
+            else if (v == 1)
+                hipExtLaunchKernelGGL(mh_step_kernel<true, true>, grid, b, s->uni_lds, stream, e0, e1, 0, dc, fast_only,
+                                      row.p, row.t, t, rows, tw, nmh);
+            else
+                hipExtLaunchKernelGGL(mh_step_kernel<true, false>, grid, b, s->uni_lds, stream, e0, e1, 0, dc,
+                                      fast_only, row.p, row.t, t, rows, tw, nmh);
+        });
+        HIP_CHECK(hipGetLastError());
+    } catch (...) {
+        s->tail_ready = 0;   // the counters and the epoch are set up afresh next time
+        throw;
+    }
+    if (accept) s->tail_epoch++;
 }
 
 void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
@@ -2717,6 +2924,17 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (n_steps <= 0) return;
     // propose(1) | likes | accept(1)+propose(2) | likes | ... | likes | accept(n)
     const int G = s->n_groups;
+    sampler_check_pipe(s);
+    if (G == 1 && s->pipe_mode == 3 && tail_setup(s, fast_only)) {
+        // unified: propose(1) + pass(1) | tails(1) + pass(2) + accept(1) + propose(2) | ... |
+        // tails(n) + accept(n): one launch per step
+        launch_unified(s, stream, true, -1, 0, HistRow{}, fast_only);
+        for (int k = 0; k < n_steps; k++)
+            launch_unified(s, stream, k + 1 < n_steps, k % 2, k + 1 < n_steps ? (k + 1) % 2 : -1, next_hist(s),
+                           fast_only);
+        pipe_status_post(s, stream);
+        return;
+    }
     if (G == 1 && tail_setup(s, fast_only)) {
         // split pipelined: pass(1) | mh(propose 1) | tails(1) + pass(2) | mh(accept 1 + propose 2) |
         // tails(2) + pass(3) | ... | tails(n) | mh(accept n)
@@ -2736,6 +2954,7 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
             eval_likes(s, stream, false, 0, s->W, s->ws.p, true, true);
         }
         launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W, false);
+        pipe_status_post(s, stream);
         return;
     }
     if (G == 1) {
@@ -3236,13 +3455,18 @@ extern "C" int cmamd_debug_tp_items(const cmbs *s, int *out, int cap) {   // (fi
     return s->tpass->n_items();
 }
 extern "C" int cmamd_debug_pipeline(cmbs *s, int mode) {   // fast-step schedule (sampler_step): 0 unpipelined,
-    if (!s || mode < 0 || mode > 2) return -1;              // 1 mh_pass_kernel, 2 step tails
+    if (!s || mode < 0 || mode > 3) return -1;              // 1 mh_pass_kernel, 2 step tails, 3 unified launches
     s->pipe_mode = mode;
     return 0;
 }
 extern "C" int cmamd_debug_corun(cmbs *s, int on) {     // the lensing chi^2 inside plik's quadratic-form launch
     if (!s) return -1;
     s->no_corun = !on;
+    return 0;
+}
+extern "C" int cmamd_debug_tail_nosignal(cmbs *s, int on) {   // the unified launch's producers never arrive
+    if (!s) return -1;
+    s->tail_nosignal = on;
     return 0;
 }
 extern "C" int cmamd_debug_tail(const cmbs *s) { return s ? s->tail_ready : 0; }   // W of the step tails' set-up

@@ -34,7 +34,9 @@ template <int WT> constexpr int small_gauss_lds_doubles(int nX) {
 
 // RAWCAL: partial rows are raw window sums; rows flagged in a.row_cal are
 // divided by the walker's cal^2 as they are loaded (SmallGaussLaunch)
-template <int WT, bool RAWCAL = false>
+// SIGNAL: -lnL is stored agent-scope (write-through) for a consumer in the
+// same launch (the sampler's unified step launch)
+template <int WT, bool RAWCAL = false, bool SIGNAL = false>
 __device__ __forceinline__ void small_gauss_body(const SmallGaussLaunch &a, double *lds, int blk)
 {
     constexpr int NG = 256 / WT;             // thread groups of WT walkers
@@ -115,7 +117,10 @@ __device__ __forceinline__ void small_gauss_body(const SmallGaussLaunch &a, doub
             const double t = log(cal) / c.log_cal_prior;
             chisq = chisq + t * t;
         }
-        a.out[w] = chisq / 2;
+        if (SIGNAL)
+            __hip_atomic_store(a.out + w, chisq / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            a.out[w] = chisq / 2;
     }
 }
 

@@ -14,6 +14,8 @@
 // Metropolis kernel that proposes step k + 1 runs alone, between two tails).
 #pragma once
 
+#include <vector>
+
 #include "common.h"
 #include "theorypass.h"
 
@@ -39,6 +41,13 @@ struct StepTail {
     int np = 0;              // pass workgroups (TheoryPass::n_blocks), 0: none
     int W = 0;
 };
+
+// Workgroup roles by rows of 8 (block b runs on XCD b % 8, so each role's own
+// block numbering keeps the XCD placement its body assumes: qf_place,
+// TheoryPass::plan_units): row k is role rows[k].x's rows[k].y-th row.  nm
+// Metropolis workgroups (sampler.hip's unified step launch) come last.
+enum { TAIL_QF = 0, TAIL_GAUSS = 1, TAIL_PASS = 2, TAIL_MH = 3 };
+std::vector<int2> tail_rows(int nq, int ng, int np, int nm);
 
 // the launch's workgroup rows for its role counts (owned by the caller)
 struct StepTailPlan {

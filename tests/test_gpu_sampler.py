@@ -701,11 +701,14 @@ def test_corun_tails_bitwise(cmbl_golden, refdata, tmp_path, W):
 
 @pytest.mark.parametrize("W", [1, 100, 1024])
 def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
-    """The fast-step schedules give the same bits.  Mode 2 (the default, the
-    split pipelined steps): the fused pass of step k + 1 runs in step k's tail
-    launch and stores raw sums, which step k + 1's quadratic form and lensing
-    chi^2 calibrate as they read them (steptail.hip), with the proposing
-    Metropolis kernel alone in between.  Mode 1: the pass of step k in the
+    """The fast-step schedules give the same bits.  Mode 3 (the unified step
+    launch): one launch per step holds step k's quadratic form and lensing
+    chi^2, the pass storing step k + 1's raw sums, and the Metropolis
+    workgroups that wait for their tile's tails, accept step k and propose
+    step k + 1 (mh_step_kernel).  Mode 2 (the split pipelined steps): the
+    fused pass of step k + 1 runs in step k's tail launch and stores raw sums,
+    which step k + 1's quadratic form and lensing chi^2 calibrate as they read
+    them (steptail.hip), with the proposing Metropolis kernel alone in between.  Mode 1: the pass of step k in the
     launch of the mh_kernel proposing it (mh_pass_kernel).  Mode 0: the
     unpipelined schedule.  Chains, CurLike and both likelihood terms are
     bit-identical over step() calls of 1, 2 and 5 steps.  The headline path is
@@ -726,7 +729,7 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
     calls = (1, 2, 5)
     steps = sum(calls)
     out = []
-    for mode in (2, 1, 0):
+    for mode in (3, 2, 1, 0):
         plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
         lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
         plik.nuisance_indices = [2]
@@ -742,11 +745,11 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
         s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
         for n in calls:
             s.step(n, fast_only=True)
-        if mode == 2:
+        if mode >= 2:
             assert N.lib().cmamd_debug_tail(s._h) == W        # the step tails ran
         out.append((s.history_host(0, steps), s.history_terms(0, steps)))
         assert plik.status() == 0 and lens.status() == 0
-        if mode == 2:
+        if mode == 3:
             po_plik = po.PlikLite(data)
             o_lens = co.CMBLikesOracle(os.path.join(refdata, c["dataset"]), c["overrides"], c["tag"])
             for k in (0, steps - 1):
@@ -761,6 +764,43 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
     for o in out[1:]:
         assert np.array_equal(out[0][0], o[0])
         assert np.array_equal(out[0][1], o[1])
+
+
+@pytest.mark.parametrize("mode", [3])
+def test_pipelined_handoff_giveup_fails_loudly(cmbl_golden, refdata, tmp_path, mode):
+    """The unified step launch's Metropolis workgroups wait in-launch for
+    their tile's tails; a debug switch stops the tails from arriving, so every
+    wait gives up after its 50 ms bound and sets CMBL_STATUS_PIPE_WAIT.  The
+    next readback (and the next step call) must fail instead of handing back
+    silently rejected trials."""
+    import os
+
+    from cosmomc_amd import _native as N
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    c = cmbl_golden["cases"]["lensing_consext8"]
+    W = 128
+    th = syn.walker_theory(W, seed=12, n_fields=10, ld_field=2512)
+    dl = torch.tensor(th, device="cuda")
+    plik = NativeCMBLikelihood("PLIK_LITE", syn.make_plik_lite(12345).write(str(tmp_path)))
+    lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
+    plik.nuisance_indices = [2]
+    lens.nuisance_indices = [2]
+    s = BatchedMCMC(W, 3, [2], [[1]], 0, [0.0222, 0.9, 3.05], [0.0222, 1.1, 3.05], [0.0, 1.0, 0.0],
+                    [0.0, 0.0025, 0.0], seed_ij=63, seed_kl=74)
+    s.set_covariance(np.array([[0.002 ** 2]]))
+    s.add_likelihood(plik, dl)
+    s.add_likelihood(lens, dl)
+    assert N.lib().cmamd_debug_pipeline(s._h, mode) == 0
+    s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
+    s.step(2, fast_only=True)                                  # healthy
+    s.state()
+    assert N.lib().cmamd_debug_tail_nosignal(s._h, 1) == 0
+    s.step(2, fast_only=True)                                  # every wait gives up
+    with pytest.raises(Exception, match="gave up"):
+        s.state()
+    assert N.lib().cmamd_debug_tail_nosignal(s._h, 0) == 0
+    s.close()
 
 
 def test_dragging_fused_plik_lensing(cmbl_golden, refdata, tmp_path):
@@ -858,3 +898,86 @@ def test_parallel_rotations_match_serial(blocks, W, groups):
     np.testing.assert_array_equal(sa[1], sb[1])
     assert a == b
     assert c == b          # mode 2: a last-row redraw restarts the pass instead of using the spare lanes
+
+
+def _config5_sampler(refdata, tmp_path, W, groups):
+    """BASELINE configs[4] as bench.py's config5_bk15_plik builds it: BK15 (12
+    B maps x 9 bins, HL, batch3/BK15.ini foreground parameters) + plik_lite
+    TTTEEE on one shared slow point, 8 fast parameters in the blocks the
+    reference's SetFastSlowParams makes (plik_lite, then BK15)."""
+    import os
+
+    from cosmomc_amd.likelihood import LikelihoodList, NativeCMBLikelihood
+    from cosmomc_amd.params import set_fast_slow_params
+    from cosmomc_amd.sampler import BatchedMCMC
+    maps = ("BK15_95_B BK15_150_B BK15_220_B W023_B P030_B W033_B P044_B P070_B P100_B P143_B P217_B "
+            "P353_B")
+    data = syn.make_plik_lite(12345)
+    plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    bk = NativeCMBLikelihood("BKPLANCK", os.path.join(refdata, "BK15/BK15_dust.dataset"), {"maps_use": maps})
+    plik.nuisance_indices = [1]
+    bk.nuisance_indices = list(range(2, 18))
+    P0 = np.array([1.0, 3.0, 1.0, -0.42, 1.59, 19.6, -0.6, -3.1, 0.2, 2.0, 2.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0])
+    pmin, pmax = P0.copy(), P0.copy()
+    for i, lo, hi in ((0, 0.9, 1.1), (1, 0.0, 15.0), (2, 0.0, 50.0), (3, -1.0, 0.0), (4, 1.04, 2.14),
+                      (6, -1.0, 0.0), (7, -4.5, -2.0), (8, -1.0, 1.0)):
+        pmin[i], pmax[i] = lo, hi
+    pm, ps = np.zeros(17), np.zeros(17)
+    pm[0], ps[0] = 1.0, 0.0025
+    pm[4], ps[4] = 1.59, 0.11
+    pm[7], ps[7] = -3.1, 0.3
+    used = [1, 2, 3, 4, 5, 7, 8, 9]
+    ll = LikelihoodList()
+    ll.add(plik)
+    ll.add(bk)
+    ll.add_nuisance_parameters([])
+    blk = set_fast_slow_params(17, [i + 1 in used for i in range(17)], list(ll), num_theory_params=0)
+    width = np.array([0.0025, 0.5, 1.0, 0.1, 0.1, 0.1, 0.3, 0.2])
+    s = BatchedMCMC(W, 17, used, blk.param_blocks, blk.slow_block_max, pmin, pmax, pm, ps, propose_scale=2.4,
+                    seed_ij=3003, seed_kl=9373)
+    s.set_covariance(np.diag(width ** 2))
+    s.set_groups(groups)
+    th = syn.walker_theory(1, n_fields=10, ld_field=2512)
+    dl = torch.tensor(th, device="cuda").expand(W, th.shape[1], th.shape[2])
+    s.add_likelihood(plik, dl)
+    s.add_likelihood(bk, dl)
+    start = np.tile(P0, (W, 1))
+    g = syn.gaussians(91, W * 8).reshape(W, 8)
+    for c, i in enumerate([u - 1 for u in used]):
+        start[:, i] = np.clip(P0[i] + 2 * width[c] * g[:, c], pmin[i] + 1e-9, pmax[i] - 1e-9)
+    s.set_start(start)
+    return s, data, th[0], maps
+
+
+def test_config5_joint_path_vs_oracles(refdata, tmp_path):
+    """The configs[4] leg exactly as bench.py runs it (BK15 12 B maps + plik_lite,
+    W = 1024, 5 fast steps): with the change mask on (one walker group: each
+    likelihood re-evaluated only for the walkers whose trial moved one of its
+    parameters, the HL kernels on compacted slots) the accept decisions,
+    multiplicities and points equal the dense path's (two walker groups:
+    every likelihood for every walker), and the terms at the final points of
+    walkers 0, 511 and 1023 are the oracles' (pyoracle.PlikLite,
+    CMBLikesOracle; rel 1e-9)."""
+    import os
+
+    import cmblikes_oracle as co
+    W, steps = 1024, 5
+    runs = []
+    for groups in (1, 2):
+        s, data, th, maps = _config5_sampler(refdata, tmp_path, W, groups)
+        s.enable_history(steps)
+        s.step(steps, fast_only=True)
+        P, lk, mult, nacc = s.state()
+        runs.append((P.copy(), lk.copy(), mult.copy(), nacc.copy(), s.history_terms(0, steps)))
+        s.close()
+    a, b = runs
+    assert np.all(a[3] > 0)
+    np.testing.assert_array_equal(a[3], b[3])
+    np.testing.assert_array_equal(a[2], b[2])
+    np.testing.assert_allclose(a[0], b[0], rtol=1e-12)
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-10)
+    ob = co.CMBLikesOracle(os.path.join(refdata, "BK15/BK15_dust.dataset"), {"maps_use": maps}, "BKPLANCK")
+    op = po.PlikLite(data)
+    for w in (0, 511, 1023):
+        assert a[4][-1, 0, w] == pytest.approx(op.loglike(th[:3], a[0][w, 0]), rel=1e-9)
+        assert a[4][-1, 1, w] == pytest.approx(ob.loglike(th, a[0][w, 1:17]), rel=1e-9)
