@@ -208,6 +208,7 @@ struct cmbs {
     // tails, step k + 1's pass and the Metropolis workgroups that accept step k
     // (waiting per tile on the tails: TailWait) and propose step k + 1
     cmamd::DevBuf tail_cnt;                  // [tiles] TailWait::cnt
+    size_t tail_cnt_bytes = 0;
     unsigned tail_epoch = 0;
     cmamd::StepTailPlan uni_plan[3];         // rows: propose + pass, tails + pass + accept/propose, tails + accept
     size_t uni_lds = 0;

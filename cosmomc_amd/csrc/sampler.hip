@@ -31,6 +31,9 @@
 // start, [pass] streaming done / wait done, end; [3] the block's role
 namespace cmamd {
 __device__ unsigned long long g_pipe_stamps[2048][5];
+// mh_step_kernel (tools/uni_stamps.py), middle launches only: start, the
+// Metropolis wait's end, XCC id, end, role + 1
+__device__ unsigned long long g_uni_stamps[2048][5];
 }
 #define TP_PIPE_STAMP(i)                                                                        \
     do {                                                                                        \
@@ -575,9 +578,15 @@ __device__ __forceinline__ void tail_wait(const TailWait &tw, int tile)
             }
             __builtin_amdgcn_s_sleep(2);
         }
+        // one acquire after the match (cdna_hip_programming.md Guideline 16 recipe): it drops this
+        // CU's L1 lines; its own wait holds the barrier, then every wave loads
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef CMAMD_STAMPS
+        if (blockIdx.x < 2048) g_uni_stamps[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 // tw: the unified step launch's wait (mh_step_kernel), else null
@@ -929,6 +938,26 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fa
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int2 rr = rows[blockIdx.x >> 3];
     const int lb = rr.y * 8 + (blockIdx.x & 7);
+#ifdef CMAMD_STAMPS
+    const bool stamp = ACCEPT && PROPOSE && threadIdx.x == 0 && blockIdx.x < 2048;
+    if (stamp) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_uni_stamps[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+        g_uni_stamps[blockIdx.x][2] = xcc & 15;
+        g_uni_stamps[blockIdx.x][4] = 0;
+    }
+    struct End {
+        bool on;
+        int role;
+        __device__ ~End() {
+            if (on) {
+                g_uni_stamps[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
+                g_uni_stamps[blockIdx.x][4] = role + 1;
+            }
+        }
+    } end_{stamp, rr.x};
+#endif
     if (rr.x == TAIL_QF) {
         if (lb >= t.nq) return;
         int item_ix, tile;
@@ -940,8 +969,15 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fa
         small_gauss_body<SMALL_WT, true, true>(t.g, lds, lb);
         tail_arrive(tw, lb * SMALL_WT / 64);
     } else if (rr.x == TAIL_PASS) {
-        if (lb < t.np)
+        if (lb >= t.np) return;
+        if (!t.p_stride) {
             tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
+            return;
+        }
+        for (int u = lb; u < t.tp.nblk; u += t.p_stride) {   // this CU's units, one after another
+            tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), u);
+            __syncthreads();                                    // the next unit reuses the LDS
+        }
     } else if (lb < nmh) {
         mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, 0, lds, lb, ACCEPT ? &tw : nullptr);
     }
@@ -2776,9 +2812,9 @@ static bool tail_setup(cmbs *s, int fast_only) {
     s->tail_rowcal.alloc(rc.size());
     s->tail_rowcal.upload(rc.data(), rc.size());
     // the unified launch's arrival counters (from 0, epoch 0) and its LDS
-    const size_t tiles = Wp / QF_TILE;
-    s->tail_cnt.alloc(tiles * 4);
-    HIP_CHECK(hipMemset(s->tail_cnt.p, 0, tiles * 4));
+    s->tail_cnt_bytes = (Wp / QF_TILE * 4 + 15) & ~(size_t)15;   // a multiple of 16 from the start
+    s->tail_cnt.alloc(s->tail_cnt_bytes);
+    HIP_CHECK(hipMemset(s->tail_cnt.p, 0, s->tail_cnt_bytes));
     s->tail_epoch = 0;
     pipe_status_init(s);
     {
@@ -2839,6 +2875,14 @@ static StepTail make_tail(cmbs *s, int rd, int wr) {
         t.ld_field = P.ld_field;
         t.ld_walker = P.ld_walker;
         t.np = s->tpass->n_blocks();
+        static const bool persist = [] {
+            const char *e = std::getenv("CMAMD_PASS_PERSIST");
+            return e && *e == '1';
+        }();
+        if (persist) {   // one workgroup per table column (a CU's units in turn)
+            t.p_stride = s->tpass->n_per_round();
+            t.np = t.p_stride;
+        }
     }
     return t;
 }
@@ -2927,7 +2971,10 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     sampler_check_pipe(s);
     if (G == 1 && s->pipe_mode == 3 && tail_setup(s, fast_only)) {
         // unified: propose(1) + pass(1) | tails(1) + pass(2) + accept(1) + propose(2) | ... |
-        // tails(n) + accept(n): one launch per step
+        // tails(n) + accept(n): one launch per step.  The arrival counters start from 0
+        // in every call (the epochs are counted within it)
+        HIP_CHECK(hipMemsetAsync(s->tail_cnt.p, 0, s->tail_cnt_bytes, stream));
+        s->tail_epoch = 0;
         launch_unified(s, stream, true, -1, 0, HistRow{}, fast_only);
         for (int k = 0; k < n_steps; k++)
             launch_unified(s, stream, k + 1 < n_steps, k % 2, k + 1 < n_steps ? (k + 1) % 2 : -1, next_hist(s),
@@ -3425,6 +3472,10 @@ void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
 extern "C" int cmamd_debug_pipe_stamps(unsigned long long *host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_pipe_stamps), sizeof(cmamd::g_pipe_stamps)) == hipSuccess ? 0
                                                                                                                  : -5;
+}
+extern "C" int cmamd_debug_uni_stamps(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_uni_stamps), sizeof(cmamd::g_uni_stamps)) == hipSuccess ? 0
+                                                                                                               : -5;
 }
 extern "C" int cmamd_debug_stamps(unsigned long long *host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_stamps), sizeof(cmamd::g_stamps)) == hipSuccess ? 0 : -5;

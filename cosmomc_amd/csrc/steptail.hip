@@ -11,6 +11,11 @@
 
 namespace cmamd {
 
+#ifdef CMAMD_STAMPS
+// step_tail_kernel with all three roles (tools/uni_stamps.py): start, -, XCC id, end, role + 1
+__device__ unsigned long long g_tail_stamps[2048][5];
+#endif
+
 // Roles by rows of 8 workgroups (tail_rows, steptail.h).
 
 __global__ __launch_bounds__(256, 3) void step_tail_kernel(StepTail t, const int2 *__restrict__ rows)
@@ -18,6 +23,26 @@ __global__ __launch_bounds__(256, 3) void step_tail_kernel(StepTail t, const int
     extern __shared__ __attribute__((aligned(16))) double tail_lds[];
     const int2 rr = rows[blockIdx.x >> 3];
     const int lb = rr.y * 8 + (blockIdx.x & 7);
+#ifdef CMAMD_STAMPS
+    const bool stamp = t.nq && t.np && threadIdx.x == 0 && blockIdx.x < 2048;
+    if (stamp) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_tail_stamps[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+        g_tail_stamps[blockIdx.x][2] = xcc & 15;
+        g_tail_stamps[blockIdx.x][4] = 0;
+    }
+    struct End {
+        bool on;
+        int role;
+        __device__ ~End() {
+            if (on) {
+                g_tail_stamps[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
+                g_tail_stamps[blockIdx.x][4] = role + 1;
+            }
+        }
+    } end_{stamp, rr.x};
+#endif
     if (rr.x == TAIL_QF) {
         if (lb >= t.nq) return;
         int item_ix, tile;
@@ -26,9 +51,12 @@ __global__ __launch_bounds__(256, 3) void step_tail_kernel(StepTail t, const int
     } else if (rr.x == TAIL_GAUSS) {
         if (lb < t.ng) small_gauss_body<SMALL_WT, true>(t.g, tail_lds, lb);
     } else if (rr.x == TAIL_PASS) {
-        if (lb < t.np)
+        if (lb >= t.np) return;
+        for (int u = lb; u < (t.p_stride ? t.tp.nblk : lb + 1); u += (t.p_stride ? t.p_stride : 1)) {
             tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(tail_lds),
-                                        lb);
+                                        u);
+            if (t.p_stride) __syncthreads();   // the next unit reuses the LDS
+        }
     }
 }
 
@@ -106,3 +134,10 @@ void launch_step_tail(const StepTail &t, StepTailPlan &plan, hipStream_t stream,
 }
 
 }  // namespace cmamd
+
+#ifdef CMAMD_STAMPS
+extern "C" int cmamd_debug_tail_stamps(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_tail_stamps), sizeof(cmamd::g_tail_stamps)) == hipSuccess ? 0
+                                                                                                                 : -5;
+}
+#endif

@@ -60,6 +60,7 @@ struct TPDev {
     const unsigned long long *emit;   // per item step: slots whose column ends there
     const unsigned char *cmap;        // per item step, [64] slots: the item's column index (255: none)
     int nitem;
+    int nblk;             // block table entries (units, including empty ones)
     TPOut out[TP_MAXOUT];
     // pipelined form (tp_vec_body<.., true>, the sampler's mh_pass_kernel):
     // the step's calibrations come from the Metropolis workgroups of the same
@@ -83,6 +84,9 @@ class TheoryPass {
     // its arguments and block count for W walkers (theorypass_body.h)
     TPDev dev_args(const TPOut *outs, int W);
     int n_blocks() const { return nblk; }
+    // the block table's rounds: entry j of round r is block r * n_per_round() + j
+    // (plan_units: CU c of an XCD gets its units in rounds)
+    int n_per_round() const { return per_round; }
 
     int n_items() const { return (int)items.size(); }
     const TPItem &item(int k) const { return items[k]; }
@@ -94,7 +98,7 @@ class TheoryPass {
     std::vector<TPItem> items;
     DevBuf d_items, d_cols, d_w, d_units, d_emit, d_cmap;
     int nstage = 0;
-    int unit_tiles = -1, nblk = 0, max_nsb = 0;
+    int unit_tiles = -1, nblk = 0, max_nsb = 0, per_round = 0;
 };
 
 }  // namespace cmamd

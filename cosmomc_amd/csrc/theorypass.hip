@@ -460,6 +460,7 @@ void TheoryPass::plan_units(int tiles) {
         for (int k = 0; k < cpx; k++)
             for (size_t r = 0; r < cu[x][k].size(); r++) table[((size_t)r * cpx + k) * NX + x] = cu[x][k][r];
     nblk = (int)table.size();
+    per_round = NX * cpx;
     d_units.alloc(table.size() * sizeof(int2));
     d_units.upload(table.data(), table.size() * sizeof(int2));
     unit_tiles = tiles;
@@ -482,6 +483,7 @@ TPDev TheoryPass::dev_args(const TPOut *outs, int W) {
     const int tiles = (W + 63) / 64;
     if (tiles != unit_tiles) plan_units(tiles);
     c.units = d_units.as<int2>();
+    c.nblk = nblk;
     return c;
 }
 

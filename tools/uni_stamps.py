@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Block timeline of the step launches of the split (mode 2: step_tail_kernel)
+and unified (mode 3: mh_step_kernel) pipelined fast steps from in-kernel
+s_memrealtime stamps (100 MHz): per role (quadratic form, chi^2, pass,
+Metropolis) when its workgroups start and end, and for the Metropolis
+workgroups when their tile's wait ends.  Builds the instrumented library
+(tools/_stamps/, -DCMAMD_STAMPS) unless --no-build, then runs 20 headline fast
+steps in each mode and reports the last middle launch.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "tools", "_stamps")
+ROLES = {1: "quadform", 2: "chi2", 3: "pass", 4: "metropolis"}
+
+if __name__ == "__main__":
+    if "--no-build" not in sys.argv:
+        subprocess.run(["make", "-C", os.path.join(ROOT, "cosmomc_amd", "csrc"), "-j8", f"OUT={OUT}",
+                        "EXTRA=-DCMAMD_STAMPS"], check=True, stdout=subprocess.DEVNULL)
+        sys.exit(0)
+    os.environ["COSMOMC_AMD_LIB"] = os.path.join(OUT, "libcosmomc_amd.so")
+    sys.path.insert(0, ROOT)
+    import torch
+    import bench
+    from cosmomc_amd import _native as N
+    q = lambda a: " ".join(f"{np.percentile(a, p):6.2f}" for p in (0, 10, 50, 90, 100))
+    for mode, fn in ((3, "cmamd_debug_uni_stamps"), (2, "cmamd_debug_tail_stamps")):
+        with tempfile.TemporaryDirectory() as td:
+            smp, *_ = bench.build_problem(1024, 0, td)
+            assert N.lib().cmamd_debug_pipeline(smp._h, mode) == 0
+            smp.step(20, fast_only=True)
+            torch.cuda.synchronize()
+            st = np.zeros((2048, 5), dtype=np.uint64)
+            assert getattr(N.lib(), fn)(st.ctypes.data_as(C.c_void_p)) == 0
+        s = st[st[:, 4] > 0].astype(np.int64)
+        t0 = s[:, 0].min()
+        us = lambda x: (x - t0) / 100.0
+        print(f"mode {mode} ({os.environ.get('CMAMD_TAIL_ORDER', 'qpg')}): quantiles 0/10/50/90/100, "
+              f"us from the first block's start; launch {us(s[:, 3].max()):.2f} us")
+        for r, name in ROLES.items():
+            b = s[s[:, 4] == r]
+            if not len(b):
+                continue
+            print(f"  {name:10s} {len(b):4d}  start {q(us(b[:, 0]))}   end {q(us(b[:, 3]))}   "
+                  f"dur {q((b[:, 3] - b[:, 0]) / 100.0)}")
+            if r == 4:
+                print(f"  {'':10s}       wait done {q(us(b[:, 1]))}")
