@@ -626,9 +626,11 @@ def kernel_roofline(kern, avg_ms, W, fused_bytes, lens_bytes):
         "mh_kernel": W * 1024,                                 # ~1 KB of walker state read + written (latency-bound)
         # the unified step launch: the step tail's bytes + the Metropolis state
         "mh_step_kernel": pass_bytes + 2 * 8 * N_B * W + 8 * N_B * N_B + W * 1024,
+        # an interleaved launch: half the walkers' pass, raw sums and state, C^-1 once
+        "mh_half_kernel": (pass_bytes + 2 * 8 * N_B * W + W * 1024) / 2 + 8 * N_B * N_B,
     }
     mfma = {"plik_quadform_ksplit": qf_flops, "plik_quadform_corun": qf_flops, "step_tail_last": qf_flops,
-            "step_tail_kernel": qf_flops, "mh_step_kernel": qf_flops}
+            "step_tail_kernel": qf_flops, "mh_step_kernel": qf_flops, "mh_half_kernel": qf_flops / 2}
     parts = {}
     if kern in hbm:
         a = hbm[kern] / t / 1e9
@@ -739,7 +741,7 @@ def main():
         kern = {k: N.profile_read(k) for k in ("theory_window_kernel", "plik_bin_delta", "plik_quadform_ksplit",
                                                 "plik_quadform_corun", "mh_kernel", "mh_pass_kernel",
                                                 "step_tail_kernel", "step_tail_last", "step_tail_pass",
-                                                "mh_step_first", "mh_step_kernel", "mh_step_last",
+                                                "mh_step_first", "mh_step_kernel", "mh_step_last", "mh_half_kernel",
                                                 "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_gauss_small_kernel",
                                                 "cmbl_quadform")}
         kern = {k: v for k, v in kern.items() if v[1]}

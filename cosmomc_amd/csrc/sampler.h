@@ -211,6 +211,7 @@ struct cmbs {
     size_t tail_cnt_bytes = 0;
     unsigned tail_epoch = 0;
     cmamd::StepTailPlan uni_plan[3];         // rows: propose + pass, tails + pass + accept/propose, tails + accept
+    cmamd::StepTailPlan half_plan[4];        // interleaved launches (pipe_mode 4), by Metropolis variant
     size_t uni_lds = 0;
     int tail_nosignal = 0;                   // debug (cmamd_debug_tail_nosignal)
     // a pipelined hand-off that gave up (modes 1 and 3): the device word, its

@@ -55,10 +55,13 @@ static constexpr int NB = 64;          // walker tile of the history / collector
 // 16-walker blocks a W = 1024 step spreads over 64 CUs instead of 16: each
 // block stages a quarter of the state image (round 3: 64-walker blocks, 16
 // waves, 12.9 us).
-static constexpr int MB = 16;
+#ifndef CMAMD_MB
+#define CMAMD_MB 16
+#endif
+static constexpr int MB = CMAMD_MB;
 static constexpr int MH_THREADS = 256;
 static constexpr int NV = MH_THREADS / MB;
-static_assert(NV == QF_GROUPS, "one group per split-K group sum");
+static_assert(NV >= QF_GROUPS && NV % QF_GROUPS == 0, "a group per split-K group sum");
 static_assert(64 % MB == 0, "blocks tile the 64-walker rows of the split-K partials");
 
 // strided per-walker column view (LDS: stride MB; HBM: stride W)
@@ -656,7 +659,7 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
             if (d >= c.n_def) break;
             const double *tp = c.def_part[d] + (size_t)tile * c.def_items[d] * QF_TILE;
             double *row = dq + (size_t)d * (QF_GROUPS + 1) * MB;
-            row[(size_t)grp * MB + lane] = qf_group_sum(tp, c.def_items[d], grp, col);
+            if (grp < QF_GROUPS) row[(size_t)grp * MB + lane] = qf_group_sum(tp, c.def_items[d], grp, col);
             if (grp == NV - 1) row[(size_t)QF_GROUPS * MB + lane] = (c.def_add[d] && act) ? c.def_add[d][w] : 0.0;
         }
     }
@@ -890,7 +893,10 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
 // latency-bound Metropolis blocks (64 CUs at W = 1024) overlap the HBM-bound
 // pass instead of preceding it.
 template <bool ACCEPT>
-__global__ __launch_bounds__(MH_THREADS, 3) void mh_pass_kernel(DevCfg c, int fast_only, double *hist_row,
+#ifndef CMAMD_TP_OCC
+#define CMAMD_TP_OCC 3
+#endif
+__global__ __launch_bounds__(MH_THREADS, CMAMD_TP_OCC) void mh_pass_kernel(DevCfg c, int fast_only, double *hist_row,
                                                                 double *hist_terms, int nmh, int nmh_pad, TPDev tp,
                                                                 const double *dl, long long ld_field,
                                                                 long long ld_walker)
@@ -980,6 +986,43 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fa
         }
     } else if (lb < nmh) {
         mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, 0, lds, lb, ACCEPT ? &tw : nullptr);
+    }
+}
+
+// The interleaved step launches (pipe_mode 4): the walkers form two halves a
+// step apart, and every launch runs one half's tails (quadratic form from raw
+// sums, lensing chi^2) beside the other half's Metropolis workgroups (accept
+// from the partials the previous launch left, propose) and window pass (raw
+// sums for that half's next tails).  No role waits on another inside the
+// launch: each consumes only what an earlier launch produced, so all of them
+// are resident together from the start.  A step costs two launches.
+struct HalfCfg {
+    int q_tile0;    // first walker tile of this launch's quadratic form
+    int g_blk0;     // first chi^2 workgroup (SMALL_WT walkers each)
+    int m_blk0;     // first Metropolis walker block (MB walkers each)
+    int nmh;        // Metropolis workgroups
+};
+
+template <bool ACCEPT, bool PROPOSE>
+__global__ __launch_bounds__(MH_THREADS, 3) void mh_half_kernel(DevCfg c, int fast_only, double *hist_row,
+                                                                double *hist_terms, StepTail t,
+                                                                const int2 *__restrict__ rows, HalfCfg h)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int2 rr = rows[blockIdx.x >> 3];
+    const int lb = rr.y * 8 + (blockIdx.x & 7);
+    if (rr.x == TAIL_QF) {
+        if (lb >= t.nq) return;
+        int item_ix, tile;
+        qf_place(lb, t.q.src.n_items, t.q.src.xcd_map, item_ix, tile);
+        qfs_body<false>(lds, item_ix, h.q_tile0 + tile, t.q);
+    } else if (rr.x == TAIL_GAUSS) {
+        if (lb < t.ng) small_gauss_body<SMALL_WT, true, false>(t.g, lds, h.g_blk0 + lb);
+    } else if (rr.x == TAIL_PASS) {
+        if (lb < t.np)
+            tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
+    } else if (lb < h.nmh) {
+        mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, h.m_blk0, lds, lb);
     }
 }
 
@@ -2826,10 +2869,12 @@ static bool tail_setup(cmbs *s, int fast_only) {
         s->uni_lds = std::max({s->mh_lds, (size_t)QFS_LDS_DOUBLES * 8, (size_t)tp_vec_lds_bytes<2, false>(),
                                (size_t)small_gauss_lds_doubles<SMALL_WT>(g.d.nX) * 8});
         for (const void *k : {(const void *)mh_step_kernel<false, true>, (const void *)mh_step_kernel<true, true>,
-                              (const void *)mh_step_kernel<true, false>})
+                              (const void *)mh_step_kernel<true, false>, (const void *)mh_half_kernel<false, true>,
+                              (const void *)mh_half_kernel<true, true>, (const void *)mh_half_kernel<true, false>})
             HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->uni_lds));
     }
     for (auto &pl : s->uni_plan) pl.key[0] = -1;
+    for (auto &pl : s->half_plan) pl.key[0] = -1;
     s->tail_ready = s->W;
     return true;
 }
@@ -2959,6 +3004,96 @@ static void launch_unified(cmbs *s, hipStream_t stream, bool propose, int rd, in
     if (accept) s->tail_epoch++;
 }
 
+// Walker halves of the interleaved steps: [0, half_w) and [half_w, W), the
+// same whole number of 64-walker tiles each (so the pass's one unit plan
+// serves both); 0 when W does not split so.
+static int half_w(const cmbs *s) { return (s->W % 128 == 0 && s->W >= 128) ? s->W / 2 : 0; }
+
+// One interleaved launch (pipe_mode 4): half qh's tails (qh < 0: none), half
+// mh's Metropolis workgroups (mh < 0: none; accept: from the partials of the
+// previous launch, propose: the next trial) and half ph's pass (ph < 0: none).
+static void launch_half(cmbs *s, hipStream_t stream, int qh, int mh, bool accept, bool propose, int ph,
+                        const HistRow &row, int fast_only) {
+    const int Wh = half_w(s), th = Wh / QF_TILE, W = s->W;
+    StepTail t;
+    t.W = W;
+    HalfCfg h{};
+    if (qh >= 0) {
+        t = make_tail(s, 0, -1);
+        t.q.src.xcd_map = th % 8 == 0 ? 1 : 0;
+        t.nq = t.q.src.n_items * th;
+        t.ng = (Wh + SMALL_WT - 1) / SMALL_WT;
+        h.q_tile0 = qh * th;
+        h.g_blk0 = qh * (Wh / SMALL_WT);
+    }
+    if (ph >= 0) {
+        TPOut o[2];
+        for (int k = 0; k < 2; k++) {
+            const int i = s->tp_like[k];
+            const WinStage &st = s->tp_stage[k];
+            Like &L = *s->likes[i].like->like;
+            o[k] = TPOut{st.kind, st.cal_index, st.ld, 0, s->tail_S[0][k].as<double>(), st.X, s->dc.like_nuis[i],
+                         (long long)std::max(1, L.n_nuis)};
+        }
+        t.tp = s->tpass->dev_args(o, Wh);   // the plan for one half's tiles
+        t.tp.tile_off = ph * th;
+        const LikeSlot &P = s->likes[s->tp_like[0]];
+        t.dl = P.dl;
+        t.ld_field = P.ld_field;
+        t.ld_walker = P.ld_walker;
+        t.np = s->tpass->n_blocks();
+    }
+    DevCfg dc = s->dc;
+    dc.mask_on = 0;
+    dc.pub_on = 0;
+    dc.n_def = 0;
+    s->pending_def = 0;
+    if (mh >= 0) {
+        h.m_blk0 = mh * (Wh / MB);
+        h.nmh = Wh / MB;
+        if (accept) {   // plik's combine from the partials the previous launch left for this half
+            QFSource src;
+            const int qi = s->tp_like[s->tail_qf];
+            if (!s->likes[qi].like->like->qf_source(src, W, s->like_ws[qi].p))
+                fail(CMBL_ERR_ARG, "internal: interleaved step quadratic form");
+            dc.n_def = 1;
+            dc.def_like[0] = qi;
+            dc.def_items[0] = src.n_items;
+            dc.def_part[0] = src.partial;
+            dc.def_add[0] = nullptr;
+        }
+    }
+    const int v = mh < 0 ? 0 : !accept ? 1 : propose ? 2 : 3;   // kernel variant
+    StepTailPlan &pl = s->half_plan[v];
+    if (pl.key[0] != t.nq || pl.key[1] != t.ng || pl.key[2] != t.np) {
+        // the Metropolis rows first: their chain is the launch's longest; nothing waits, so any order is safe
+        std::vector<int2> rows;
+        for (int k = 0; k < (h.nmh + 7) / 8; k++) rows.push_back(int2{TAIL_MH, k});
+        const std::vector<int2> rest = tail_rows(t.nq, t.ng, t.np, 0);
+        rows.insert(rows.end(), rest.begin(), rest.end());
+        pl.d_rows.alloc(rows.size() * sizeof(int2));
+        pl.d_rows.upload(rows.data(), rows.size() * sizeof(int2));
+        pl.nrows = (int)rows.size();
+        pl.key[0] = t.nq;
+        pl.key[1] = t.ng;
+        pl.key[2] = t.np;
+    }
+    const dim3 grid((unsigned)pl.nrows * 8), b(MH_THREADS);
+    const int2 *rows = pl.d_rows.as<int2>();
+    timed_launch("mh_half_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+        if (v <= 1)
+            hipExtLaunchKernelGGL(mh_half_kernel<false, true>, grid, b, s->uni_lds, stream, e0, e1, 0, dc, fast_only,
+                                  row.p, row.t, t, rows, h);
+        else if (v == 2)
+            hipExtLaunchKernelGGL(mh_half_kernel<true, true>, grid, b, s->uni_lds, stream, e0, e1, 0, dc, fast_only,
+                                  row.p, row.t, t, rows, h);
+        else
+            hipExtLaunchKernelGGL(mh_half_kernel<true, false>, grid, b, s->uni_lds, stream, e0, e1, 0, dc, fast_only,
+                                  row.p, row.t, t, rows, h);
+    });
+    HIP_CHECK(hipGetLastError());
+}
+
 void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (!s->started) fail(CMBL_ERR_ARG, "cmbs_set_start must be called before cmbs_step");
     check_theory_fresh(s);
@@ -2969,6 +3104,22 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     // propose(1) | likes | accept(1)+propose(2) | likes | ... | likes | accept(n)
     const int G = s->n_groups;
     sampler_check_pipe(s);
+    if (G == 1 && s->pipe_mode == 4 && half_w(s) && tail_setup(s, fast_only)) {
+        // interleaved halves A, B: M_A(propose 1) + P_A | Q_A(1) + M_B(propose 1) + P_B |
+        // Q_B(1) + M_A(accept 1, propose 2) + P_A | Q_A(2) + M_B(accept 1, propose 2) + P_B | ... |
+        // Q_B(n) + M_A(accept n) | M_B(accept n); the step-k history row is written by A's
+        // accept and, one launch later, by B's
+        launch_half(s, stream, -1, 0, false, true, 0, HistRow{}, fast_only);
+        HistRow rowB{};
+        for (int k = 1; k <= n_steps; k++) {
+            launch_half(s, stream, 0, 1, k > 1, true, 1, rowB, fast_only);
+            const HistRow rowA = next_hist(s);
+            launch_half(s, stream, 1, 0, true, k < n_steps, k < n_steps ? 0 : -1, rowA, fast_only);
+            rowB = rowA;
+        }
+        launch_half(s, stream, -1, 1, true, false, -1, rowB, fast_only);
+        return;
+    }
     if (G == 1 && s->pipe_mode == 3 && tail_setup(s, fast_only)) {
         // unified: propose(1) + pass(1) | tails(1) + pass(2) + accept(1) + propose(2) | ... |
         // tails(n) + accept(n): one launch per step.  The arrival counters start from 0
@@ -3506,7 +3657,7 @@ extern "C" int cmamd_debug_tp_items(const cmbs *s, int *out, int cap) {   // (fi
     return s->tpass->n_items();
 }
 extern "C" int cmamd_debug_pipeline(cmbs *s, int mode) {   // fast-step schedule (sampler_step): 0 unpipelined,
-    if (!s || mode < 0 || mode > 3) return -1;              // 1 mh_pass_kernel, 2 step tails, 3 unified launches
+    if (!s || mode < 0 || mode > 4) return -1;    // 1 mh_pass_kernel, 2 step tails, 3 unified, 4 interleaved halves
     s->pipe_mode = mode;
     return 0;
 }

@@ -61,6 +61,7 @@ struct TPDev {
     const unsigned char *cmap;        // per item step, [64] slots: the item's column index (255: none)
     int nitem;
     int nblk;             // block table entries (units, including empty ones)
+    int tile_off;         // the units' walker tiles start here (a walker half of the sampler's interleaved steps)
     TPOut out[TP_MAXOUT];
     // pipelined form (tp_vec_body<.., true>, the sampler's mh_pass_kernel):
     // the step's calibrations come from the Metropolis workgroups of the same

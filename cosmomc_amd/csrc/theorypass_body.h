@@ -47,7 +47,12 @@ template <int NB, bool PIPE = false> constexpr int tp_vec_lds_bytes() {
 // the consumers apply the calibrations of the step that reads them with the
 // emit's own operations (X - v / cal^2 in the quadratic form's operand, v /
 // cal^2 in the small chi^2's partial rows), so the results are the same bits.
-template <int NB, bool PIPE, bool RAW = false>
+#ifndef CMAMD_TP_DEPTH
+#define CMAMD_TP_DEPTH 2
+#endif
+// DEPTH: theory steps in flight ahead of the one being multiplied (2: three
+// register buffers; 3: four, for items of three steps or more)
+template <int NB, bool PIPE, bool RAW = false, int DEPTH = CMAMD_TP_DEPTH>
 __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__restrict__ dl, long long ld_field,
                                             long long ld_walker, int W, char *lds, int b)
 {
@@ -73,13 +78,13 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
     const TPItem it = c.items[item];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, kq = lane >> 4;
-    const int w = tile * 64 + wave * 16 + li;
+    const int w = (c.tile_off + tile) * 64 + wave * 16 + li;
     const int wl = min(w, W - 1);
     const double *Df = dl + (long long)wl * ld_walker + (long long)it.field * ld_field;
     const int lcap = ((int)ld_field - 2) & ~1;
     const int ncb = it.nsb;
     const int nstep = it.nst;
-    double tA[LPL], tB[LPL], tC[LPL], a[LPL];
+    double tA[LPL], tB[LPL], tC[LPL], tD[LPL], a[LPL];
     auto load_t = [&](int st, double *dst) {  // raw rows, addresses clamped into the row
         const int lb = it.l0 + st * STEP + 2 * kq;
 #pragma unroll
@@ -125,6 +130,8 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
     // prologue: theory steps 0, 1; weights of step 0 into LDS, of step 1 in registers
     load_t(0, tA);
     load_t(1, tB);                       // nstep >= 2: an item is whole 64-l chunks
+    const bool deep = DEPTH == 3 && nstep >= 3;
+    if (deep) load_t(2, tC);
     fetch_w(0);
     if (tid < it.ncol) {
         const TPCol d = c.cols[it.cdesc + tid];
@@ -223,35 +230,78 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
         __syncthreads();
     };
     int st = 0;
-    while (st + 2 < nstep) {
-        step(st, tA, tC);
-        if (++st + 2 >= nstep) break;
-        step(st, tB, tA);
-        if (++st + 2 >= nstep) break;
-        step(st, tC, tB);
-        ++st;
-    }
-    // the last two steps: nothing more to load
-    auto tail = [&](const double *t0, const double *t1) {
-        fetch_w(st + 1);
-        compute(st, t0, true);
-        store_w((st & 1) ^ 1);
-        __syncthreads();
-        closes(st);
-        compute(st + 1, t1, true);
-        closes(st + 1);
-    };
-    switch (st % 3) {
-        case 0: tail(tA, tB); break;
-        case 1: tail(tB, tC); break;
-        default: tail(tC, tA); break;
+    if (DEPTH == 3 && deep) {
+        // theory of st + 3 in flight; step s in buffer s mod 4 (A, B, C, D)
+        auto step3 = [&](int st, const double *tc, double *tl) {
+            fetch_w(st + 1);
+            load_t(st + 3, tl);
+            compute(st, tc, false);
+            closes(st);
+            store_w((st & 1) ^ 1);
+            __syncthreads();
+        };
+        while (st + 3 < nstep) {
+            step3(st, tA, tD);
+            if (++st + 3 >= nstep) break;
+            step3(st, tB, tA);
+            if (++st + 3 >= nstep) break;
+            step3(st, tC, tB);
+            if (++st + 3 >= nstep) break;
+            step3(st, tD, tC);
+            ++st;
+        }
+        // the last three steps: nothing more to load
+        auto tail3 = [&](const double *t0, const double *t1, const double *t2) {
+            fetch_w(st + 1);
+            compute(st, t0, true);
+            store_w((st & 1) ^ 1);
+            __syncthreads();
+            closes(st);
+            fetch_w(st + 2);
+            compute(st + 1, t1, true);
+            store_w(((st + 1) & 1) ^ 1);
+            __syncthreads();
+            closes(st + 1);
+            compute(st + 2, t2, true);
+            closes(st + 2);
+        };
+        switch (st % 4) {
+            case 0: tail3(tA, tB, tC); break;
+            case 1: tail3(tB, tC, tD); break;
+            case 2: tail3(tC, tD, tA); break;
+            default: tail3(tD, tA, tB); break;
+        }
+    } else {
+        while (st + 2 < nstep) {
+            step(st, tA, tC);
+            if (++st + 2 >= nstep) break;
+            step(st, tB, tA);
+            if (++st + 2 >= nstep) break;
+            step(st, tC, tB);
+            ++st;
+        }
+        // the last two steps: nothing more to load
+        auto tail = [&](const double *t0, const double *t1) {
+            fetch_w(st + 1);
+            compute(st, t0, true);
+            store_w((st & 1) ^ 1);
+            __syncthreads();
+            closes(st);
+            compute(st + 1, t1, true);
+            closes(st + 1);
+        };
+        switch (st % 3) {
+            case 0: tail(tA, tB); break;
+            case 1: tail(tB, tC); break;
+            default: tail(tC, tA); break;
+        }
     }
     if constexpr (PIPE) {
         TP_PIPE_STAMP(1);
         __syncthreads();   // every wave's sums in lsum
         // thread: walker tid % 64 of the tile, columns tid / 64, + 4, ...; it
         // polls its walker's two published calibrations (bounded)
-        const int wl2 = tid & 63, wv = tile * 64 + wl2;
+        const int wl2 = tid & 63, wv = (c.tile_off + tile) * 64 + wl2;
         if (wv < W) {
             double c2p[TP_MAXOUT];
 #pragma unroll

@@ -701,7 +701,11 @@ def test_corun_tails_bitwise(cmbl_golden, refdata, tmp_path, W):
 
 @pytest.mark.parametrize("W", [1, 100, 1024])
 def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
-    """The fast-step schedules give the same bits.  Mode 3 (the unified step
+    """The fast-step schedules give the same bits.  Mode 4 (interleaved
+    halves, W = 1024; smaller W fall back to mode 2): the walkers form two
+    halves a step apart, and each launch runs one half's quadratic form and
+    chi^2 beside the other half's Metropolis workgroups and window pass, none
+    waiting on another (mh_half_kernel).  Mode 3 (the unified step
     launch): one launch per step holds step k's quadratic form and lensing
     chi^2, the pass storing step k + 1's raw sums, and the Metropolis
     workgroups that wait for their tile's tails, accept step k and propose
@@ -729,7 +733,7 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
     calls = (1, 2, 5)
     steps = sum(calls)
     out = []
-    for mode in (3, 2, 1, 0):
+    for mode in (4, 3, 2, 1, 0):
         plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
         lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
         plik.nuisance_indices = [2]
@@ -749,7 +753,7 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
             assert N.lib().cmamd_debug_tail(s._h) == W        # the step tails ran
         out.append((s.history_host(0, steps), s.history_terms(0, steps)))
         assert plik.status() == 0 and lens.status() == 0
-        if mode == 3:
+        if mode == 4:
             po_plik = po.PlikLite(data)
             o_lens = co.CMBLikesOracle(os.path.join(refdata, c["dataset"]), c["overrides"], c["tag"])
             for k in (0, steps - 1):
