@@ -211,25 +211,34 @@ def convergence_run(W, rank, world, tmpdir, seconds, lensing=True):
     return out
 
 
-def kernel_profile(smp, steps):
+KERNELS = ("plik_bin_delta", "plik_quadform_ksplit", "plik_quadform_corun", "mh_kernel", "mh_pass_kernel",
+           "rot_kernel", "cmbl_bk_prologue", "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_hl_kernel",
+           "cmbl_quadform", "cmbl_gauss_small_kernel", "theory_window_kernel", "drag_kernel",
+           "step_tail_kernel", "step_tail_last", "step_tail_pass", "mh_step_first", "mh_step_kernel",
+           "mh_step_last", "mh_half_kernel")
+
+
+def kernel_profile(smp, steps, stepper=None, per_step=False):
     """Average device time (us) per launch of every library kernel over `steps`
-    more fast steps (HIP events on the launch stream)."""
+    more steps (HIP events on the launch stream); per_step: also the total per
+    step of each kernel (its launches per step x its average)."""
     import torch
     from cosmomc_amd import _native as N
-    names = ("plik_bin_delta", "plik_quadform_ksplit", "plik_quadform_corun", "mh_kernel", "mh_pass_kernel",
-             "rot_kernel", "cmbl_bk_prologue", "cmbl_window_kernel", "cmbl_reduce_kernel",
-             "cmbl_hl_kernel", "cmbl_quadform", "cmbl_gauss_small_kernel")
     N.profile_reset()
     N.profile_enable(True)
-    smp.step(steps, fast_only=True)
+    if stepper:
+        stepper(steps)
+    else:
+        smp.step(steps, fast_only=True)
     torch.cuda.synchronize()
     N.profile_enable(False)
-    out = {}
-    for k in names:
+    out, tot = {}, {}
+    for k in KERNELS:
         ms, cnt = N.profile_read(k)
         if cnt:
             out[k] = round(ms / cnt * 1e3, 2)
-    return out
+            tot[k] = round(ms / steps * 1e3, 2)
+    return (out, tot) if per_step else out
 
 
 def drag_run(W, rank, world, tmpdir, seconds, steps=20, dragging_steps=3.0):
@@ -290,6 +299,9 @@ def drag_run(W, rank, world, tmpdir, seconds, steps=20, dragging_steps=3.0):
            "walkers_total": W * world, "drag_steps_per_s": W * world * steps / dt,
            "likelihood_evals_per_s": W * world * steps * evals / dt, "evals_per_drag": evals,
            "ms_per_drag_step": dt / steps * 1e3}
+    avg, tot = kernel_profile(smp, 5, stepper=stepper, per_step=True)
+    out["avg_kernel_us"] = avg
+    out["kernel_us_per_drag_step"] = tot
     if seconds > 0:
         out.update(run_to_convergence(smp, 1, 1, seconds, world, 40000, stepper=stepper))
     return out
@@ -738,12 +750,7 @@ def main():
         smp.step(args.steps, fast_only=True)
         torch.cuda.synchronize()
         N.profile_enable(False)
-        kern = {k: N.profile_read(k) for k in ("theory_window_kernel", "plik_bin_delta", "plik_quadform_ksplit",
-                                                "plik_quadform_corun", "mh_kernel", "mh_pass_kernel",
-                                                "step_tail_kernel", "step_tail_last", "step_tail_pass",
-                                                "mh_step_first", "mh_step_kernel", "mh_step_last", "mh_half_kernel",
-                                                "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_gauss_small_kernel",
-                                                "cmbl_quadform")}
+        kern = {k: N.profile_read(k) for k in KERNELS}
         kern = {k: v for k, v in kern.items() if v[1]}
         _, _, _, nacc = smp.state()
         acc_rate = float(nacc.sum()) / (W * (args.warmup + 2 * args.steps))

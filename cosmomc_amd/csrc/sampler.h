@@ -155,6 +155,7 @@ struct cmbs {
     cmamd::DevBuf ws_g[cmamd::MAXGROUPS];
     // fast dragging (cmbs_step_drag): scratch rows, second likelihood set, end-point theories
     cmamd::DevBuf drag_dd, drag_di, like_terms2;
+    bool drag_hbm = false;                   // debug: drag_kernel on the HBM state (cmamd_debug_drag_hbm)
     cmamd::DevBuf nuis_bufs2[cmamd::MAXLIKE];
     struct EndTheory { double *dl = nullptr; long long ld_field = 0, ld_walker = 0; };
     EndTheory end_theory[cmamd::MAXLIKE];

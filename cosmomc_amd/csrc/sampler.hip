@@ -1502,45 +1502,31 @@ struct DragCfg {
     double *like_nuis2[MAXLIKE];          // [W][nn] DataParams at T2
 };
 
+// One walker's part of a drag stage (TFastDraggingSampler_GetNewSample,
+// MCMC.f90:338-452) on views of its state: in HBM (drag_kernel) or in an LDS
+// image (drag_staged_kernel).  STAGE 0 proposes the slow trial, 1 scores the
+// end point, 2 runs interpolation step g.istep.
+struct DragView {
+    Col<double> T, CE, CS, T2, ET, lk1, lk2;
+    double *cur, *mult, *cel, *csl, *ss, *se;
+    int *nacc, *dst;
+};
+
 template <int STAGE>
-__global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *hist_row, double *hist_terms)
+__device__ __forceinline__ void drag_logic(const DevCfg &c, const DragCfg &g, const Tabs &t, Walker &k,
+                                           const DragView &v, int w, double *hist_row, double *hist_terms)
 {
-    const int w = blockIdx.x * 64 + threadIdx.x;
-    if (w >= c.W) return;
     const size_t ld = c.ld;
-    const Rows &R = c.rows;
     const int np = c.np;
-    auto drow = [&](double *b, int r) { return Col<double>{b + (size_t)r * ld + w, (int)ld}; };
-    auto irow = [&](int *b, int r) { return Col<int>{b + (size_t)r * ld + w, (int)ld}; };
-    const Tabs t = make_tabs(c, c.tab_i, c.tab_d);
-    Walker k;
-    k.r.u = drow(c.sd, R.U);
-    k.r.c = c.sd[(size_t)R.C * ld + w];
-    k.r.gset = c.sd[(size_t)R.G * ld + w];
-    k.r.i97 = c.si[(size_t)R.I97 * ld + w];
-    k.r.j97 = c.si[(size_t)R.J97 * ld + w];
-    k.r.iset = c.si[(size_t)R.ISET * ld + w];
-    k.R = drow(c.sd, R.R);
-    k.P = drow(c.sd, R.P);
-    k.trial = drow(c.sd, R.T);
-    k.vec = drow(g.dd, 3 * np + 4);
-    k.cyc = irow(c.si, R.CYC);
-    k.cyclp = irow(c.si, R.CYCLP);
-    k.blklp = irow(c.si, R.BLKLP);
-    k.itmp = irow(g.di, 1);
-    k.fast_ix = c.si[(size_t)R.FASTIX * ld + w];
-    const Col<double> T = k.trial, CE = drow(g.dd, 0), CS = drow(g.dd, np), T2 = drow(g.dd, 2 * np);
-    double &cur = c.sd[(size_t)R.L * ld + w];
-    double &mult = c.sd[(size_t)R.M * ld + w];
-    int &nacc = c.si[(size_t)R.NACC * ld + w];
-    double &cel = g.dd[(size_t)(3 * np + 0) * ld + w];
-    double &csl = g.dd[(size_t)(3 * np + 1) * ld + w];
-    double &ss = g.dd[(size_t)(3 * np + 2) * ld + w];
-    double &se = g.dd[(size_t)(3 * np + 3) * ld + w];
-    int &dst = g.di[w];
-    const Col<double> lk1{const_cast<double *>(c.like_terms) + w, (int)ld};
-    const Col<double> lk2{const_cast<double *>(g.like_terms2) + w, (int)ld};
-    const Col<double> ET = drow(g.dd, 3 * np + 4 + c.max_blk);   // terms at CE
+    const Col<double> T = v.T, CE = v.CE, CS = v.CS, T2 = v.T2, ET = v.ET, lk1 = v.lk1, lk2 = v.lk2;
+    double &cur = *v.cur;
+    double &mult = *v.mult;
+    int &nacc = *v.nacc;
+    double &cel = *v.cel;
+    double &csl = *v.csl;
+    double &ss = *v.ss;
+    double &se = *v.se;
+    int &dst = *v.dst;
     auto keep_end_terms = [&]() {
         for (int l = 0; l < c.n_like; l++) ET[l] = lk1[l];
     };
@@ -1656,12 +1642,167 @@ __global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *h
                 for (int l = 0; l < c.n_like; l++) hist_terms[(size_t)l * c.W + w] = c.cur_terms[(size_t)l * ld + w];
         }
     }
+}
+
+template <int STAGE>
+__global__ __launch_bounds__(64) void drag_kernel(DevCfg c, DragCfg g, double *hist_row, double *hist_terms)
+{
+    const int w = blockIdx.x * 64 + threadIdx.x;
+    if (w >= c.W) return;
+    const size_t ld = c.ld;
+    const Rows &R = c.rows;
+    const int np = c.np;
+    auto drow = [&](double *b, int r) { return Col<double>{b + (size_t)r * ld + w, (int)ld}; };
+    auto irow = [&](int *b, int r) { return Col<int>{b + (size_t)r * ld + w, (int)ld}; };
+    const Tabs t = make_tabs(c, c.tab_i, c.tab_d);
+    Walker k;
+    k.r.u = drow(c.sd, R.U);
+    k.r.c = c.sd[(size_t)R.C * ld + w];
+    k.r.gset = c.sd[(size_t)R.G * ld + w];
+    k.r.i97 = c.si[(size_t)R.I97 * ld + w];
+    k.r.j97 = c.si[(size_t)R.J97 * ld + w];
+    k.r.iset = c.si[(size_t)R.ISET * ld + w];
+    k.R = drow(c.sd, R.R);
+    k.P = drow(c.sd, R.P);
+    k.trial = drow(c.sd, R.T);
+    k.vec = drow(g.dd, 3 * np + 4);
+    k.cyc = irow(c.si, R.CYC);
+    k.cyclp = irow(c.si, R.CYCLP);
+    k.blklp = irow(c.si, R.BLKLP);
+    k.itmp = irow(g.di, 1);
+    k.fast_ix = c.si[(size_t)R.FASTIX * ld + w];
+    DragView v;
+    v.T = k.trial;
+    v.CE = drow(g.dd, 0);
+    v.CS = drow(g.dd, np);
+    v.T2 = drow(g.dd, 2 * np);
+    v.ET = drow(g.dd, 3 * np + 4 + c.max_blk);   // terms at CE
+    v.lk1 = Col<double>{const_cast<double *>(c.like_terms) + w, (int)ld};
+    v.lk2 = Col<double>{const_cast<double *>(g.like_terms2) + w, (int)ld};
+    v.cur = c.sd + (size_t)R.L * ld + w;
+    v.mult = c.sd + (size_t)R.M * ld + w;
+    v.nacc = c.si + (size_t)R.NACC * ld + w;
+    v.cel = g.dd + (size_t)(3 * np + 0) * ld + w;
+    v.csl = g.dd + (size_t)(3 * np + 1) * ld + w;
+    v.ss = g.dd + (size_t)(3 * np + 2) * ld + w;
+    v.se = g.dd + (size_t)(3 * np + 3) * ld + w;
+    v.dst = g.di + w;
+    drag_logic<STAGE>(c, g, t, k, v, w, hist_row, hist_terms);
     c.sd[(size_t)R.C * ld + w] = k.r.c;
     c.sd[(size_t)R.G * ld + w] = k.r.gset;
     c.si[(size_t)R.I97 * ld + w] = k.r.i97;
     c.si[(size_t)R.J97 * ld + w] = k.r.j97;
     c.si[(size_t)R.ISET * ld + w] = k.r.iset;
     c.si[(size_t)R.FASTIX * ld + w] = k.fast_ix;
+}
+
+// The same stage on an LDS image of MB walkers' state (mh_kernel's staging:
+// the sampler rows, the drag rows, both likelihood-term sets and the tables by
+// LDS-DMA, one wait), so the chain's dependent reads are LDS round trips
+// instead of HBM ones; then the image is written back.  Used when the image
+// fits (drag_lds_bytes).
+__host__ __device__ inline int drag_rows(const DevCfg &c) { return 3 * c.np + 4 + c.max_blk + c.n_like; }
+
+template <int STAGE>
+__global__ __launch_bounds__(MH_THREADS) void drag_staged_kernel(DevCfg c, DragCfg g, double *hist_row,
+                                                                 double *hist_terms)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const Rows &R = c.rows;
+    const int lane = threadIdx.x % MB;
+    const int wl64 = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = MH_THREADS / 64;
+    const int wb = blockIdx.x * MB;
+    const int w = wb + lane;
+    const size_t W = c.ld;
+    const int np = c.np;
+    const int nlk = (c.n_like + 1) & ~1;            // LDS rows (even); nl, nr of them are moved
+    const int nl = c.n_like;
+    const int nr = drag_rows(c);
+    const int ndd = (nr + 1) & ~1;
+    const int nd_st = c.stage_R ? R.ND : R.ND - R.RR;
+    const int ni_st = c.stage_cyc ? R.NI : R.CYC;
+    const int ntd = c.stage_cov ? c.tl.n_dbl : c.tl.covinv;
+    const bool skipR = !c.stage_R;
+    double *sd = lds;                                        // [nd_st][MB]
+    double *dd = sd + (size_t)nd_st * MB;                    // [ndd][MB] drag rows
+    double *l1 = dd + (size_t)ndd * MB;                      // [nlk][MB] terms at T
+    double *l2 = l1 + (size_t)nlk * MB;                      // [nlk][MB] terms at T2
+    double *td = l2 + (size_t)nlk * MB;                      // [ntd rounded to 32]
+    int *si = reinterpret_cast<int *>(td + ((ntd + 31) & ~31));   // [ni_st][MB]
+    int *dst_l = si + (size_t)ni_st * MB;                    // [4][MB] dst (row 0)
+    int *it = dst_l + 4 * MB;                                // [all_n][MB] RandIndices scratch
+    int *ti = it + (size_t)c.all_n * MB;                     // [n_int rounded to 64]
+#define SROW(r) ((skipR && (r) >= R.R) ? (r) - R.RR : (r))
+    const int rEnd = R.R + R.RR;
+    if (skipR) {
+        dma_rows_f64(sd, 0, c.sd, 0, R.R, W, wb, wl64, wave, nwave);
+        dma_rows_f64(sd, R.R, c.sd, rEnd, R.ND - rEnd, W, wb, wl64, wave, nwave);
+    } else {
+        dma_rows_f64(sd, 0, c.sd, 0, R.ND, W, wb, wl64, wave, nwave);
+    }
+    dma_rows_f64(dd, 0, g.dd, 0, nr, W, wb, wl64, wave, nwave);
+    dma_rows_f64(l1, 0, c.like_terms, 0, nl, W, wb, wl64, wave, nwave);
+    dma_rows_f64(l2, 0, g.like_terms2, 0, nl, W, wb, wl64, wave, nwave);
+    dma_rows_i32(si, c.si, ni_st, W, wb, wl64, wave, nwave);
+    dma_rows_i32(dst_l, g.di, 1, W, wb, wl64, wave, nwave);
+    dma_words(td, c.tab_d, 2 * ntd, wl64, wave, nwave);
+    dma_words(ti, c.tab_i, c.tl.n_int, wl64, wave, nwave);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < MB && w < c.W) {
+        const Tabs t = make_tabs(c, ti, td, c.stage_cov ? td : c.tab_d);
+        auto lrow = [&](double *b, int r) { return Col<double>{b + (size_t)r * MB + lane, MB}; };
+        Walker k;
+        k.r.u = lrow(sd, R.U);
+        k.r.c = sd[(size_t)R.C * MB + lane];
+        k.r.gset = sd[(size_t)R.G * MB + lane];
+        k.r.i97 = si[(size_t)R.I97 * MB + lane];
+        k.r.j97 = si[(size_t)R.J97 * MB + lane];
+        k.r.iset = si[(size_t)R.ISET * MB + lane];
+        k.R = c.stage_R ? lrow(sd, R.R) : Col<double>{c.sd + (size_t)R.R * W + w, c.ld};
+        k.P = lrow(sd, SROW(R.P));
+        k.trial = lrow(sd, SROW(R.T));
+        k.vec = lrow(dd, 3 * np + 4);
+        k.cyc = c.stage_cyc ? Col<int>{si + (size_t)R.CYC * MB + lane, MB} : Col<int>{c.si + (size_t)R.CYC * W + w, c.ld};
+        k.cyclp = Col<int>{si + (size_t)R.CYCLP * MB + lane, MB};
+        k.blklp = Col<int>{si + (size_t)R.BLKLP * MB + lane, MB};
+        k.itmp = Col<int>{it + lane, MB};
+        k.fast_ix = si[(size_t)R.FASTIX * MB + lane];
+        DragView v;
+        v.T = k.trial;
+        v.CE = lrow(dd, 0);
+        v.CS = lrow(dd, np);
+        v.T2 = lrow(dd, 2 * np);
+        v.ET = lrow(dd, 3 * np + 4 + c.max_blk);
+        v.lk1 = lrow(l1, 0);
+        v.lk2 = lrow(l2, 0);
+        v.cur = sd + (size_t)SROW(R.L) * MB + lane;
+        v.mult = sd + (size_t)SROW(R.M) * MB + lane;
+        v.nacc = si + (size_t)R.NACC * MB + lane;
+        v.cel = dd + (size_t)(3 * np + 0) * MB + lane;
+        v.csl = dd + (size_t)(3 * np + 1) * MB + lane;
+        v.ss = dd + (size_t)(3 * np + 2) * MB + lane;
+        v.se = dd + (size_t)(3 * np + 3) * MB + lane;
+        v.dst = dst_l + lane;
+        drag_logic<STAGE>(c, g, t, k, v, w, hist_row, hist_terms);
+        sd[(size_t)R.C * MB + lane] = k.r.c;
+        sd[(size_t)R.G * MB + lane] = k.r.gset;
+        si[(size_t)R.I97 * MB + lane] = k.r.i97;
+        si[(size_t)R.J97 * MB + lane] = k.r.j97;
+        si[(size_t)R.ISET * MB + lane] = k.r.iset;
+        si[(size_t)R.FASTIX * MB + lane] = k.fast_ix;
+    }
+    __syncthreads();
+    if (skipR) {
+        stage_out(c.sd, sd, 0, 0, R.R, W, wb);
+        stage_out(c.sd, sd, R.R, rEnd, R.ND, W, wb);
+    } else {
+        stage_out(c.sd, sd, 0, 0, R.ND, W, wb);
+    }
+    stage_out(g.dd, dd, 0, 0, nr, W, wb);
+    stage_out(c.si, si, 0, 0, ni_st, W, wb);
+    stage_out(g.di, dst_l, 0, 0, 1, W, wb);
+#undef SROW
 }
 
 // accepted moves: the trial (end) slow point's theory becomes the walker's theory
@@ -3235,6 +3376,32 @@ static void eval_likes_drag(cmbs *s, int set, hipStream_t stream) {
     }
 }
 
+// drag_staged_kernel's LDS image (0 when it would not fit a CU's 160 KB)
+static size_t drag_lds_bytes(const cmbs *s) {
+    const DevCfg &d = s->dc;
+    const int nd_st = d.stage_R ? d.rows.ND : d.rows.ND - d.rows.RR;
+    const int ni_st = d.stage_cyc ? d.rows.NI : d.rows.CYC;
+    const int ntd = d.stage_cov ? d.tl.n_dbl : d.tl.covinv;
+    const int nlk = (d.n_like + 1) & ~1, ndd = (drag_rows(d) + 1) & ~1;
+    const size_t b = (size_t)(nd_st + ndd + 2 * nlk) * MB * 8 + (size_t)((ntd + 31) & ~31) * 8 +
+                     (size_t)(ni_st + 4 + d.all_n) * MB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4;
+    return b <= 160 * 1024 ? b : 0;
+}
+
+template <int STAGE>
+static void launch_drag(cmbs *s, const DragCfg &g, const HistRow &row, hipStream_t stream) {
+    const size_t lds = drag_lds_bytes(s);
+    timed_launch("drag_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+        if (lds && !s->drag_hbm)
+            hipExtLaunchKernelGGL(drag_staged_kernel<STAGE>, dim3((s->W + MB - 1) / MB), dim3(MH_THREADS), lds, stream,
+                                  e0, e1, 0, s->dc, g, row.p, row.t);
+        else
+            hipExtLaunchKernelGGL(drag_kernel<STAGE>, dim3((s->W + 63) / 64), dim3(64), 0, stream, e0, e1, 0, s->dc,
+                                  g, row.p, row.t);
+    });
+    HIP_CHECK(hipGetLastError());
+}
+
 void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_fn fn, void *user,
                        hipStream_t stream) {
     rot_schedule_unknown(s);           // the drag proposals move the blocks' loop indices
@@ -3269,7 +3436,10 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
     int interp = (int)std::lround(dragging_steps * s->fast_n) + 1;   // MCMC.f90:386
     if (interp < 2) interp = 2;
     g.interp = interp;
-    const dim3 grid((s->W + 63) / 64), blk(64);
+    if (const size_t lds = drag_lds_bytes(s))
+        for (const void *k : {(const void *)drag_staged_kernel<0>, (const void *)drag_staged_kernel<1>,
+                              (const void *)drag_staged_kernel<2>})
+            HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     for (int step = 0; step < n_steps; step++) {
         s->num_drag++;
         if (s->num_drag % s->dc.oversample_fast != 0) {   // FastParameterSample (:357-361)
@@ -3281,19 +3451,13 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
             continue;
         }
         g.istep = 0;
-        timed_launch("drag_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(drag_kernel<0>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, (double *)nullptr, (double *)nullptr);
-        });
-        HIP_CHECK(hipGetLastError());
+        launch_drag<0>(s, g, HistRow{}, stream);
         if (nl > 0) {
             const double *Pend = s->dc.sd + (size_t)s->dc.rows.T * ld;
             if (fn(user, s->W, Pend, (long long)ld, stream) != 0) fail(CMBL_ERR_ARG, "theory function failed");
             eval_likes_drag(s, 1, stream);
         }
-        timed_launch("drag_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(drag_kernel<1>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, (double *)nullptr, (double *)nullptr);
-        });
-        HIP_CHECK(hipGetLastError());
+        launch_drag<1>(s, g, HistRow{}, stream);
         for (int is = 1; is <= interp - 1; is++) {
             if (nl > 0) {
                 eval_likes_drag(s, 1, stream);
@@ -3301,10 +3465,7 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
             }
             g.istep = is;
             const HistRow row = is == interp - 1 ? next_hist(s) : HistRow{};
-            timed_launch("drag_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                hipExtLaunchKernelGGL(drag_kernel<2>, grid, blk, 0, stream, e0, e1, 0, s->dc, g, row.p, row.t);
-            });
-            HIP_CHECK(hipGetLastError());
+            launch_drag<2>(s, g, row, stream);
         }
         s->theory_moved = s->theory_moved || nl > 0;
         for (int i = 0; i < nl; i++) {               // accepted drags keep the end theory
@@ -3669,6 +3830,11 @@ extern "C" int cmamd_debug_corun(cmbs *s, int on) {     // the lensing chi^2 ins
 extern "C" int cmamd_debug_tail_nosignal(cmbs *s, int on) {   // the unified launch's producers never arrive
     if (!s) return -1;
     s->tail_nosignal = on;
+    return 0;
+}
+extern "C" int cmamd_debug_drag_hbm(cmbs *s, int on) {   // the drag stages on the HBM state (no LDS image)
+    if (!s) return -1;
+    s->drag_hbm = on != 0;
     return 0;
 }
 extern "C" int cmamd_debug_tail(const cmbs *s) { return s ? s->tail_ready : 0; }   // W of the step tails' set-up

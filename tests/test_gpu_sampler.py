@@ -857,6 +857,50 @@ def test_dragging_fused_plik_lensing(cmbl_golden, refdata, tmp_path):
         assert lk[w] == pytest.approx(ref, rel=1e-12)
 
 
+@pytest.mark.parametrize("W", [130, 1024])
+def test_drag_staged_matches_hbm(cmbl_golden, refdata, tmp_path, W):
+    """The drag stages on an LDS image of the walkers' state (drag_staged_kernel,
+    the default) and on the HBM state (drag_kernel) give the same chains bit
+    for bit: history rows, terms and the final state."""
+    import os
+
+    from cosmomc_amd import _native as N
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    c = cmbl_golden["cases"]["lensing_consext8"]
+    data = syn.make_plik_lite(12345)
+    base = torch.tensor(syn.walker_theory(1, seed=4, n_fields=10, ld_field=2512), device="cuda")[0]
+    out = []
+    for hbm in (0, 1):
+        plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+        lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
+        plik.nuisance_indices = [2]
+        lens.nuisance_indices = [2]
+        theory = base.unsqueeze(0).repeat(W, 1, 1).contiguous()
+        end = torch.empty_like(theory)
+        s = BatchedMCMC(W, 2, [1, 2], [[1], [2]], 1, np.array([0.95, 0.9]), np.array([1.05, 1.1]),
+                        np.array([0.0, 1.0]), np.array([0.0, 0.0025]), propose_scale=2.4, seed_ij=95, seed_kl=96)
+        s.set_covariance(np.diag([0.002 ** 2, 0.0025 ** 2]))
+        s.add_likelihood(plik, theory)
+        s.add_likelihood(lens, theory)
+        assert N.lib().cmamd_debug_drag_hbm(s._h, hbm) == 0
+        s.set_drag_theory(0, end)
+        s.set_drag_theory(1, end)
+        s.set_start(np.tile([1.0, 1.0], (W, 1)))
+        s.enable_history(64)
+
+        def theory_fn(P_end):
+            torch.mul(base.unsqueeze(0), P_end[0].reshape(-1, 1, 1), out=end)
+        s.step_drag(10, theory_fn=theory_fn)
+        n = s.history_count()
+        out.append((s.history_host(0, n), s.history_terms(0, n), *s.state()))
+        s.close()
+    a, b = out
+    assert np.any(a[5] > 0), "no drag was accepted"
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
 @pytest.mark.parametrize("blocks,W,groups", [([21], 512, 1), ([12, 9], 576, 1), ([32], 200, 1), ([8, 13], 320, 2)])
 def test_parallel_rotations_match_serial(blocks, W, groups):
     """rot_kernel's parallel rotation (64-lane RANMAR rounds, ballot-placed
