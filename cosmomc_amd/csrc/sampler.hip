@@ -889,9 +889,16 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
 // multiple of 8 idle so the pass's blocks keep their XCDs), the rest run the
 // pass (tp_vec_body<2, true>), which needs the new trial calibrations only for
 // its last phase and waits for its tile's Metropolis workgroups there.  Those
-// are dispatched first and wait on nothing, so the wait always ends.  The
-// latency-bound Metropolis blocks (64 CUs at W = 1024) overlap the HBM-bound
-// pass instead of preceding it.
+// wait on nothing and have the lowest workgroup ids.  The HIP model does not
+// promise that workgroups are dispatched in id order (cdna_hip_programming.md
+// "Workgroups, grid, and XCD partitioning"); the hardware's dispatcher is
+// observed to, so the Metropolis workgroups are resident before any waiting
+// pass workgroup takes a slot and the wait ends.  The design does not rely on
+// it for correctness: the wait is bounded, and a give-up sets
+// CMBL_STATUS_PIPE_WAIT in the sampler's status word, which the next step
+// call or state readback turns into an error (sampler_check_pipe) instead of
+// silently rejected trials.  The latency-bound Metropolis blocks (64 CUs at
+// W = 1024) overlap the HBM-bound pass instead of preceding it.
 template <bool ACCEPT>
 #ifndef CMAMD_TP_OCC
 #define CMAMD_TP_OCC 3
@@ -2875,7 +2882,7 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
     dc.pub_on = 0;
     if (pipe) {   // mh_pass_kernel: this launch proposes the step whose pass rides along
         if (!propose || g0 != 0 || g1 != s->W || rot) fail(CMBL_ERR_ARG, "internal: pipelined step launch");
-        dc.pub_on = 1;
+        dc.pub_on = s->tail_nosignal ? 0 : 1;   // debug: never publish (the give-up test)
         for (int k = 0; k < 2; k++) {
             const WinStage &st = s->tp_stage[k];
             dc.pub_pcal[k] = st.cal_index >= 0 ? s->likes[s->tp_like[k]].nidx[st.cal_index] : -1;
@@ -3827,7 +3834,7 @@ extern "C" int cmamd_debug_corun(cmbs *s, int on) {     // the lensing chi^2 ins
     s->no_corun = !on;
     return 0;
 }
-extern "C" int cmamd_debug_tail_nosignal(cmbs *s, int on) {   // the unified launch's producers never arrive
+extern "C" int cmamd_debug_tail_nosignal(cmbs *s, int on) {   // in-launch producers never arrive / publish (modes 1, 3)
     if (!s) return -1;
     s->tail_nosignal = on;
     return 0;

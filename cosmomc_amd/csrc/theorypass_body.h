@@ -17,6 +17,14 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 #define TP_PIPE_STAMP(i) ((void)0)
 #endif
 
+// The outputs' stores: non-temporal (CMAMD_NT_STORES: streamed to memory as
+// they are made, no dirty L2 lines left for the kernel-end write-back) or plain
+#ifdef CMAMD_NT_STORES
+#define TP_STORE(p, v) __builtin_nontemporal_store((v), (p))
+#else
+#define TP_STORE(p, v) (*(p) = (v))
+#endif
+
 // PIPE adds the unit's column sums, [TP_MAXCOL][64 walkers]
 template <int NB, bool PIPE = false> constexpr int tp_vec_lds_bytes() {
     return 2 * NB * 16 * (32 + 2) * 8 + TP_MAXCOL * (int)sizeof(TPCol) + TP_MAXCOL * 8 + TP_MAXSTEP * 8 +
@@ -187,9 +195,9 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
             } else if (on[r] && w < W) {
                 double *out = o1 ? c.out[1].out : c.out[0].out;
                 if ((o1 ? c.out[1].kind : c.out[0].kind) == 0)
-                    out[(long long)d[r].row * W + w] = q;
+                    TP_STORE(out + (long long)d[r].row * W + w, q);
                 else
-                    out[(long long)w * (o1 ? c.out[1].ld : c.out[0].ld) + d[r].row] = RAW ? v : x[r] - q;
+                    TP_STORE(out + (long long)w * (o1 ? c.out[1].ld : c.out[0].ld) + d[r].row, RAW ? v : x[r] - q);
             }
         }
     };
@@ -325,9 +333,9 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
                 const double q = d.cal ? v / (o1 ? c2p[1] : c2p[0]) : v;
                 double *out = o1 ? c.out[1].out : c.out[0].out;
                 if ((o1 ? c.out[1].kind : c.out[0].kind) == 0)
-                    out[(long long)d.row * W + wv] = q;
+                    TP_STORE(out + (long long)d.row * W + wv, q);
                 else
-                    out[(long long)wv * (o1 ? c.out[1].ld : c.out[0].ld) + d.row] = xsh[col] - q;
+                    TP_STORE(out + (long long)wv * (o1 ? c.out[1].ld : c.out[0].ld) + d.row, xsh[col] - q);
             }
         }
     }

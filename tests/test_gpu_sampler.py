@@ -770,13 +770,15 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
         assert np.array_equal(out[0][1], o[1])
 
 
-@pytest.mark.parametrize("mode", [3])
+@pytest.mark.parametrize("mode", [3, 1])
 def test_pipelined_handoff_giveup_fails_loudly(cmbl_golden, refdata, tmp_path, mode):
-    """The unified step launch's Metropolis workgroups wait in-launch for
-    their tile's tails; a debug switch stops the tails from arriving, so every
-    wait gives up after its 50 ms bound and sets CMBL_STATUS_PIPE_WAIT.  The
-    next readback (and the next step call) must fail instead of handing back
-    silently rejected trials."""
+    """In-launch hand-offs fail loudly.  Mode 3: the unified step launch's
+    Metropolis workgroups wait for their tile's tails; mode 1: mh_pass_kernel's
+    pass workgroups wait for the calibrations the Metropolis workgroups
+    publish.  A debug switch stops the producers (no arrivals / no
+    publication), so every wait gives up at its bound and sets
+    CMBL_STATUS_PIPE_WAIT; the next readback (and the next step call) must fail
+    instead of handing back silently rejected trials."""
     import os
 
     from cosmomc_amd import _native as N
