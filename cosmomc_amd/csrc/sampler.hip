@@ -776,10 +776,7 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
         }
         STAMP(11);
         si[(size_t)R.ACCF * MB + lane] = acc ? 1 : 0;
-        if (hist_row) {
-            for (int i = 0; i < c.n_used; i++) hist_row[(size_t)i * c.W + w] = k.P[t.params_used[i]];
-            hist_row[(size_t)c.n_used * c.W + w] = cur;
-        }
+        if (hist_row) hist_row[(size_t)c.n_used * c.W + w] = cur;   // the parameters: every group, below
         if (hist_terms) {
 #pragma unroll
             for (int l = 0; l < MAXLIKE; l++)
@@ -851,6 +848,11 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     }
     __syncthreads();
     STAMP(13);
+    if (ACCEPT && hist_row && act) {   // the history row's parameters (P is final), rows spread over the groups
+        const int *pu = ti + c.tl.params_used;
+        for (int i = grp; i < c.n_used; i += NV)
+            hist_row[(size_t)i * c.W + w] = sd[(size_t)(SROW(R.P) + pu[i]) * MB + lane];
+    }
     if (PROPOSE && c.pub_on && threadIdx.x < MB && act)   // the fused pass in this launch polls for these
         for (int k = 0; k < 2; k++) {
             const int pc = c.pub_pcal[k];

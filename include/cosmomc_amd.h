@@ -197,7 +197,10 @@ int  cmbs_set_start(cmbs_t *s, const double *P0, void *stream);
 /* n_steps Metropolis steps for every walker.  fast_only != 0:
  * FastParameterSample (MCMC.f90:309-335, GetProposalFast) every step;
  * otherwise TMetropolisSampler_GetNewSample (MCMC.f90:269-307, GetProposal).
- * Asynchronous on stream. */
+ * Asynchronous on stream.  The pipelined fast-step schedules hand data from
+ * one workgroup to another inside a launch with bounded waits; a wait that
+ * gives up marks the call's steps invalid, and the next cmbs_step or state /
+ * history readback returns CMBL_ERR_NUMERIC ("... gave up waiting ..."). */
 int  cmbs_step(cmbs_t *s, int n_steps, int fast_only, void *stream);
 
 /* Fast dragging, TFastDraggingSampler_GetNewSample (MCMC.f90:338-452;
