@@ -3846,5 +3846,12 @@ extern "C" int cmamd_debug_drag_hbm(cmbs *s, int on) {   // the drag stages on t
     s->drag_hbm = on != 0;
     return 0;
 }
+extern "C" int cmamd_debug_pipe_status(cmbs *s) {   // the device give-up word (synchronises the device)
+    if (!s || !s->pipe_status.p) return -1;
+    int v = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&v, s->pipe_status.p, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return -2;
+    return v;
+}
 extern "C" int cmamd_debug_tail(const cmbs *s) { return s ? s->tail_ready : 0; }   // W of the step tails' set-up
 extern "C" int cmamd_debug_fused(const cmbs *s) { return !s ? 0 : s->tpass ? s->tpass->n_items() : -s->tp_why; }
