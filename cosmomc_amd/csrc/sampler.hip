@@ -902,10 +902,7 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
 // silently rejected trials.  The latency-bound Metropolis blocks (64 CUs at
 // W = 1024) overlap the HBM-bound pass instead of preceding it.
 template <bool ACCEPT>
-#ifndef CMAMD_TP_OCC
-#define CMAMD_TP_OCC 3
-#endif
-__global__ __launch_bounds__(MH_THREADS, CMAMD_TP_OCC) void mh_pass_kernel(DevCfg c, int fast_only, double *hist_row,
+__global__ __launch_bounds__(MH_THREADS, 3) void mh_pass_kernel(DevCfg c, int fast_only, double *hist_row,
                                                                 double *hist_terms, int nmh, int nmh_pad, TPDev tp,
                                                                 const double *dl, long long ld_field,
                                                                 long long ld_walker)

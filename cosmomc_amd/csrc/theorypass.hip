@@ -258,10 +258,7 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_kernel(TPD
 
 // The vectorised pass (theorypass_body.h) as a kernel of its own
 template <int NB>
-#ifndef CMAMD_TP_OCC
-#define CMAMD_TP_OCC 3
-#endif
-__global__ __launch_bounds__(256, NB <= 2 ? CMAMD_TP_OCC : 2) void theory_window_vec(TPDev c, const double *__restrict__ dl,
+__global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev c, const double *__restrict__ dl,
                                                                          long long ld_field, long long ld_walker, int W)
 {
     __shared__ __attribute__((aligned(16))) char lds[tp_vec_lds_bytes<NB>()];

@@ -17,14 +17,6 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 #define TP_PIPE_STAMP(i) ((void)0)
 #endif
 
-// The outputs' stores: non-temporal (CMAMD_NT_STORES: streamed to memory as
-// they are made, no dirty L2 lines left for the kernel-end write-back) or plain
-#ifdef CMAMD_NT_STORES
-#define TP_STORE(p, v) __builtin_nontemporal_store((v), (p))
-#else
-#define TP_STORE(p, v) (*(p) = (v))
-#endif
-
 // PIPE adds the unit's column sums, [TP_MAXCOL][64 walkers]
 template <int NB, bool PIPE = false> constexpr int tp_vec_lds_bytes() {
     return 2 * NB * 16 * (32 + 2) * 8 + TP_MAXCOL * (int)sizeof(TPCol) + TP_MAXCOL * 8 + TP_MAXSTEP * 8 +
@@ -55,12 +47,7 @@ template <int NB, bool PIPE = false> constexpr int tp_vec_lds_bytes() {
 // the consumers apply the calibrations of the step that reads them with the
 // emit's own operations (X - v / cal^2 in the quadratic form's operand, v /
 // cal^2 in the small chi^2's partial rows), so the results are the same bits.
-#ifndef CMAMD_TP_DEPTH
-#define CMAMD_TP_DEPTH 2
-#endif
-// DEPTH: theory steps in flight ahead of the one being multiplied (2: three
-// register buffers; 3: four, for items of three steps or more)
-template <int NB, bool PIPE, bool RAW = false, int DEPTH = CMAMD_TP_DEPTH>
+template <int NB, bool PIPE, bool RAW = false>
 __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__restrict__ dl, long long ld_field,
                                             long long ld_walker, int W, char *lds, int b)
 {
@@ -92,7 +79,7 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
     const int lcap = ((int)ld_field - 2) & ~1;
     const int ncb = it.nsb;
     const int nstep = it.nst;
-    double tA[LPL], tB[LPL], tC[LPL], tD[LPL], a[LPL];
+    double tA[LPL], tB[LPL], tC[LPL], a[LPL];
     auto load_t = [&](int st, double *dst) {  // raw rows, addresses clamped into the row
         const int lb = it.l0 + st * STEP + 2 * kq;
 #pragma unroll
@@ -138,8 +125,6 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
     // prologue: theory steps 0, 1; weights of step 0 into LDS, of step 1 in registers
     load_t(0, tA);
     load_t(1, tB);                       // nstep >= 2: an item is whole 64-l chunks
-    const bool deep = DEPTH == 3 && nstep >= 3;
-    if (deep) load_t(2, tC);
     fetch_w(0);
     if (tid < it.ncol) {
         const TPCol d = c.cols[it.cdesc + tid];
@@ -195,9 +180,9 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
             } else if (on[r] && w < W) {
                 double *out = o1 ? c.out[1].out : c.out[0].out;
                 if ((o1 ? c.out[1].kind : c.out[0].kind) == 0)
-                    TP_STORE(out + (long long)d[r].row * W + w, q);
+                    out[(long long)d[r].row * W + w] = q;
                 else
-                    TP_STORE(out + (long long)w * (o1 ? c.out[1].ld : c.out[0].ld) + d[r].row, RAW ? v : x[r] - q);
+                    out[(long long)w * (o1 ? c.out[1].ld : c.out[0].ld) + d[r].row] = RAW ? v : x[r] - q;
             }
         }
     };
@@ -238,71 +223,28 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
         __syncthreads();
     };
     int st = 0;
-    if (DEPTH == 3 && deep) {
-        // theory of st + 3 in flight; step s in buffer s mod 4 (A, B, C, D)
-        auto step3 = [&](int st, const double *tc, double *tl) {
-            fetch_w(st + 1);
-            load_t(st + 3, tl);
-            compute(st, tc, false);
-            closes(st);
-            store_w((st & 1) ^ 1);
-            __syncthreads();
-        };
-        while (st + 3 < nstep) {
-            step3(st, tA, tD);
-            if (++st + 3 >= nstep) break;
-            step3(st, tB, tA);
-            if (++st + 3 >= nstep) break;
-            step3(st, tC, tB);
-            if (++st + 3 >= nstep) break;
-            step3(st, tD, tC);
-            ++st;
-        }
-        // the last three steps: nothing more to load
-        auto tail3 = [&](const double *t0, const double *t1, const double *t2) {
-            fetch_w(st + 1);
-            compute(st, t0, true);
-            store_w((st & 1) ^ 1);
-            __syncthreads();
-            closes(st);
-            fetch_w(st + 2);
-            compute(st + 1, t1, true);
-            store_w(((st + 1) & 1) ^ 1);
-            __syncthreads();
-            closes(st + 1);
-            compute(st + 2, t2, true);
-            closes(st + 2);
-        };
-        switch (st % 4) {
-            case 0: tail3(tA, tB, tC); break;
-            case 1: tail3(tB, tC, tD); break;
-            case 2: tail3(tC, tD, tA); break;
-            default: tail3(tD, tA, tB); break;
-        }
-    } else {
-        while (st + 2 < nstep) {
-            step(st, tA, tC);
-            if (++st + 2 >= nstep) break;
-            step(st, tB, tA);
-            if (++st + 2 >= nstep) break;
-            step(st, tC, tB);
-            ++st;
-        }
-        // the last two steps: nothing more to load
-        auto tail = [&](const double *t0, const double *t1) {
-            fetch_w(st + 1);
-            compute(st, t0, true);
-            store_w((st & 1) ^ 1);
-            __syncthreads();
-            closes(st);
-            compute(st + 1, t1, true);
-            closes(st + 1);
-        };
-        switch (st % 3) {
-            case 0: tail(tA, tB); break;
-            case 1: tail(tB, tC); break;
-            default: tail(tC, tA); break;
-        }
+    while (st + 2 < nstep) {
+        step(st, tA, tC);
+        if (++st + 2 >= nstep) break;
+        step(st, tB, tA);
+        if (++st + 2 >= nstep) break;
+        step(st, tC, tB);
+        ++st;
+    }
+    // the last two steps: nothing more to load
+    auto tail = [&](const double *t0, const double *t1) {
+        fetch_w(st + 1);
+        compute(st, t0, true);
+        store_w((st & 1) ^ 1);
+        __syncthreads();
+        closes(st);
+        compute(st + 1, t1, true);
+        closes(st + 1);
+    };
+    switch (st % 3) {
+        case 0: tail(tA, tB); break;
+        case 1: tail(tB, tC); break;
+        default: tail(tC, tA); break;
     }
     if constexpr (PIPE) {
         TP_PIPE_STAMP(1);
@@ -333,9 +275,9 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
                 const double q = d.cal ? v / (o1 ? c2p[1] : c2p[0]) : v;
                 double *out = o1 ? c.out[1].out : c.out[0].out;
                 if ((o1 ? c.out[1].kind : c.out[0].kind) == 0)
-                    TP_STORE(out + (long long)d.row * W + wv, q);
+                    out[(long long)d.row * W + wv] = q;
                 else
-                    TP_STORE(out + (long long)wv * (o1 ? c.out[1].ld : c.out[0].ld) + d.row, xsh[col] - q);
+                    out[(long long)wv * (o1 ? c.out[1].ld : c.out[0].ld) + d.row] = xsh[col] - q;
             }
         }
     }
