@@ -213,7 +213,7 @@ def convergence_run(W, rank, world, tmpdir, seconds, lensing=True):
 
 KERNELS = ("plik_bin_delta", "plik_quadform_ksplit", "plik_quadform_corun", "mh_kernel", "mh_pass_kernel",
            "rot_kernel", "cmbl_bk_prologue", "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_hl_kernel",
-           "cmbl_quadform", "cmbl_gauss_small_kernel", "theory_window_kernel", "drag_kernel",
+           "cmbl_quadform", "cmbl_gauss_small_kernel", "theory_window_kernel", "drag_kernel", "plik_quadform_pair",
            "step_tail_kernel", "step_tail_last", "step_tail_pass", "mh_step_first", "mh_step_kernel",
            "mh_step_last", "mh_half_kernel")
 

@@ -178,6 +178,9 @@ struct QFSource {
     int n_items = 0;
     double *partial = nullptr;    // [tiles][n_items][64]
     const double *X = nullptr;    // [Np] data vector, zero padded
+    const double *delta = nullptr;   // [Wp][Np] the window stage's Delta rows (the in-launch-combine form)
+    unsigned int *counters = nullptr;   // [tiles] split-K arrival tickets (zero between launches)
+    int n_counters = 0;
 };
 
 // A small gaussian CMBlikes chi^2 (smallgauss.h) as one launch's arguments:

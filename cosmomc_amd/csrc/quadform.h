@@ -95,6 +95,13 @@ class QuadForm {
     int choose_kb(int tiles);
 };
 
+// Two in-launch-combined quadratic forms (QFSource with delta / counters; the
+// tickets zero at launch) and optionally two small chi^2s in one launch
+// (quadform_pair_ticket): out_a / out_b get -lnL of the two walker sets.
+// qb / gb null: set a alone (its quadratic form and chi^2 in one launch)
+void launch_qf_pair(const QFSource &qa, double *out_a, const QFSource *qb, double *out_b, int W,
+                    const SmallGaussLaunch *ga, const SmallGaussLaunch *gb, hipStream_t stream, const char *prof_name);
+
 // host symmetric-matrix helpers (row-major)
 void spd_inverse(std::vector<double> &A, int n);                       // Matrix_Inverse
 void sym_eigen(std::vector<double> A, int n, std::vector<double> &evals,

@@ -361,7 +361,53 @@ QFSource QuadForm::source(int W, void *ws, const double *X) {
     q.n_items = (int)items[kb].size();
     q.partial = x_rows(ws) + (size_t)wpad(W) * Np;
     q.X = X;
+    q.delta = x_rows(ws);
+    q.counters = counters(ws, W);
+    q.n_counters = n_counters(W);
     return q;
+}
+
+// Two evaluations' quadratic forms (the dragging steps' end and start points,
+// each on its own workspace) with the in-launch combine, and their small
+// gaussian chi^2s riding along: [quadratic form a][quadratic form b][chi^2 a]
+// [chi^2 b] (set b absent: nq_b = 0 and no chi^2 b).  The tickets must be zero at launch (the pass zeroes them:
+// theory_window_pair); each tile's last arriver leaves its ticket zero again.
+template <int WT>
+__global__ __launch_bounds__(256, 2) void quadform_pair_ticket(QFSource qa, double *out_a, QFSource qb, double *out_b,
+                                                               int W, int nq, SmallGaussLaunch ga, SmallGaussLaunch gb,
+                                                               int ng, int nq_b)
+{
+    static_assert(small_gauss_lds_doubles<WT>() <= QF_LDS_DOUBLES, "co-run LDS");
+    __shared__ __attribute__((aligned(16))) double smem[QF_LDS_DOUBLES];
+    int b = blockIdx.x;
+    if (b < nq + nq_b) {
+        const bool second = b >= nq;
+        const QFSource &q = second ? qb : qa;
+        int item_ix, tile;
+        qf_place(b - (second ? nq : 0), q.n_items, q.xcd_map, item_ix, tile);
+        quadform_body<true>(smem, item_ix, tile, q.Ct, q.Np, q.delta, W, q.items, q.n_items, q.partial, q.counters,
+                            nullptr, second ? out_b : out_a, nullptr);
+        return;
+    }
+    b -= nq + nq_b;
+    if (b < ng) small_gauss_body<WT>(ga, smem, b);
+    else if (b < 2 * ng) small_gauss_body<WT>(gb, smem, b - ng);
+}
+
+void launch_qf_pair(const QFSource &qa, double *out_a, const QFSource *qb, double *out_b, int W,
+                    const SmallGaussLaunch *ga, const SmallGaussLaunch *gb, hipStream_t stream, const char *prof_name) {
+    if (!qa.delta || (qb && (qb->n_items != qa.n_items || !qb->delta))) fail(CMBL_ERR_ARG, "internal: quadratic-form pair");
+    const int nq = qa.n_items * (QuadForm::wpad(W) / QF_TILE);
+    const int ng = ga ? (W + SMALL_WT - 1) / SMALL_WT : 0;
+    const SmallGaussLaunch none{};
+    // one set: [quadratic form a][chi^2 a]
+    const int nq_b = qb ? nq : 0, ng_b = gb ? ng : 0;
+    const dim3 grid(nq + nq_b + ng + ng_b);
+    timed_launch(prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
+        hipExtLaunchKernelGGL(quadform_pair_ticket<SMALL_WT>, grid, dim3(256), 0, stream, e0, e1, 0, qa, out_a,
+                              qb ? *qb : qa, out_b, W, nq, ga ? *ga : none, gb ? *gb : none, ng, nq_b);
+    });
+    HIP_CHECK(hipGetLastError());
 }
 
 // Cholesky inverse of an SPD matrix (Matrix_Inverse: dpotrf 'L' + dpotri,

@@ -155,6 +155,8 @@ struct cmbs {
     cmamd::DevBuf ws_g[cmamd::MAXGROUPS];
     // fast dragging (cmbs_step_drag): scratch rows, second likelihood set, end-point theories
     cmamd::DevBuf drag_dd, drag_di, like_terms2;
+    cmamd::DevBuf like_ws2[cmamd::MAXLIKE];  // the fused likelihoods' workspaces for the start-point set (drag pairs)
+    bool no_drag_pair = false;               // debug: the drag's two evaluation sets one after the other
     bool drag_hbm = false;                   // debug: drag_kernel on the HBM state (cmamd_debug_drag_hbm)
     cmamd::DevBuf nuis_bufs2[cmamd::MAXLIKE];
     struct EndTheory { double *dl = nullptr; long long ld_field = 0, ld_walker = 0; };
@@ -199,7 +201,7 @@ struct cmbs {
     // step k + 1 runs in step k's tail launch (steptail.h) and stores raw sums,
     // which step k + 1's tails calibrate as they read them; the Metropolis
     // kernel between two tails runs alone
-    int pipe_mode = 2;                       // 0 off, 1 mh_pass_kernel, 2 step tails (cmamd_debug_pipeline)
+    int pipe_mode = 1;                       // 0 off, 1 mh_pass_kernel (default), 2 step tails, 3 unified, 4 halves
     cmamd::DevBuf tail_S[2][2];              // [parity][stage] the pass's raw sums
     cmamd::DevBuf tail_rowcal;               // the chi^2 stage's calibrated partial rows (SmallGaussLaunch::row_cal)
     cmamd::StepTailPlan tail_plan[3];        // workgroup rows: tails + pass, tails, pass

@@ -3408,6 +3408,68 @@ static void launch_drag(cmbs *s, const DragCfg &g, const HistRow &row, hipStream
     HIP_CHECK(hipGetLastError());
 }
 
+// Both evaluation sets of a drag's interpolation step (the end points T with
+// the end theories, the start points T2 with the walkers' theories) as two
+// launches instead of eight: the fused window pass over both theory sets
+// (theory_window_pair, which also zeroes the tickets), then plik_lite's two
+// in-launch-combined quadratic forms with both lensing chi^2s riding along
+// (launch_qf_pair).  Set 2 works in its own workspaces (like_ws2).  False when
+// the sets cannot be fused (then eval_likes_drag runs each).
+static bool eval_likes_drag_pair(cmbs *s, hipStream_t stream, bool both = true) {
+    if (!s->tpass || s->no_drag_pair) return false;
+    int kq = -1, kg = -1;
+    for (int k = 0; k < 2; k++) (s->tp_stage[k].kind == 1 ? kq : kg) = k;
+    if (kq < 0 || kg < 0) return false;
+    const int qi = s->tp_like[kq], gi = s->tp_like[kg];
+    const auto &ea = s->end_theory[qi], &eb = s->end_theory[gi];
+    if (ea.dl != eb.dl || ea.ld_field != eb.ld_field || ea.ld_walker != eb.ld_walker) return false;
+    const LikeSlot &P = s->likes[qi];
+    if (!s->tpass->vec_ok(ea.dl, ea.ld_field, ea.ld_walker) || !s->tpass->vec_ok(P.dl, P.ld_field, P.ld_walker))
+        return false;
+    const int W = s->W;
+    for (int k = 0; k < 2; k++) {
+        const int i = s->tp_like[k];
+        const size_t need = s->likes[i].like->like->workspace_size(W);
+        if (s->like_ws2[i].bytes < need) s->like_ws2[i].alloc(need);
+    }
+    Like &Q = *s->likes[qi].like->like;
+    Like &G = *s->likes[gi].like->like;
+    QFSource qa, qb;
+    if (!Q.qf_source(qa, W, s->like_ws[qi].p) || !Q.qf_source(qb, W, s->like_ws2[qi].p)) return false;
+    SmallGaussLaunch ga{}, gb{};
+    const size_t ld = s->dc.ld;
+    double *t1 = s->like_terms.as<double>(), *t2 = s->like_terms2.as<double>();
+    if (!G.corun_small(ga, W, s->dc.like_nuis[gi], G.n_nuis, t1 + (size_t)gi * ld, s->like_ws[gi].p) ||
+        !G.corun_small(gb, W, s->nuis_bufs2[gi].as<double>(), G.n_nuis, t2 + (size_t)gi * ld, s->like_ws2[gi].p))
+        return false;
+    TPOut oa[2], ob[2];
+    for (int k = 0; k < 2; k++) {
+        const int i = s->tp_like[k];
+        const WinStage &st = s->tp_stage[k];
+        Like &L = *s->likes[i].like->like;
+        const long long ldn = std::max(1, L.n_nuis);
+        oa[k] = TPOut{st.kind, st.cal_index, st.ld, 0, L.window_out(s->like_ws[i].p, W), st.X, s->dc.like_nuis[i], ldn};
+        ob[k] = TPOut{st.kind, st.cal_index, st.ld, 0, L.window_out(s->like_ws2[i].p, W), st.X,
+                      s->nuis_bufs2[i].as<double>(), ldn};
+    }
+    s->tpass->launch_pair(ea.dl, ea.ld_field, ea.ld_walker, oa, qa.counters, both ? P.dl : nullptr, P.ld_field,
+                          P.ld_walker, ob, qb.counters, qa.n_counters, W, stream);
+    launch_qf_pair(qa, t1 + (size_t)qi * ld, both ? &qb : nullptr, t2 + (size_t)qi * ld, W, &ga, both ? &gb : nullptr,
+                   stream, "plik_quadform_pair");
+    for (size_t i = 0; i < s->likes.size(); i++) {   // any other likelihood, one set after the other
+        if (fused(s, i)) continue;
+        auto &l = s->likes[i];
+        const int nn = l.like->like->n_nuis;
+        const auto &e = s->end_theory[i];
+        l.like->like->loglike_batch(W, e.dl, e.ld_field, e.ld_walker, s->dc.like_nuis[i], nn, t1 + i * ld, s->ws.p,
+                                    stream);
+        if (both)
+            l.like->like->loglike_batch(W, l.dl, l.ld_field, l.ld_walker, s->nuis_bufs2[i].as<double>(), nn,
+                                        t2 + i * ld, s->ws.p, stream);
+    }
+    return true;
+}
+
 void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_fn fn, void *user,
                        hipStream_t stream) {
     rot_schedule_unknown(s);           // the drag proposals move the blocks' loop indices
@@ -3461,11 +3523,11 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
         if (nl > 0) {
             const double *Pend = s->dc.sd + (size_t)s->dc.rows.T * ld;
             if (fn(user, s->W, Pend, (long long)ld, stream) != 0) fail(CMBL_ERR_ARG, "theory function failed");
-            eval_likes_drag(s, 1, stream);
+            if (!eval_likes_drag_pair(s, stream, false)) eval_likes_drag(s, 1, stream);
         }
         launch_drag<1>(s, g, HistRow{}, stream);
         for (int is = 1; is <= interp - 1; is++) {
-            if (nl > 0) {
+            if (nl > 0 && !eval_likes_drag_pair(s, stream)) {
                 eval_likes_drag(s, 1, stream);
                 eval_likes_drag(s, 2, stream);
             }
@@ -3484,7 +3546,7 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
                                e.ld_walker, const_cast<double *>(l.dl), l.ld_walker, n);
             HIP_CHECK(hipGetLastError());
         }
-        HIP_CHECK(hipMemsetAsync(g.di, 0, (size_t)s->W * 4, stream));
+        // (every walker's dst is set again by the next drag's stage 0)
     }
 }
 
@@ -3836,6 +3898,11 @@ extern "C" int cmamd_debug_corun(cmbs *s, int on) {     // the lensing chi^2 ins
 extern "C" int cmamd_debug_tail_nosignal(cmbs *s, int on) {   // in-launch producers never arrive / publish (modes 1, 3)
     if (!s) return -1;
     s->tail_nosignal = on;
+    return 0;
+}
+extern "C" int cmamd_debug_drag_pair(cmbs *s, int on) {   // both drag evaluation sets in two launches
+    if (!s) return -1;
+    s->no_drag_pair = on == 0;
     return 0;
 }
 extern "C" int cmamd_debug_drag_hbm(cmbs *s, int on) {   // the drag stages on the HBM state (no LDS image)

@@ -79,6 +79,12 @@ class TheoryPass {
     bool build(const std::vector<WinStage> &stages);
     void launch(const double *dl, long long ld_field, long long ld_walker, const TPOut *outs, int W,
                 hipStream_t stream);
+    // the pass over two theory sets in one launch (theory_window_pair; both
+    // vec_ok), zeroing nz tickets at za / zb for the quadratic form after it
+    // (dlb null: set a alone)
+    void launch_pair(const double *dla, long long lfa, long long lwa, const TPOut *oa, unsigned int *za,
+                     const double *dlb, long long lfb, long long lwb, const TPOut *ob, unsigned int *zb, int nz, int W,
+                     hipStream_t stream);
     // The vectorised kernel applies (16-byte aligned rows, at most two MFMA
     // blocks per item): the form the sampler's pipelined steps run
     bool vec_ok(const double *dl, long long ld_field, long long ld_walker) const;

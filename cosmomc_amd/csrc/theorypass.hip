@@ -265,6 +265,25 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev 
     tp_vec_body<NB, false>(c, dl, ld_field, ld_walker, W, lds, blockIdx.x);
 }
 
+// The pass over two theory sets in one launch (the dragging steps' end and
+// start points): blocks [0, n) run set a's table, [n, 2n) set b's; the first
+// block of each also zeroes that set's quadratic-form tickets (zero[k], nz[k]
+// words) for the in-launch-combined quadratic form that follows.
+__global__ __launch_bounds__(256, 3) void theory_window_pair(TPDev ca, const double *__restrict__ dla, long long lfa,
+                                                             long long lwa, TPDev cb, const double *__restrict__ dlb,
+                                                             long long lfb, long long lwb, int W, int n,
+                                                             unsigned int *za, unsigned int *zb, int nz)
+{
+    __shared__ __attribute__((aligned(16))) char lds[tp_vec_lds_bytes<2>()];
+    const bool second = (int)blockIdx.x >= n;
+    const int b = (int)blockIdx.x - (second ? n : 0);
+    if (b == 0 && (int)threadIdx.x < nz) (second ? zb : za)[threadIdx.x] = 0u;
+    if (second)
+        tp_vec_body<2, false>(cb, dlb, lfb, lwb, W, lds, b);
+    else
+        tp_vec_body<2, false>(ca, dla, lfa, lwa, W, lds, b);
+}
+
 // ------------------------------------------------------------------ host side
 
 bool TheoryPass::build(const std::vector<WinStage> &stages) {
@@ -464,6 +483,19 @@ void TheoryPass::plan_units(int tiles) {
     d_units.alloc(table.size() * sizeof(int2));
     d_units.upload(table.data(), table.size() * sizeof(int2));
     unit_tiles = tiles;
+}
+
+void TheoryPass::launch_pair(const double *dla, long long lfa, long long lwa, const TPOut *oa, unsigned int *za,
+                             const double *dlb, long long lfb, long long lwb, const TPOut *ob, unsigned int *zb,
+                             int nz, int W, hipStream_t stream) {
+    if (W <= 0 || items.empty()) return;
+    if (!vec_ok(dla, lfa, lwa) || (dlb && !vec_ok(dlb, lfb, lwb)) || nz > 256) fail(CMBL_ERR_ARG, "internal: pass pair");
+    const TPDev ca = dev_args(oa, W), cb = dlb ? dev_args(ob, W) : ca;
+    timed_launch("theory_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+        hipExtLaunchKernelGGL(theory_window_pair, dim3(dlb ? 2 * nblk : nblk), dim3(256), 0, stream, e0, e1, 0, ca, dla,
+                              lfa, lwa, cb, dlb, lfb, lwb, W, nblk, za, zb, nz);
+    });
+    HIP_CHECK(hipGetLastError());
 }
 
 bool TheoryPass::vec_ok(const double *dl, long long ld_field, long long ld_walker) const {

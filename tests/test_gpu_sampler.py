@@ -862,8 +862,10 @@ def test_dragging_fused_plik_lensing(cmbl_golden, refdata, tmp_path):
 @pytest.mark.parametrize("W", [130, 1024])
 def test_drag_staged_matches_hbm(cmbl_golden, refdata, tmp_path, W):
     """The drag stages on an LDS image of the walkers' state (drag_staged_kernel,
-    the default) and on the HBM state (drag_kernel) give the same chains bit
-    for bit: history rows, terms and the final state."""
+    the default) and on the HBM state (drag_kernel), and the interpolation
+    steps' two evaluation sets paired into two launches (theory_window_pair +
+    quadform_pair_ticket, the default) or run one after the other, give the
+    same chains bit for bit: history rows, terms and the final state."""
     import os
 
     from cosmomc_amd import _native as N
@@ -873,7 +875,7 @@ def test_drag_staged_matches_hbm(cmbl_golden, refdata, tmp_path, W):
     data = syn.make_plik_lite(12345)
     base = torch.tensor(syn.walker_theory(1, seed=4, n_fields=10, ld_field=2512), device="cuda")[0]
     out = []
-    for hbm in (0, 1):
+    for hbm, pair in ((0, 1), (1, 1), (0, 0)):
         plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
         lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
         plik.nuisance_indices = [2]
@@ -886,6 +888,7 @@ def test_drag_staged_matches_hbm(cmbl_golden, refdata, tmp_path, W):
         s.add_likelihood(plik, theory)
         s.add_likelihood(lens, theory)
         assert N.lib().cmamd_debug_drag_hbm(s._h, hbm) == 0
+        assert N.lib().cmamd_debug_drag_pair(s._h, pair) == 0
         s.set_drag_theory(0, end)
         s.set_drag_theory(1, end)
         s.set_start(np.tile([1.0, 1.0], (W, 1)))
@@ -897,10 +900,11 @@ def test_drag_staged_matches_hbm(cmbl_golden, refdata, tmp_path, W):
         n = s.history_count()
         out.append((s.history_host(0, n), s.history_terms(0, n), *s.state()))
         s.close()
-    a, b = out
+    a = out[0]
     assert np.any(a[5] > 0), "no drag was accepted"
-    for x, y in zip(a, b):
-        assert np.array_equal(x, y)
+    for b in out[1:]:
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
 
 
 @pytest.mark.parametrize("blocks,W,groups", [([21], 512, 1), ([12, 9], 576, 1), ([32], 200, 1), ([8, 13], 320, 2)])
