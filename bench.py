@@ -215,7 +215,7 @@ KERNELS = ("plik_bin_delta", "plik_quadform_ksplit", "plik_quadform_corun", "mh_
            "rot_kernel", "cmbl_bk_prologue", "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_hl_kernel",
            "cmbl_quadform", "cmbl_gauss_small_kernel", "theory_window_kernel", "drag_kernel", "plik_quadform_pair",
            "step_tail_kernel", "step_tail_last", "step_tail_pass", "mh_step_first", "mh_step_kernel",
-           "mh_step_last", "mh_half_kernel")
+           "mh_step_last", "mh_half_kernel", "mh_bin_kernel")
 
 
 def kernel_profile(smp, steps, stepper=None, per_step=False):
@@ -360,8 +360,8 @@ def config4_run(W, rank, world, tmpdir, seconds, steps=200):
     out = {"workload": "plik_lite_TTTEEE + correlated 20-d Gaussian nuisance posterior (full plik's 21 fast "
                        "parameters as a sampler-throughput stand-in: clik absent), one 21-parameter fast block, "
                        "one shared slow point",
-           "walkers_total": W * world, "evals_per_s": W * world * steps / dt, "ms_per_step": dt / steps * 1e3,
-           "avg_kernel_us": kernel_profile(smp, 50)}
+           "walkers_total": W * world, "evals_per_s": W * world * steps / dt, "ms_per_step": dt / steps * 1e3}
+    out["avg_kernel_us"], out["kernel_us_per_step"] = kernel_profile(smp, 42, per_step=True)
     if seconds > 0:
         out.update(run_to_convergence(smp, 0, n, seconds, world, 60 * 40 * n))
     return out

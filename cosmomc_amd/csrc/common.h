@@ -157,6 +157,8 @@ std::vector<std::string> split_ws(const std::string &s);
 // .paramnames file -> space-separated names (derived '*' stripped), count
 std::string load_paramnames(const std::string &path, int *count);
 
+struct PlikBinArgs;   // plikbin.h
+
 // What a deferred quadratic-form launch (QuadForm::launch_deferred) leaves
 // for the kernel that consumes it: -lnL of walker w is the fixed-order combine
 // of quadform.h (qf_group_sum / qf_tree) over the partials of walker tile
@@ -284,6 +286,12 @@ struct Like {
         fail(CMBL_ERR_UNSUPPORTED, "%s: no window stage", name.c_str());
     }
     virtual bool accepts_corun() const { return false; }
+    // plik_lite's binning as a co-run body's arguments (plikbin.h) over theory
+    // rows dl; false: not a plik_lite likelihood, or the layout does not fit
+    virtual bool bin_args(PlikBinArgs &a, const double *dl, long long ld_field, long long ld_walker) const {
+        (void)a, (void)dl, (void)ld_field, (void)ld_walker;
+        return false;
+    }
     // The deferred quadratic form after this likelihood's window stage as a
     // QFSource (its workspace ws for W walkers); false if it has none.
     virtual bool qf_source(QFSource &q, int W, void *ws) {

@@ -20,6 +20,7 @@
 #include <fstream>
 #include <functional>
 
+#include "plikbin.h"
 #include "quadform.h"
 
 namespace cmamd {
@@ -27,72 +28,28 @@ namespace cmamd {
 
 // ------------------------------------------------------------------ kernels
 
-struct BinInfo {
-    int field;   // 0 TT, 1 TE, 2 EE  (Theory%Cls (1,1) (2,1) (2,2))
-    int lmin;    // absolute l
-    int lmax;
-    int pad;
-};
-
-struct FieldRanges {   // per used field: l range staged in LDS (even-aligned), its bins [b0, b1)
-    int lo[3], hi[3], b0[3], b1[3];
-};
-
-// Binning + residual.  One workgroup per (walker, field): the field's D_l row
-// is read once (16-byte loads when the layout allows; issuing all of a thread's
-// loads up front measured no faster),
-// multiplied by the plik weights and kept in LDS; each thread then sums whole
-// bins in l order (the reference's dot_product order) and writes
-// Delta = X - cl / cal^2 for the field's bins.  Per-field blocks need at most
-// 20 KB of LDS, so a W = 1024 launch (3072 blocks) runs in even rounds (one
-// 51 KB block per walker: 768 resident, a 1.33-round tail).  Block (0, 0) also
-// zeroes the split-K arrival counters of the quadratic-form kernel that
-// follows on the same stream and the Delta padding.
+// Binning + residual (plik_bin_body, plikbin.h): one workgroup per (walker,
+// field).  Per-field blocks need at most 20 KB of LDS, so a W = 1024 launch
+// (3072 blocks) runs in even rounds (one 51 KB block per walker: 768
+// resident, a 1.33-round tail).  Block (0, 0) also zeroes the split-K arrival
+// counters of the quadratic-form kernel that follows on the same stream, and
+// the field-0 blocks the Delta padding.
 __global__ __launch_bounds__(256) void plik_bin_delta(
-    const double *__restrict__ dl, long long ld_field, long long ld_walker,
-    const double *__restrict__ nuis, long long ld_nuis,
-    const double *__restrict__ wts,          // by absolute l, zero outside the bins
-    const BinInfo *__restrict__ bins, const double *__restrict__ X,
-    int nused, int Np, FieldRanges fr, int vec_ok,
+    PlikBinArgs a, const double *__restrict__ nuis, long long ld_nuis,
     double *__restrict__ delta, unsigned int *__restrict__ counters, int n_counters,
     const int *__restrict__ wcount)   // sparse evaluation: walkers [0, *wcount) live (null: all)
 {
     extern __shared__ __attribute__((aligned(16))) double prod[];
     const int w = blockIdx.x, f = blockIdx.y;
     const int tid = threadIdx.x;
-    double *out = delta + (long long)w * Np;
     if (f == 0) {
         if (w == 0)
             for (int i = tid; i < n_counters; i += blockDim.x) counters[i] = 0u;
-        for (int i = nused + tid; i < Np; i += blockDim.x) out[i] = 0.0;
+        double *out = delta + (long long)w * a.Np;
+        for (int i = a.nused + tid; i < a.Np; i += blockDim.x) out[i] = 0.0;
     }
     if (wcount && w >= *wcount) return;
-    const int lo = fr.lo[f], hi = fr.hi[f];
-    if (hi < lo) return;
-    const double *Df = dl + (long long)w * ld_walker + f * ld_field;
-    double *P = prod - lo;
-    if (vec_ok) {
-        // lo is even, hi odd: pairs (l, l+1)
-#pragma unroll 4
-        for (int l = lo + 2 * tid; l <= hi; l += 2 * blockDim.x) {
-            const double2 d = *reinterpret_cast<const double2 *>(Df + l);
-            const double2 q = *reinterpret_cast<const double2 *>(wts + l);
-            *reinterpret_cast<double2 *>(P + l) = make_double2(d.x * q.x, d.y * q.y);
-        }
-    } else {
-        const int hs = hi < ld_field ? hi : (int)ld_field - 1;   // never read past the row
-#pragma unroll 4
-        for (int l = lo + tid; l <= hs; l += blockDim.x) P[l] = Df[l] * wts[l];
-    }
-    __syncthreads();
-    const double cal = nuis[(long long)w * ld_nuis];
-    const double c2 = cal * cal;
-    for (int i = fr.b0[f] + tid; i < fr.b1[f]; i += blockDim.x) {
-        const BinInfo b = bins[i];
-        double acc = 0.0;
-        for (int l = b.lmin; l <= b.lmax; l++) acc += P[l];
-        out[i] = X[i] - acc / c2;
-    }
+    plik_bin_body<false>(a, prod, w, f, nuis, ld_nuis, delta);
 }
 
 // clik packing (cliklike.f90:138-163) -> D_l fields TT, TE, EE for the native kernel
@@ -330,6 +287,30 @@ struct PlikLite final : Like {
 
     bool deferred_capable() const override { return true; }
 
+    PlikBinArgs bin_args_for(const double *dl, long long ld_field, long long ld_walker) const {
+        PlikBinArgs a;
+        a.dl = dl;
+        a.ld_field = ld_field;
+        a.ld_walker = ld_walker;
+        a.wts = d_wts.as<double>();
+        a.bins = d_bins.as<BinInfo>();
+        a.X = d_X.as<double>();
+        a.nused = nused;
+        a.Np = Np;
+        a.fr = fr;
+        // 16-byte D_l loads need 16-byte aligned rows and the widened ranges inside each row
+        a.vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && (ld_field % 2 == 0) && (ld_walker % 2 == 0);
+        for (int f = 0; f < 3; f++)
+            if (fr.hi[f] >= fr.lo[f] && fr.hi[f] >= ld_field) a.vec_ok = 0;
+        a.lds_doubles = lds_doubles;
+        return a;
+    }
+    bool bin_args(PlikBinArgs &a, const double *dl, long long ld_field, long long ld_walker) const override {
+        if (ld_field < lmax_needed + 1 || (ld_walker != 0 && ld_walker < 3 * ld_field)) return false;
+        a = bin_args_for(dl, ld_field, ld_walker);
+        return true;
+    }
+
     // window stage: bin i = sum_{l in bin} D_l w_l of field TT / TE / EE, then
     // Delta_i = X_i - bin_i / cal^2 (CMB.f90:315-326), in the quadratic form's rows
     bool window_stage(WinStage &st) const override {
@@ -384,14 +365,10 @@ struct PlikLite final : Like {
         }
         double *delta = qf.x_rows(ws);
         unsigned int *counters = qf.counters(ws, W);
-        // 16-byte D_l loads need 16-byte aligned rows and the widened ranges inside each row
-        int vec_ok = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && (ld_field % 2 == 0) && (ld_walker % 2 == 0);
-        for (int f = 0; f < 3; f++)
-            if (fr.hi[f] >= fr.lo[f] && fr.hi[f] >= ld_field) vec_ok = 0;
+        const PlikBinArgs a = bin_args_for(dl, ld_field, ld_walker);
         timed_launch("plik_bin_delta", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(plik_bin_delta, dim3(W, 3), dim3(256), (size_t)lds_doubles * 8, stream, e0, e1, 0, dl, ld_field,
-                               ld_walker, nuis, ld_nuis, d_wts.as<double>(), d_bins.as<BinInfo>(), d_X.as<double>(),
-                               nused, Np, fr, vec_ok, delta, counters, qf.n_counters(W), wcount);
+            hipExtLaunchKernelGGL(plik_bin_delta, dim3(W, 3), dim3(256), (size_t)lds_doubles * 8, stream, e0, e1, 0, a,
+                                  nuis, ld_nuis, delta, counters, qf.n_counters(W), wcount);
         });
         HIP_CHECK(hipGetLastError());
         if (defer) return qf.launch_deferred(W, ws, nullptr, stream, "plik_quadform_ksplit");

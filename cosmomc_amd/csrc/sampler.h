@@ -61,6 +61,8 @@ struct DevCfg {
     double *sd;             // [ND][ld]
     int *si;                // [NI][ld]
     int stage_R;            // R rows staged in LDS (else read in place, stride W)
+    int pre_blk;            // the only fast block (0-based; -1: several, or one parameter wide): with R
+                            //   in place, fast-only proposals have its next column fetched beside the image
     int stage_cyc;          // CYC rows + RandIndices scratch in LDS (else in place / itmp_g)
     int stage_cov;          // test-Gaussian covinv + center tables in LDS (else read from tab_d)
     int *itmp_g;            // [all_n][ld] RandIndices scratch when !stage_cyc
@@ -96,6 +98,11 @@ struct DevCfg {
     int pub_pcal[2];                        // the stages' calibration parameters (0-based, -1: none)
     double *calbuf;                         // [2 stages][ld], this launch's half
     double *calbuf_next;                    // the next launch's half
+    // bin co-run (mh_bin_kernel): rot_kernel forms the Delta rows of the
+    // walkers it finishes from the co-run's raw sums (bin_on: set per launch)
+    int bin_on, bin_nused, bin_Np, bin_cal;  // bin_cal: plik's calibration among its nuisances
+    const double *bin_S, *bin_X;            // [wpad(W)][Np] raw sums; [Np] data vector
+    double *bin_delta;                      // [wpad(W)][Np] plik's Delta rows
 };
 
 // The unified step launch (pipe_mode 3, sampler.hip mh_step_kernel): its
@@ -132,7 +139,7 @@ struct cmbs {
     std::vector<int> rot_lp;            // per 64-walker range: the single fast block's loop index mod n, or -1 (rot_may_pend)
     bool rot_fast_any = false;          // some fast block is wide enough to defer its rotations
     int rot_fast_n = 0;                 // width of the only fast block when it is deferred, else 0
-    bool no_stage_R = false;            // debug: keep the rotation rows in HBM (cmamd_debug_stage_R)
+    int stage_R_force = -1;             // debug: rotation rows staged (1) / in HBM (0) / by set_mh_lds (-1)
     cmamd::DevBuf tab_i, tab_d, sd, si, like_terms, cur_terms, ws, hist, hist_terms, mom, itmp_g;
     cmamd::DevBuf nuis_bufs[cmamd::MAXLIKE];
     std::vector<int> h_tab_i;
@@ -223,6 +230,11 @@ struct cmbs {
     int *pipe_status_host = nullptr;
     hipEvent_t pipe_ev = nullptr;
     bool pipe_ev_pending = false;
+    // bin co-run (a lone plik_lite likelihood, no fused pass): the proposing
+    // launch also bins every walker's theory into raw sums (mh_bin_kernel);
+    // plik's deferred evaluation continues from them (Like::deferred_from_sums)
+    cmamd::DevBuf bin_S;                     // [wpad(W)][Np] raw bin sums (padding zero)
+    size_t bin_lds = 0;                      // mh_bin_kernel's LDS
     int tp_why = 0;                          // set-up progress when no pass was built (debug)
     ~cmbs() {
         if (pipe_status_host) (void)hipHostFree(pipe_status_host);

@@ -22,6 +22,7 @@
 
 #include <cstdlib>
 
+#include "plikbin.h"
 #include "qfs_body.h"
 #include "quadform.h"
 #include "sampler.h"
@@ -193,6 +194,7 @@ struct Walker {
     int defer_rot = 0;   // leave a new rotation of a wide block to rot_kernel (block index in pend_rot)
     int pend_rot = -1;
     double r1 = 0.0;     // a one-parameter block's rotation, just drawn (R may live in HBM: no read-back)
+    int col_pre = 0;     // vec already holds the proposal's column of R (mh_body's pre_col)
 };
 
 __device__ int cyc_next(Walker &k, int which, int n, int base)
@@ -273,7 +275,7 @@ static constexpr int ROT_DEFER_MIN = 8;   // blocks this wide get their rotation
 __device__ void proposal_tail(const DevCfg &c, const Tabs &t, Walker &k, int b, int lp);
 __device__ void proposal_r(const DevCfg &c, const Tabs &t, Walker &k, int b, int n, double r1);
 
-__device__ void block_proposal(const DevCfg &c, const Tabs &t, Walker &k, int bi /*1-based*/)
+__device__ __forceinline__ void block_proposal(const DevCfg &c, const Tabs &t, Walker &k, int bi /*1-based*/)
 {   // GetBlockProposal :247-254 -> ProposeVec :105-120 -> Propose_r :122-139 -> UpdateParams :142-149
     const int b = bi - 1;
     const int n = t.blk_n[b];
@@ -304,7 +306,7 @@ __device__ void proposal_tail(const DevCfg &c, const Tabs &t, Walker &k, int b, 
     k.blklp[b] = lp;
     // vec(q) = R(q, loopix) (the column of R is read once: R may live in HBM
     // when it is too big to stage), scaled by Propose_r's step below
-    for (int q0 = 0; q0 < n; q0 += RCH) {
+    for (int q0 = 0; !k.col_pre && q0 < n; q0 += RCH) {
         double rv[RCH];
 #pragma unroll
         for (int u = 0; u < RCH; u++) rv[u] = q0 + u < n ? k.R[off + (q0 + u) * n + (lp - 1)] : 0.0;
@@ -337,7 +339,14 @@ __device__ void proposal_r(const DevCfg &c, const Tabs &t, Walker &k, int b, int
     const int *chg = t.changed + t.blk_changed_off[b];
     if (r1 != 0.0) k.vec[0] = r1 * scale;
     else
-        for (int q = 0; q < n; q++) k.vec[q] = k.vec[q] * scale;
+        for (int q0 = 0; q0 < n; q0 += RCH) {   // RCH loads in flight
+            double v[RCH];
+#pragma unroll
+            for (int u = 0; u < RCH; u++) v[u] = k.vec[q0 + u < n ? q0 + u : 0];
+#pragma unroll
+            for (int u = 0; u < RCH; u++)
+                if (q0 + u < n) k.vec[q0 + u] = v[u] * scale;
+        }
     if (k.defer) {
         k.pend_b = b;
         return;
@@ -349,19 +358,19 @@ __device__ void proposal_r(const DevCfg &c, const Tabs &t, Walker &k, int b, int
     }
 }
 
-__device__ void proposal_fast(const DevCfg &c, const Tabs &t, Walker &k)
+__device__ __forceinline__ void proposal_fast(const DevCfg &c, const Tabs &t, Walker &k)
 {   // :283-289
     const int q = cyc_next(k, 2, c.fast_n, c.all_n + c.slow_n);
     block_proposal(c, t, k, t.pfi[c.slow_n + q - 1]);
 }
 
-__device__ void proposal_slow(const DevCfg &c, const Tabs &t, Walker &k)
+__device__ __forceinline__ void proposal_slow(const DevCfg &c, const Tabs &t, Walker &k)
 {   // :275-281
     const int q = cyc_next(k, 1, c.slow_n, c.all_n);
     block_proposal(c, t, k, t.pfi[q - 1]);
 }
 
-__device__ void proposal(const DevCfg &c, const Tabs &t, Walker &k)
+__device__ __forceinline__ void proposal(const DevCfg &c, const Tabs &t, Walker &k)
 {   // GetProposal :257-273
     if (k.fast_ix != 0) {
         proposal_fast(c, t, k);
@@ -386,8 +395,9 @@ __device__ inline double test_row(const DevCfg &c, const Tabs &t, const Q &q, in
     return s;
 }
 
-// trows (stride MB), when given, holds test_row(i) for every i, computed by
-// the other waves of mh_kernel: the same sums in the same order
+// trows (stride MB), when given, holds (q - center)_i x test_row(i) for every
+// i, computed by the other waves of mh_kernel: the same products, summed here
+// in the same order (built with -ffp-contract=off: no fused multiply-add)
 // zrows / oobv (stride MB), when given, hold every parameter's squared prior z
 // (0 where there is no prior) and the bounds verdict of q, formed by the other
 // thread groups: the same terms, summed here in the same order
@@ -416,10 +426,16 @@ __device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const 
     if (c.test_like) {                                               // TestLikelihoodFunction :180-199
         const int n = c.n_used;
         double d = 0.0;
-        for (int i = 0; i < n; i++) {
-            const double s = trows ? trows[(size_t)i * MB] : test_row(c, t, q, i);
-            d += (q[t.params_used[i]] - t.center[t.params_used[i]]) * s;
+        for (int i0 = 0; trows && i0 < n; i0 += RCH) {   // the products, formed by the thread groups
+            double v[RCH];
+#pragma unroll
+            for (int u = 0; u < RCH; u++) v[u] = trows[(size_t)(i0 + u < n ? i0 + u : 0) * MB];
+#pragma unroll
+            for (int u = 0; u < RCH; u++)
+                if (i0 + u < n) d += v[u];
         }
+        for (int i = 0; !trows && i < n; i++)
+            d += (q[t.params_used[i]] - t.center[t.params_used[i]]) * test_row(c, t, q, i);
         main = d / 2.0;
     }
     for (int l = 0; l < c.n_like; l++) {
@@ -679,18 +695,45 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     }
     // the test-Gaussian rows of covinv . (trial - center) are spread over the
     // waves (each row summed by one thread, in order) instead of run serially
-    // by the chain wave
-    const bool par_test = ACCEPT && c.test_like && c.n_used >= 4 && c.tq_rows >= c.n_used;
-    const bool par_map = PROPOSE && c.max_blk >= 4 && c.tq_rows >= 1;
+    // by the chain wave: first the differences (trial - center)_j, one row
+    // each (tq rows n_used ..), then the rows' sums and their products with
+    // the differences (tq rows 0 ..), every sum's loads in flight together
+    const bool par_test = ACCEPT && c.test_like && c.n_used >= 4 && c.tq_rows >= 2 * c.n_used;
+    const bool par_map = PROPOSE && c.max_blk >= 4 && c.tq_rows >= 2;
     // the trial's bounds check and squared Gaussian-prior z of every parameter,
     // spread over the thread groups (the chain thread then only sums them in order)
     const bool par_prior = ACCEPT;
-    if (par_test || par_prior) {
+    // fast-only proposals with R in HBM: the only fast block's next column
+    // (R(:, lp + 1) when no rotation is due) fetched into the vec rows by the
+    // thread groups, the loads issued before the other per-parameter work
+    // (proposal_tail then skips its own read; a block that rotates writes R
+    // only in rot_kernel)
+    const bool pre_col = PROPOSE && fast_only && !c.stage_R && c.pre_blk >= 0;
+    if (par_test || par_prior || pre_col) {
+        constexpr int NRQ = (MAXBLK + NV - 1) / NV;
+        double rq[NRQ];
+        int col = -1, ncol = 0;
+        if (pre_col && act) {
+            const int b = c.pre_blk, off = ti[c.tl.blk_R_off + b];
+            ncol = ti[c.tl.blk_n + b];
+            const int lp = si[(size_t)(R.BLKLP + b) * MB + lane];
+            if (lp % ncol != 0) col = off + lp;
+#pragma unroll
+            for (int u = 0; u < NRQ; u++) {
+                const int q = grp + u * NV;
+                if (col >= 0 && q < ncol) rq[u] = c.sd[(size_t)(R.R + col + q * ncol) * W + w];
+            }
+        }
+        const Tabs t0 = make_tabs(c, ti, td, c.stage_cov ? td : c.tab_d);
+        const Col<double> q{sd + (size_t)SROW(R.T) * MB + lane, MB};
+        const int nu = c.n_used;
+        double *dif = tq + (size_t)nu * MB + lane;
         if (act) {
-            const Tabs t0 = make_tabs(c, ti, td, c.stage_cov ? td : c.tab_d);
-            const Col<double> q{sd + (size_t)SROW(R.T) * MB + lane, MB};
             if (par_test)
-                for (int i = grp; i < c.n_used; i += NV) tq[(size_t)i * MB + lane] = test_row(c, t0, q, i);
+                for (int i = grp; i < nu; i += NV) {
+                    const int pi = t0.params_used[i];
+                    dif[(size_t)i * MB] = q[pi] - t0.center[pi];
+                }
             if (par_prior) {
                 int oob = 0;
                 for (int i = grp; i < c.np; i += NV) {
@@ -705,6 +748,32 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
                 }
                 if (oob) atomicOr(&oobw[lane], 1);
             }
+        }
+        if (par_test) {
+            __syncthreads();
+            if (act)
+                for (int i = grp; i < nu; i += NV) {   // test_row's sum, same order
+                    const double *ci = t0.covinv + (size_t)i * nu;
+                    double s = 0.0;
+                    for (int j0 = 0; j0 < nu; j0 += RCH) {
+                        double cv[RCH], dv[RCH];
+#pragma unroll
+                        for (int u = 0; u < RCH; u++) {
+                            const int j = j0 + u < nu ? j0 + u : 0;
+                            cv[u] = ci[j];
+                            dv[u] = dif[(size_t)j * MB];
+                        }
+#pragma unroll
+                        for (int u = 0; u < RCH; u++)
+                            if (j0 + u < nu) s += cv[u] * dv[u];
+                    }
+                    tq[(size_t)i * MB + lane] = dif[(size_t)i * MB] * s;
+                }
+        }
+#pragma unroll
+        for (int u = 0; u < NRQ; u++) {
+            const int qq = grp + u * NV;
+            if (col >= 0 && qq < ncol) vc[(size_t)qq * MB + lane] = rq[u];
         }
         __syncthreads();
     }
@@ -732,6 +801,7 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     double &mult = sd[(size_t)SROW(R.M) * MB + lane];
     int &nacc = si[(size_t)R.NACC * MB + lane];
 
+    bool moved = false;   // accepted: P = trial already
     if (ACCEPT) {
         if (c.mask_on) {   // unchanged likelihoods keep the current point's term (calclike.f90:377-384)
             for (int l = 0; l < c.n_like; l++) {
@@ -753,6 +823,7 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
             if (!acc) acc = (double)randexp1(k.r) > like - cur;
         }
         STAMP(10);
+        moved = acc;
         if (acc) {
             if (mult > 0) nacc += 1;
             mult = 1.0;
@@ -785,7 +856,7 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     }
     STAMP(3);
     if (PROPOSE) {
-        for (int i0 = 0; i0 < c.np; i0 += RCH) {                     // Trial = CurParams, RCH loads in flight
+        for (int i0 = 0; !moved && i0 < c.np; i0 += RCH) {           // Trial = CurParams, RCH loads in flight
             double v[RCH];
 #pragma unroll
             for (int u = 0; u < RCH; u++) v[u] = k.P[i0 + u < c.np ? i0 + u : 0];
@@ -793,10 +864,13 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
             for (int u = 0; u < RCH; u++)
                 if (i0 + u < c.np) k.trial[i0 + u] = v[u];
         }
+        STAMP(14);
         k.defer = par_map;
         k.defer_rot = c.rot_defer;
+        k.col_pre = pre_col && k.blklp[c.pre_blk] % t.blk_n[c.pre_blk] != 0;
         if (fast_only) proposal_fast(c, t, k);
         else proposal(c, t, k);
+        STAMP(15);
         si[(size_t)R.PROT * MB + lane] = k.pend_rot + 1;             // rot_kernel finishes this walker
         if (k.pend_rot >= 0) {
             const int slot = atomicAdd(c.rot_cnt + 2 * (blk0 * MB / 64) + c.rot_par, 1);
@@ -830,6 +904,7 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
             const double *vec = vc + lane;
             for (int j = grp; j < nc; j += NV) {
                 double s = 0.0;
+#pragma unroll 4
                 for (int q = 0; q < n; q++) s += M[j * n + q] * vec[(size_t)q * MB];
                 trial[(size_t)chg[j] * MB] += s;
             }
@@ -853,10 +928,12 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
         for (int i = grp; i < c.n_used; i += NV)
             hist_row[(size_t)i * c.W + w] = sd[(size_t)(SROW(R.P) + pu[i]) * MB + lane];
     }
-    if (PROPOSE && c.pub_on && threadIdx.x < MB && act)   // the fused pass in this launch polls for these
+    if (PROPOSE && c.pub_on && threadIdx.x < MB && act)   // the fused pass / bins in this launch poll for these
         for (int k = 0; k < 2; k++) {
             const int pc = c.pub_pcal[k];
-            const double v = pc >= 0 ? sd[(size_t)(SROW(R.T) + pc) * MB + lane] : 1.0;
+            const bool rp = si[(size_t)R.PROT * MB + lane] != 0;   // rot_kernel proposes it (bin co-run only)
+            const double v = rp ? __longlong_as_double((long long)TP_PIPE_ROT)
+                                : pc >= 0 ? sd[(size_t)(SROW(R.T) + pc) * MB + lane] : 1.0;
             __hip_atomic_store(c.calbuf + (size_t)k * W + w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(c.calbuf_next + (size_t)k * W + w, __longlong_as_double((long long)TP_PIPE_UNSET),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // read by the next launch only
@@ -923,6 +1000,79 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_pass_kernel(DevCfg c, int fa
 #ifdef CMAMD_STAMPS
     if (threadIdx.x == 0 && b < 2048) cmamd::g_pipe_stamps[b][4] = 2;
 #endif
+}
+
+// A proposing mh_kernel with plik_lite's binning riding along (the bin
+// co-run of sampler_step): workgroups [0, nmh) are mh_kernel's, the pad up to
+// a multiple of 8 idle, the rest bin a walker each (its three fields in
+// turn: one workgroup per walker keeps the whole grid resident beside the
+// Metropolis workgroups' LDS size; plik_bin_products and the bin sums), wait for the walker's trial
+// calibration (published by its Metropolis workgroup, as for mh_pass_kernel)
+// and emit Delta = X - S / cal^2 into plik's rows -- or, for a walker whose proposal waits on a new
+// rotation (TP_PIPE_ROT), the raw sums, from which rot_kernel forms its
+// Delta after the launch.  The binning runs on the CUs the latency-bound
+// Metropolis chain leaves idle (it takes 32 of 256 at W = 512); only its
+// emit waits.  The bins wait on workgroups with lower ids (see mh_pass_kernel
+// for the dispatch-order assumption), bounded by TAIL_WAIT_TICKS with the
+// give-up reported by the next step call.
+template <bool ACCEPT>
+__global__ __launch_bounds__(MH_THREADS) void mh_bin_kernel(DevCfg c, int fast_only, double *hist_row,
+                                                            double *hist_terms, int nmh, int nmh_pad, PlikBinArgs pb,
+                                                            int *status)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ double cal_s;
+    const int b = blockIdx.x;
+    if (b < nmh_pad) {
+        if (b < nmh) mh_body<ACCEPT, true>(c, fast_only, hist_row, hist_terms, 0, lds, b);
+        return;
+    }
+    const int w = b - nmh_pad;
+    for (int i = pb.nused + (int)threadIdx.x; i < pb.Np; i += MH_THREADS)   // the Delta row's padding columns
+        c.bin_delta[(size_t)w * pb.Np + i] = 0.0;
+    // the three fields in turn through one LDS image: this thread's bin sums
+    // (plik_bin_emit's, at most two bins a field: bin_setup) before the wait,
+    // so only the emit follows the calibration
+    double acc[3][2] = {};
+#pragma unroll
+    for (int f = 0; f < 3; f++) {
+        if (f > 0) __syncthreads();   // the previous field's sums have read the image
+        if (!plik_bin_products(pb, lds, w, f)) continue;
+        const double *P = lds - pb.fr.lo[f];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int i = pb.fr.b0[f] + (int)threadIdx.x + k * MH_THREADS;
+            if (i < pb.fr.b1[f]) {
+                const BinInfo bi = pb.bins[i];
+                for (int l = bi.lmin; l <= bi.lmax; l++) acc[f][k] += P[l];
+            }
+        }
+    }
+    if (threadIdx.x == 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        double cl;
+        for (;;) {
+            cl = __hip_atomic_load(c.calbuf + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned long long)__double_as_longlong(cl) != TP_PIPE_UNSET) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > TAIL_WAIT_TICKS) {   // a safety net: reported loudly
+                atomicOr(status, CMBL_STATUS_PIPE_WAIT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(24);   // ~1500 cycles: 3 W pollers must not crowd the L2
+        }
+        cal_s = cl;
+    }
+    __syncthreads();
+    const double cl = cal_s, c2 = cl * cl;
+    const bool rot = (unsigned long long)__double_as_longlong(cl) == TP_PIPE_ROT;
+    double *out = (rot ? const_cast<double *>(c.bin_S) : c.bin_delta) + (size_t)w * pb.Np;
+#pragma unroll
+    for (int f = 0; f < 3; f++)
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int i = pb.fr.b0[f] + (int)threadIdx.x + k * MH_THREADS;
+            if (pb.fr.hi[f] >= pb.fr.lo[f] && i < pb.fr.b1[f]) out[i] = rot ? acc[f][k] : pb.X[i] - acc[f][k] / c2;
+        }
 }
 
 // The unified step launch (pipe_mode 3): one launch per fast step.  Rows of
@@ -1454,10 +1604,12 @@ __device__ void rot_walker(const DevCfg &c, int w, int lane, RotLds &L, bool sta
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the trial row's stores, before lane 0 reads it
     __builtin_amdgcn_wave_barrier();
+    double calr = 0.0;   // bin co-run: plik's trial calibration
     if (lane == 0) {
         for (int l = 0; l < c.n_like; l++)
             for (int q = 0; q < c.like_nn[l]; q++)
                 c.like_nuis[l][(size_t)w * c.like_nn[l] + q] = k.trial[t.ti[c.like_nidx[l] + q]];
+        if (c.bin_on) calr = k.trial[t.ti[c.like_nidx[0] + c.bin_cal]];
         if (c.mask_on) write_like_flags(c, k.trial, k.P, w);
         c.sd[(size_t)R.C * ld + w] = k.r.c;
         c.sd[(size_t)R.G * ld + w] = k.r.gset;
@@ -1468,6 +1620,12 @@ __device__ void rot_walker(const DevCfg &c, int w, int lane, RotLds &L, bool sta
     }
     wave_sync();
     for (int i = lane; i < 97; i += 64) c.sd[(size_t)(R.U + i) * ld + w] = L.u[i];
+    if (c.bin_on) {   // the walker's Delta rows from the bin co-run's raw sums (plik_bin_emit's operations)
+        const double cl = __shfl(calr, 0), c2 = cl * cl;
+        const size_t r = (size_t)w * c.bin_Np;
+#pragma unroll 4
+        for (int i = lane; i < c.bin_nused; i += 64) c.bin_delta[r + i] = c.bin_X[i] - c.bin_S[r + i] / c2;
+    }
 }
 
 // One wave per listed walker (the launch's list counter is wave-uniform).
@@ -2051,9 +2209,16 @@ static void set_mh_lds(cmbs *s) {
     // multi-wave scratch rows stay in HBM and are read in place.
     DevCfg &d = s->dc;
     const size_t cap = 160 * 1024;
-    d.stage_R = s->no_stage_R ? 0 : 1;
+    // the rotation rows stay in HBM when every rotation wider than one
+    // parameter is drawn by rot_kernel: the chain then only reads one column
+    // per proposal (fetched beside the image, pre_blk), and staging the n x n
+    // rows in and out of LDS is most of the image (config4_fast21: 441 of
+    // ~600 rows)
+    bool all_deferred = d.rot_defer != 0;
+    for (int bn : s->blk_n) all_deferred = all_deferred && (bn == 1 || bn >= ROT_DEFER_MIN);
+    d.stage_R = s->stage_R_force >= 0 ? s->stage_R_force : (all_deferred ? 0 : 1);
     d.stage_cyc = d.stage_cov = 1;
-    d.tq_rows = d.test_like ? s->n_used : 1;   // a row per test-Gaussian row, or one (the proposal's block)
+    d.tq_rows = d.test_like ? 2 * s->n_used : 2;   // two per test-Gaussian row, or the proposal's block and step
     d.def_cap = (int)s->defer_likes.size();
     if (mh_lds_bytes(s) > cap) {               // the deferred combines go first: the likelihoods combine in-launch
         d.def_cap = 0;
@@ -2166,6 +2331,7 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
     d.max_blk = 1;
     for (int bn : s->blk_n) d.max_blk = std::max(d.max_blk, bn);
     d.rot_defer = d.max_blk >= ROT_DEFER_MIN ? 1 : 0;
+    d.bin_on = 0;
 
     // ---- shared tables
     TabLayout &tl = d.tl;
@@ -2258,6 +2424,7 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
         s->rot_fast_any = false;
         for (int b : fb) s->rot_fast_any = s->rot_fast_any || s->blk_n[b] >= ROT_DEFER_MIN;
         s->rot_fast_n = (fb.size() == 1 && s->blk_n[fb[0]] >= ROT_DEFER_MIN) ? s->blk_n[fb[0]] : 0;
+        d.pre_blk = (fb.size() == 1 && s->blk_n[fb[0]] >= 2) ? fb[0] : -1;
     }
     HIP_CHECK(hipFuncSetAttribute((const void *)rot_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(ROT_WAVES * sizeof(RotLds))));
@@ -2863,8 +3030,55 @@ static bool pipe_setup(cmbs *s, int fast_only) {
     return true;
 }
 
+// Whether this run of fast steps can take the bin co-run: one likelihood,
+// plik_lite, deferred (its quadratic form's combine in the next mh launch),
+// no fused pass, one walker group, no change mask.  Allocates the raw sums and
+// sets up the calibration hand-off (as pipe_setup).
+static bool bin_setup(cmbs *s, int fast_only, PlikBinArgs &pb) {
+    if (s->pipe_mode != 1 || !fast_only || s->tpass || s->n_groups != 1 || s->mask_on || s->likes.size() != 1 ||
+        !is_deferred(s, 0))
+        return false;
+    const LikeSlot &L = s->likes[0];
+    WinStage st;
+    if (!L.like->like->bin_args(pb, L.dl, L.ld_field, L.ld_walker) || !L.like->like->window_stage(st) ||
+        st.cal_index < 0)
+        return false;
+    const size_t need = (size_t)QuadForm::wpad(s->W) * pb.Np * 8;
+    if (s->bin_S.bytes < need) {
+        s->bin_S.alloc(need);
+        HIP_CHECK(hipMemset(s->bin_S.p, 0, need));
+    }
+    for (int f = 0; f < 3; f++)
+        if (pb.fr.b1[f] - pb.fr.b0[f] > 2 * MH_THREADS) return false;   // mh_bin_kernel: two bins a thread
+    s->bin_lds = std::max(s->mh_lds, (size_t)pb.lds_doubles * 8);
+    if (s->bin_lds > 160 * 1024) return false;
+    HIP_CHECK(hipFuncSetAttribute((const void *)mh_bin_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)s->bin_lds));
+    HIP_CHECK(hipFuncSetAttribute((const void *)mh_bin_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)s->bin_lds));
+    if (s->pipe_ready == s->W) return true;
+    pipe_status_init(s);
+    {   // both halves unset: the first launch publishes into half 1, resets half 0
+        const std::vector<unsigned long long> unset((size_t)4 * s->dc.ld, TP_PIPE_UNSET);
+        s->pipe_cal.alloc(unset.size() * 8);
+        s->pipe_cal.upload(unset.data(), unset.size() * 8);
+    }
+    s->pipe_epoch = 0;
+    s->pipe_ready = s->W;
+    return true;
+}
+
+// plik's deferred quadratic form over the Delta rows the bin co-run (and
+// rot_kernel) formed; its combine runs in the next Metropolis launch
+static void launch_bin_qf(cmbs *s, hipStream_t stream) {
+    Like &Q = *s->likes[0].like->like;
+    const QFDeferred d = Q.after_window(s->W, s->dc.like_nuis[0], std::max(1, Q.n_nuis), nullptr, s->like_ws[0].p,
+                                        stream, true);
+    record_deferred(s, 0, d);
+}
+
 static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const HistRow &row, hipStream_t stream,
-                      int g0, int g1, bool masked = false, bool pipe = false) {
+                      int g0, int g1, bool masked = false, bool pipe = false, const PlikBinArgs *bin = nullptr) {
     const dim3 g((g1 - g0 + MB - 1) / MB), b(MH_THREADS);
     const int blk0 = g0 / MB;
     const size_t lds = s->mh_lds;
@@ -2915,6 +3129,42 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
         s->pipe_epoch = e;       // only a launched step moves the halves' parity
         return;
     }
+    if (bin) {   // mh_bin_kernel: the proposing launch bins the theory beside the Metropolis workgroups
+        if (!propose || g0 != 0 || g1 != s->W) fail(CMBL_ERR_ARG, "internal: bin co-run launch");
+        Like &Q = *s->likes[0].like->like;
+        WinStage st;
+        Q.window_stage(st);
+        dc.pub_on = s->tail_nosignal ? 0 : 1;   // debug: never publish (the give-up test)
+        dc.pub_pcal[0] = s->likes[0].nidx[st.cal_index];
+        dc.pub_pcal[1] = -1;
+        const unsigned e = s->pipe_epoch + 1;   // this launch's half e % 2; it resets the other for the next
+        dc.calbuf = s->pipe_cal.as<double>() + (size_t)(e % 2) * 2 * dc.ld;
+        dc.calbuf_next = s->pipe_cal.as<double>() + (size_t)((e + 1) % 2) * 2 * dc.ld;
+        dc.bin_on = 1;
+        dc.bin_nused = bin->nused;
+        dc.bin_Np = bin->Np;
+        dc.bin_cal = st.cal_index;
+        dc.bin_S = s->bin_S.as<double>();
+        dc.bin_X = bin->X;
+        dc.bin_delta = Q.window_out(s->like_ws[0].p, s->W);
+        const int nmh = (int)g.x, nmh_pad = (nmh + 7) / 8 * 8;
+        const dim3 gb(nmh_pad + s->W);
+        try {
+            timed_launch("mh_bin_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+                if (accept)
+                    hipExtLaunchKernelGGL(mh_bin_kernel<true>, gb, b, s->bin_lds, stream, e0, e1, 0, dc, fast_only,
+                                          row.p, row.t, nmh, nmh_pad, *bin, s->pipe_status.as<int>());
+                else
+                    hipExtLaunchKernelGGL(mh_bin_kernel<false>, gb, b, s->bin_lds, stream, e0, e1, 0, dc, fast_only,
+                                          row.p, row.t, nmh, nmh_pad, *bin, s->pipe_status.as<int>());
+            });
+            HIP_CHECK(hipGetLastError());
+        } catch (...) {
+            s->pipe_ready = 0;   // both halves re-uploaded as unset next time
+            throw;
+        }
+        s->pipe_epoch = e;
+    } else
     timed_launch("mh_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
         if (accept && propose)
             hipExtLaunchKernelGGL(mh_kernel<true, true>, g, b, lds, stream, e0, e1, 0, dc, fast_only, row.p, row.t, blk0);
@@ -3297,6 +3547,18 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
         for (int k = 0; k < n_steps; k++) {
             launch_mh(s, k > 0, true, fast_only, k > 0 ? next_hist(s) : HistRow{}, stream, 0, s->W, false, true);
             eval_likes(s, stream, false, 0, s->W, s->ws.p, true, true);
+        }
+        launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W, false);
+        pipe_status_post(s, stream);
+        return;
+    }
+    PlikBinArgs pb;
+    if (G == 1 && bin_setup(s, fast_only, pb)) {
+        // bin co-run: propose(1) + bins(1) | [rotations] | quadform(1) | accept(1) + propose(2) + bins(2) |
+        // ... | quadform(n) | accept(n)
+        for (int k = 0; k < n_steps; k++) {
+            launch_mh(s, k > 0, true, fast_only, k > 0 ? next_hist(s) : HistRow{}, stream, 0, s->W, false, false, &pb);
+            launch_bin_qf(s, stream);
         }
         launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W, false);
         pipe_status_post(s, stream);
@@ -3871,7 +4133,7 @@ extern "C" int cmamd_debug_rot_serial(cmbs *s, int mode) {   // 1: rotations by 
 }
 extern "C" int cmamd_debug_stage_R(cmbs *s, int on) {     // rotation rows staged in mh_kernel's LDS image
     if (!s) return -1;
-    s->no_stage_R = !on;
+    s->stage_R_force = on;   // -1: set_mh_lds decides
     cmamd::set_mh_lds(s);
     return 0;
 }

@@ -37,7 +37,10 @@ struct TPOut {            // a stage's output for one launch
 static constexpr int TP_MAXSTEP = 16;
 // a calibration slot not yet published in this launch (a NaN payload no
 // calibration takes; compared by bits)
-static constexpr unsigned long long TP_PIPE_UNSET = 0x7ff4c0ffee0dd00dull;   // 32-l steps per work item (the active-block mask)
+static constexpr unsigned long long TP_PIPE_UNSET = 0x7ff4c0ffee0dd00dull;
+// published instead of a calibration when the walker's proposal waits on a new
+// rotation (rot_kernel finishes it after the launch; the bin co-run)
+static constexpr unsigned long long TP_PIPE_ROT = 0x7ff4c0ffee0dd00eull;   // 32-l steps per work item (the active-block mask)
 
 struct TPItem {           // one workgroup's l range of one theory field, with <= 64 columns
     int field, l0, l1, nch, ncol, cdesc;

@@ -770,12 +770,12 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
         assert np.array_equal(out[0][1], o[1])
 
 
-@pytest.mark.parametrize("mode", [3, 1])
+@pytest.mark.parametrize("mode", [3, 1, "bin"])
 def test_pipelined_handoff_giveup_fails_loudly(cmbl_golden, refdata, tmp_path, mode):
     """In-launch hand-offs fail loudly.  Mode 3: the unified step launch's
     Metropolis workgroups wait for their tile's tails; mode 1: mh_pass_kernel's
     pass workgroups wait for the calibrations the Metropolis workgroups
-    publish.  A debug switch stops the producers (no arrivals / no
+    publish; "bin": mh_bin_kernel's bin workgroups wait for them likewise.  A debug switch stops the producers (no arrivals / no
     publication), so every wait gives up at its bound and sets
     CMBL_STATUS_PIPE_WAIT; the next readback (and the next step call) must fail
     instead of handing back silently rejected trials."""
@@ -796,8 +796,9 @@ def test_pipelined_handoff_giveup_fails_loudly(cmbl_golden, refdata, tmp_path, m
                     [0.0, 0.0025, 0.0], seed_ij=63, seed_kl=74)
     s.set_covariance(np.array([[0.002 ** 2]]))
     s.add_likelihood(plik, dl)
-    s.add_likelihood(lens, dl)
-    assert N.lib().cmamd_debug_pipeline(s._h, mode) == 0
+    if mode != "bin":   # "bin": plik alone, the bin co-run's bins wait for the calibrations
+        s.add_likelihood(lens, dl)
+    assert N.lib().cmamd_debug_pipeline(s._h, 1 if mode == "bin" else mode) == 0
     s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
     s.step(2, fast_only=True)                                  # healthy
     s.state()
@@ -952,6 +953,114 @@ def test_parallel_rotations_match_serial(blocks, W, groups):
     np.testing.assert_array_equal(sa[1], sb[1])
     assert a == b
     assert c == b          # mode 2: a last-row redraw restarts the pass instead of using the spare lanes
+
+
+@pytest.mark.parametrize("blocks,W,force", [([21], 512, 1), ([12, 9], 320, 1), ([4, 17], 256, 0)])
+def test_rotation_rows_in_place_match_staged(blocks, W, force):
+    """The rotation rows in HBM (set_mh_lds's choice when rot_kernel draws
+    every rotation wider than one parameter; the only fast block's next column
+    fetched by the thread groups beside the image) and staged in mh_kernel's
+    LDS image leave every walker's whole state bit-identical, over several
+    rotations per walker, rotating steps (rot_kernel) and fast-only steps
+    alike; [4, 17] forces the in-place rows with a 4-wide block rotating inside
+    the chain."""
+    from cosmomc_amd import _native as N
+    from cosmomc_amd.sampler import BatchedMCMC
+    n = sum(blocks)
+    rng = np.random.default_rng(7 * n + W)
+    width = rng.uniform(0.05, 2.0, n)
+    A = rng.standard_normal((n, n))
+    cov = (A @ A.T / n + np.eye(n)) * np.outer(width, width) / 2
+    P0 = rng.uniform(-1.0, 1.0, n)
+    used = list(range(1, n + 1))
+    split, k = [], 0
+    for b in blocks:
+        split.append(used[k:k + b])
+        k += b
+    start = np.tile(P0, (W, 1)) + 0.1 * rng.standard_normal((W, n)) * width
+    images = []
+    for mode in (-1, force):
+        s = BatchedMCMC(W, n, used, split, 0, P0 - 20 * width, P0 + 20 * width, propose_scale=2.4,
+                        seed_ij=4114, seed_kl=9373)
+        s.set_covariance(np.diag(width ** 2))
+        s.set_test_gaussian(cov, P0)
+        assert N.lib().cmamd_debug_stage_R(s._h, mode) == 0
+        s.set_start(start)
+        s.step(2 * max(blocks) + 3, fast_only=True)
+        s.step(3, fast_only=False)
+        s.step(max(blocks), fast_only=True)
+        images.append((s.save_state(), s.state()))
+        s.close()
+    (a, sa), (b, sb) = images
+    assert np.any(sa[3] > 0)
+    for x, y in zip(sa, sb):
+        np.testing.assert_array_equal(x, y)
+    assert a == b
+
+
+@pytest.mark.parametrize("W,shared", [(512, True), (200, False)])
+def test_bin_corun_bitwise(tmp_path, W, shared):
+    """The bin co-run (config4_fast21's schedule: plik_lite binned into raw
+    sums inside the proposing launch, its quadratic form forming Delta = X -
+    S / cal^2 from them) leaves every walker's state, history row and
+    likelihood terms bit-identical to the unpipelined steps (plik_bin_delta +
+    quadform_ksplit), across the 21-wide block's rotations (rot_kernel between
+    the proposing launch and the quadratic form); the walkers' terms match
+    the plik_lite oracle."""
+    from cosmomc_amd import _native as N
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    n = 21
+    data = syn.make_plik_lite(12345)
+    rng = np.random.default_rng(2121)
+    width = np.concatenate([[0.0025], rng.uniform(0.05, 2.0, n - 1)])
+    A = rng.standard_normal((n - 1, n - 1))
+    corr = A @ A.T / (n - 1) + np.eye(n - 1)
+    d = np.sqrt(np.diag(corr))
+    cov = np.zeros((n, n))
+    cov[0, 0] = 1.0
+    cov[1:, 1:] = corr / d[:, None] / d[None, :] * np.outer(width[1:], width[1:])
+    P0 = np.concatenate([[1.0], rng.uniform(-1.0, 1.0, n - 1)])
+    pmin, pmax = P0 - 20 * width, P0 + 20 * width
+    pmin[0], pmax[0] = 0.9, 1.1
+    pm, ps = np.zeros(n), np.zeros(n)
+    pm[0], ps[0] = 1.0, 0.0025
+    used = list(range(1, n + 1))
+    th = syn.walker_theory(1 if shared else W, seed=5, n_fields=3, ld_field=2512)
+    dl = torch.tensor(th, device="cuda")
+    if shared:
+        dl = dl.expand(W, th.shape[1], th.shape[2])
+    g = syn.gaussians(123, W * n).reshape(W, n)
+    start = np.clip(P0 + 2 * width * g, pmin + 1e-9, pmax - 1e-9)
+    out = []
+    for mode in (1, 0):
+        plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path / f"m{mode}")))
+        plik.nuisance_indices = [1]
+        smp = BatchedMCMC(W, n, used, [used], 0, pmin, pmax, pm, ps, propose_scale=2.4, seed_ij=4004, seed_kl=9373)
+        smp.set_covariance(np.diag(width ** 2))
+        smp.set_test_gaussian(cov, P0)
+        smp.add_likelihood(plik, dl)
+        assert N.lib().cmamd_debug_pipeline(smp._h, mode) == 0
+        smp.set_start(start)
+        smp.enable_history(64)
+        smp.step(25, fast_only=True)
+        smp.step(19, fast_only=True)
+        k = smp.history_count()
+        out.append((smp.history_host(0, k), smp.history_terms(0, k), smp.save_state(), *smp.state()))
+        smp.close()
+    a, b = out
+    assert np.any(a[6] > 0)
+    for x, y in zip(a, b):
+        if isinstance(x, bytes):
+            assert x == y
+        else:
+            np.testing.assert_array_equal(x, y)
+    orc = po.PlikLite(data)
+    terms = a[1]
+    P = a[3]
+    for w in (0, W // 2 - 1, W - 1):   # the last history row's plik term at the walker's point
+        ref = orc.loglike(th[0 if shared else w], P[w, 0])
+        assert terms[-1, 0, w] == pytest.approx(ref, rel=1e-9)
 
 
 def _config5_sampler(refdata, tmp_path, W, groups):

@@ -27,14 +27,14 @@ if len(sys.argv) > 2 and sys.argv[1] == "--summary":
 
 import bench  # noqa: E402
 
-if os.environ.get("C4_NO_STAGE_R"):         # debug: rotation rows read in place instead of staged
+if os.environ.get("C4_STAGE_R"):            # debug: rotation rows staged (1) or read in place (0)
     from cosmomc_amd import _native as N
     from cosmomc_amd.sampler import BatchedMCMC
     _orig = BatchedMCMC.set_covariance
 
     def _patched(self, cov):
         _orig(self, cov)
-        assert N.lib().cmamd_debug_stage_R(self._h, 0) == 0
+        assert N.lib().cmamd_debug_stage_R(self._h, int(os.environ["C4_STAGE_R"])) == 0
     BatchedMCMC.set_covariance = _patched
 with tempfile.TemporaryDirectory() as td:
     print(bench.config4_run(512, 0, 1, td, -1, steps=42))

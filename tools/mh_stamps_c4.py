@@ -32,6 +32,8 @@ smp = BatchedMCMC(W, n, used, [used], 0, P0 - 20 * width, P0 + 20 * width, propo
                   seed_kl=9373)
 smp.set_covariance(np.diag(width ** 2))
 smp.set_test_gaussian(cov, P0)
+if os.environ.get("C4_STAGE_R"):     # force the rotation rows staged (1) or in HBM (0)
+    assert N.lib().cmamd_debug_stage_R(smp._h, int(os.environ["C4_STAGE_R"])) == 0
 smp.set_start(np.tile(P0, (W, 1)))
 rows = []
 for step in range(44):
@@ -40,14 +42,18 @@ for step in range(44):
     st = np.zeros((64, 16), dtype=np.uint64)
     assert N.lib().cmamd_debug_stamps(st.ctypes.data_as(C.c_void_p)) == 0
     d = np.diff(st[:W // 16, :7].astype(np.int64), axis=1)   # 16-walker blocks
-    rows.append(np.median(d, axis=0))
+    fine = [(2, 8), (8, 9), (9, 10), (10, 11), (11, 3), (3, 14), (14, 15), (15, 4), (4, 12), (12, 13), (13, 5)]
+    f = [np.median(st[:W // 16, b].astype(np.int64) - st[:W // 16, a].astype(np.int64)) if st[:W // 16, b].any()
+         else 0 for a, b in fine]
+    rows.append(np.concatenate([np.median(d, axis=0), f]))
 rows = np.array(rows)
 rt = np.zeros(3, dtype=np.uint64)
 fn = N.lib().cmamd_debug_rot_ticks
 fn.argtypes = [C.c_void_p]
 assert fn(rt.ctypes.data) == 0
 print(f"rot_kernel first listed walker, last rotation: total {rt[0]} ticks, Gaussian draws {rt[1]}, Gram-Schmidt {rt[2]}")
-names = ["dma issue", "dma wait", "accept", "propose", "wb issue", "drain"]
-print("step  " + " ".join(f"{x:>10s}" for x in names))
+names = ["dma issue", "dma wait", "accept", "propose", "wb issue", "drain", "a:terms", "a:target", "a:randexp",
+         "a:move", "a:hist", "p:copy", "p:prop", "p:post", "p:map", "p:scatter", "p:wb"]
+print("step  " + " ".join(f"{x:>9s}" for x in names))
 for i, r in enumerate(rows):
-    print(f"{i:4d}  " + " ".join(f"{v:10.0f}" for v in r))
+    print(f"{i:4d}  " + " ".join(f"{v:9.0f}" for v in r))
