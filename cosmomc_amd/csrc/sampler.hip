@@ -270,7 +270,10 @@ __device__ void rot_matrix(Walker &k, int off, int n)
     }
 }
 
-static constexpr int ROT_DEFER_MIN = 8;   // blocks this wide get their rotations from rot_kernel
+// blocks this wide get their rotations from rot_kernel.  (Narrower ones stay
+// in the chain: config5_bk15_plik's 7-wide foreground block deferred measured
+// mh_kernel 34.2 -> 20.7 us plus rot_kernel 15.0 us a step, no gain.)
+static constexpr int ROT_DEFER_MIN = 8;
 
 __device__ void proposal_tail(const DevCfg &c, const Tabs &t, Walker &k, int b, int lp);
 __device__ void proposal_r(const DevCfg &c, const Tabs &t, Walker &k, int b, int n, double r1);
@@ -2209,12 +2212,13 @@ static void set_mh_lds(cmbs *s) {
     // multi-wave scratch rows stay in HBM and are read in place.
     DevCfg &d = s->dc;
     const size_t cap = 160 * 1024;
-    // the rotation rows stay in HBM when every rotation wider than one
-    // parameter is drawn by rot_kernel: the chain then only reads one column
+    // the rotation rows stay in HBM when they are many (128 or more) and
+    // every rotation wider than one parameter is drawn by rot_kernel: the
+    // chain then only reads one column
     // per proposal (fetched beside the image, pre_blk), and staging the n x n
     // rows in and out of LDS is most of the image (config4_fast21: 441 of
     // ~600 rows)
-    bool all_deferred = d.rot_defer != 0;
+    bool all_deferred = d.rot_defer != 0 && s->R_total >= 128;
     for (int bn : s->blk_n) all_deferred = all_deferred && (bn == 1 || bn >= ROT_DEFER_MIN);
     d.stage_R = s->stage_R_force >= 0 ? s->stage_R_force : (all_deferred ? 0 : 1);
     d.stage_cyc = d.stage_cov = 1;
@@ -3015,7 +3019,11 @@ void sampler_check_pipe(cmbs *s, bool wait) {
 // vectorised form and every walker proposes in one launch (one group, no
 // change mask, no rotations left to rot_kernel).
 static bool pipe_setup(cmbs *s, int fast_only) {
-    if (s->pipe_mode != 1 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on || s->dc.rot_defer) return false;
+    // (a wide block whose rotations rot_kernel draws is no obstacle when it is
+    // not a fast block: fast-only steps never propose it)
+    if (s->pipe_mode != 1 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on ||
+        (s->dc.rot_defer && s->rot_fast_any))
+        return false;
     const LikeSlot &P = s->likes[s->tp_like[0]];
     if (!s->tpass->vec_ok(P.dl, P.ld_field, P.ld_walker)) return false;
     if (s->pipe_ready == s->W) return true;
@@ -3211,7 +3219,8 @@ static void check_theory_fresh(const cmbs *s) {
 // quadratic form (plik_lite: every row calibrated) and a small chi^2 another
 // launch can carry (Planck lensing).  Sets up the raw-sum buffers once per W.
 static bool tail_setup(cmbs *s, int fast_only) {
-    if (s->pipe_mode < 2 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on || s->dc.rot_defer)
+    if (s->pipe_mode < 2 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on ||
+        (s->dc.rot_defer && s->rot_fast_any))
         return false;
     {
         const LikeSlot &P = s->likes[s->tp_like[0]];

@@ -770,6 +770,55 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
         assert np.array_equal(out[0][1], o[1])
 
 
+def test_pipelined_with_wide_slow_block(cmbl_golden, refdata, tmp_path):
+    """A slow block wide enough for rot_kernel's rotations (9 parameters) does
+    not keep fast-only steps off the pipelined schedule (fast-only steps never
+    propose it): mh_pass_kernel runs (mode 1) and the chains equal the
+    unpipelined steps' (mode 0) bit for bit."""
+    import os
+
+    from cosmomc_amd import _native as N
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    c = cmbl_golden["cases"]["lensing_consext8"]
+    W, n = 256, 10
+    data = syn.make_plik_lite(12345)
+    th = syn.walker_theory(W, seed=13, n_fields=10, ld_field=2512)
+    dl = torch.tensor(th, device="cuda")
+    P0 = np.concatenate([np.linspace(0.1, 0.9, n - 1), [1.0]])
+    pmin, pmax = P0 - 1.0, P0 + 1.0
+    pmin[-1], pmax[-1] = 0.9, 1.1
+    pm, ps = np.zeros(n), np.zeros(n)
+    pm[-1], ps[-1] = 1.0, 0.0025
+    out = []
+    for mode in (1, 0):
+        plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+        lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
+        plik.nuisance_indices = [n]
+        lens.nuisance_indices = [n]
+        s = BatchedMCMC(W, n, list(range(1, n + 1)), [list(range(1, n)), [n]], 1, pmin, pmax, pm, ps,
+                        seed_ij=81, seed_kl=92)
+        s.set_covariance(np.diag(np.concatenate([np.full(n - 1, 0.01), [0.002]]) ** 2))
+        s.add_likelihood(plik, dl)
+        s.add_likelihood(lens, dl)
+        assert N.lib().cmamd_debug_pipeline(s._h, mode) == 0
+        s.enable_history(12)
+        s.set_start(np.tile(P0, (W, 1)))
+        N.profile_enable(True)
+        N.profile_reset()
+        s.step(5, fast_only=True)
+        s.step(7, fast_only=True)
+        torch.cuda.synchronize()
+        launches = N.profile_read("mh_pass_kernel")[1]
+        N.profile_enable(False)
+        assert (launches == 12) if mode == 1 else (launches == 0)
+        out.append((s.history_host(0, 12), s.history_terms(0, 12), s.save_state()))
+        s.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2]
+
+
 @pytest.mark.parametrize("mode", [3, 1, "bin"])
 def test_pipelined_handoff_giveup_fails_loudly(cmbl_golden, refdata, tmp_path, mode):
     """In-launch hand-offs fail loudly.  Mode 3: the unified step launch's
@@ -963,7 +1012,7 @@ def test_rotation_rows_in_place_match_staged(blocks, W, force):
     LDS image leave every walker's whole state bit-identical, over several
     rotations per walker, rotating steps (rot_kernel) and fast-only steps
     alike; [4, 17] forces the in-place rows with a 4-wide block rotating inside
-    the chain."""
+    the chain (below ROT_DEFER_MIN)."""
     from cosmomc_amd import _native as N
     from cosmomc_amd.sampler import BatchedMCMC
     n = sum(blocks)
