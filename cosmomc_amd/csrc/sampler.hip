@@ -1135,14 +1135,7 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fa
         tail_arrive(tw, lb * SMALL_WT / 64);
     } else if (rr.x == TAIL_PASS) {
         if (lb >= t.np) return;
-        if (!t.p_stride) {
-            tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
-            return;
-        }
-        for (int u = lb; u < t.tp.nblk; u += t.p_stride) {   // this CU's units, one after another
-            tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), u);
-            __syncthreads();                                    // the next unit reuses the LDS
-        }
+        tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
     } else if (lb < nmh) {
         mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, 0, lds, lb, ACCEPT ? &tw : nullptr);
     }
@@ -3326,14 +3319,6 @@ static StepTail make_tail(cmbs *s, int rd, int wr) {
         t.ld_field = P.ld_field;
         t.ld_walker = P.ld_walker;
         t.np = s->tpass->n_blocks();
-        static const bool persist = [] {
-            const char *e = std::getenv("CMAMD_PASS_PERSIST");
-            return e && *e == '1';
-        }();
-        if (persist) {   // one workgroup per table column (a CU's units in turn)
-            t.p_stride = s->tpass->n_per_round();
-            t.np = t.p_stride;
-        }
     }
     return t;
 }

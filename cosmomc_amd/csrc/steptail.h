@@ -39,7 +39,6 @@ struct StepTail {
     const double *dl = nullptr;
     long long ld_field = 0, ld_walker = 0;
     int np = 0;              // pass workgroups (TheoryPass::n_blocks), 0: none
-    int p_stride = 0;        // persistent pass (0: off): workgroup j runs table entries j, j + p_stride, ...
     int W = 0;
 };
 

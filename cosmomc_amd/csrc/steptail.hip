@@ -52,11 +52,7 @@ __global__ __launch_bounds__(256, 3) void step_tail_kernel(StepTail t, const int
         if (lb < t.ng) small_gauss_body<SMALL_WT, true>(t.g, tail_lds, lb);
     } else if (rr.x == TAIL_PASS) {
         if (lb >= t.np) return;
-        for (int u = lb; u < (t.p_stride ? t.tp.nblk : lb + 1); u += (t.p_stride ? t.p_stride : 1)) {
-            tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(tail_lds),
-                                        u);
-            if (t.p_stride) __syncthreads();   // the next unit reuses the LDS
-        }
+        tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(tail_lds), lb);
     }
 }
 

@@ -94,9 +94,6 @@ class TheoryPass {
     // its arguments and block count for W walkers (theorypass_body.h)
     TPDev dev_args(const TPOut *outs, int W);
     int n_blocks() const { return nblk; }
-    // the block table's rounds: entry j of round r is block r * n_per_round() + j
-    // (plan_units: CU c of an XCD gets its units in rounds)
-    int n_per_round() const { return per_round; }
 
     int n_items() const { return (int)items.size(); }
     const TPItem &item(int k) const { return items[k]; }
