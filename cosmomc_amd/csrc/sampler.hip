@@ -3726,6 +3726,22 @@ static bool eval_likes_drag_pair(cmbs *s, hipStream_t stream, bool both = true) 
     return true;
 }
 
+// Whether likelihood i's accepted-theory copy repeats an earlier likelihood's
+// (the same end and walker theory buffers and strides: fused likelihoods
+// usually read one): then it is skipped, the copy being idempotent
+static bool same_theory_swap(const cmbs *s, int i) {
+    const auto &e = s->end_theory[i];
+    const auto &l = s->likes[i];
+    for (int j = 0; j < i; j++) {
+        const auto &ej = s->end_theory[j];
+        const auto &lj = s->likes[j];
+        if (ej.dl == e.dl && ej.ld_walker == e.ld_walker && lj.dl == l.dl && lj.ld_walker == l.ld_walker &&
+            std::min(ej.ld_walker, lj.ld_walker) >= std::min(e.ld_walker, l.ld_walker))
+            return true;
+    }
+    return false;
+}
+
 void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_fn fn, void *user,
                        hipStream_t stream) {
     rot_schedule_unknown(s);           // the drag proposals move the blocks' loop indices
@@ -3798,6 +3814,7 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
             const long long n = std::min(e.ld_walker, l.ld_walker) > 0 ? std::min(e.ld_walker, l.ld_walker)
                                                                         : 10 * l.ld_field;
             if (l.ld_walker == 0) fail(CMBL_ERR_ARG, "dragging needs per-walker theory rows (ld_walker > 0)");
+            if (same_theory_swap(s, i)) continue;
             hipLaunchKernelGGL(drag_swap_theory, dim3(16, s->W), dim3(256), 0, stream, g.di, 4, s->W, e.dl,
                                e.ld_walker, const_cast<double *>(l.dl), l.ld_walker, n);
             HIP_CHECK(hipGetLastError());
@@ -3817,6 +3834,7 @@ static void swap_accepted_theory(cmbs *s, hipStream_t stream) {
         const auto &e = s->end_theory[i];
         const auto &l = s->likes[i];
         const long long n = std::min(e.ld_walker, l.ld_walker);
+        if (same_theory_swap(s, (int)i)) continue;
         hipLaunchKernelGGL(drag_swap_theory, dim3(16, s->W), dim3(256), 0, stream, flag, 1, s->W, e.dl, e.ld_walker,
                            const_cast<double *>(l.dl), l.ld_walker, n);
         HIP_CHECK(hipGetLastError());
