@@ -1972,8 +1972,17 @@ __global__ void drag_swap_theory(const int *flag, int value, int W, const double
 {
     const int w = blockIdx.y;
     if (w >= W || flag[w] != value) return;
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-        dstth[(long long)w * dst_ld + i] = src[(long long)w * src_ld + i];
+    const double *a = src + (long long)w * src_ld;
+    double *d = dstth + (long long)w * dst_ld;
+    const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x, stride = (long long)gridDim.x * blockDim.x;
+    if (((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {   // 16-byte moves
+        const long long n2 = n / 2;
+        for (long long i = t; i < n2; i += stride)
+            reinterpret_cast<double2 *>(d)[i] = reinterpret_cast<const double2 *>(a)[i];
+        if (t == 0 && (n & 1)) d[n - 1] = a[n - 1];
+    } else {
+        for (long long i = t; i < n; i += stride) d[i] = a[i];
+    }
 }
 
 // Starting point: -lnL of P = trial (likelihood terms already evaluated)
@@ -3815,7 +3824,7 @@ void sampler_step_drag(cmbs *s, int n_steps, double dragging_steps, cmbs_theory_
                                                                         : 10 * l.ld_field;
             if (l.ld_walker == 0) fail(CMBL_ERR_ARG, "dragging needs per-walker theory rows (ld_walker > 0)");
             if (same_theory_swap(s, i)) continue;
-            hipLaunchKernelGGL(drag_swap_theory, dim3(16, s->W), dim3(256), 0, stream, g.di, 4, s->W, e.dl,
+            hipLaunchKernelGGL(drag_swap_theory, dim3(8, s->W), dim3(256), 0, stream, g.di, 4, s->W, e.dl,
                                e.ld_walker, const_cast<double *>(l.dl), l.ld_walker, n);
             HIP_CHECK(hipGetLastError());
         }
