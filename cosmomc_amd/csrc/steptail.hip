@@ -60,12 +60,12 @@ __global__ __launch_bounds__(256, 3) void step_tail_kernel(StepTail t, const int
 
 // The rows' order: CMAMD_TAIL_ORDER lists the roles (q: quadratic form, g:
 // chi^2, p: pass) in dispatch order; "q*p" deals the q and p rows in
-// proportion to their counts, interleaved.  Default "qpg".
+// proportion to their counts, interleaved.  Default "qpg" for the step tails
+// and "gqp" for the unified launch (nm > 0; "qpg" measured 58.4 against 40.9
+// us/step there).
 std::vector<int2> tail_rows(int nq, int ng, int np, int nm) {
-    static const std::string order = [] {
-        const char *e = std::getenv("CMAMD_TAIL_ORDER");
-        return std::string(e && *e ? e : "qpg");
-    }();
+    static const char *env = std::getenv("CMAMD_TAIL_ORDER");
+    const std::string order = env && *env ? env : (nm > 0 ? "gqp" : "qpg");
     const int cnt[3] = {(nq + 7) / 8, (ng + 7) / 8, (np + 7) / 8};
     auto role = [](char c) { return c == 'q' ? TAIL_QF : c == 'g' ? TAIL_GAUSS : c == 'p' ? TAIL_PASS : -1; };
     std::vector<int2> rows;
