@@ -3023,7 +3023,8 @@ void sampler_check_pipe(cmbs *s, bool wait) {
 static bool pipe_setup(cmbs *s, int fast_only) {
     // (a wide block whose rotations rot_kernel draws is no obstacle when it is
     // not a fast block: fast-only steps never propose it)
-    if (s->pipe_mode != 1 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on ||
+    // (mode 3 falls back here when its step tails cannot be set up)
+    if ((s->pipe_mode != 1 && s->pipe_mode != 3) || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on ||
         (s->dc.rot_defer && s->rot_fast_any))
         return false;
     const LikeSlot &P = s->likes[s->tp_like[0]];
@@ -3045,8 +3046,9 @@ static bool pipe_setup(cmbs *s, int fast_only) {
 // no fused pass, one walker group, no change mask.  Allocates the raw sums and
 // sets up the calibration hand-off (as pipe_setup).
 static bool bin_setup(cmbs *s, int fast_only, PlikBinArgs &pb) {
-    if (s->pipe_mode != 1 || !fast_only || s->tpass || s->n_groups != 1 || s->mask_on || s->likes.size() != 1 ||
-        !is_deferred(s, 0))
+    // (mode 3 needs the fused pass, so it falls back here with plik_lite alone)
+    if ((s->pipe_mode != 1 && s->pipe_mode != 3) || !fast_only || s->tpass || s->n_groups != 1 || s->mask_on ||
+        s->likes.size() != 1 || !is_deferred(s, 0))
         return false;
     const LikeSlot &L = s->likes[0];
     WinStage st;
