@@ -207,9 +207,10 @@ class ChainCollector:
         # the list capacity when that is smaller, so a long run thins and goes on instead of overflowing.
         # The items are history steps: the ring must still hold the second half of each list's window.
         self.thin_limit = min(500000, max(1, cap // 2)) if thin_limit is None else thin_limit
-        if self.thin_limit < 500000:
-            # a known divergence from the reference: its lists thin at 500000 items whatever
-            # their length; R-1 and the learnt proposals differ once a list passes this limit
+        if thin_limit is None and self.thin_limit < 500000:
+            # a known divergence from the reference, chosen here rather than by the caller: its
+            # lists thin at 500000 items whatever their length; R-1 and the learnt proposals
+            # differ once a list passes this limit (an explicit thin_limit is the caller's choice)
             warnings.warn(f"ChainCollector: lists are thinned at {self.thin_limit} items (history capacity "
                           f"{cap}), not at the reference's 500000 (SampleCollector.f90:300-304); size "
                           f"sample_capacity >= 1000000 to thin where the reference does", stacklevel=2)

@@ -867,10 +867,13 @@ static constexpr bool HL_VFREE = CMAMD_HL_VFREE;   // as DSYEV's own iteration l
 // traffic); the column norms are carried across rounds, so a round forms one
 // dot product, and the arithmetic is fused multiply-adds (the eigensolver is
 // not the reference's DSYEV, so no operation order is there to follow).  Pairs
-// with |a_lh| > 1e-15 sqrt(a_ll a_hh) are rotated; a sweep in which no pair had
-// |a_lh| > 1e-9 sqrt(a_ll a_hh) ends the solve (its own rotations, by the
-// quadratic convergence of cyclic Jacobi, leave every pair near 1e-18: no
-// separate check sweep).
+// with |a_lh| > 1e-15 sqrt(a_ll a_hh) are rotated; a sweep in which no pair of
+// a problem had |a_lh| > 1e-6 sqrt(a_ll a_hh) (HL_SWEEP_COS2 = 1e-12 on the
+// squares) ends that problem's solve (its own rotations, by the quadratic
+// convergence of cyclic Jacobi, leave every pair near 1e-12: no separate check
+// sweep).  The stop is per problem: a problem whose sweep met it rotates no
+// more while the other problems of its wave go on, so its result depends on
+// its own matrix only, not on which walkers share its wave.
 // Returns true on lanes whose pair still needed rotating in sweep
 // HL_MAX_SWEEPS (the caller fails that problem: NaN and a status bit).
 // VF (V-free): the matrices here are symmetric positive definite (C, and
@@ -895,6 +898,8 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
         __syncthreads();
     }
     bool failed = false;
+    bool done = !on;                              // this lane's problem has met the sweep stop
+    const unsigned long long gmask = (M == 64 ? ~0ull : ((1ull << M) - 1)) << ((on ? grp : 0) * M);
 #ifdef CMAMD_STAMPS
     unsigned long long ph0 = 0, ph1 = 0, ph2 = 0, nround = 0;
 #endif
@@ -923,7 +928,7 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
                 if (!VF) Vp[k] = __shfl(V[k], src);
             }
             const double np_ = __shfl(nrm, src);
-            if (on) {
+            if (!done) {
                 const bool low = r < p;
                 const double all = low ? nrm : np_, ahh = low ? np_ : nrm;
                 double alh = 0.0;
@@ -975,7 +980,11 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
         if (!__any(big) || sweep == HL_MAX_SWEEPS)
             if (lane == 0) atomicAdd(&g_hl_sweeps[which][sweep < 63 ? sweep : 63], 1u);
 #endif
-        if (!__any(big)) break;          // wave-uniform: converged groups keep checking
+        // per problem: a sweep with no big pair is its last (wave-uniform exit once
+        // every problem of the wave is done)
+        const unsigned long long bal = __ballot(big);
+        if (!(bal & gmask)) done = true;
+        if (!bal) break;
         if (sweep == HL_MAX_SWEEPS) {
             failed = big;
             break;

@@ -44,7 +44,27 @@ struct TabLayout {
     int mapping, pmin, pmax, pmean, pstd, lin_w, lin_m, lin_s, covinv, center, n_dbl;
 };
 
+// The lean Metropolis chain (mhlean.h): fast-only steps whose only fast
+// parameter is a one-parameter block (the headline's calPlanck).  The host
+// resolves the block's rows, changed parameters, mapping column and the
+// likelihoods' nuisance indices into this struct per launch, so the chain
+// reads them from kernel arguments instead of LDS table lookups.
+static constexpr int LEAN_MAXC = 8;     // changed parameters of the block
+static constexpr int LEAN_MAXQ = 4;     // nuisance indices per likelihood
+// (every array below is indexed by compile-time indices only: an index known
+// only at run time would make the compiler copy the kernel arguments to scratch)
+struct LeanCfg {
+    int on;                             // this launch runs mh_lean
+    int nc;                             // changed parameters of the fast block
+    int r_row, cyc_row, blklp_row;      // its rotation row (sd), cyclic-index row, loop-index row (si)
+    int chg[LEAN_MAXC];                 // changed parameters (0-based)
+    double map[LEAN_MAXC];              // the block's mapping column (UpdateParams, propose.f90:142-149)
+    int nn[MAXLIKE];                    // likelihood l's nuisance parameters
+    int nuis[MAXLIKE][LEAN_MAXQ];       // their 0-based parameter indices
+};
+
 struct DevCfg {
+    LeanCfg lean;           // first: read in one batch at the start of the lean chain
     int W, np, n_used, nblocks, slow_n, fast_n, all_n, oversample_fast, max_blk, R_total;
     int ld;                 // row stride of sd / si / like_terms: W rounded up to 64
     double propose_scale, temperature;
@@ -236,6 +256,7 @@ struct cmbs {
     cmamd::DevBuf bin_S;                     // [wpad(W)][Np] raw bin sums (padding zero)
     size_t bin_lds = 0;                      // mh_bin_kernel's LDS
     int tp_why = 0;                          // set-up progress when no pass was built (debug)
+    bool lean_off = false;                   // debug: the generic chain where the lean one applies (cmamd_debug_lean)
     ~cmbs() {
         if (pipe_status_host) (void)hipHostFree(pipe_status_host);
         if (pipe_ev) (void)hipEventDestroy(pipe_ev);

@@ -79,15 +79,17 @@ struct Rng {
     double c;
     int i97, j97, iset;
     double gset;
+    int nd = 0;     // draws so far (the lean chain writes back the ring entries they overwrote)
 };
 
-__device__ double ranmar(Rng &r)
+__device__ __forceinline__ double ranmar(Rng &r)
 {   // RandUtils.f90:350-374
     double uni = r.u[r.i97 - 1] - r.u[r.j97 - 1];
     if (uni < 0.0) uni += 1.0;
     r.u[r.i97 - 1] = uni;
     if (--r.i97 == 0) r.i97 = 97;
     if (--r.j97 == 0) r.j97 = 97;
+    r.nd++;
     const double cd = 7654321.0 / 16777216.0, cm = 16777213.0 / 16777216.0;
     r.c -= cd;
     if (r.c < 0.0) r.c += cm;
@@ -96,7 +98,7 @@ __device__ double ranmar(Rng &r)
     return uni;
 }
 
-__device__ double gaussian1(Rng &r)
+__device__ __forceinline__ double gaussian1(Rng &r)
 {   // RandUtils.f90:156-178
     if (r.iset == 0) {
         double v1, v2, rr;
@@ -114,7 +116,7 @@ __device__ double gaussian1(Rng &r)
     return r.gset;
 }
 
-__device__ float randexp1(Rng &r)
+__device__ __forceinline__ float randexp1(Rng &r)
 {   // RandUtils.f90:189-233, REAL(4) arithmetic (built with -ffp-contract=off)
     const float alog2 = 0.6931471805599453f, a = 5.7133631526454228f, b = 3.4142135623730950f;
     const float c = -1.6734053240284925f, p = 0.9802581434685472f, aa = 5.6005707569738080f;
@@ -405,7 +407,7 @@ __device__ inline double test_row(const DevCfg &c, const Tabs &t, const Q &q, in
 // (0 where there is no prior) and the bounds verdict of q, formed by the other
 // thread groups: the same terms, summed here in the same order
 template <class Q, class L>
-__device__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const L &likes,
+__device__ __forceinline__ double target_like(const DevCfg &c, const Tabs &t, const Q &q, const L &likes,
                               const double *trows = nullptr, const double *zrows = nullptr, const int *oobv = nullptr)
 {
     // the parameter loops load RCH entries at a time (all in flight together;
@@ -580,9 +582,11 @@ __device__ inline void write_like_flags(const DevCfg &c, const QT &trial, const 
 // walker tile's quadratic-form and chi^2 workgroups have arrived (TailWait),
 // then acquires their write-through outputs.  The producers are all earlier in
 // the grid and wait on nothing, so the count arrives; the wait still gives up
-// after TAIL_WAIT_TICKS (10 ns s_memrealtime ticks) and sets the status word,
-// which the next step call reports as an error (sampler_check_pipe).
-static constexpr unsigned long long TAIL_WAIT_TICKS = 5000000ull;   // 50 ms
+// after TAIL_WAIT_SPINS polls and sets the status word, which the next step
+// call reports as an error (sampler_check_pipe).  The bound counts polls, not
+// wall-clock time: a poll does not advance while the wave is switched out (a
+// shared GPU), so a waiter restored before its producers never gives up early.
+static constexpr long TAIL_WAIT_SPINS = 1l << 24;   // x s_sleep(2) (~128 cycles): ~1 s
 
 __device__ __forceinline__ void tail_wait(const TailWait &tw, int tile)
 {
@@ -590,11 +594,10 @@ __device__ __forceinline__ void tail_wait(const TailWait &tw, int tile)
         const int gpt = 64 / tw.gwt, g0 = tile * gpt;
         const int gq = max(0, min(gpt, tw.ng - g0));
         const unsigned target = tw.epoch * (unsigned)(tw.nq_items + gq);
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        for (;;) {
+        for (long it = 0;; it++) {
             const unsigned v = __hip_atomic_load(tw.cnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (v >= target) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > TAIL_WAIT_TICKS) {
+            if (it == TAIL_WAIT_SPINS) {
                 atomicOr(tw.status, CMBL_STATUS_PIPE_WAIT);
                 break;
             }
@@ -611,11 +614,17 @@ __device__ __forceinline__ void tail_wait(const TailWait &tw, int tile)
     __syncthreads();
 }
 
+#include "mhlean.h"
+
 // tw: the unified step launch's wait (mh_step_kernel), else null
 template <bool ACCEPT, bool PROPOSE>
 __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *hist_row, double *hist_terms, int blk0,
                                         double *lds, int bx, const TailWait *tw = nullptr)
 {
+    if (c.lean.on) {   // a single one-parameter fast block (mhlean.h)
+        mh_lean<ACCEPT, PROPOSE>(c, hist_row, hist_terms, blk0, lds, bx, tw);
+        return;
+    }
     const Rows &R = c.rows;
     const int lane = threadIdx.x % MB, grp = threadIdx.x / MB;    // walker in block, thread group
     const int wl64 = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = MH_THREADS / 64;
@@ -1016,7 +1025,7 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_pass_kernel(DevCfg c, int fa
 // Delta after the launch.  The binning runs on the CUs the latency-bound
 // Metropolis chain leaves idle (it takes 32 of 256 at W = 512); only its
 // emit waits.  The bins wait on workgroups with lower ids (see mh_pass_kernel
-// for the dispatch-order assumption), bounded by TAIL_WAIT_TICKS with the
+// for the dispatch-order assumption), bounded by a count of polls (TAIL_WAIT_SPINS) with the
 // give-up reported by the next step call.
 template <bool ACCEPT>
 __global__ __launch_bounds__(MH_THREADS) void mh_bin_kernel(DevCfg c, int fast_only, double *hist_row,
@@ -1052,12 +1061,11 @@ __global__ __launch_bounds__(MH_THREADS) void mh_bin_kernel(DevCfg c, int fast_o
         }
     }
     if (threadIdx.x == 0) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         double cl;
-        for (;;) {
+        for (long it = 0;; it++) {   // bounded by polls (tail_wait): a safety net, reported loudly
             cl = __hip_atomic_load(c.calbuf + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((unsigned long long)__double_as_longlong(cl) != TP_PIPE_UNSET) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > TAIL_WAIT_TICKS) {   // a safety net: reported loudly
+            if (it == TAIL_WAIT_SPINS / 16) {
                 atomicOr(status, CMBL_STATUS_PIPE_WAIT);
                 break;
             }
@@ -3089,6 +3097,40 @@ static void launch_bin_qf(cmbs *s, hipStream_t stream) {
     record_deferred(s, 0, d);
 }
 
+// The lean chain's LDS (mhlean.h's carve)
+static size_t lean_lds_bytes(const cmbs *s) {
+    const Rows &R = s->dc.rows;
+    return (size_t)(R.R + R.ND - R.P + MAXDEF * (QF_GROUPS + 1) + s->np) * MB * 8 + (size_t)(8 + 3) * MB * 4;
+}
+
+// Whether a launch of fast-only steps takes the lean chain (mhlean.h): the
+// only fast parameter is a one-parameter block, no test likelihood, no
+// linear-combination priors, no change mask; and that block's constants.
+static LeanCfg lean_cfg(const cmbs *s, int fast_only, bool masked) {
+    LeanCfg L{};
+    const DevCfg &d = s->dc;
+    if (s->lean_off || !fast_only || masked || s->fast_n != 1 || d.test_like || d.n_lin || d.n_like > MAXLIKE)
+        return L;
+    const int b = s->proposer_for_index[s->slow_n] - 1;
+    if (s->blk_n[b] != 1 || s->blk_nchanged[b] > LEAN_MAXC || lean_lds_bytes(s) > s->mh_lds) return L;
+    for (int l = 0; l < d.n_like; l++) {
+        const std::vector<int> &ni = s->likes[l].nidx;
+        if ((int)ni.size() > LEAN_MAXQ) return LeanCfg{};
+        L.nn[l] = (int)ni.size();
+        for (size_t q = 0; q < ni.size(); q++) L.nuis[l][q] = ni[q];
+    }
+    L.nc = s->blk_nchanged[b];
+    for (int j = 0; j < L.nc; j++) {
+        L.chg[j] = s->changed[s->blk_changed_off[b] + j];
+        L.map[j] = s->h_tab_d[d.tl.mapping + s->blk_map_off[b] + j];
+    }
+    L.r_row = d.rows.R + s->blk_R_off[b];
+    L.cyc_row = d.rows.CYC + s->all_n + s->slow_n;
+    L.blklp_row = d.rows.BLKLP + b;
+    L.on = 1;
+    return L;
+}
+
 static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const HistRow &row, hipStream_t stream,
                       int g0, int g1, bool masked = false, bool pipe = false, const PlikBinArgs *bin = nullptr) {
     const dim3 g((g1 - g0 + MB - 1) / MB), b(MH_THREADS);
@@ -3096,6 +3138,7 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
     const size_t lds = s->mh_lds;
     DevCfg dc = s->dc;
     dc.mask_on = masked ? 1 : 0;
+    dc.lean = lean_cfg(s, fast_only, masked);
     if (s->pending_def && !accept) fail(CMBL_ERR_ARG, "internal: deferred likelihoods without an accepting step");
     const bool rot = propose && rot_may_pend(s, fast_only, g0);
     if (rot) {                       // alternate the two rotation-list counters of this walker range
@@ -3223,8 +3266,10 @@ static void check_theory_fresh(const cmbs *s) {
 // quadratic form (plik_lite: every row calibrated) and a small chi^2 another
 // launch can carry (Planck lensing).  Sets up the raw-sum buffers once per W.
 static bool tail_setup(cmbs *s, int fast_only) {
+    // (the step tails carry the fused pair alone: a third likelihood falls back to mode 1,
+    // whose eval_likes runs every likelihood)
     if (s->pipe_mode < 2 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on ||
-        (s->dc.rot_defer && s->rot_fast_any))
+        (s->dc.rot_defer && s->rot_fast_any) || s->likes.size() != 2)
         return false;
     {
         const LikeSlot &P = s->likes[s->tp_like[0]];
@@ -3353,6 +3398,7 @@ static void launch_unified(cmbs *s, hipStream_t stream, bool propose, int rd, in
     StepTail t = make_tail(s, rd, wr);
     DevCfg dc = s->dc;
     dc.mask_on = 0;
+    dc.lean = lean_cfg(s, fast_only, false);
     dc.pub_on = 0;
     dc.n_def = 0;
     s->pending_def = 0;
@@ -4173,6 +4219,11 @@ extern "C" int cmamd_debug_tp_items(const cmbs *s, int *out, int cap) {   // (fi
 extern "C" int cmamd_debug_pipeline(cmbs *s, int mode) {   // fast-step schedule (sampler_step): 0 unpipelined,
     if (!s || mode < 0 || mode > 4) return -1;    // 1 mh_pass_kernel, 2 step tails, 3 unified, 4 interleaved halves
     s->pipe_mode = mode;
+    return 0;
+}
+extern "C" int cmamd_debug_lean(cmbs *s, int on) {   // the lean chain where it applies (1, default) or mh_body (0)
+    if (!s) return CMBL_ERR_ARG;
+    s->lean_off = !on;
     return 0;
 }
 extern "C" int cmamd_debug_corun(cmbs *s, int on) {     // the lensing chi^2 inside plik's quadratic-form launch

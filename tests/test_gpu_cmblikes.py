@@ -148,3 +148,35 @@ def test_hl_non_positive_definite_theory_is_nan(cmbl_golden, refdata, case):
     good = [w for w in range(W) if w not in bad]
     ref = np.array([o.loglike(th[w], nu[w]) for w in good])
     np.testing.assert_allclose(got[good], ref, rtol=1e-9, atol=1e-8)
+
+
+@pytest.mark.parametrize("case", ["bkplanck_all_maps", "bk15_B_12maps"])
+def test_hl_result_independent_of_walker_order(cmbl_golden, refdata, case):
+    """A walker's HL -lnL depends on its own theory and nuisances only: the
+    Jacobi sweep stop is per problem (cmblikes.hip hl_ojacobi), so which
+    walkers share its wave does not change its bits.  The same 192 walkers in
+    their order, reversed, and in a random permutation give the same values
+    bit for bit, against one another and against each walker evaluated alone."""
+    c = cmbl_golden["cases"][case]
+    like = _open(refdata, c)
+    W = 192
+    th = syn.walker_theory(W, seed=5, lmax=c["lmax"])
+    base = np.array(c["nuis"])
+    nu = base[np.arange(W) % len(base)] * (1.0 + 1e-3 * np.sin(np.arange(W)))[:, None]
+    th[W // 2:] *= 1.0 + 0.05 * np.cos(np.arange(W - W // 2))[:, None, None]   # walkers far from the fiducial too
+
+    def run(order):
+        t = torch.tensor(np.ascontiguousarray(th[order]), device="cuda")
+        n = torch.tensor(np.ascontiguousarray(nu[order]), device="cuda")
+        out = np.empty(W)
+        out[order] = like.loglike_batch(t, n).cpu().numpy()
+        return out
+
+    ref = run(np.arange(W))
+    assert np.all(np.isfinite(ref))
+    for order in (np.arange(W)[::-1], np.random.default_rng(3).permutation(W)):
+        np.testing.assert_array_equal(run(order), ref)
+    for w in (0, 17, W - 1):
+        one = like.loglike_batch(torch.tensor(th[w:w + 1], device="cuda"), torch.tensor(nu[w:w + 1], device="cuda"))
+        assert one.cpu().numpy()[0] == ref[w]
+    assert like.status() == 0

@@ -596,8 +596,9 @@ def test_change_mask_matches_dense(cmbl_golden, refdata, tmp_path, shared_theory
     assert np.all(a[3] > 0)
     np.testing.assert_array_equal(a[3], b[3])
     np.testing.assert_array_equal(a[2], b[2])
-    np.testing.assert_allclose(a[0], b[0], rtol=1e-12)
-    np.testing.assert_allclose(a[1], b[1], rtol=1e-10)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[4], b[4])
     np.testing.assert_allclose(a[4], b[4], rtol=1e-10)
     # the terms at the final points are the oracles' values there
     import cmblikes_oracle as co
@@ -714,9 +715,12 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
     which step k + 1's quadratic form and lensing chi^2 calibrate as they read
     them (steptail.hip), with the proposing Metropolis kernel alone in between.  Mode 1: the pass of step k in the
     launch of the mh_kernel proposing it (mh_pass_kernel).  Mode 0: the
-    unpipelined schedule.  Chains, CurLike and both likelihood terms are
-    bit-identical over step() calls of 1, 2 and 5 steps.  The headline path is
-    pinned to the oracles directly: at the first and last recorded steps the
+    unpipelined schedule.  Each runs the lean Metropolis chain (mhlean.h: the
+    only fast parameter is a one-parameter block); modes 0 and 1 also run the
+    generic chain (mh_body), which the reference chains pin.  Chains, CurLike
+    and both likelihood terms are bit-identical over step() calls of 1, 2 and
+    5 steps.  The default schedule's own run is pinned to the oracles
+    directly: at the first and last recorded steps the
     terms of walkers 0, W/2 - 1 and W - 1 equal pyoracle.PlikLite's and
     CMBLikesOracle's -lnL at the recorded calibrations (rel 1e-9), and every
     walker's equals each likelihood's own loglike_batch (rtol 1e-12)."""
@@ -733,7 +737,7 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
     calls = (1, 2, 5)
     steps = sum(calls)
     out = []
-    for mode in (4, 3, 2, 1, 0):
+    for mode, lean in ((-1, 1), (4, 1), (3, 1), (2, 1), (1, 1), (0, 1), (1, 0), (0, 0)):
         plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
         lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
         plik.nuisance_indices = [2]
@@ -744,7 +748,9 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
         s.add_likelihood(plik, dl)
         s.add_likelihood(lens, dl)
         assert N.lib().cmamd_debug_fused(s._h) > 0
-        assert N.lib().cmamd_debug_pipeline(s._h, mode) == 0
+        if mode >= 0:                                     # -1: the default schedule
+            assert N.lib().cmamd_debug_pipeline(s._h, mode) == 0
+        assert N.lib().cmamd_debug_lean(s._h, lean) == 0
         s.enable_history(steps)
         s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
         for n in calls:
@@ -753,7 +759,7 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
             assert N.lib().cmamd_debug_tail(s._h) == W        # the step tails ran
         out.append((s.history_host(0, steps), s.history_terms(0, steps)))
         assert plik.status() == 0 and lens.status() == 0
-        if mode == 4:
+        if mode == -1:
             po_plik = po.PlikLite(data)
             o_lens = co.CMBLikesOracle(os.path.join(refdata, c["dataset"]), c["overrides"], c["tag"])
             for k in (0, steps - 1):
@@ -1166,10 +1172,11 @@ def test_config5_joint_path_vs_oracles(refdata, tmp_path):
     W = 1024, 5 fast steps): with the change mask on (one walker group: each
     likelihood re-evaluated only for the walkers whose trial moved one of its
     parameters, the HL kernels on compacted slots) the accept decisions,
-    multiplicities and points equal the dense path's (two walker groups:
-    every likelihood for every walker), and the terms at the final points of
-    walkers 0, 511 and 1023 are the oracles' (pyoracle.PlikLite,
-    CMBLikesOracle; rel 1e-9)."""
+    multiplicities, points and -lnL equal the dense path's (two walker groups:
+    every likelihood for every walker) bit for bit -- the HL eigensolves stop
+    per problem, so a walker's terms do not depend on which walkers share its
+    wave -- and the terms at the final points of walkers 0, 511 and 1023 are
+    the oracles' (pyoracle.PlikLite, CMBLikesOracle; rel 1e-9)."""
     import os
 
     import cmblikes_oracle as co
@@ -1186,8 +1193,9 @@ def test_config5_joint_path_vs_oracles(refdata, tmp_path):
     assert a[3].sum() > W // 4                       # walkers did move (about a third of the trials accepted)
     np.testing.assert_array_equal(a[3], b[3])
     np.testing.assert_array_equal(a[2], b[2])
-    np.testing.assert_allclose(a[0], b[0], rtol=1e-12)
-    np.testing.assert_allclose(a[1], b[1], rtol=1e-10)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[4], b[4])
     ob = co.CMBLikesOracle(os.path.join(refdata, "BK15/BK15_dust.dataset"), {"maps_use": maps}, "BKPLANCK")
     op = po.PlikLite(data)
     for w in (0, 511, 1023):
