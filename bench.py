@@ -19,7 +19,9 @@ per-step collective ("weak" scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 1024] [--no-lensing]
 
 The JSON line also carries, outside the headline value: "convergence" (R-1 vs
-wall-clock for the headline workload), "config4_fast21" (BASELINE configs[3]
+wall-clock for the headline workload), "config1_tt" (BASELINE configs[1]:
+plik_lite TT on the reference's fixed best-fit theory, 256 walkers per GPU),
+"config4_fast21" (BASELINE configs[3]
 as a sampler-throughput workload: 21 fast parameters, 512 walkers per GPU;
 full plik needs the absent clik), "config5_bk15_plik" (BASELINE
 configs[4]: BK15 + plik_lite jointly, fast-step throughput and R-1 vs
@@ -66,6 +68,8 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse ranks")
     p.add_argument("--converge-seconds", type=float, default=20.0,
                    help="R-1 vs wall-clock run after the throughput timing (0 = skip)")
+    p.add_argument("--config1-seconds", type=float, default=10.0,
+                   help="plik_lite TT at 256 walkers (BASELINE configs[1]) throughput and R-1 run (< 0 = skip)")
     p.add_argument("--config4-seconds", type=float, default=30.0,
                    help="21-fast-parameter sampler workload (BASELINE configs[3]) throughput and R-1 run (< 0 = skip)")
     p.add_argument("--config5-seconds", type=float, default=60.0,
@@ -304,6 +308,62 @@ def drag_run(W, rank, world, tmpdir, seconds, steps=20, dragging_steps=3.0):
     out["kernel_us_per_drag_step"] = tot
     if seconds > 0:
         out.update(run_to_convergence(smp, 1, 1, seconds, world, 40000, stepper=stepper))
+    return out
+
+
+N_B_TT = 215                                    # plik_lite TT bins
+N_L_TT = 2479                                   # l = 30..2508
+FLOPS_EVAL_TT = 2 * N_L_TT + 2 * N_B_TT * N_B_TT + 4 * N_B_TT   # 98,268 (SURVEY 8d with TT's sizes)
+BYTES_BIN_TT = 8 * N_L_TT + 8
+
+
+def config1_run(W, rank, world, tmpdir, seconds, steps=300):
+    """BASELINE configs[1]: plik_lite TT (batch2/plik_lite_TT.ini; the native
+    TT path stands in for its clik file) on fixed CAMB C_l -- the reference's
+    own base_plikHM best-fit theory_cl (tests/golden npz), one theory row for
+    every walker (ld_walker = 0) -- with calPlanck fast and its prior
+    (batch2/planck_calibration.ini), 256 walkers per GPU.  Fast-step
+    throughput, the per-kernel times and the step's roofline with TT's F and B
+    (F = 2 N_l + 2 N_b^2 + 4 N_b, B = 8 N_l + 8 per eval + C^-1
+    once per launch), and, when seconds > 0, R-1 vs wall-clock from an
+    overdispersed calPlanck start."""
+    import torch
+    from cosmomc_amd import synthetic as syn
+    from cosmomc_amd.likelihood import NativeCMBLikelihood
+    from cosmomc_amd.sampler import BatchedMCMC
+    plik = NativeCMBLikelihood("PLIK_LITE", syn.make_plik_lite(12345).write(os.path.join(tmpdir, "c1p"), use_cl="TT"))
+    plik.nuisance_indices = [1]
+    smp = BatchedMCMC(W, 1, [1], [[1]], 0, [0.9], [1.1], [1.0], [0.0025], propose_scale=2.4, seed_ij=1101 + rank,
+                      seed_kl=9373, first_walker=rank * W)
+    smp.set_covariance(np.array([[0.0025 ** 2]]))
+    base = syn.base_theory()[:3]
+    th = torch.zeros((1, 3, 2512), dtype=torch.float64, device="cuda")
+    th[0, :, :base.shape[1]] = torch.tensor(base, device="cuda")
+    smp.add_likelihood(plik, th.expand(W, 3, 2512))
+    smp.set_start((1.0 + 0.01 * syn.gaussians(11 + rank, W)).reshape(W, 1))
+    smp.step(20, fast_only=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    smp.step(steps, fast_only=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    per_gpu = W * steps / dt
+    ai = FLOPS_EVAL_TT / (BYTES_BIN_TT + 8 * N_B_TT * N_B_TT / W)
+    ceil = min(PEAK_FP64_TFLOPS * 1e12, ai * PEAK_HBM_GBS * 1e9)
+    out = {"workload": "plik_lite TT (215 bins, l 30..2508; batch2/plik_lite_TT.ini) on the reference's fixed "
+                       "base_plikHM theory_cl, calPlanck fast + prior",
+           "walkers_total": W * world, "evals_per_s": W * world * steps / dt, "ms_per_step": dt / steps * 1e3,
+           "step_roofline": {"achieved_tflops": per_gpu * FLOPS_EVAL_TT / 1e12, "ceiling_tflops": ceil / 1e12,
+                             "frac": per_gpu * FLOPS_EVAL_TT / ceil,
+                             "note": "per GPU: F = 98,268 flop/eval, B = 19,840 + 369,800 / W bytes/eval"}}
+    out["avg_kernel_us"], out["kernel_us_per_step"] = kernel_profile(smp, 100, per_step=True)
+    if seconds > 0:
+        out.update(run_to_convergence(smp, 0, 1, seconds, world, 20000))
     return out
 
 
@@ -757,6 +817,9 @@ def main():
         conv = None
         if args.converge_seconds > 0:
             conv = convergence_run(W, rank, world, td, args.converge_seconds, lensing=not args.no_lensing)
+        c1 = None
+        if args.config1_seconds >= 0:
+            c1 = config1_run(256, rank, world, td, args.config1_seconds)
         c4 = None
         if args.config4_seconds >= 0:
             c4 = config4_run(512, rank, world, td, args.config4_seconds)
@@ -802,6 +865,8 @@ def main():
         }
         if conv is not None:
             out["convergence"] = conv
+        if c1 is not None:
+            out["config1_tt"] = c1
         if c4 is not None:
             out["config4_fast21"] = c4
         if c5 is not None:

@@ -840,9 +840,14 @@ __device__ inline int hl_partner(int rr, int r) {   // round-robin pairing of ro
 }
 
 static constexpr int HL_MAX_SWEEPS = 40;
-// a sweep in which no pair was further from orthogonal than cos = 1e-6 is the
-// last (its own rotations leave every pair near cos 1e-12: -lnL moves by
-// ~1e-14 relative against the reference's DSYEV, tools/hl_margin.py)
+// a sweep in which no pair of a problem was further from orthogonal than
+// cos = 1e-6 is that problem's last (its own rotations leave every pair near
+// cos 1e-12: -lnL within 2.4e-14 relative of the reference's DSYEV on the BK
+// goldens, tools/hl_margin.py).  With the stop per problem a looser one buys
+// little, since a wave runs until its slowest problem stops: BK15 at W = 1024
+// HL 173.7 / 170.9 / 167.5 us at cos 1e-6 / 1e-5 / 1e-4, golden margins
+// 2.4e-14 / 2.3e-12 / 2.1e-10, and cos 1e-4 fails the 9-map width test's
+// rtol 1e-9 (round 5, profiles/r05_hl_stop.txt)
 #ifndef CMAMD_HL_SWEEP_COS2
 #define CMAMD_HL_SWEEP_COS2 1e-12
 #endif

@@ -281,8 +281,14 @@ unsigned int *QuadForm::counters(void *ws, int W) const {
 
 // Column-block chunk per work item: the largest chunk whose longest-first
 // greedy schedule over 2 workgroups/CU x 256 CUs is (near) the fastest,
-// counting a fixed per-workgroup overhead of half a block.
-int QuadForm::choose_kb(int tiles) {
+// counting a fixed per-workgroup overhead of half a block.  The chunk is
+// chosen once per matrix, for 16 walker tiles (W = 1024), not per launch:
+// the items fix the order in which a walker's sum is formed, so one choice
+// for every walker count keeps each walker's -lnL independent of how many
+// walkers share the launch (a walker group, a compacted change-mask slot
+// list or a single walker give the same bits).
+int QuadForm::choose_kb(int /*tiles*/) {
+    const int tiles = 16;
     auto itk = kb_for_tiles.find(tiles);
     if (itk != kb_for_tiles.end()) return itk->second;
     const int slots = 512;

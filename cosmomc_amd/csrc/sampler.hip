@@ -3409,24 +3409,25 @@ static void launch_unified(cmbs *s, hipStream_t stream, bool propose, int rd, in
         dc.def_part[0] = t.q.src.partial;
         dc.def_add[0] = nullptr;
     }
+    const int ng_rows = t.ng;
     TailWait tw{};
     tw.cnt = s->tail_cnt.as<unsigned int>();
     tw.epoch = s->tail_epoch + (accept ? 1u : 0u);
     tw.nq_items = t.q.src.n_items;
-    tw.ng = t.ng;
+    tw.ng = ng_rows;
     tw.gwt = SMALL_WT;
     tw.status = s->pipe_status.as<int>();
     tw.nosignal = s->tail_nosignal;
     const int nmh = (s->W + MB - 1) / MB;
     const int v = accept ? (propose ? 1 : 2) : 0;
     StepTailPlan &pl = s->uni_plan[v];
-    if (pl.key[0] != t.nq || pl.key[1] != t.ng || pl.key[2] != t.np) {
-        const std::vector<int2> rows = tail_rows(t.nq, t.ng, t.np, nmh);
+    if (pl.key[0] != t.nq || pl.key[1] != ng_rows || pl.key[2] != t.np) {
+        const std::vector<int2> rows = tail_rows(t.nq, ng_rows, t.np, nmh);
         pl.d_rows.alloc(rows.size() * sizeof(int2));
         pl.d_rows.upload(rows.data(), rows.size() * sizeof(int2));
         pl.nrows = (int)rows.size();
         pl.key[0] = t.nq;
-        pl.key[1] = t.ng;
+        pl.key[1] = ng_rows;
         pl.key[2] = t.np;
     }
     const dim3 grid((unsigned)pl.nrows * 8), b(MH_THREADS);

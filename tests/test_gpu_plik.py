@@ -184,3 +184,19 @@ def test_bad_dataset_errors(tmp_path, dataset):
         NativeCMBLikelihood("PLIK_LITE", dataset, {"use_cl": "BB"})   # selects no bins
     with pytest.raises(N.NativeError):
         NativeCMBLikelihood("NOT_A_TAG", dataset)
+
+
+def test_plik_tt_configs1_shape_vs_oracle(data, dataset):
+    """BASELINE configs[1]'s shape: plik_lite TT (batch2/plik_lite_TT.ini) on
+    one fixed theory (the reference's base_plikHM best fit, ld_walker = 0) for
+    256 walkers with their own calibrations: every walker's -lnL equals the
+    C oracle's (TT selection) to rtol 1e-10."""
+    like = _open(dataset, {"use_cl": "TT"})
+    orc = po.PlikLite(data, "TT")
+    W = 256
+    base = syn.base_theory()[:3]
+    th = torch.tensor(base, device="cuda").reshape(1, 3, -1).expand(W, 3, base.shape[-1])
+    cal = syn.walker_calibrations(W, seed=256)
+    got = like.loglike_batch(th, torch.tensor(cal, device="cuda").reshape(-1, 1)).cpu().numpy()
+    ref = np.array([orc.loglike(base, c) for c in cal])
+    np.testing.assert_allclose(got, ref, rtol=RTOL, atol=0)

@@ -107,17 +107,29 @@ def test_wide_chains_many_walkers_vs_oracle(rng_golden, name):
         assert like[w] == pytest.approx(likes[-1], rel=1e-9)
 
 
-def test_plik_fast_chain_vs_oracle(tmp_path):
-    """Fast-only Metropolis on calPlanck with native plik_lite TTTEEE on per-walker
-    cached theory + the calPlanck prior (batch2/planck_calibration.ini)."""
+@pytest.mark.parametrize("case", ["TTTEEE_per_walker", "TT_configs1"])
+def test_plik_fast_chain_vs_oracle(tmp_path, case):
+    """Fast-only Metropolis on calPlanck with native plik_lite + the calPlanck
+    prior (batch2/planck_calibration.ini): TTTEEE on per-walker cached theory
+    (96 walkers), and BASELINE configs[1]'s shape -- plik_lite TT
+    (batch2/plik_lite_TT.ini) on one fixed theory (the reference's
+    base_plikHM best fit, ld_walker = 0) for 256 walkers.  The one fast
+    parameter takes the lean chain (mhlean.h); checked walkers follow the C
+    oracle's chain step by step."""
     from cosmomc_amd.likelihood import NativeCMBLikelihood
     from cosmomc_amd.sampler import BatchedMCMC, walker_seed
     data = syn.make_plik_lite(12345)
-    like = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
+    tt = case == "TT_configs1"
+    like = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path), use_cl="TT" if tt else "TT TE EE"))
     like.nuisance_indices = [2]
-    W, steps = 96, 60
-    th = syn.walker_theory(W, seed=3, n_fields=3)
-    dl = torch.tensor(th, device="cuda")
+    W, steps = (256, 40) if tt else (96, 60)
+    if tt:
+        base = syn.base_theory()[:3]
+        th = np.broadcast_to(base, (W,) + base.shape)
+        dl = torch.tensor(base, device="cuda").reshape(1, 3, -1).expand(W, 3, base.shape[-1])
+    else:
+        th = syn.walker_theory(W, seed=3, n_fields=3)
+        dl = torch.tensor(th, device="cuda")
     np_ = 3
     P0 = np.array([0.0222, 1.0, 3.05])
     pmin = np.array([0.0222, 0.9, 3.05])
@@ -131,8 +143,8 @@ def test_plik_fast_chain_vs_oracle(tmp_path):
     s.step(steps, fast_only=True)
     P, lk, _, nacc = s.state()
     assert np.all(nacc > 0)
-    orc = po.PlikLite(data)
-    for w in (0, 5, 64, 95):
+    orc = po.PlikLite(data, "TT" if tt else "TT TE EE")
+    for w in ((0, 127, 128, 255) if tt else (0, 5, 64, 95)):
         ij, kl = walker_seed(55, 66, w)
         bn = np.array([1], dtype=np.int32)
         h = po.lib().orc_proposer_create(1, bn, np.array([1], dtype=np.int32), 0, 1, 2.4, 1,

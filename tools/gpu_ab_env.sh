@@ -1,8 +1,24 @@
-# A/B: headline bench with environment switches ("NAME=VALUE" arguments)
+#!/bin/bash
+# Interleaved A/B of the headline bench under environment switches.
+#   tools/gpu_ab_env.sh "base" "CMAMD_PIPE=3" "HIP_FORCE_DEV_KERNARG=0 CMAMD_PIPE=1" ...
+# Each argument is one variant ("base": no extra environment); REPS (default 2)
+# rounds run every variant in turn; BENCH_ARGS replaces the default bench
+# arguments (headline only, 300 steps).
 set -u
-mkdir -p gpurun_out
-for v in base "$@"; do
-  if [ "$v" = base ]; then envs=""; else envs="$v"; fi
-  env $envs timeout -k 10 300 python bench.py --steps 300 --no-cpu-baseline --converge-seconds 0 --config5-seconds -1 > gpurun_out/abe.json 2> gpurun_out/abe.err || exit $?
-  python -c "import json; d=json.load(open('gpurun_out/abe.json')); print('$v', round(d['value']/1e6,3), {k: round(v, 2) for k, v in d['roofline']['avg_kernel_us'].items() if v})"
+mkdir -p gpurun_out/ab
+REPS=${REPS:-2}
+ARGS=${BENCH_ARGS:---steps 300 --warmup 20 --no-cpu-baseline --converge-seconds 0 --config1-seconds -1 --config4-seconds -1 --config5-seconds -1 --drag-seconds -1}
+for rep in $(seq 1 $REPS); do
+  i=0
+  for v in "$@"; do
+    i=$((i + 1))
+    if [ "$v" = base ]; then envs=""; else envs="$v"; fi
+    env $envs timeout -k 10 300 python3 bench.py $ARGS > gpurun_out/ab/v${i}_$rep.json 2> gpurun_out/ab/v${i}_$rep.err || exit $?
+    python3 - "$v" "$rep" gpurun_out/ab/v${i}_$rep.json <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])
+print(f"[{sys.argv[1]}] rep {sys.argv[2]}: {d['value'] / 1e6:.3f} M evals/s {d['ms_per_step'] * 1e3:.2f} us/step",
+      {k: round(v, 2) for k, v in d["roofline"]["avg_kernel_us"].items() if v}, flush=True)
+PY
+  done
 done

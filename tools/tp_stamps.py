@@ -14,7 +14,7 @@ import tempfile
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "tools", "_stamps")
+OUT = os.environ.get("STAMP_OUT", os.path.join(ROOT, "tools", "_stamps"))
 if __name__ == "__main__":
     if "--no-build" not in sys.argv:
         subprocess.run(["make", "-C", os.path.join(ROOT, "cosmomc_amd", "csrc"), "-j8", f"OUT={OUT}",

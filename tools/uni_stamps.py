@@ -16,7 +16,7 @@ import tempfile
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "tools", "_stamps")
+OUT = os.environ.get("STAMP_OUT", os.path.join(ROOT, "tools", "_stamps"))
 ROLES = {1: "quadform", 2: "chi2", 3: "pass", 4: "metropolis"}
 
 if __name__ == "__main__":
