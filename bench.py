@@ -215,11 +215,10 @@ def convergence_run(W, rank, world, tmpdir, seconds, lensing=True):
     return out
 
 
-KERNELS = ("plik_bin_delta", "plik_quadform_ksplit", "plik_quadform_corun", "mh_kernel", "mh_pass_kernel",
-           "rot_kernel", "cmbl_bk_prologue", "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_hl_kernel",
-           "cmbl_quadform", "cmbl_gauss_small_kernel", "theory_window_kernel", "drag_kernel", "plik_quadform_pair",
-           "step_tail_kernel", "step_tail_last", "step_tail_pass", "mh_step_first", "mh_step_kernel",
-           "mh_step_last", "mh_half_kernel", "mh_bin_kernel")
+KERNELS = ("plik_bin_delta", "plik_quadform_ksplit", "plik_quadform_corun", "mh_kernel", "rot_kernel",
+           "cmbl_bk_prologue", "cmbl_window_kernel", "cmbl_reduce_kernel", "cmbl_hl_kernel", "cmbl_quadform",
+           "cmbl_gauss_small_kernel", "theory_window_kernel", "drag_kernel", "plik_quadform_pair", "mh_step_first",
+           "mh_step_kernel", "mh_step_last", "mh_bin_kernel")
 
 
 def kernel_profile(smp, steps, stepper=None, per_step=False):
@@ -671,7 +670,7 @@ def pmc_traffic(kernel, W):
                "cmbl_window_kernel": ("cmbl_window_direct",),
                "theory_window_kernel": ("theory_window_vec<2, 0>", "theory_window_kernel<2>", "theory_window_kernel<4>",
                                         "theory_window_kernel"),
-               "mh_pass_kernel": ("mh_pass_kernel<true>", "mh_pass_kernel")}.get(kernel, (kernel,))
+               "mh_step_kernel": ("mh_step_kernel<true, true>", "mh_step_kernel")}.get(kernel, (kernel,))
     t = next((d["per_launch"][k] for k in symbols if k in d["per_launch"]), None)
     if not t:
         return None, None
@@ -681,9 +680,9 @@ def pmc_traffic(kernel, W):
 def kernel_roofline(kern, avg_ms, W, fused_bytes, lens_bytes):
     """Roofline of one library kernel on this workload: its algorithmic work
     per launch (bytes for HBM-bound kernels, flops for MFMA-bound ones, both
-    for the step tail, which runs an HBM-bound pass and an MFMA-bound
-    quadratic form side by side) over its average launch time (HIP events).
-    Every library kernel has an entry, so frac is never null."""
+    for the unified step launch, which runs an HBM-bound pass and an
+    MFMA-bound quadratic form side by side) over its average launch time (HIP
+    events).  Every library kernel has an entry, so frac is never null."""
     t = avg_ms * 1e-3
     pass_bytes = W * fused_bytes[0] + fused_bytes[1]          # theory rows (each read once) + window weights
     qf_flops = W * FLOPS_QUADFORM                               # 2 N_b^2 + 2 N_b per walker (the kernel does ~half)
@@ -691,18 +690,14 @@ def kernel_roofline(kern, avg_ms, W, fused_bytes, lens_bytes):
         "plik_bin_delta": W * BYTES_BIN + 8 * N_B * W,
         "cmbl_window_kernel": W * lens_bytes[0] + lens_bytes[1],
         "theory_window_kernel": pass_bytes + 8 * N_B * W,      # + plik's Delta rows written
-        "mh_pass_kernel": pass_bytes + 8 * N_B * W,
-        "step_tail_pass": pass_bytes + 8 * N_B * W,            # + the raw bin sums written
-        # the pass (theory, weights, raw sums written) + the quadratic form's raw sums read and C^-1 once
-        "step_tail_kernel": pass_bytes + 2 * 8 * N_B * W + 8 * N_B * N_B,
         "mh_kernel": W * 1024,                                 # ~1 KB of walker state read + written (latency-bound)
-        # the unified step launch: the step tail's bytes + the Metropolis state
-        "mh_step_kernel": pass_bytes + 2 * 8 * N_B * W + 8 * N_B * N_B + W * 1024,
-        # an interleaved launch: half the walkers' pass, raw sums and state, C^-1 once
-        "mh_half_kernel": (pass_bytes + 2 * 8 * N_B * W + W * 1024) / 2 + 8 * N_B * N_B,
+        # the unified step launch, algorithmic bytes only: every walker's theory rows read once, the
+        # window weights and C^-1 once (not the raw sums the pass hands to the next launch's
+        # quadratic form, nor the ~1 KB per walker of Metropolis state)
+        "mh_step_kernel": pass_bytes + 8 * N_B * N_B,
     }
-    mfma = {"plik_quadform_ksplit": qf_flops, "plik_quadform_corun": qf_flops, "step_tail_last": qf_flops,
-            "step_tail_kernel": qf_flops, "mh_step_kernel": qf_flops, "mh_half_kernel": qf_flops / 2}
+    mfma = {"plik_quadform_ksplit": qf_flops, "plik_quadform_corun": qf_flops, "mh_step_kernel": qf_flops,
+            "mh_step_last": qf_flops}
     parts = {}
     if kern in hbm:
         a = hbm[kern] / t / 1e9

@@ -110,10 +110,10 @@ struct DevCfg {
     int def_like[MAXDEF], def_items[MAXDEF];
     const double *def_part[MAXDEF];         // [tiles][def_items][64]
     const double *def_add[MAXDEF];          // [W] or null
-    // pipelined fast steps (mh_pass_kernel): a proposing launch publishes the
-    // fused pass's two stage calibrations of every walker's trial into calbuf
-    // (this launch's half) and resets the other half to PIPE_UNSET for the
-    // next launch; the pass polls for its walkers' values
+    // bin co-run (mh_bin_kernel): a proposing launch publishes the trial
+    // calibrations of every walker into calbuf (this launch's half) and resets
+    // the other half to PIPE_UNSET for the next launch; the bin workgroups
+    // poll for their walkers' values
     int pub_on;                             // set per launch
     int pub_pcal[2];                        // the stages' calibration parameters (0-based, -1: none)
     double *calbuf;                         // [2 stages][ld], this launch's half
@@ -125,7 +125,7 @@ struct DevCfg {
     double *bin_delta;                      // [wpad(W)][Np] plik's Delta rows
 };
 
-// The unified step launch (pipe_mode 3, sampler.hip mh_step_kernel): its
+// The unified step launch (sampler.hip mh_step_kernel): its
 // Metropolis workgroups wait for their walker tile's quadratic-form and
 // chi^2 workgroups of the same launch, which arrive on a per-tile counter
 // after their outputs are stored write-through.  The counters only grow: a
@@ -218,33 +218,28 @@ struct cmbs {
     int tp_like[2] = {-1, -1};               // [0] plik_lite (Delta rows), [1] CMBlikes (partial rows)
     cmamd::WinStage tp_stage[2];
     bool no_corun = false;                   // debug: the fused pass's tails as separate launches
-    // pipelined fast steps: the fused pass of step k runs in the launch of
-    // the mh_kernel proposing it (sampler_step, mh_pass_kernel)
+    // the bin co-run's calibration hand-off (mh_bin_kernel)
     cmamd::DevBuf pipe_cal;                  // [2 halves][2 stages][ld] (DevCfg::calbuf)
-    size_t pipe_lds = 0;                     // mh_pass_kernel's LDS
-    unsigned pipe_epoch = 0;                 // proposing pipelined launches so far (its parity: the half)
+    unsigned pipe_epoch = 0;                 // proposing bin co-run launches so far (its parity: the half)
     int pipe_ready = 0;                      // set up for this W (0: not yet)
-    // split pipelined fast steps (pipe_mode 2, sampler_step): the fused pass of
-    // step k + 1 runs in step k's tail launch (steptail.h) and stores raw sums,
-    // which step k + 1's tails calibrate as they read them; the Metropolis
-    // kernel between two tails runs alone
-    int pipe_mode = 1;                       // 0 off, 1 mh_pass_kernel (default), 2 step tails, 3 unified, 4 halves
+    // fast-step schedule: 3 the unified step launch (default, where it applies;
+    // else the bin co-run or the unpipelined steps), 0 unpipelined (debug /
+    // A/B: CMAMD_PIPE, cmamd_debug_pipeline)
+    int pipe_mode = 3;
     cmamd::DevBuf tail_S[2][2];              // [parity][stage] the pass's raw sums
     cmamd::DevBuf tail_rowcal;               // the chi^2 stage's calibrated partial rows (SmallGaussLaunch::row_cal)
-    cmamd::StepTailPlan tail_plan[3];        // workgroup rows: tails + pass, tails, pass
     int tail_ready = 0;                      // W it is set up for (0: not yet, -W: not possible)
     int tail_qf = -1, tail_g = -1;           // the stage (0 / 1) of the quadratic form / of the chi^2
-    // unified step launches (pipe_mode 3): one launch per step holds step k's
+    // unified step launches: one launch per step holds step k's
     // tails, step k + 1's pass and the Metropolis workgroups that accept step k
     // (waiting per tile on the tails: TailWait) and propose step k + 1
     cmamd::DevBuf tail_cnt;                  // [tiles] TailWait::cnt
     size_t tail_cnt_bytes = 0;
     unsigned tail_epoch = 0;
     cmamd::StepTailPlan uni_plan[3];         // rows: propose + pass, tails + pass + accept/propose, tails + accept
-    cmamd::StepTailPlan half_plan[4];        // interleaved launches (pipe_mode 4), by Metropolis variant
     size_t uni_lds = 0;
     int tail_nosignal = 0;                   // debug (cmamd_debug_tail_nosignal)
-    // a pipelined hand-off that gave up (modes 1 and 3): the device word, its
+    // a pipelined hand-off that gave up (unified launch, bin co-run): the device word, its
     // pinned copy taken at the end of each step call, checked at the next
     cmamd::DevBuf pipe_status;
     int *pipe_status_host = nullptr;

@@ -28,19 +28,11 @@
 #include "sampler.h"
 #include "smallgauss.h"
 #ifdef CMAMD_STAMPS
-// mh_pass_kernel block timeline (tools/pipe_stamps.py): s_memrealtime at the
-// start, [pass] streaming done / wait done, end; [3] the block's role
 namespace cmamd {
-__device__ unsigned long long g_pipe_stamps[2048][5];
 // mh_step_kernel (tools/uni_stamps.py), middle launches only: start, the
 // Metropolis wait's end, XCC id, end, role + 1
 __device__ unsigned long long g_uni_stamps[2048][5];
 }
-#define TP_PIPE_STAMP(i)                                                                        \
-    do {                                                                                        \
-        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                         \
-        if (threadIdx.x == 0 && blockIdx.x < 2048) cmamd::g_pipe_stamps[blockIdx.x][i] = t_;    \
-    } while (0)
 #endif
 #include "theorypass_body.h"
 
@@ -974,59 +966,27 @@ __global__ __launch_bounds__(MH_THREADS) void mh_kernel(DevCfg c, int fast_only,
     mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, blk0, lds, blockIdx.x);
 }
 
-// A proposing mh_kernel and the fused window pass of the step it proposes in
-// one launch (the pipelined fast steps of sampler_step): the first nmh
-// workgroups are mh_kernel's (walker blocks 0 .. nmh - 1, the pad up to a
-// multiple of 8 idle so the pass's blocks keep their XCDs), the rest run the
-// pass (tp_vec_body<2, true>), which needs the new trial calibrations only for
-// its last phase and waits for its tile's Metropolis workgroups there.  Those
-// wait on nothing and have the lowest workgroup ids.  The HIP model does not
-// promise that workgroups are dispatched in id order (cdna_hip_programming.md
-// "Workgroups, grid, and XCD partitioning"); the hardware's dispatcher is
-// observed to, so the Metropolis workgroups are resident before any waiting
-// pass workgroup takes a slot and the wait ends.  The design does not rely on
-// it for correctness: the wait is bounded, and a give-up sets
-// CMBL_STATUS_PIPE_WAIT in the sampler's status word, which the next step
-// call or state readback turns into an error (sampler_check_pipe) instead of
-// silently rejected trials.  The latency-bound Metropolis blocks (64 CUs at
-// W = 1024) overlap the HBM-bound pass instead of preceding it.
-template <bool ACCEPT>
-__global__ __launch_bounds__(MH_THREADS, 3) void mh_pass_kernel(DevCfg c, int fast_only, double *hist_row,
-                                                                double *hist_terms, int nmh, int nmh_pad, TPDev tp,
-                                                                const double *dl, long long ld_field,
-                                                                long long ld_walker)
-{
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int b = blockIdx.x;
-    TP_PIPE_STAMP(0);
-    if (b < nmh_pad) {
-        if (b < nmh) mh_body<ACCEPT, true>(c, fast_only, hist_row, hist_terms, 0, lds, b);
-        TP_PIPE_STAMP(3);
-#ifdef CMAMD_STAMPS
-        if (threadIdx.x == 0 && b < 2048) cmamd::g_pipe_stamps[b][4] = 1;
-#endif
-        return;
-    }
-    tp_vec_body<2, true>(tp, dl, ld_field, ld_walker, c.W, reinterpret_cast<char *>(lds), b - nmh_pad);
-    TP_PIPE_STAMP(3);
-#ifdef CMAMD_STAMPS
-    if (threadIdx.x == 0 && b < 2048) cmamd::g_pipe_stamps[b][4] = 2;
-#endif
-}
-
 // A proposing mh_kernel with plik_lite's binning riding along (the bin
 // co-run of sampler_step): workgroups [0, nmh) are mh_kernel's, the pad up to
 // a multiple of 8 idle, the rest bin a walker each (its three fields in
 // turn: one workgroup per walker keeps the whole grid resident beside the
-// Metropolis workgroups' LDS size; plik_bin_products and the bin sums), wait for the walker's trial
-// calibration (published by its Metropolis workgroup, as for mh_pass_kernel)
-// and emit Delta = X - S / cal^2 into plik's rows -- or, for a walker whose proposal waits on a new
-// rotation (TP_PIPE_ROT), the raw sums, from which rot_kernel forms its
-// Delta after the launch.  The binning runs on the CUs the latency-bound
-// Metropolis chain leaves idle (it takes 32 of 256 at W = 512); only its
-// emit waits.  The bins wait on workgroups with lower ids (see mh_pass_kernel
-// for the dispatch-order assumption), bounded by a count of polls (TAIL_WAIT_SPINS) with the
-// give-up reported by the next step call.
+// Metropolis workgroups' LDS size; plik_bin_products and the bin sums), wait
+// for the walker's trial calibration (published by its Metropolis workgroup
+// into DevCfg::calbuf straight after the proposal) and emit
+// Delta = X - S / cal^2 into plik's rows -- or, for a walker whose proposal
+// waits on a new rotation (TP_PIPE_ROT), the raw sums, from which rot_kernel
+// forms its Delta after the launch.  The binning runs on the CUs the
+// latency-bound Metropolis chain leaves idle (it takes 32 of 256 at
+// W = 512); only its emit waits.
+// The bins wait on workgroups with lower ids.  The HIP model does not promise
+// that workgroups are dispatched in id order (cdna_hip_programming.md
+// "Workgroups, grid, and XCD partitioning"); the hardware's dispatcher is
+// observed to, so the Metropolis workgroups are resident before any waiting
+// bin workgroup takes a slot and the wait ends.  The design does not rely on
+// it for correctness: the wait is bounded by a count of polls
+// (TAIL_WAIT_SPINS), and a give-up sets CMBL_STATUS_PIPE_WAIT in the
+// sampler's status word, which the next step call or state readback turns
+// into an error (sampler_check_pipe) instead of silently rejected trials.
 template <bool ACCEPT>
 __global__ __launch_bounds__(MH_THREADS) void mh_bin_kernel(DevCfg c, int fast_only, double *hist_row,
                                                             double *hist_terms, int nmh, int nmh_pad, PlikBinArgs pb,
@@ -1143,46 +1103,9 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fa
         tail_arrive(tw, lb * SMALL_WT / 64);
     } else if (rr.x == TAIL_PASS) {
         if (lb >= t.np) return;
-        tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
+        tp_vec_body<2, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
     } else if (lb < nmh) {
         mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, 0, lds, lb, ACCEPT ? &tw : nullptr);
-    }
-}
-
-// The interleaved step launches (pipe_mode 4): the walkers form two halves a
-// step apart, and every launch runs one half's tails (quadratic form from raw
-// sums, lensing chi^2) beside the other half's Metropolis workgroups (accept
-// from the partials the previous launch left, propose) and window pass (raw
-// sums for that half's next tails).  No role waits on another inside the
-// launch: each consumes only what an earlier launch produced, so all of them
-// are resident together from the start.  A step costs two launches.
-struct HalfCfg {
-    int q_tile0;    // first walker tile of this launch's quadratic form
-    int g_blk0;     // first chi^2 workgroup (SMALL_WT walkers each)
-    int m_blk0;     // first Metropolis walker block (MB walkers each)
-    int nmh;        // Metropolis workgroups
-};
-
-template <bool ACCEPT, bool PROPOSE>
-__global__ __launch_bounds__(MH_THREADS, 3) void mh_half_kernel(DevCfg c, int fast_only, double *hist_row,
-                                                                double *hist_terms, StepTail t,
-                                                                const int2 *__restrict__ rows, HalfCfg h)
-{
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int2 rr = rows[blockIdx.x >> 3];
-    const int lb = rr.y * 8 + (blockIdx.x & 7);
-    if (rr.x == TAIL_QF) {
-        if (lb >= t.nq) return;
-        int item_ix, tile;
-        qf_place(lb, t.q.src.n_items, t.q.src.xcd_map, item_ix, tile);
-        qfs_body<false>(lds, item_ix, h.q_tile0 + tile, t.q);
-    } else if (rr.x == TAIL_GAUSS) {
-        if (lb < t.ng) small_gauss_body<SMALL_WT, true, false>(t.g, lds, h.g_blk0 + lb);
-    } else if (rr.x == TAIL_PASS) {
-        if (lb < t.np)
-            tp_vec_body<2, false, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
-    } else if (lb < h.nmh) {
-        mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, h.m_blk0, lds, lb);
     }
 }
 
@@ -2249,11 +2172,6 @@ static void set_mh_lds(cmbs *s) {
         d.itmp_g = s->itmp_g.as<int>();
     }
     const int lds = (int)s->mh_lds;
-    s->pipe_lds = std::max(s->mh_lds, (size_t)tp_vec_lds_bytes<2, true>());
-    HIP_CHECK(hipFuncSetAttribute((const void *)mh_pass_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)s->pipe_lds));
-    HIP_CHECK(hipFuncSetAttribute((const void *)mh_pass_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)s->pipe_lds));
     HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     HIP_CHECK(hipFuncSetAttribute((const void *)mh_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -2873,14 +2791,12 @@ static void eval_likes_masked(cmbs *s, hipStream_t stream, bool defer = false) {
 // likelihood terms of walkers [g0, g1) at their trial points
 // defer: the accepting mh_kernel launched next finishes the deferrable
 // likelihoods (all walkers, one group)
-// pass_done: the fused pass already ran (the pipelined steps' mh_pass_kernel)
-static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1, void *ws, bool defer = false,
-                       bool pass_done = false) {
+static void eval_likes(cmbs *s, hipStream_t stream, bool gather, int g0, int g1, void *ws, bool defer = false) {
     const int Wg = g1 - g0;
     if (defer && (g0 != 0 || g1 != s->W)) fail(CMBL_ERR_ARG, "internal: deferred evaluation of a walker group");
     const size_t nl = s->likes.size();
     const bool fuse = s->tpass && g0 == 0 && g1 == s->W;
-    if (fuse && !pass_done) {   // every nuisance slice first: the pass reads both likelihoods'
+    if (fuse) {   // every nuisance slice first: the pass reads both likelihoods'
         if (gather)
             for (size_t i = 0; i < nl; i++) {
                 const int nn = s->likes[i].like->like->n_nuis;
@@ -2962,31 +2878,6 @@ static bool rot_may_pend(cmbs *s, int fast_only, int g0) {
 
 static void rot_schedule_unknown(cmbs *s) { std::fill(s->rot_lp.begin(), s->rot_lp.end(), -1); }
 
-// The pipelined fast steps (sampler_step).  The fused window pass of step k
-// runs in the launch of the mh_kernel that proposes step k (mh_pass_kernel):
-// its blocks stream the theory while the Metropolis blocks work, store raw
-// sums, and apply the new calibrations once their tile's Metropolis blocks
-// have published them (tp_vec_body<2, true>).  Step k's tails (plik's
-// deferred quadratic form with the lensing chi^2) follow as before.  Every
-// step's pass still reads the theory once; the Metropolis blocks (64 CUs at
-// W = 1024) now overlap the HBM-bound pass instead of following it.
-// The pass's workgroups hold back this long (10 ns ticks of s_memrealtime)
-// at the start of the launch: the Metropolis workgroups' loads go ahead of the
-// pass's streaming, and those workgroups, whose end the pass waits for, end
-// sooner (block stamps, tools/pipe_stamps.py: Metropolis ends 18.2-23.6 us
-// without it, 16.1-22.4 with 2 us; mh_pass_kernel 27.1 / 24.2 / 25.3 / 26.1 us
-// for 0 / 2 / 3 / 4 us, MI355X, W = 1024; 1 / 1.5 / 2.5 us: 27.0-27.5 /
-// 24.6-24.7 / 24.8 against 24.1-24.5)
-static constexpr int PIPE_DELAY = 200;
-
-static TPOut pass_out(cmbs *s, int k) {
-    const int i = s->tp_like[k];
-    const WinStage &st = s->tp_stage[k];
-    Like &L = *s->likes[i].like->like;
-    return TPOut{st.kind, st.cal_index, st.ld, 0, L.window_out(s->like_ws[i].p, s->W), st.X, s->dc.like_nuis[i],
-                 (long long)std::max(1, L.n_nuis)};
-}
-
 // The pipelined hand-offs' give-up word (modes 1 and 3): zeroed here; copied
 // to pinned memory at the end of every pipelined step call (pipe_status_post)
 // and checked at the start of the next call and by the state readbacks
@@ -3025,37 +2916,13 @@ void sampler_check_pipe(cmbs *s, bool wait) {
     }
 }
 
-// Whether this run of fast steps can be pipelined: the fused pass takes its
-// vectorised form and every walker proposes in one launch (one group, no
-// change mask, no rotations left to rot_kernel).
-static bool pipe_setup(cmbs *s, int fast_only) {
-    // (a wide block whose rotations rot_kernel draws is no obstacle when it is
-    // not a fast block: fast-only steps never propose it)
-    // (mode 3 falls back here when its step tails cannot be set up)
-    if ((s->pipe_mode != 1 && s->pipe_mode != 3) || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on ||
-        (s->dc.rot_defer && s->rot_fast_any))
-        return false;
-    const LikeSlot &P = s->likes[s->tp_like[0]];
-    if (!s->tpass->vec_ok(P.dl, P.ld_field, P.ld_walker)) return false;
-    if (s->pipe_ready == s->W) return true;
-    pipe_status_init(s);
-    {   // both halves unset: the first launch publishes into half 1, resets half 0
-        const std::vector<unsigned long long> unset((size_t)4 * s->dc.ld, TP_PIPE_UNSET);
-        s->pipe_cal.alloc(unset.size() * 8);
-        s->pipe_cal.upload(unset.data(), unset.size() * 8);
-    }
-    s->pipe_epoch = 0;
-    s->pipe_ready = s->W;
-    return true;
-}
-
 // Whether this run of fast steps can take the bin co-run: one likelihood,
 // plik_lite, deferred (its quadratic form's combine in the next mh launch),
 // no fused pass, one walker group, no change mask.  Allocates the raw sums and
 // sets up the calibration hand-off (as pipe_setup).
 static bool bin_setup(cmbs *s, int fast_only, PlikBinArgs &pb) {
     // (mode 3 needs the fused pass, so it falls back here with plik_lite alone)
-    if ((s->pipe_mode != 1 && s->pipe_mode != 3) || !fast_only || s->tpass || s->n_groups != 1 || s->mask_on ||
+    if (s->pipe_mode == 0 || !fast_only || s->tpass || s->n_groups != 1 || s->mask_on ||
         s->likes.size() != 1 || !is_deferred(s, 0))
         return false;
     const LikeSlot &L = s->likes[0];
@@ -3132,7 +2999,7 @@ static LeanCfg lean_cfg(const cmbs *s, int fast_only, bool masked) {
 }
 
 static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const HistRow &row, hipStream_t stream,
-                      int g0, int g1, bool masked = false, bool pipe = false, const PlikBinArgs *bin = nullptr) {
+                      int g0, int g1, bool masked = false, const PlikBinArgs *bin = nullptr) {
     const dim3 g((g1 - g0 + MB - 1) / MB), b(MH_THREADS);
     const int blk0 = g0 / MB;
     const size_t lds = s->mh_lds;
@@ -3148,42 +3015,6 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
     dc.n_def = s->pending_def;
     s->pending_def = 0;
     dc.pub_on = 0;
-    if (pipe) {   // mh_pass_kernel: this launch proposes the step whose pass rides along
-        if (!propose || g0 != 0 || g1 != s->W || rot) fail(CMBL_ERR_ARG, "internal: pipelined step launch");
-        dc.pub_on = s->tail_nosignal ? 0 : 1;   // debug: never publish (the give-up test)
-        for (int k = 0; k < 2; k++) {
-            const WinStage &st = s->tp_stage[k];
-            dc.pub_pcal[k] = st.cal_index >= 0 ? s->likes[s->tp_like[k]].nidx[st.cal_index] : -1;
-        }
-        const unsigned e = s->pipe_epoch + 1;   // this launch's half e % 2; it resets the other for the next
-        dc.calbuf = s->pipe_cal.as<double>() + (size_t)(e % 2) * 2 * dc.ld;
-        dc.calbuf_next = s->pipe_cal.as<double>() + (size_t)((e + 1) % 2) * 2 * dc.ld;
-        const int nmh = (int)g.x, nmh_pad = (nmh + 7) / 8 * 8;
-        const TPOut o[2] = {pass_out(s, 0), pass_out(s, 1)};
-        TPDev tp = s->tpass->dev_args(o, s->W);
-        tp.calbuf = dc.calbuf;
-        tp.cal_ld = dc.ld;
-        for (int k = 0; k < 2; k++) tp.status[k] = s->pipe_status.as<int>();
-        tp.delay = PIPE_DELAY;
-        const LikeSlot &P = s->likes[s->tp_like[0]];
-        const dim3 gp(nmh_pad + s->tpass->n_blocks());
-        try {
-            timed_launch("mh_pass_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                if (accept)
-                    hipExtLaunchKernelGGL(mh_pass_kernel<true>, gp, b, s->pipe_lds, stream, e0, e1, 0, dc, fast_only,
-                                          row.p, row.t, nmh, nmh_pad, tp, P.dl, P.ld_field, P.ld_walker);
-                else
-                    hipExtLaunchKernelGGL(mh_pass_kernel<false>, gp, b, s->pipe_lds, stream, e0, e1, 0, dc, fast_only,
-                                          row.p, row.t, nmh, nmh_pad, tp, P.dl, P.ld_field, P.ld_walker);
-            });
-            HIP_CHECK(hipGetLastError());
-        } catch (...) {
-            s->pipe_ready = 0;   // both halves re-uploaded as unset next time
-            throw;
-        }
-        s->pipe_epoch = e;       // only a launched step moves the halves' parity
-        return;
-    }
     if (bin) {   // mh_bin_kernel: the proposing launch bins the theory beside the Metropolis workgroups
         if (!propose || g0 != 0 || g1 != s->W) fail(CMBL_ERR_ARG, "internal: bin co-run launch");
         Like &Q = *s->likes[0].like->like;
@@ -3268,7 +3099,7 @@ static void check_theory_fresh(const cmbs *s) {
 static bool tail_setup(cmbs *s, int fast_only) {
     // (the step tails carry the fused pair alone: a third likelihood falls back to mode 1,
     // whose eval_likes runs every likelihood)
-    if (s->pipe_mode < 2 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on ||
+    if (s->pipe_mode == 0 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on ||
         (s->dc.rot_defer && s->rot_fast_any) || s->likes.size() != 2)
         return false;
     {
@@ -3321,15 +3152,13 @@ static bool tail_setup(cmbs *s, int fast_only) {
         SmallGaussLaunch g{};
         G.corun_small(g, s->W, s->dc.like_nuis[gi], G.n_nuis, s->like_terms.as<double>() + (size_t)gi * s->dc.ld,
                       s->like_ws[gi].p);
-        s->uni_lds = std::max({s->mh_lds, (size_t)QFS_LDS_DOUBLES * 8, (size_t)tp_vec_lds_bytes<2, false>(),
+        s->uni_lds = std::max({s->mh_lds, (size_t)QFS_LDS_DOUBLES * 8, (size_t)tp_vec_lds_bytes<2>(),
                                (size_t)small_gauss_lds_doubles<SMALL_WT>(g.d.nX) * 8});
         for (const void *k : {(const void *)mh_step_kernel<false, true>, (const void *)mh_step_kernel<true, true>,
-                              (const void *)mh_step_kernel<true, false>, (const void *)mh_half_kernel<false, true>,
-                              (const void *)mh_half_kernel<true, true>, (const void *)mh_half_kernel<true, false>})
+                              (const void *)mh_step_kernel<true, false>})
             HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->uni_lds));
     }
     for (auto &pl : s->uni_plan) pl.key[0] = -1;
-    for (auto &pl : s->half_plan) pl.key[0] = -1;
     s->tail_ready = s->W;
     return true;
 }
@@ -3377,15 +3206,6 @@ static StepTail make_tail(cmbs *s, int rd, int wr) {
         t.np = s->tpass->n_blocks();
     }
     return t;
-}
-
-static void launch_tail(cmbs *s, hipStream_t stream, int rd, int wr) {
-    const StepTail t = make_tail(s, rd, wr);
-    const int v = rd >= 0 ? (wr >= 0 ? 0 : 1) : 2;
-    static const char *names[3] = {"step_tail_kernel", "step_tail_last", "step_tail_pass"};
-    launch_step_tail(t, s->tail_plan[v], stream, names[v]);
-    if (rd >= 0) record_deferred(s, (size_t)s->tp_like[s->tail_qf],
-                                 QFDeferred{t.q.src.partial, t.q.src.n_items, nullptr});
 }
 
 // One unified step launch (pipe_mode 3, mh_step_kernel): the tails of the
@@ -3453,96 +3273,6 @@ static void launch_unified(cmbs *s, hipStream_t stream, bool propose, int rd, in
     if (accept) s->tail_epoch++;
 }
 
-// Walker halves of the interleaved steps: [0, half_w) and [half_w, W), the
-// same whole number of 64-walker tiles each (so the pass's one unit plan
-// serves both); 0 when W does not split so.
-static int half_w(const cmbs *s) { return (s->W % 128 == 0 && s->W >= 128) ? s->W / 2 : 0; }
-
-// One interleaved launch (pipe_mode 4): half qh's tails (qh < 0: none), half
-// mh's Metropolis workgroups (mh < 0: none; accept: from the partials of the
-// previous launch, propose: the next trial) and half ph's pass (ph < 0: none).
-static void launch_half(cmbs *s, hipStream_t stream, int qh, int mh, bool accept, bool propose, int ph,
-                        const HistRow &row, int fast_only) {
-    const int Wh = half_w(s), th = Wh / QF_TILE, W = s->W;
-    StepTail t;
-    t.W = W;
-    HalfCfg h{};
-    if (qh >= 0) {
-        t = make_tail(s, 0, -1);
-        t.q.src.xcd_map = th % 8 == 0 ? 1 : 0;
-        t.nq = t.q.src.n_items * th;
-        t.ng = (Wh + SMALL_WT - 1) / SMALL_WT;
-        h.q_tile0 = qh * th;
-        h.g_blk0 = qh * (Wh / SMALL_WT);
-    }
-    if (ph >= 0) {
-        TPOut o[2];
-        for (int k = 0; k < 2; k++) {
-            const int i = s->tp_like[k];
-            const WinStage &st = s->tp_stage[k];
-            Like &L = *s->likes[i].like->like;
-            o[k] = TPOut{st.kind, st.cal_index, st.ld, 0, s->tail_S[0][k].as<double>(), st.X, s->dc.like_nuis[i],
-                         (long long)std::max(1, L.n_nuis)};
-        }
-        t.tp = s->tpass->dev_args(o, Wh);   // the plan for one half's tiles
-        t.tp.tile_off = ph * th;
-        const LikeSlot &P = s->likes[s->tp_like[0]];
-        t.dl = P.dl;
-        t.ld_field = P.ld_field;
-        t.ld_walker = P.ld_walker;
-        t.np = s->tpass->n_blocks();
-    }
-    DevCfg dc = s->dc;
-    dc.mask_on = 0;
-    dc.pub_on = 0;
-    dc.n_def = 0;
-    s->pending_def = 0;
-    if (mh >= 0) {
-        h.m_blk0 = mh * (Wh / MB);
-        h.nmh = Wh / MB;
-        if (accept) {   // plik's combine from the partials the previous launch left for this half
-            QFSource src;
-            const int qi = s->tp_like[s->tail_qf];
-            if (!s->likes[qi].like->like->qf_source(src, W, s->like_ws[qi].p))
-                fail(CMBL_ERR_ARG, "internal: interleaved step quadratic form");
-            dc.n_def = 1;
-            dc.def_like[0] = qi;
-            dc.def_items[0] = src.n_items;
-            dc.def_part[0] = src.partial;
-            dc.def_add[0] = nullptr;
-        }
-    }
-    const int v = mh < 0 ? 0 : !accept ? 1 : propose ? 2 : 3;   // kernel variant
-    StepTailPlan &pl = s->half_plan[v];
-    if (pl.key[0] != t.nq || pl.key[1] != t.ng || pl.key[2] != t.np) {
-        // the Metropolis rows first: their chain is the launch's longest; nothing waits, so any order is safe
-        std::vector<int2> rows;
-        for (int k = 0; k < (h.nmh + 7) / 8; k++) rows.push_back(int2{TAIL_MH, k});
-        const std::vector<int2> rest = tail_rows(t.nq, t.ng, t.np, 0);
-        rows.insert(rows.end(), rest.begin(), rest.end());
-        pl.d_rows.alloc(rows.size() * sizeof(int2));
-        pl.d_rows.upload(rows.data(), rows.size() * sizeof(int2));
-        pl.nrows = (int)rows.size();
-        pl.key[0] = t.nq;
-        pl.key[1] = t.ng;
-        pl.key[2] = t.np;
-    }
-    const dim3 grid((unsigned)pl.nrows * 8), b(MH_THREADS);
-    const int2 *rows = pl.d_rows.as<int2>();
-    timed_launch("mh_half_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-        if (v <= 1)
-            hipExtLaunchKernelGGL(mh_half_kernel<false, true>, grid, b, s->uni_lds, stream, e0, e1, 0, dc, fast_only,
-                                  row.p, row.t, t, rows, h);
-        else if (v == 2)
-            hipExtLaunchKernelGGL(mh_half_kernel<true, true>, grid, b, s->uni_lds, stream, e0, e1, 0, dc, fast_only,
-                                  row.p, row.t, t, rows, h);
-        else
-            hipExtLaunchKernelGGL(mh_half_kernel<true, false>, grid, b, s->uni_lds, stream, e0, e1, 0, dc, fast_only,
-                                  row.p, row.t, t, rows, h);
-    });
-    HIP_CHECK(hipGetLastError());
-}
-
 void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (!s->started) fail(CMBL_ERR_ARG, "cmbs_set_start must be called before cmbs_step");
     check_theory_fresh(s);
@@ -3553,23 +3283,7 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     // propose(1) | likes | accept(1)+propose(2) | likes | ... | likes | accept(n)
     const int G = s->n_groups;
     sampler_check_pipe(s);
-    if (G == 1 && s->pipe_mode == 4 && half_w(s) && tail_setup(s, fast_only)) {
-        // interleaved halves A, B: M_A(propose 1) + P_A | Q_A(1) + M_B(propose 1) + P_B |
-        // Q_B(1) + M_A(accept 1, propose 2) + P_A | Q_A(2) + M_B(accept 1, propose 2) + P_B | ... |
-        // Q_B(n) + M_A(accept n) | M_B(accept n); the step-k history row is written by A's
-        // accept and, one launch later, by B's
-        launch_half(s, stream, -1, 0, false, true, 0, HistRow{}, fast_only);
-        HistRow rowB{};
-        for (int k = 1; k <= n_steps; k++) {
-            launch_half(s, stream, 0, 1, k > 1, true, 1, rowB, fast_only);
-            const HistRow rowA = next_hist(s);
-            launch_half(s, stream, 1, 0, true, k < n_steps, k < n_steps ? 0 : -1, rowA, fast_only);
-            rowB = rowA;
-        }
-        launch_half(s, stream, -1, 1, true, false, -1, rowB, fast_only);
-        return;
-    }
-    if (G == 1 && s->pipe_mode == 3 && tail_setup(s, fast_only)) {
+    if (G == 1 && tail_setup(s, fast_only)) {
         // unified: propose(1) + pass(1) | tails(1) + pass(2) + accept(1) + propose(2) | ... |
         // tails(n) + accept(n): one launch per step.  The arrival counters start from 0
         // in every call (the epochs are counted within it)
@@ -3582,34 +3296,12 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
         pipe_status_post(s, stream);
         return;
     }
-    if (G == 1 && tail_setup(s, fast_only)) {
-        // split pipelined: pass(1) | mh(propose 1) | tails(1) + pass(2) | mh(accept 1 + propose 2) |
-        // tails(2) + pass(3) | ... | tails(n) | mh(accept n)
-        launch_tail(s, stream, -1, 0);
-        for (int k = 0; k < n_steps; k++) {
-            launch_mh(s, k > 0, true, fast_only, k > 0 ? next_hist(s) : HistRow{}, stream, 0, s->W, false);
-            launch_tail(s, stream, k % 2, k + 1 < n_steps ? (k + 1) % 2 : -1);
-        }
-        launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W, false);
-        return;
-    }
-    if (G == 1 && pipe_setup(s, fast_only)) {
-        // pipelined: propose(1) + pass(1) | tails(1) | accept(1) + propose(2) + pass(2) |
-        // tails(2) | ... | tails(n) | accept(n)
-        for (int k = 0; k < n_steps; k++) {
-            launch_mh(s, k > 0, true, fast_only, k > 0 ? next_hist(s) : HistRow{}, stream, 0, s->W, false, true);
-            eval_likes(s, stream, false, 0, s->W, s->ws.p, true, true);
-        }
-        launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W, false);
-        pipe_status_post(s, stream);
-        return;
-    }
     PlikBinArgs pb;
     if (G == 1 && bin_setup(s, fast_only, pb)) {
         // bin co-run: propose(1) + bins(1) | [rotations] | quadform(1) | accept(1) + propose(2) + bins(2) |
         // ... | quadform(n) | accept(n)
         for (int k = 0; k < n_steps; k++) {
-            launch_mh(s, k > 0, true, fast_only, k > 0 ? next_hist(s) : HistRow{}, stream, 0, s->W, false, false, &pb);
+            launch_mh(s, k > 0, true, fast_only, k > 0 ? next_hist(s) : HistRow{}, stream, 0, s->W, false, &pb);
             launch_bin_qf(s, stream);
         }
         launch_mh(s, true, false, fast_only, next_hist(s), stream, 0, s->W, false);
@@ -4181,10 +3873,6 @@ void sampler_load_state(cmbs *s, const void *buf, size_t bytes) {
 }  // namespace cmamd
 
 #ifdef CMAMD_STAMPS
-extern "C" int cmamd_debug_pipe_stamps(unsigned long long *host) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_pipe_stamps), sizeof(cmamd::g_pipe_stamps)) == hipSuccess ? 0
-                                                                                                                 : -5;
-}
 extern "C" int cmamd_debug_uni_stamps(unsigned long long *host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_uni_stamps), sizeof(cmamd::g_uni_stamps)) == hipSuccess ? 0
                                                                                                                : -5;
@@ -4218,7 +3906,7 @@ extern "C" int cmamd_debug_tp_items(const cmbs *s, int *out, int cap) {   // (fi
     return s->tpass->n_items();
 }
 extern "C" int cmamd_debug_pipeline(cmbs *s, int mode) {   // fast-step schedule (sampler_step): 0 unpipelined,
-    if (!s || mode < 0 || mode > 4) return -1;    // 1 mh_pass_kernel, 2 step tails, 3 unified, 4 interleaved halves
+    if (!s || (mode != 0 && mode != 3)) return -1;   // 3 the unified launch (default), 0 unpipelined
     s->pipe_mode = mode;
     return 0;
 }

@@ -1,17 +1,17 @@
-// The step tail of the sampler's split pipelined fast steps (sampler_step):
-// one launch that runs, side by side,
+// The sampler's unified step launch (sampler.hip mh_step_kernel): one launch
+// per fast step runs, side by side,
 //   * plik_lite's deferred quadratic form of step k, its operand rows formed
 //     in registers from the raw bin sums of step k and the walkers' step-k
 //     calibrations (Delta = X - S / cal^2, the pass's own emit operations),
 //   * the small gaussian chi^2 of the fused CMBlikes dataset (Planck lensing)
-//     of step k, its raw partial rows calibrated as they are loaded, and
+//     of step k, its raw partial rows calibrated as they are loaded,
 //   * the fused window pass over every walker's theory for step k + 1, which
 //     stores raw sums (no calibration: those of step k + 1 are not proposed
-//     yet) into the other half of a two-half buffer.
+//     yet) into the other half of a two-half buffer, and
+//   * the Metropolis workgroups, which wait for their walker tile's quadratic
+//     form and chi^2, accept step k and propose step k + 1.
 // The pass is HBM-bound and the quadratic form MFMA / L2-bound, so they share
-// the CUs instead of following each other; and since the raw sums need no
-// calibration, no workgroup waits on another inside the launch (the
-// Metropolis kernel that proposes step k + 1 runs alone, between two tails).
+// the CUs instead of following each other.
 #pragma once
 
 #include <vector>
@@ -44,8 +44,8 @@ struct StepTail {
 
 // Workgroup roles by rows of 8 (block b runs on XCD b % 8, so each role's own
 // block numbering keeps the XCD placement its body assumes: qf_place,
-// TheoryPass::plan_units): row k is role rows[k].x's rows[k].y-th row.  nm
-// Metropolis workgroups (sampler.hip's unified step launch) come last.
+// TheoryPass::plan_units): row k is role rows[k].x's rows[k].y-th row.  The nm
+// Metropolis workgroups come last.
 enum { TAIL_QF = 0, TAIL_GAUSS = 1, TAIL_PASS = 2, TAIL_MH = 3 };
 std::vector<int2> tail_rows(int nq, int ng, int np, int nm);
 
@@ -56,8 +56,5 @@ struct StepTailPlan {
     int nrows = 0;
 };
 
-// The launch (its LDS: at most step_tail_lds_bytes()); prof_name for timed_launch.
-void launch_step_tail(const StepTail &t, StepTailPlan &plan, hipStream_t stream, const char *prof_name);
-size_t step_tail_lds_bytes();
 
 }  // namespace cmamd

@@ -64,15 +64,8 @@ struct TPDev {
     const unsigned char *cmap;        // per item step, [64] slots: the item's column index (255: none)
     int nitem;
     int nblk;             // block table entries (units, including empty ones)
-    int tile_off;         // the units' walker tiles start here (a walker half of the sampler's interleaved steps)
+    int tile_off;         // the units' walker tiles start here (0: the pass over every walker)
     TPOut out[TP_MAXOUT];
-    // pipelined form (tp_vec_body<.., true>, the sampler's mh_pass_kernel):
-    // the step's calibrations come from the Metropolis workgroups of the same
-    // launch, which publish them per walker over TP_PIPE_UNSET
-    const double *calbuf;      // [TP_MAXOUT][cal_ld] each stage's calibration of walker w
-    long long cal_ld;
-    int delay;                 // 10 ns ticks the pass holds back at the start
-    int *status[TP_MAXOUT];    // the stages' sticky status words (CMBL_STATUS_PIPE_WAIT)
 };
 
 class TheoryPass {

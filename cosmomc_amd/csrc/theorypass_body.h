@@ -1,7 +1,7 @@
 // Device body of the fused window pass's vectorised kernel (theorypass.hip),
-// shared by theory_window_vec and by the sampler's pipelined launch, whose
-// workgroups run it beside mh_kernel's (sampler.hip, mh_pass_kernel).  The
-// LDS comes from the caller (tp_vec_lds_bytes).
+// shared by theory_window_vec and by the sampler's unified step launch, whose
+// workgroups run it beside the quadratic form's and mh_kernel's (sampler.hip,
+// mh_step_kernel).  The LDS comes from the caller (tp_vec_lds_bytes).
 #pragma once
 
 #include "theorypass.h"
@@ -13,14 +13,9 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 #ifndef TP_STAMP
 #define TP_STAMP(i) ((void)0)
 #endif
-#ifndef TP_PIPE_STAMP
-#define TP_PIPE_STAMP(i) ((void)0)
-#endif
-
-// PIPE adds the unit's column sums, [TP_MAXCOL][64 walkers]
-template <int NB, bool PIPE = false> constexpr int tp_vec_lds_bytes() {
+template <int NB> constexpr int tp_vec_lds_bytes() {
     return 2 * NB * 16 * (32 + 2) * 8 + TP_MAXCOL * (int)sizeof(TPCol) + TP_MAXCOL * 8 + TP_MAXSTEP * 8 +
-           TP_MAXSTEP * TP_MAXCOL + (PIPE ? TP_MAXCOL * 64 * 8 : 0);
+           TP_MAXSTEP * TP_MAXCOL;
 }
 
 // The same pass when every theory row is 16-byte aligned (the sampler's
@@ -33,32 +28,22 @@ template <int NB, bool PIPE = false> constexpr int tp_vec_lds_bytes() {
 // its own data instead of draining the prefetch (vmcnt(0)) at the weight
 // store, which held every step to a full memory latency.
 //
-// PIPE (the sampler's pipelined steps, mh_pass_kernel): the calibrations of
-// the step are being proposed by the Metropolis workgroups of the same
-// launch, so every column's sum is kept in LDS as it comes out of the MFMAs;
-// after its last step each thread polls its walker's published calibrations
-// (TPDev::calbuf, TP_PIPE_UNSET until published), applies them with the
-// emit's own operations (v / cal^2, X - v / cal^2: the same bits as the
-// unpipelined pass) and stores the outputs.
-//
-// RAW (the sampler's split pipelined steps, steptail.hip): no calibration at
+// RAW (the sampler's unified step launch, mh_step_kernel): no calibration at
 // all -- every column's sum v is stored as it comes out of the MFMAs, at the
 // index its stage's output would take (out is then the stage's raw-sum buffer);
 // the consumers apply the calibrations of the step that reads them with the
 // emit's own operations (X - v / cal^2 in the quadratic form's operand, v /
 // cal^2 in the small chi^2's partial rows), so the results are the same bits.
-template <int NB, bool PIPE, bool RAW = false>
+template <int NB, bool RAW = false>
 __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__restrict__ dl, long long ld_field,
                                             long long ld_walker, int W, char *lds, int b)
 {
-    static_assert(!(PIPE && RAW), "one output mode");
     constexpr int LPL = 8, STEP = 4 * LPL, NSUB = TP_CHUNK / STEP, WROW = STEP + 2;
     double *wsh = reinterpret_cast<double *>(lds);                                   // [buf][col block][col][l]
     TPCol *csh = reinterpret_cast<TPCol *>(wsh + 2 * NB * 16 * WROW);               // [TP_MAXCOL]
     double *xsh = reinterpret_cast<double *>(csh + TP_MAXCOL);                       // [TP_MAXCOL]
     unsigned long long *esh = reinterpret_cast<unsigned long long *>(xsh + TP_MAXCOL);   // [TP_MAXSTEP]
     unsigned char *msh = reinterpret_cast<unsigned char *>(esh + TP_MAXSTEP);        // [TP_MAXSTEP][TP_MAXCOL]
-    double *lsum = reinterpret_cast<double *>(msh + TP_MAXSTEP * TP_MAXCOL);         // PIPE: [TP_MAXCOL][64]
     const int2 unit = c.units[b];
     const int item = unit.x, tile = unit.y;
     if (item < 0) return;
@@ -66,10 +51,6 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
 #ifdef CMAMD_TP_STAMPS
     const unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (PIPE && c.delay > 0) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)c.delay) __builtin_amdgcn_s_sleep(8);
-    }
     const TPItem it = c.items[item];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, kq = lane >> 4;
@@ -138,7 +119,7 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
         reinterpret_cast<unsigned int *>(msh)[q] =
             reinterpret_cast<const unsigned int *>(c.cmap + (long long)it.soff * TP_MAXCOL)[q];
     double c2[TP_MAXOUT] = {1.0, 1.0};
-    if (!PIPE && !RAW) {
+    if (!RAW) {
 #pragma unroll
         for (int o = 0; o < TP_MAXOUT; o++) {
             const int ci = o ? c.out[1].cal_index : c.out[0].cal_index;
@@ -174,10 +155,8 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
             a0[r] = on[r] ? 0.0 : a0[r];
             b0[r] = on[r] ? 0.0 : b0[r];
             const bool o1 = d[r].out != 0;
-            const double q = (!PIPE && !RAW && d[r].cal) ? v / (o1 ? c2[1] : c2[0]) : v;
-            if (PIPE) {
-                if (on[r]) lsum[col[r] * 64 + wave * 16 + li] = v;
-            } else if (on[r] && w < W) {
+            const double q = (!RAW && d[r].cal) ? v / (o1 ? c2[1] : c2[0]) : v;
+            if (on[r] && w < W) {
                 double *out = o1 ? c.out[1].out : c.out[0].out;
                 if ((o1 ? c.out[1].kind : c.out[0].kind) == 0)
                     out[(long long)d[r].row * W + w] = q;
@@ -245,41 +224,6 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
         case 0: tail(tA, tB); break;
         case 1: tail(tB, tC); break;
         default: tail(tC, tA); break;
-    }
-    if constexpr (PIPE) {
-        TP_PIPE_STAMP(1);
-        __syncthreads();   // every wave's sums in lsum
-        // thread: walker tid % 64 of the tile, columns tid / 64, + 4, ...; it
-        // polls its walker's two published calibrations (bounded)
-        const int wl2 = tid & 63, wv = (c.tile_off + tile) * 64 + wl2;
-        if (wv < W) {
-            double c2p[TP_MAXOUT];
-#pragma unroll
-            for (int o = 0; o < TP_MAXOUT; o++) {
-                double cl = 0.0;
-                long it2 = 0;
-                for (; it2 < (1l << 24); it2++) {
-                    cl = __hip_atomic_load(c.calbuf + o * c.cal_ld + wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((unsigned long long)__double_as_longlong(cl) != TP_PIPE_UNSET) break;
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                if (it2 == (1l << 24) && c.status[o])   // gave up (a safety net: the wait ends by construction)
-                    atomicOr(c.status[o], CMBL_STATUS_PIPE_WAIT);
-                c2p[o] = cl * cl;
-            }
-            TP_PIPE_STAMP(2);
-            for (int col = tid >> 6; col < it.ncol; col += 4) {
-                const TPCol d = csh[col];
-                const bool o1 = d.out != 0;
-                const double v = lsum[col * 64 + wl2];
-                const double q = d.cal ? v / (o1 ? c2p[1] : c2p[0]) : v;
-                double *out = o1 ? c.out[1].out : c.out[0].out;
-                if ((o1 ? c.out[1].kind : c.out[0].kind) == 0)
-                    out[(long long)d.row * W + wv] = q;
-                else
-                    out[(long long)wv * (o1 ? c.out[1].ld : c.out[0].ld) + d.row] = xsh[col] - q;
-            }
-        }
     }
     TP_STAMP(2);
 #ifdef CMAMD_TP_STAMPS

@@ -714,28 +714,20 @@ def test_corun_tails_bitwise(cmbl_golden, refdata, tmp_path, W):
 
 @pytest.mark.parametrize("W", [1, 100, 1024])
 def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
-    """The fast-step schedules give the same bits.  Mode 4 (interleaved
-    halves, W = 1024; smaller W fall back to mode 2): the walkers form two
-    halves a step apart, and each launch runs one half's quadratic form and
-    chi^2 beside the other half's Metropolis workgroups and window pass, none
-    waiting on another (mh_half_kernel).  Mode 3 (the unified step
-    launch): one launch per step holds step k's quadratic form and lensing
-    chi^2, the pass storing step k + 1's raw sums, and the Metropolis
-    workgroups that wait for their tile's tails, accept step k and propose
-    step k + 1 (mh_step_kernel).  Mode 2 (the split pipelined steps): the
-    fused pass of step k + 1 runs in step k's tail launch and stores raw sums,
-    which step k + 1's quadratic form and lensing chi^2 calibrate as they read
-    them (steptail.hip), with the proposing Metropolis kernel alone in between.  Mode 1: the pass of step k in the
-    launch of the mh_kernel proposing it (mh_pass_kernel).  Mode 0: the
-    unpipelined schedule.  Each runs the lean Metropolis chain (mhlean.h: the
-    only fast parameter is a one-parameter block); modes 0 and 1 also run the
-    generic chain (mh_body), which the reference chains pin.  Chains, CurLike
-    and both likelihood terms are bit-identical over step() calls of 1, 2 and
-    5 steps.  The default schedule's own run is pinned to the oracles
-    directly: at the first and last recorded steps the
-    terms of walkers 0, W/2 - 1 and W - 1 equal pyoracle.PlikLite's and
-    CMBLikesOracle's -lnL at the recorded calibrations (rel 1e-9), and every
-    walker's equals each likelihood's own loglike_batch (rtol 1e-12)."""
+    """The fast-step schedules give the same bits.  Mode 3 (the default, the
+    unified step launch): one launch per step holds step k's quadratic form
+    and lensing chi^2, the pass storing step k + 1's raw sums, and the
+    Metropolis workgroups that wait for their tile's tails, accept step k and
+    propose step k + 1 (mh_step_kernel).  Mode 0: the unpipelined schedule.
+    Each runs the lean Metropolis chain (mhlean.h: the only fast parameter is
+    a one-parameter block) and the generic chain (mh_body), which the
+    reference chains pin.  Chains, CurLike and both likelihood terms are
+    bit-identical over step() calls of 1, 2 and 5 steps.  The default
+    schedule's own run is pinned to the oracles directly: at the first and
+    last recorded steps the terms of walkers 0, W/2 - 1 and W - 1 equal
+    pyoracle.PlikLite's and CMBLikesOracle's -lnL at the recorded calibrations
+    (rel 1e-9), and every walker's equals each likelihood's own loglike_batch
+    (rtol 1e-12)."""
     import os
 
     import cmblikes_oracle as co
@@ -749,7 +741,7 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
     calls = (1, 2, 5)
     steps = sum(calls)
     out = []
-    for mode, lean in ((-1, 1), (4, 1), (3, 1), (2, 1), (1, 1), (0, 1), (1, 0), (0, 0)):
+    for mode, lean in ((-1, 1), (3, 1), (0, 1), (3, 0), (0, 0)):
         plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
         lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
         plik.nuisance_indices = [2]
@@ -767,8 +759,8 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
         s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
         for n in calls:
             s.step(n, fast_only=True)
-        if mode >= 2:
-            assert N.lib().cmamd_debug_tail(s._h) == W        # the step tails ran
+        if mode != 0:
+            assert N.lib().cmamd_debug_tail(s._h) == W        # the unified launch ran
         out.append((s.history_host(0, steps), s.history_terms(0, steps)))
         assert plik.status() == 0 and lens.status() == 0
         if mode == -1:
@@ -791,8 +783,8 @@ def test_pipelined_steps_bitwise(cmbl_golden, refdata, tmp_path, W):
 def test_pipelined_with_wide_slow_block(cmbl_golden, refdata, tmp_path):
     """A slow block wide enough for rot_kernel's rotations (9 parameters) does
     not keep fast-only steps off the pipelined schedule (fast-only steps never
-    propose it): mh_pass_kernel runs (mode 1) and the chains equal the
-    unpipelined steps' (mode 0) bit for bit."""
+    propose it): the unified step launch runs (mode 3) and the chains equal
+    the unpipelined steps' (mode 0) bit for bit."""
     import os
 
     from cosmomc_amd import _native as N
@@ -809,7 +801,7 @@ def test_pipelined_with_wide_slow_block(cmbl_golden, refdata, tmp_path):
     pm, ps = np.zeros(n), np.zeros(n)
     pm[-1], ps[-1] = 1.0, 0.0025
     out = []
-    for mode in (1, 0):
+    for mode in (3, 0):
         plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path)))
         lens = NativeCMBLikelihood(c["tag"], os.path.join(refdata, c["dataset"]), c["overrides"])
         plik.nuisance_indices = [n]
@@ -827,9 +819,9 @@ def test_pipelined_with_wide_slow_block(cmbl_golden, refdata, tmp_path):
         s.step(5, fast_only=True)
         s.step(7, fast_only=True)
         torch.cuda.synchronize()
-        launches = N.profile_read("mh_pass_kernel")[1]
+        launches = N.profile_read("mh_step_kernel")[1]
         N.profile_enable(False)
-        assert (launches == 12) if mode == 1 else (launches == 0)
+        assert (launches == 10) if mode == 3 else (launches == 0)   # the middle launches of the two calls
         out.append((s.history_host(0, 12), s.history_terms(0, 12), s.save_state()))
         s.close()
     assert np.array_equal(out[0][0], out[1][0])
@@ -837,12 +829,12 @@ def test_pipelined_with_wide_slow_block(cmbl_golden, refdata, tmp_path):
     assert out[0][2] == out[1][2]
 
 
-@pytest.mark.parametrize("mode", [3, 1, "bin"])
+@pytest.mark.parametrize("mode", [3, "bin"])
 def test_pipelined_handoff_giveup_fails_loudly(cmbl_golden, refdata, tmp_path, mode):
     """In-launch hand-offs fail loudly.  Mode 3: the unified step launch's
-    Metropolis workgroups wait for their tile's tails; mode 1: mh_pass_kernel's
-    pass workgroups wait for the calibrations the Metropolis workgroups
-    publish; "bin": mh_bin_kernel's bin workgroups wait for them likewise.  A debug switch stops the producers (no arrivals / no
+    Metropolis workgroups wait for their tile's tails; "bin": mh_bin_kernel's
+    bin workgroups wait for the calibrations the Metropolis workgroups
+    publish.  A debug switch stops the producers (no arrivals / no
     publication), so every wait gives up at its bound and sets
     CMBL_STATUS_PIPE_WAIT; the next readback (and the next step call) must fail
     instead of handing back silently rejected trials."""
@@ -865,7 +857,7 @@ def test_pipelined_handoff_giveup_fails_loudly(cmbl_golden, refdata, tmp_path, m
     s.add_likelihood(plik, dl)
     if mode != "bin":   # "bin": plik alone, the bin co-run's bins wait for the calibrations
         s.add_likelihood(lens, dl)
-    assert N.lib().cmamd_debug_pipeline(s._h, 1 if mode == "bin" else mode) == 0
+    assert N.lib().cmamd_debug_pipeline(s._h, 3) == 0
     s.set_start(np.tile([0.0222, 1.0, 3.05], (W, 1)))
     s.step(2, fast_only=True)                                  # healthy
     s.state()
@@ -1100,7 +1092,7 @@ def test_bin_corun_bitwise(tmp_path, W, shared):
     g = syn.gaussians(123, W * n).reshape(W, n)
     start = np.clip(P0 + 2 * width * g, pmin + 1e-9, pmax - 1e-9)
     out = []
-    for mode in (1, 0):
+    for mode in (3, 0):
         plik = NativeCMBLikelihood("PLIK_LITE", data.write(str(tmp_path / f"m{mode}")))
         plik.nuisance_indices = [1]
         smp = BatchedMCMC(W, n, used, [used], 0, pmin, pmax, pm, ps, propose_scale=2.4, seed_ij=4004, seed_kl=9373)

@@ -29,6 +29,9 @@ if __name__ == "__main__":
     W = int(os.environ.get("W", "1024"))
     with tempfile.TemporaryDirectory() as td:
         smp, *_ = bench.build_problem(W, 0, td)
+        # the unpipelined steps: mh_kernel's workgroups are the first 64 of
+        # their launch (in the unified launch they come last, past the stamps)
+        assert N.lib().cmamd_debug_pipeline(smp._h, 0) == 0
         smp.step(20, fast_only=True)
         torch.cuda.synchronize()
         st = np.zeros((64, 16), dtype=np.uint64)

@@ -30,7 +30,7 @@ for f in sorted(glob.glob(os.path.join(root, "*", "*kernel_stats.csv"))):
         dur[k] = float(r["AverageNs"]) * 1e-3
 out = {}
 for k, v in agg.items():
-    if not any(t in k for t in ("plik", "mh_kernel", "mh_pass", "rot_kernel", "cmbl", "quadform", "theory")):
+    if not any(t in k for t in ("plik", "mh_kernel", "mh_step", "mh_bin", "rot_kernel", "cmbl", "quadform", "theory")):
         continue
     avg = {c: sum(x) / len(x) for c, x in v.items()}
     rec = {"counters": {c: round(a, 1) for c, a in avg.items()}, "launches": max(len(x) for x in v.values())}

@@ -1,11 +1,10 @@
 #!/usr/bin/env python3
-"""Block timeline of the step launches of the split (mode 2: step_tail_kernel)
-and unified (mode 3: mh_step_kernel) pipelined fast steps from in-kernel
+"""Block timeline of the unified step launch (mh_step_kernel) from in-kernel
 s_memrealtime stamps (100 MHz): per role (quadratic form, chi^2, pass,
 Metropolis) when its workgroups start and end, and for the Metropolis
 workgroups when their tile's wait ends.  Builds the instrumented library
-(tools/_stamps/, -DCMAMD_STAMPS) unless --no-build, then runs 20 headline fast
-steps in each mode and reports the last middle launch.
+(tools/_stamps/ or STAMP_OUT, -DCMAMD_STAMPS) unless --no-build, then runs 20
+headline fast steps and reports the last middle launch.
 """
 import ctypes as C
 import os
@@ -30,7 +29,7 @@ if __name__ == "__main__":
     import bench
     from cosmomc_amd import _native as N
     q = lambda a: " ".join(f"{np.percentile(a, p):6.2f}" for p in (0, 10, 50, 90, 100))
-    for mode, fn in ((3, "cmamd_debug_uni_stamps"), (2, "cmamd_debug_tail_stamps")):
+    for mode, fn in ((3, "cmamd_debug_uni_stamps"),):
         with tempfile.TemporaryDirectory() as td:
             smp, *_ = bench.build_problem(1024, 0, td)
             assert N.lib().cmamd_debug_pipeline(smp._h, mode) == 0
@@ -41,7 +40,7 @@ if __name__ == "__main__":
         s = st[st[:, 4] > 0].astype(np.int64)
         t0 = s[:, 0].min()
         us = lambda x: (x - t0) / 100.0
-        print(f"mode {mode} ({os.environ.get('CMAMD_TAIL_ORDER', 'qpg')}): quantiles 0/10/50/90/100, "
+        print(f"mode {mode} ({os.environ.get('CMAMD_TAIL_ORDER', 'gqp')}): quantiles 0/10/50/90/100, "
               f"us from the first block's start; launch {us(s[:, 3].max()):.2f} us")
         for r, name in ROLES.items():
             b = s[s[:, 4] == r]
