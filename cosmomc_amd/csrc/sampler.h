@@ -138,6 +138,8 @@ struct TailWait {
     int ng, gwt;             // chi^2 workgroups and walkers per chi^2 workgroup
     int *status;             // CMBL_STATUS_PIPE_WAIT when a wait gives up
     int nosignal;            // debug: the producers never arrive (the give-up test)
+    int stamp_slot;          // instrumented builds: the stamp buffer (0 middle launches, 1 the last)
+    int ntiles;              // counters (the first launch of a call zeroes them)
 };
 
 struct LikeSlot {
@@ -241,8 +243,8 @@ struct cmbs {
     int tail_nosignal = 0;                   // debug (cmamd_debug_tail_nosignal)
     // a pipelined hand-off that gave up (unified launch, bin co-run): the device word, its
     // pinned copy taken at the end of each step call, checked at the next
-    cmamd::DevBuf pipe_status;
-    int *pipe_status_host = nullptr;
+    int *pipe_status_host = nullptr;         // pinned, mapped (pipe_status_init)
+    int *pipe_status_dev = nullptr;          // its device address
     hipEvent_t pipe_ev = nullptr;
     bool pipe_ev_pending = false;
     // bin co-run (a lone plik_lite likelihood, no fused pass): the proposing

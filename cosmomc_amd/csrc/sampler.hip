@@ -29,9 +29,9 @@
 #include "smallgauss.h"
 #ifdef CMAMD_STAMPS
 namespace cmamd {
-// mh_step_kernel (tools/uni_stamps.py), middle launches only: start, the
-// Metropolis wait's end, XCC id, end, role + 1
-__device__ unsigned long long g_uni_stamps[2048][5];
+// mh_step_kernel (tools/uni_stamps.py), [0] the middle launches, [1] the last
+// (accept-only) launch: start, the Metropolis wait's end, XCC id, end, role + 1
+__device__ unsigned long long g_uni_stamps[2][2048][5];
 }
 #endif
 #include "theorypass_body.h"
@@ -578,7 +578,28 @@ __device__ inline void write_like_flags(const DevCfg &c, const QT &trial, const 
 // call reports as an error (sampler_check_pipe).  The bound counts polls, not
 // wall-clock time: a poll does not advance while the wave is switched out (a
 // shared GPU), so a waiter restored before its producers never gives up early.
-static constexpr long TAIL_WAIT_SPINS = 1l << 24;   // x s_sleep(2) (~128 cycles): ~1 s
+// The per-tile arrival counters each on a line of their own (TW_PAD words
+// apart), and the waiters poll them every TW_SLEEP x 64 cycles: the counters
+// are agent-scope, so every poll and arrival goes past the XCD's L2, and 64
+// waiters polling one line in a tight loop slow the quadratic form's own
+// loads on the chip.
+#ifndef CMAMD_TW_SLEEP
+#define CMAMD_TW_SLEEP 20
+#endif
+#ifndef CMAMD_TW_PAD
+#define CMAMD_TW_PAD 64
+#endif
+static constexpr int TW_PAD = CMAMD_TW_PAD;
+static constexpr long TAIL_WAIT_SPINS = (1l << 25) / CMAMD_TW_SLEEP;   // polls: ~1 s
+
+// A give-up: the sampler's status word lives in pinned host memory (mapped),
+// so the host reads it once the step call's event has completed, without a
+// copy launch; every writer stores the same bit, so a plain system-scope store
+// serves (no read-modify-write over the bus)
+__device__ __forceinline__ void pipe_giveup(int *status)
+{
+    __hip_atomic_store(status, CMBL_STATUS_PIPE_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __device__ __forceinline__ void tail_wait(const TailWait &tw, int tile)
 {
@@ -587,20 +608,20 @@ __device__ __forceinline__ void tail_wait(const TailWait &tw, int tile)
         const int gq = max(0, min(gpt, tw.ng - g0));
         const unsigned target = tw.epoch * (unsigned)(tw.nq_items + gq);
         for (long it = 0;; it++) {
-            const unsigned v = __hip_atomic_load(tw.cnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned v = __hip_atomic_load(tw.cnt + tile * TW_PAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (v >= target) break;
             if (it == TAIL_WAIT_SPINS) {
-                atomicOr(tw.status, CMBL_STATUS_PIPE_WAIT);
+                pipe_giveup(tw.status);
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(CMAMD_TW_SLEEP);
         }
         // one acquire after the match (cdna_hip_programming.md Guideline 16 recipe): it drops this
         // CU's L1 lines; its own wait holds the barrier, then every wave loads
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef CMAMD_STAMPS
-        if (blockIdx.x < 2048) g_uni_stamps[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+        if (blockIdx.x < 2048) g_uni_stamps[tw.stamp_slot][blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
 #endif
     }
     __syncthreads();
@@ -1025,8 +1046,8 @@ __global__ __launch_bounds__(MH_THREADS) void mh_bin_kernel(DevCfg c, int fast_o
         for (long it = 0;; it++) {   // bounded by polls (tail_wait): a safety net, reported loudly
             cl = __hip_atomic_load(c.calbuf + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((unsigned long long)__double_as_longlong(cl) != TP_PIPE_UNSET) break;
-            if (it == TAIL_WAIT_SPINS / 16) {
-                atomicOr(status, CMBL_STATUS_PIPE_WAIT);
+            if (it == (1l << 20)) {   // x s_sleep(24): ~0.7 s
+                pipe_giveup(status);
                 break;
             }
             __builtin_amdgcn_s_sleep(24);   // ~1500 cycles: 3 W pollers must not crowd the L2
@@ -1060,7 +1081,7 @@ __device__ __forceinline__ void tail_arrive(const TailWait &tw, int tile)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are done
     __syncthreads();
     if (threadIdx.x == 0 && !tw.nosignal)
-        __hip_atomic_fetch_add(tw.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(tw.cnt + tile * TW_PAD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool ACCEPT, bool PROPOSE>
@@ -1071,25 +1092,28 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fa
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int2 rr = rows[blockIdx.x >> 3];
     const int lb = rr.y * 8 + (blockIdx.x & 7);
+    if (!ACCEPT && blockIdx.x == 0)   // a call's first launch (no tails): the arrival counters start from 0
+        for (int i = threadIdx.x; i < tw.ntiles; i += MH_THREADS) tw.cnt[i] = 0u;
 #ifdef CMAMD_STAMPS
-    const bool stamp = ACCEPT && PROPOSE && threadIdx.x == 0 && blockIdx.x < 2048;
+    const bool stamp = ACCEPT && threadIdx.x == 0 && blockIdx.x < 2048;
+    const int slot = PROPOSE ? 0 : 1;
     if (stamp) {
         unsigned xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        g_uni_stamps[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
-        g_uni_stamps[blockIdx.x][2] = xcc & 15;
-        g_uni_stamps[blockIdx.x][4] = 0;
+        g_uni_stamps[slot][blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+        g_uni_stamps[slot][blockIdx.x][2] = xcc & 15;
+        g_uni_stamps[slot][blockIdx.x][4] = 0;
     }
     struct End {
         bool on;
-        int role;
+        int role, slot;
         __device__ ~End() {
             if (on) {
-                g_uni_stamps[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
-                g_uni_stamps[blockIdx.x][4] = role + 1;
+                g_uni_stamps[slot][blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
+                g_uni_stamps[slot][blockIdx.x][4] = role + 1;
             }
         }
-    } end_{stamp, rr.x};
+    } end_{stamp, rr.x, slot};
 #endif
     if (rr.x == TAIL_QF) {
         if (lb >= t.nq) return;
@@ -2878,24 +2902,24 @@ static bool rot_may_pend(cmbs *s, int fast_only, int g0) {
 
 static void rot_schedule_unknown(cmbs *s) { std::fill(s->rot_lp.begin(), s->rot_lp.end(), -1); }
 
-// The pipelined hand-offs' give-up word (modes 1 and 3): zeroed here; copied
-// to pinned memory at the end of every pipelined step call (pipe_status_post)
-// and checked at the start of the next call and by the state readbacks
-// (sampler_check_pipe), so a hand-off that gave up fails the run loudly
+// The in-launch hand-offs' give-up word (the unified launch, the bin co-run):
+// a word of pinned host memory that the kernels write through its device
+// mapping (pipe_giveup); zeroed here, checked once the step call's event has
+// completed -- at the start of the next call and by the state readbacks
+// (sampler_check_pipe) -- so a hand-off that gave up fails the run loudly
 // instead of leaving silently rejected trials.
 static void pipe_status_init(cmbs *s) {
-    if (!s->pipe_status.p) {
-        s->pipe_status.alloc(256);
-        HIP_CHECK(hipHostMalloc((void **)&s->pipe_status_host, 64, hipHostMallocDefault));
+    if (!s->pipe_status_host) {
+        HIP_CHECK(hipHostMalloc((void **)&s->pipe_status_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_CHECK(hipHostGetDevicePointer((void **)&s->pipe_status_dev, s->pipe_status_host, 0));
         HIP_CHECK(hipEventCreateWithFlags(&s->pipe_ev, hipEventDisableTiming));
     }
-    HIP_CHECK(hipMemset(s->pipe_status.p, 0, 256));
-    *s->pipe_status_host = 0;
+    HIP_CHECK(hipDeviceSynchronize());   // no kernel of an earlier call still writes it
+    *reinterpret_cast<volatile int *>(s->pipe_status_host) = 0;
     s->pipe_ev_pending = false;
 }
 
 static void pipe_status_post(cmbs *s, hipStream_t stream) {
-    HIP_CHECK(hipMemcpyAsync(s->pipe_status_host, s->pipe_status.p, 4, hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipEventRecord(s->pipe_ev, stream));
     s->pipe_ev_pending = true;
 }
@@ -2907,8 +2931,8 @@ void sampler_check_pipe(cmbs *s, bool wait) {
     if (q == hipErrorNotReady) return;   // checked at a later call
     HIP_CHECK(q);
     s->pipe_ev_pending = false;
-    if (*s->pipe_status_host & CMBL_STATUS_PIPE_WAIT) {
-        *s->pipe_status_host = 0;
+    if (*reinterpret_cast<volatile int *>(s->pipe_status_host) & CMBL_STATUS_PIPE_WAIT) {
+        *reinterpret_cast<volatile int *>(s->pipe_status_host) = 0;
         s->tail_ready = 0;
         s->pipe_ready = 0;
         fail(CMBL_ERR_NUMERIC, "a pipelined step's in-launch hand-off gave up waiting (CMBL_STATUS_PIPE_WAIT): "
@@ -3039,10 +3063,10 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
             timed_launch("mh_bin_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
                 if (accept)
                     hipExtLaunchKernelGGL(mh_bin_kernel<true>, gb, b, s->bin_lds, stream, e0, e1, 0, dc, fast_only,
-                                          row.p, row.t, nmh, nmh_pad, *bin, s->pipe_status.as<int>());
+                                          row.p, row.t, nmh, nmh_pad, *bin, s->pipe_status_dev);
                 else
                     hipExtLaunchKernelGGL(mh_bin_kernel<false>, gb, b, s->bin_lds, stream, e0, e1, 0, dc, fast_only,
-                                          row.p, row.t, nmh, nmh_pad, *bin, s->pipe_status.as<int>());
+                                          row.p, row.t, nmh, nmh_pad, *bin, s->pipe_status_dev);
             });
             HIP_CHECK(hipGetLastError());
         } catch (...) {
@@ -3141,7 +3165,7 @@ static bool tail_setup(cmbs *s, int fast_only) {
     s->tail_rowcal.alloc(rc.size());
     s->tail_rowcal.upload(rc.data(), rc.size());
     // the unified launch's arrival counters (from 0, epoch 0) and its LDS
-    s->tail_cnt_bytes = (Wp / QF_TILE * 4 + 15) & ~(size_t)15;   // a multiple of 16 from the start
+    s->tail_cnt_bytes = (Wp / QF_TILE * TW_PAD * 4 + 15) & ~(size_t)15;   // a multiple of 16 from the start
     s->tail_cnt.alloc(s->tail_cnt_bytes);
     HIP_CHECK(hipMemset(s->tail_cnt.p, 0, s->tail_cnt_bytes));
     s->tail_epoch = 0;
@@ -3236,8 +3260,10 @@ static void launch_unified(cmbs *s, hipStream_t stream, bool propose, int rd, in
     tw.nq_items = t.q.src.n_items;
     tw.ng = ng_rows;
     tw.gwt = SMALL_WT;
-    tw.status = s->pipe_status.as<int>();
+    tw.status = s->pipe_status_dev;
     tw.nosignal = s->tail_nosignal;
+    tw.stamp_slot = propose ? 0 : 1;
+    tw.ntiles = (int)(s->tail_cnt_bytes / 4);
     const int nmh = (s->W + MB - 1) / MB;
     const int v = accept ? (propose ? 1 : 2) : 0;
     StepTailPlan &pl = s->uni_plan[v];
@@ -3286,8 +3312,7 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
     if (G == 1 && tail_setup(s, fast_only)) {
         // unified: propose(1) + pass(1) | tails(1) + pass(2) + accept(1) + propose(2) | ... |
         // tails(n) + accept(n): one launch per step.  The arrival counters start from 0
-        // in every call (the epochs are counted within it)
-        HIP_CHECK(hipMemsetAsync(s->tail_cnt.p, 0, s->tail_cnt_bytes, stream));
+        // in every call (the first launch zeroes them; the epochs are counted within it)
         s->tail_epoch = 0;
         launch_unified(s, stream, true, -1, 0, HistRow{}, fast_only);
         for (int k = 0; k < n_steps; k++)
@@ -3935,12 +3960,10 @@ extern "C" int cmamd_debug_drag_hbm(cmbs *s, int on) {   // the drag stages on t
     s->drag_hbm = on != 0;
     return 0;
 }
-extern "C" int cmamd_debug_pipe_status(cmbs *s) {   // the device give-up word (synchronises the device)
-    if (!s || !s->pipe_status.p) return -1;
-    int v = 0;
-    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&v, s->pipe_status.p, 4, hipMemcpyDeviceToHost) != hipSuccess)
-        return -2;
-    return v;
+extern "C" int cmamd_debug_pipe_status(cmbs *s) {   // the give-up word (synchronises the device)
+    if (!s || !s->pipe_status_host) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return *reinterpret_cast<volatile int *>(s->pipe_status_host);
 }
 extern "C" int cmamd_debug_tail(const cmbs *s) { return s ? s->tail_ready : 0; }   // W of the step tails' set-up
 extern "C" int cmamd_debug_fused(const cmbs *s) { return !s ? 0 : s->tpass ? s->tpass->n_items() : -s->tp_why; }

@@ -20,7 +20,16 @@ std::vector<int2> tail_rows(int nq, int ng, int np, int nm) {
     std::vector<int2> rows;
     int done[3] = {0, 0, 0};
     auto emit = [&](int r) { rows.push_back(int2{r, done[r]++}); };
+    bool mh_done = false;
+    auto emit_mh = [&]() {
+        for (int k = 0; k < (nm + 7) / 8; k++) rows.push_back(int2{TAIL_MH, k});
+        mh_done = true;
+    };
     for (size_t i = 0; i < order.size(); i++) {
+        if (order[i] == 'm' && !mh_done) {   // the Metropolis rows here: they then wait resident for
+            emit_mh();                       // their tiles' producers (64 of the launch's >= 512 slots)
+            continue;
+        }
         const int r = role(order[i]);
         if (r < 0) continue;
         if (i + 2 < order.size() && order[i + 1] == '*' && role(order[i + 2]) >= 0) {
@@ -41,9 +50,9 @@ std::vector<int2> tail_rows(int nq, int ng, int np, int nm) {
     }
     for (int r = 0; r < 3; r++)   // roles the order left out
         while (done[r] < cnt[r]) emit(r);
-    // the Metropolis rows last, whatever the order: they wait for their tile's
-    // quadratic-form and chi^2 workgroups, which are then all dispatched first
-    for (int k = 0; k < (nm + 7) / 8; k++) rows.push_back(int2{TAIL_MH, k});
+    // the Metropolis rows last unless the order places them ('m'): they wait
+    // for their tile's quadratic-form and chi^2 workgroups
+    if (!mh_done) emit_mh();
     return rows;
 }
 

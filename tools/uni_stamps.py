@@ -29,18 +29,17 @@ if __name__ == "__main__":
     import bench
     from cosmomc_amd import _native as N
     q = lambda a: " ".join(f"{np.percentile(a, p):6.2f}" for p in (0, 10, 50, 90, 100))
-    for mode, fn in ((3, "cmamd_debug_uni_stamps"),):
-        with tempfile.TemporaryDirectory() as td:
-            smp, *_ = bench.build_problem(1024, 0, td)
-            assert N.lib().cmamd_debug_pipeline(smp._h, mode) == 0
-            smp.step(20, fast_only=True)
-            torch.cuda.synchronize()
-            st = np.zeros((2048, 5), dtype=np.uint64)
-            assert getattr(N.lib(), fn)(st.ctypes.data_as(C.c_void_p)) == 0
+    with tempfile.TemporaryDirectory() as td:
+        smp, *_ = bench.build_problem(1024, 0, td)
+        smp.step(20, fast_only=True)
+        torch.cuda.synchronize()
+        st2 = np.zeros((2, 2048, 5), dtype=np.uint64)
+        assert N.lib().cmamd_debug_uni_stamps(st2.ctypes.data_as(C.c_void_p)) == 0
+    for which, st in (("a middle launch", st2[0]), ("the last (accept-only) launch", st2[1])):
         s = st[st[:, 4] > 0].astype(np.int64)
         t0 = s[:, 0].min()
         us = lambda x: (x - t0) / 100.0
-        print(f"mode {mode} ({os.environ.get('CMAMD_TAIL_ORDER', 'gqp')}): quantiles 0/10/50/90/100, "
+        print(f"{which} ({os.environ.get('CMAMD_TAIL_ORDER', 'gqp')}): quantiles 0/10/50/90/100, "
               f"us from the first block's start; launch {us(s[:, 3].max()):.2f} us")
         for r, name in ROLES.items():
             b = s[s[:, 4] == r]
