@@ -590,6 +590,12 @@ __device__ inline void write_like_flags(const DevCfg &c, const QT &trial, const 
 #define CMAMD_TW_PAD 64
 #endif
 static constexpr int TW_PAD = CMAMD_TW_PAD;
+// walkers per chi^2 workgroup in the unified launch (4 / 8 / 16: 35.7-35.8 /
+// 35.9-36.0 / 35.9-36.0 us per middle launch, round 5)
+#ifndef CMAMD_UNI_WT
+#define CMAMD_UNI_WT 4
+#endif
+static constexpr int UNI_WT = CMAMD_UNI_WT;
 static constexpr long TAIL_WAIT_SPINS = (1l << 25) / CMAMD_TW_SLEEP;   // polls: ~1 s
 
 // A give-up: the sampler's status word lives in pinned host memory (mapped),
@@ -1123,8 +1129,8 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fa
         tail_arrive(tw, tile);
     } else if (rr.x == TAIL_GAUSS) {
         if (lb >= t.ng) return;
-        small_gauss_body<SMALL_WT, true, true>(t.g, lds, lb);
-        tail_arrive(tw, lb * SMALL_WT / 64);
+        small_gauss_body<UNI_WT, true, true>(t.g, lds, lb);
+        tail_arrive(tw, lb * UNI_WT / 64);
     } else if (rr.x == TAIL_PASS) {
         if (lb >= t.np) return;
         tp_vec_body<2, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
@@ -3177,7 +3183,7 @@ static bool tail_setup(cmbs *s, int fast_only) {
         G.corun_small(g, s->W, s->dc.like_nuis[gi], G.n_nuis, s->like_terms.as<double>() + (size_t)gi * s->dc.ld,
                       s->like_ws[gi].p);
         s->uni_lds = std::max({s->mh_lds, (size_t)QFS_LDS_DOUBLES * 8, (size_t)tp_vec_lds_bytes<2>(),
-                               (size_t)small_gauss_lds_doubles<SMALL_WT>(g.d.nX) * 8});
+                               (size_t)small_gauss_lds_doubles<UNI_WT>(g.d.nX) * 8});
         for (const void *k : {(const void *)mh_step_kernel<false, true>, (const void *)mh_step_kernel<true, true>,
                               (const void *)mh_step_kernel<true, false>})
             HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->uni_lds));
@@ -3211,7 +3217,7 @@ static StepTail make_tail(cmbs *s, int rd, int wr) {
         t.g.partial = s->tail_S[rd][s->tail_g].as<double>();
         t.g.row_cal = s->tail_rowcal.as<unsigned char>();
         t.g.stage_cal = s->tp_stage[s->tail_g].cal_index;
-        t.ng = (W + SMALL_WT - 1) / SMALL_WT;
+        t.ng = (W + UNI_WT - 1) / UNI_WT;
     }
     if (wr >= 0) {
         TPOut o[2];
@@ -3259,7 +3265,7 @@ static void launch_unified(cmbs *s, hipStream_t stream, bool propose, int rd, in
     tw.epoch = s->tail_epoch + (accept ? 1u : 0u);
     tw.nq_items = t.q.src.n_items;
     tw.ng = ng_rows;
-    tw.gwt = SMALL_WT;
+    tw.gwt = UNI_WT;
     tw.status = s->pipe_status_dev;
     tw.nosignal = s->tail_nosignal;
     tw.stamp_slot = propose ? 0 : 1;

@@ -1,21 +1,23 @@
 #!/bin/bash
-# PMC counter passes over a short bench run (one rocprofv3 run per pass, no
-# tracing domains combined with --pmc).  Extra args go to bench.py.
+# PMC counter passes over a short headline bench run (one rocprofv3 run per
+# pass, no tracing domain combined with --pmc), plus the kernel-trace --stats
+# pass whose durations tools/pmc_summary.py divides by.  Extra args go to bench.py.
 set -u
-mkdir -p gpurun_out/pmc
+OUTD=${PMC_OUT:-pmc}
+mkdir -p gpurun_out/$OUTD
 cd /tmp && export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"
-timeout -k 10 120 rocprofv3 -L > "$R/gpurun_out/pmc/counters.txt" 2>&1 || true
+B="--no-cpu-baseline --steps 60 --warmup 5 --converge-seconds 0 --config1-seconds -1 --config4-seconds -1 --config5-seconds -1 --drag-seconds -1"
 pass() {
   name=$1; shift
-  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$R/gpurun_out/pmc/$name" -o run \
-    -- python3 "$R/bench.py" --no-cpu-baseline --steps 60 --warmup 5 $BENCH_ARGS > "$R/gpurun_out/pmc/$name.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$R/gpurun_out/$OUTD/$name" -o run \
+    -- python3 "$R/bench.py" $B > "$R/gpurun_out/$OUTD/$name.log" 2>&1
   rc=$?; echo "pmc pass $name rc=$rc"; return $rc
 }
-BENCH_ARGS="${BENCH_ARGS:-}"
-pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/$OUTD/stats" -o run \
+  -- python3 "$R/bench.py" $B > "$R/gpurun_out/$OUTD/stats.log" 2>&1 && rm -f "$R"/gpurun_out/$OUTD/stats/*kernel_trace.csv && \
 pass fetch FETCH_SIZE && \
-pass write WRITE_SIZE TCC_HIT_sum && \
-pass l2 TCC_HIT_sum TCC_MISS_sum SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE && \
-pass inst SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_INSTS_MFMA && \
-pass inst2 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR
+pass write WRITE_SIZE && \
+pass mfma SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE && \
+pass lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAVES SQ_BUSY_CYCLES
+rc=$?; cd "$R"; python3 tools/pmc_summary.py gpurun_out/$OUTD gpurun_out/$OUTD/pmc_traffic.json; exit $rc
