@@ -14,7 +14,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["COSMOMC_AMD_LIB"] = os.path.join(ROOT, "tools", "_stamps", "libcosmomc_amd.so")
+os.environ["COSMOMC_AMD_LIB"] = os.path.join(os.environ.get("STAMP_OUT", os.path.join(ROOT, "tools", "_stamps")), "libcosmomc_amd.so")
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
