@@ -83,6 +83,9 @@ struct DevCfg {
     int stage_R;            // R rows staged in LDS (else read in place, stride W)
     int pre_blk;            // the only fast block (0-based; -1: several, or one parameter wide): with R
                             //   in place, fast-only proposals have its next column fetched beside the image
+    int pre_lp;             // pre_blk's loop index for every walker of this launch when the host knows it
+                            //   (rot_may_pend), else -1: the column's loads then go out with the image's
+    int pre_off, pre_n;     // pre_blk's R offset and width
     int stage_cyc;          // CYC rows + RandIndices scratch in LDS (else in place / itmp_g)
     int stage_cov;          // test-Gaussian covinv + center tables in LDS (else read from tab_d)
     int *itmp_g;            // [all_n][ld] RandIndices scratch when !stage_cyc

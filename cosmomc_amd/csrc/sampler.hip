@@ -667,6 +667,8 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     int *ti = it + (size_t)(c.stage_cyc ? c.all_n : 0) * MB;     // [n_int rounded to 64]
     int *oobw = ti + ((c.tl.n_int + 63) & ~63);                  // [MB] trial out of bounds (par_prior)
     double *zz = reinterpret_cast<double *>(oobw + MB);          // [np][MB] the trial's squared prior z (par_prior)
+    int *ndw = reinterpret_cast<int *>(zz + (size_t)c.np * MB);  // [MB] ring entries the chain's draws wrote
+    int *i0w = ndw + MB;                                         // [MB] the ring index before them
     if (threadIdx.x < MB) oobw[threadIdx.x] = 0;
     // the rotation list of this walker range: this launch appends to counter
     // rot_par; the other one (read by the previous step's rot_kernel) restarts
@@ -689,6 +691,26 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     dma_rows_i32(si, c.si, ni_st, W, wb, wl64, wave, nwave);
     dma_words(td, c.tab_d, 2 * ntd, wl64, wave, nwave);
     dma_words(ti, c.tab_i, c.tl.n_int, wl64, wave, nwave);
+    // fast-only proposals with R in HBM: the only fast block's next column
+    // (R(:, lp + 1) when no rotation is due) fetched into the vec rows by the
+    // thread groups (proposal_tail then skips its own read; a block that
+    // rotates writes R only in rot_kernel).  When the host knows the loop
+    // index (pre_lp) the loads go out here, beside the image; otherwise after
+    // it, from the staged index
+    const bool pre_col = PROPOSE && fast_only && !c.stage_R && c.pre_blk >= 0;
+    constexpr int NRQ = (MAXBLK + NV - 1) / NV;
+    double rq[NRQ];
+    int col = -1, ncol = 0;
+    const bool rq_early = pre_col && c.pre_lp >= 0;
+    if (rq_early && act) {
+        ncol = c.pre_n;
+        if (c.pre_lp % ncol != 0) col = c.pre_off + c.pre_lp;
+#pragma unroll
+        for (int u = 0; u < NRQ; u++) {
+            const int q = grp + u * NV;
+            if (col >= 0 && q < ncol) rq[u] = c.sd[(size_t)(R.R + col + q * ncol) * W + w];
+        }
+    }
     if (tw) tail_wait(*tw, wb / 64);   // the trial's terms below come from this launch's producers
     dma_rows_f64(lk, 0, c.like_terms, 0, nlk, W, wb, wl64, wave, nwave);
     // per-likelihood terms of the current point, for the history (rejected walkers keep theirs)
@@ -734,17 +756,8 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     // the trial's bounds check and squared Gaussian-prior z of every parameter,
     // spread over the thread groups (the chain thread then only sums them in order)
     const bool par_prior = ACCEPT;
-    // fast-only proposals with R in HBM: the only fast block's next column
-    // (R(:, lp + 1) when no rotation is due) fetched into the vec rows by the
-    // thread groups, the loads issued before the other per-parameter work
-    // (proposal_tail then skips its own read; a block that rotates writes R
-    // only in rot_kernel)
-    const bool pre_col = PROPOSE && fast_only && !c.stage_R && c.pre_blk >= 0;
     if (par_test || par_prior || pre_col) {
-        constexpr int NRQ = (MAXBLK + NV - 1) / NV;
-        double rq[NRQ];
-        int col = -1, ncol = 0;
-        if (pre_col && act) {
+        if (pre_col && !rq_early && act) {
             const int b = c.pre_blk, off = ti[c.tl.blk_R_off + b];
             ncol = ti[c.tl.blk_n + b];
             const int lp = si[(size_t)(R.BLKLP + b) * MB + lane];
@@ -828,6 +841,7 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     k.blklp = Col<int>{si + (size_t)R.BLKLP * MB + lane, MB};
     k.itmp = c.stage_cyc ? Col<int>{it + lane, MB} : Col<int>{c.itmp_g + w, c.ld};
     k.fast_ix = si[(size_t)R.FASTIX * MB + lane];
+    const int i97_0 = k.r.i97;
     double &cur = sd[(size_t)SROW(R.L) * MB + lane];
     double &mult = sd[(size_t)SROW(R.M) * MB + lane];
     int &nacc = si[(size_t)R.NACC * MB + lane];
@@ -858,7 +872,7 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
         if (acc) {
             if (mult > 0) nacc += 1;
             mult = 1.0;
-            for (int i0 = 0; i0 < c.np; i0 += RCH) {   // P = trial, RCH loads in flight
+            for (int i0 = 0; !par_map && i0 < c.np; i0 += RCH) {   // P = trial (par_map: the groups, below)
                 double v[RCH];
 #pragma unroll
                 for (int u = 0; u < RCH; u++) v[u] = k.trial[i0 + u < c.np ? i0 + u : 0];
@@ -878,6 +892,7 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
         }
         STAMP(11);
         si[(size_t)R.ACCF * MB + lane] = acc ? 1 : 0;
+        if (par_map) oobw[lane] = acc ? 1 : 0;   // (target_like has read the bounds verdict)
         if (hist_row) hist_row[(size_t)c.n_used * c.W + w] = cur;   // the parameters: every group, below
         if (hist_terms) {
 #pragma unroll
@@ -887,7 +902,7 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     }
     STAMP(3);
     if (PROPOSE) {
-        for (int i0 = 0; !moved && i0 < c.np; i0 += RCH) {           // Trial = CurParams, RCH loads in flight
+        for (int i0 = 0; !moved && !par_map && i0 < c.np; i0 += RCH) {   // Trial = CurParams (par_map: below)
             double v[RCH];
 #pragma unroll
             for (int u = 0; u < RCH; u++) v[u] = k.P[i0 + u < c.np ? i0 + u : 0];
@@ -898,7 +913,8 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
         STAMP(14);
         k.defer = par_map;
         k.defer_rot = c.rot_defer;
-        k.col_pre = pre_col && k.blklp[c.pre_blk] % t.blk_n[c.pre_blk] != 0;
+        k.col_pre = pre_col && k.blklp[c.pre_blk] % t.blk_n[c.pre_blk] != 0 &&
+                    (!rq_early || k.blklp[c.pre_blk] == c.pre_lp);   // else proposal_tail reads the column itself
         if (fast_only) proposal_fast(c, t, k);
         else proposal(c, t, k);
         STAMP(15);
@@ -922,8 +938,21 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
     si[(size_t)R.J97 * MB + lane] = k.r.j97;
     si[(size_t)R.ISET * MB + lane] = k.r.iset;
     si[(size_t)R.FASTIX * MB + lane] = k.fast_ix;
+    ndw[lane] = k.r.nd < 97 ? k.r.nd : 97;
+    i0w[lane] = i97_0;
     }
     if (par_map) {   // UpdateParams' mapping product, rows spread over the waves (one thread per row, same order)
+        __syncthreads();
+        // first P = trial (accepted) or trial = P (rejected, or no accept in
+        // this launch: oobw is 0), the chain having left both to the groups
+        if (act) {
+            double *Pr = sd + (size_t)SROW(R.P) * MB + lane, *Tr = sd + (size_t)SROW(R.T) * MB + lane;
+            const bool mv = oobw[lane] != 0;
+            for (int i = grp; i < c.np; i += NV) {
+                if (mv) Pr[(size_t)i * MB] = Tr[(size_t)i * MB];
+                else Tr[(size_t)i * MB] = Pr[(size_t)i * MB];
+            }
+        }
         __syncthreads();
         if (act && tq[lane] >= 0.0) {
             const Tabs t = make_tabs(c, ti, td, c.stage_cov ? td : c.tab_d);
@@ -970,12 +999,22 @@ __device__ __forceinline__ void mh_body(const DevCfg &c, int fast_only, double *
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // read by the next launch only
         }
     // write back the image (rows of walkers past W are padding of the ld-wide
-    // rows: written back unchanged)
+    // rows: written back unchanged) -- of the RANMAR ring only the entries
+    // this launch's draws overwrote (positions i97 - 1, i97 - 2, ... mod 97
+    // of the first index)
+    if (act) {
+        const int nd = ndw[lane], i0 = i0w[lane];
+        for (int t = grp; t < nd; t += NV) {
+            int p = i0 - 1 - t;
+            if (p < 0) p += 97;
+            c.sd[(size_t)(R.U + p) * W + w] = sd[(size_t)(R.U + p) * MB + lane];
+        }
+    }
     if (skipR) {
-        stage_out(c.sd, sd, 0, 0, R.R, W, wb);
+        stage_out(c.sd, sd, R.C, R.C, R.R, W, wb);
         stage_out(c.sd, sd, R.R, rEnd, R.ND, W, wb);
     } else {
-        stage_out(c.sd, sd, 0, 0, R.ND, W, wb);
+        stage_out(c.sd, sd, R.C, R.C, R.ND, W, wb);
     }
     stage_out(c.si, si, 0, 0, ni_st, W, wb);
     STAMP(5);
@@ -2165,7 +2204,7 @@ static size_t mh_lds_bytes(const cmbs *s) {
     return (size_t)(nd_st + MAXLIKE + d.max_blk + d.tq_rows + d.def_cap * (QF_GROUPS + 1)) * MB * 8 +
            (size_t)((ntd + 31) & ~31) * 8 +
            (size_t)(ni_st + (d.stage_cyc ? d.all_n : 0)) * MB * 4 + (size_t)((d.tl.n_int + 63) & ~63) * 4 +
-           MB * 4 + (size_t)d.np * MB * 8 + 64;
+           MB * 4 + (size_t)d.np * MB * 8 + 2 * MB * 4 + 64;
 }
 
 static void set_mh_lds(cmbs *s) {
@@ -2387,6 +2426,9 @@ void sampler_create(cmbs *s, const cmbs_config_t *cfg) {
         for (int b : fb) s->rot_fast_any = s->rot_fast_any || s->blk_n[b] >= ROT_DEFER_MIN;
         s->rot_fast_n = (fb.size() == 1 && s->blk_n[fb[0]] >= ROT_DEFER_MIN) ? s->blk_n[fb[0]] : 0;
         d.pre_blk = (fb.size() == 1 && s->blk_n[fb[0]] >= 2) ? fb[0] : -1;
+        d.pre_off = d.pre_blk >= 0 ? s->blk_R_off[d.pre_blk] : 0;
+        d.pre_n = d.pre_blk >= 0 ? s->blk_n[d.pre_blk] : 0;
+        d.pre_lp = -1;
     }
     HIP_CHECK(hipFuncSetAttribute((const void *)rot_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(ROT_WAVES * sizeof(RotLds))));
@@ -3037,6 +3079,9 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
     dc.mask_on = masked ? 1 : 0;
     dc.lean = lean_cfg(s, fast_only, masked);
     if (s->pending_def && !accept) fail(CMBL_ERR_ARG, "internal: deferred likelihoods without an accepting step");
+    dc.pre_lp = -1;   // the single deferred block's loop index before this launch's proposals (rot_may_pend)
+    if (propose && fast_only && s->dc.rot_defer && s->rot_fast_n > 0 && dc.pre_blk >= 0 && s->rot_lp[g0 / 64] >= 0)
+        dc.pre_lp = s->rot_lp[g0 / 64];
     const bool rot = propose && rot_may_pend(s, fast_only, g0);
     if (rot) {                       // alternate the two rotation-list counters of this walker range
         dc.rot_par = s->rot_par[g0 / 64];
