@@ -819,17 +819,30 @@ __device__ unsigned int g_hl_sweeps[2][64];      // waves per sweep count, first
 // every wave: [0] column write + barrier, [1] partner read, dot product and
 // angle, [2] rotation + barrier, [3] rounds
 __device__ unsigned long long g_hl_phase[4];
+// s_memtime ticks per kernel phase, summed over lane 0 of every wave (tools/hl_stamps.py)
+__device__ unsigned long long g_hl_tp[12];
 #define HL_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #else
 #define HL_STAMP(v) ((void)0)
 #endif
 
+// one problem's buffers; per-problem strides of 2 mod 32 LDS dwords put the
+// groups' broadcast reads of one element on distinct bank pairs (at 16 mod 32,
+// BK15's M = 12, groups 0, 2 and 4 shared a pair: 3-way conflicts)
+template <int M>
+struct HLGrpLds {
+    static constexpr int SZ = 2 * M * (M + 1) + 2 * M;          // doubles before the pad
+    double rows[2][M][M + 1];       // two row buffers (odd stride: fewer bank conflicts within a problem);
+                                    // in the Jacobi, buffer 1 holds each row as of the round start
+    double dg[M];                   // a diagonal / g(x) broadcast
+    double isd[M];                  // 1 / sqrt of the first eigensolve's eigenvalues
+    double pad[((1 - SZ) % 16 + 16) % 16 + 1];
+};
+
 template <int M>
 struct HLRowsLds {
     static constexpr int G = 64 / M;   // problems per wave: M lanes each, packed (5 for M = 12)
-    double rows[G][2][M][M + 1];    // two row buffers per problem (odd stride: fewer bank conflicts);
-                                    // in the Jacobi, buffer 1 holds each row as of the round start
-    double dg[G][M];                // a diagonal / g(x) broadcast
+    HLGrpLds<M> g[G];
 };
 
 template <int M>
@@ -899,7 +912,7 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
     if (VF) {   // the input matrix (row r = column r), for the eigenvalues' signs after the solve
         if (on)
 #pragma unroll
-            for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = G[k];
+            for (int k = 0; k < M; k++) S.g[grp].rows[0][r][k] = G[k];
         __syncthreads();
     }
     bool failed = false;
@@ -1026,7 +1039,7 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
         double d = 0.0;
         if (on)
 #pragma unroll
-            for (int k = 0; k < M; k++) d = fma(S.rows[grp][0][im][k], V[k], d);
+            for (int k = 0; k < M; k++) d = fma(S.g[grp].rows[0][im][k], V[k], d);
         __syncthreads();   // the callers reuse the row buffers
         lam = (d * vm < 0.0) ? -sg : sg;
         return failed;
@@ -1053,8 +1066,9 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     const int w = live ? prob / h.nb : 0, b = live ? prob % h.nb : 0;
     const int n = h.n;
     const bool row_ok = on && r < n;
-    auto U_row = [&](int k, int j) { return S.rows[grp][0][k][j]; };
+    auto U_row = [&](int k, int j) { return S.g[grp].rows[0][k][j]; };
     // C row r from its lower-triangle elements (ElementsToMatrix :950-965), zero padded to M
+    HL_STAMP(q0);
     double A[M], V[M];
     const double *cm = cmat + ((long long)w * h.nb + b) * h.ncl;
 #pragma unroll
@@ -1073,25 +1087,25 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     auto to_basis = [&](const double *B0) {
         if (on)
 #pragma unroll
-            for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = (row_ok && k < n) ? B0[r * n + k] : (k == r ? 1.0 : 0.0);
+            for (int k = 0; k < M; k++) S.g[grp].rows[1][r][k] = (row_ok && k < n) ? B0[r * n + k] : (k == r ? 1.0 : 0.0);
         __syncthreads();
         double T[M];
 #pragma unroll
         for (int j = 0; j < M; j++) {             // T = A B0, row r
             double s = 0.0;
 #pragma unroll
-            for (int k = 0; k < M; k++) s += A[k] * S.rows[grp][1][k][j];
+            for (int k = 0; k < M; k++) s += A[k] * S.g[grp].rows[1][k][j];
             T[j] = s;
         }
         if (on)
 #pragma unroll
-            for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = T[k];
+            for (int k = 0; k < M; k++) S.g[grp].rows[0][r][k] = T[k];
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < M; j++) {             // B0^T T, row r
             double s = 0.0;
 #pragma unroll
-            for (int k = 0; k < M; k++) s += S.rows[grp][1][k][r] * S.rows[grp][0][k][j];
+            for (int k = 0; k < M; k++) s += S.g[grp].rows[1][k][r] * S.g[grp].rows[0][k][j];
             A[j] = s;
         }
         __syncthreads();
@@ -1102,7 +1116,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
         for (int i = 0; i < M; i++) {
             double s = 0.0;
 #pragma unroll
-            for (int k = 0; k < M; k++) s += S.rows[grp][1][i][k] * V[k];
+            for (int k = 0; k < M; k++) s += S.g[grp].rows[1][i][k] * V[k];
             U[i] = s;
         }
 #pragma unroll
@@ -1111,13 +1125,20 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     };
     // (1) C = U diag U^T (lane r: eigenvector r, i.e. column r of U)
     double dgr;
+#ifdef CMAMD_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    HL_STAMP(q1);
     if (h.u0) to_basis(h.u0 + (long long)b * n * n);
+    HL_STAMP(q2);
     bool unconverged = hl_ojacobi<M, HL_VFREE>(A, V, S, grp, r, lane, 0, dgr);
+    HL_STAMP(q3);
     if (h.u0) from_basis();
     if (on) {
-        S.dg[grp][r] = dgr;
+        S.g[grp].dg[r] = dgr;
+        S.g[grp].isd[r] = 1.0 / sqrt(dgr);
 #pragma unroll
-        for (int k = 0; k < M; k++) S.rows[grp][0][k][r] = V[k];     // U rows, from its columns
+        for (int k = 0; k < M; k++) S.g[grp].rows[0][k][r] = V[k];     // U rows, from its columns
     }
     __syncthreads();
     // (2) T = Chat U ; R = U^T T scaled by 1/sqrt(diag) (:878-889)
@@ -1139,7 +1160,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     }
     if (on)
 #pragma unroll
-        for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = T[k];
+        for (int k = 0; k < M; k++) S.g[grp].rows[1][r][k] = T[k];
     __syncthreads();
     double R[M];
 #pragma unroll
@@ -1148,18 +1169,18 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
         if (row_ok && j < n) {
 #pragma unroll
             for (int k = 0; k < M; k++)
-                if (k < n) s += U_row(k, r) * S.rows[grp][1][k][j];
+                if (k < n) s += U_row(k, r) * S.g[grp].rows[1][k][j];
             const int lo = r < j ? r : j, hi = r < j ? j : r;
-            s = s / sqrt(S.dg[grp][lo]);
-            s = s / sqrt(S.dg[grp][hi]);
+            s = s * S.g[grp].isd[lo] * S.g[grp].isd[hi];   // the reference divides by each root (:886-889)
         }
         R[j] = s;
     }
     __syncthreads();
+    HL_STAMP(q4);
     // (3) Rot = U R U^T (:891): T2 = R U^T (rows through LDS), A = U T2
     if (on)
 #pragma unroll
-        for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = R[k];
+        for (int k = 0; k < M; k++) S.g[grp].rows[1][r][k] = R[k];
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < M; j++) {        // T2[r][j] = sum_k R[r][k] U[j][k]
@@ -1173,7 +1194,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     __syncthreads();
     if (on)
 #pragma unroll
-        for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = T[k];
+        for (int k = 0; k < M; k++) S.g[grp].rows[1][r][k] = T[k];
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < M; j++) {        // A[r][j] = sum_k U[r][k] T2[k][j]
@@ -1181,14 +1202,17 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
         if (row_ok && j < n)
 #pragma unroll
             for (int k = 0; k < M; k++)
-                if (k < n) s += U_row(r, k) * S.rows[grp][1][k][j];
+                if (k < n) s += U_row(r, k) * S.g[grp].rows[1][k][j];
         A[j] = s;
     }
     __syncthreads();
     // (4) Rot = V diag V^T; g(x) = sign(x - 1) sqrt(2 max(0, x - ln x - 1))  (:892-894)
     double x;
+    HL_STAMP(q5);
     if (h.v0) to_basis(h.v0 + (long long)b * n * n);
+    HL_STAMP(q6);
     unconverged = hl_ojacobi<M, HL_VFREE>(A, V, S, grp, r, lane, 1, x) || unconverged;
+    HL_STAMP(q7);
     if (h.v0) from_basis();
     __syncthreads();                               // the solve's last reads of the row buffers
     if (on) {
@@ -1196,11 +1220,12 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
         // fmax(0, NaN) would make it 0 and the point's chi^2 finite
         const double arg = x - log(x) - 1;
         const double g = arg == arg ? sqrt(2 * fmax(0.0, arg)) : arg;
-        S.dg[grp][r] = (x - 1 >= 0) ? g : -g;
+        S.g[grp].dg[r] = (x - 1 >= 0) ? g : -g;
 #pragma unroll
-        for (int k = 0; k < M; k++) S.rows[grp][0][k][r] = V[k];     // V rows, from its columns
+        for (int k = 0; k < M; k++) S.g[grp].rows[0][k][r] = V[k];     // V rows, from its columns
     }
     __syncthreads();
+    HL_STAMP(q8);
     // (5) U = Cfhalf V ; C = U diag(g) U^T (:907-912)
     const double *cf = h.cfhalf + (long long)b * n * n;
 #pragma unroll
@@ -1217,7 +1242,7 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
     __syncthreads();
     if (on)
 #pragma unroll
-        for (int k = 0; k < M; k++) S.rows[grp][1][r][k] = T[k];
+        for (int k = 0; k < M; k++) S.g[grp].rows[1][r][k] = T[k];
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < M; j++) {        // C[r][j] = sum_k (T[r][k] g_k) T[j][k]
@@ -1225,13 +1250,13 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
         if (row_ok && j < n)
 #pragma unroll
             for (int k = 0; k < M; k++)
-                if (k < n) s += (T[k] * S.dg[grp][k]) * S.rows[grp][1][j][k];
+                if (k < n) s += (T[k] * S.g[grp].dg[k]) * S.g[grp].rows[1][j][k];
         A[j] = s;
     }
     __syncthreads();
     if (on)
 #pragma unroll
-        for (int k = 0; k < M; k++) S.rows[grp][0][r][k] = A[k];
+        for (int k = 0; k < M; k++) S.g[grp].rows[0][r][k] = A[k];
     __syncthreads();
     // an eigensolve that hit the sweep cap fails its (walker, bin): NaN bigX entries
     // (so -lnL is NaN) and a sticky status bit (cmbl_status); the reference stops the run
@@ -1246,9 +1271,18 @@ __global__ __launch_bounds__(64, (M <= 12 ? 2 : 1)) void cmbl_hl_rows_kernel(HLD
             int i = 0;
             while ((i + 1) * (i + 2) / 2 <= k) i++;
             const int j = k - i * (i + 1) / 2;
-            x[u] = failed ? __builtin_nan("") : S.rows[grp][0][i][j];
+            x[u] = failed ? __builtin_nan("") : S.g[grp].rows[0][i][j];
         }
     }
+#ifdef CMAMD_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    HL_STAMP(q9);
+    if (lane == 0) {
+        const unsigned long long q[10] = {q0, q1, q2, q3, q4, q5, q6, q7, q8, q9};
+        for (int i = 0; i < 9; i++) atomicAdd(&g_hl_tp[i], q[i + 1] - q[i]);
+        atomicAdd(&g_hl_tp[11], 1ull);
+    }
+#endif
 }
 
 // ------------------------------------------------------- exact (unbinned)
@@ -2561,5 +2595,8 @@ extern "C" int cmamd_debug_hl_sweeps(unsigned int *host) {
 }
 extern "C" int cmamd_debug_hl_phase(unsigned long long *host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_hl_phase), sizeof(cmamd::g_hl_phase)) == hipSuccess ? 0 : -5;
+}
+extern "C" int cmamd_debug_hl_tp(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(cmamd::g_hl_tp), sizeof(cmamd::g_hl_tp)) == hipSuccess ? 0 : -5;
 }
 #endif

@@ -37,3 +37,11 @@ if __name__ == "__main__":
     print(f"Jacobi rounds (lane 0 of every wave): {n}; s_memtime ticks per round: "
           f"write+barrier {ph[0] / n:.0f}, read+dot+angle {ph[1] / n:.0f}, rotate+barrier {ph[2] / n:.0f}, "
           f"total {(ph[0] + ph[1] + ph[2]) / n:.0f}")
+    tp = np.zeros(12, dtype=np.uint64)
+    assert N.lib().cmamd_debug_hl_tp(tp.ctypes.data_as(C.c_void_p)) == 0
+    nw = max(int(tp[11]), 1)
+    names = ["loads", "to_basis 1", "solve 1", "from_basis 1 + U rows + T = Chat U, R (2)", "Rot = U R U^T (3)",
+             "to_basis 2", "solve 2", "from_basis 2 + g(x) + V rows (4)", "(5) + output"]
+    print(f"kernel phases, s_memtime ticks per wave (lane 0 of {nw} waves):")
+    for i, nm in enumerate(names):
+        print(f"   {nm:45s} {tp[i] / nw:9.0f}")
