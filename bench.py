@@ -715,6 +715,9 @@ def kernel_roofline(kern, avg_ms, W, fused_bytes, lens_bytes):
             "frac": p["frac"], "traffic": None, "avg_launch_us": avg_ms * 1e3}
     if len(parts) > 1:
         roof["components"] = parts
+        # the launch's time against its two components run back to back at their
+        # peaks (frac above is the larger one alone, i.e. against perfect overlap)
+        roof["components_serial_frac"] = sum(q["frac"] for q in parts.values())
     return roof
 
 
