@@ -1121,6 +1121,14 @@ __global__ __launch_bounds__(MH_THREADS) void mh_bin_kernel(DevCfg c, int fast_o
 // partials of this launch) and propose step k + 1.  The pass waits on
 // nothing; the Metropolis chain of a tile starts as soon as its tails are
 // done instead of at a kernel boundary, and overlaps the pass.
+// The hand-off is cdna_hip_programming.md's counter recipe in its
+// write-through form (the note to its split-K combine, after Guideline 16):
+// the producers' stores are sc1 (write-through past the XCD L2), so no
+// release fence precedes the relaxed agent-scope fetch_add -- every wave
+// drains its stores, the workgroup barriers, one lane adds; the consumer
+// polls relaxed and takes one acquire fence after the match (tail_wait).
+// A release fence here would be a whole-L2 write-back per producer
+// workgroup (measured on the pass units: 35.8 -> 122 us a launch).
 __device__ __forceinline__ void tail_arrive(const TailWait &tw, int tile)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are done
