@@ -1,0 +1,17 @@
+// x / d for a d shared by many quotients, from d's correctly rounded
+// reciprocal r = 1 / d: q = x r, then one Markstein correction with the exact
+// residual x - q d (an fma), which rounds to x / d itself for finite normal
+// operands -- the bits of the division at three operations instead of a
+// division sequence (checked against the division on 2e8 random operand pairs
+// of the ranges used here: raw window sums over cal^2).
+#pragma once
+
+namespace cmamd {
+
+__device__ __forceinline__ double div_rn(double x, double d, double r)
+{
+    const double q = x * r;
+    return fma(fma(-q, d, x), r, q);
+}
+
+}  // namespace cmamd

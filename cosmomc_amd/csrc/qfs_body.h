@@ -3,6 +3,7 @@
 // sampler.hip's unified step launch).
 #pragma once
 
+#include "divrn.h"
 #include "qftile.h"
 #include "steptail.h"
 
@@ -60,20 +61,23 @@ __device__ __forceinline__ void qfs_body(double *smem, int item_ix, int tile, co
     f64x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-    double c2 = 1.0;
+    double c2 = 1.0, rc2 = 1.0;
     for (int s = 0; s < nsteps; s++) {
         const int buf = s & 1;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();                        // A tile s and this lane's sums landed; buf^1 free
-        if (s == 0) c2 = c2s[16 * wave + li];
+        if (s == 0) {
+            c2 = c2s[16 * wave + li];
+            rc2 = 1.0 / c2;
+        }
         double2 b[4];
         {
             const double *xk = xs + s * BK + 8 * lk;
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const double2 x2 = *reinterpret_cast<const double2 *>(xk + 2 * u);
-                b[u].x = x2.x - sv[u].x / c2;
-                b[u].y = x2.y - sv[u].y / c2;
+                b[u].x = x2.x - div_rn(sv[u].x, c2, rc2);
+                b[u].y = x2.y - div_rn(sv[u].y, c2, rc2);
             }
         }
         if (s + 1 < nsteps) {
@@ -113,9 +117,9 @@ __device__ __forceinline__ void qfs_body(double *smem, int item_ix, int tile, co
         const int e = tid + 256 * u, r = e >> 5, c = (e & 31) * 2;
         double2 v = make_double2(0.0, 0.0);
         if (w0 + r < W) {
-            const double cr = c2s[r];
-            v.x = xI[c] - dI[u].x / cr;
-            v.y = xI[c + 1] - dI[u].y / cr;
+            const double cr = c2s[r], rr = 1.0 / cr;
+            v.x = xI[c] - div_rn(dI[u].x, cr, rr);
+            v.y = xI[c + 1] - div_rn(dI[u].y, cr, rr);
         }
         *reinterpret_cast<double2 *>(smem + r * (QF_TILE + 2) + c) = v;
     }

@@ -15,6 +15,7 @@
 #pragma once
 
 #include "common.h"
+#include "divrn.h"
 
 namespace cmamd {
 
@@ -54,10 +55,11 @@ __device__ __forceinline__ void small_gauss_body(const SmallGaussLaunch &a, doub
     const bool act = w < Wc;
     const bool calp = c.log_cal_prior > 0 && c.cal_index >= 0;
     const double cal = (g == 0 && act && calp) ? a.nuis[(long long)w * a.ld_nuis + c.cal_index] : 1.0;   // likewise
-    double c2 = 1.0;   // RAWCAL: the stage calibration's square, as the pass's emit forms it
+    double c2 = 1.0, rc2 = 1.0;   // RAWCAL: the stage calibration's square, as the pass's emit forms it
     if (RAWCAL && act && a.stage_cal >= 0) {
         const double cl = a.nuis[(long long)w * a.ld_nuis + a.stage_cal];
         c2 = cl * cl;
+        rc2 = 1.0 / c2;
     }
     struct Elem { int ix, m0, m1, c0, c1; double mc, cc, fc, ch; };
     auto elem = [&](int e) {   // element e's table entries
@@ -82,7 +84,7 @@ __device__ __forceinline__ void small_gauss_body(const SmallGaussLaunch &a, doub
         if (RAWCAL)
 #pragma unroll
             for (int u = 0; u < 8; u++)
-                if (r[u] >= 0 && a.row_cal[r[u]]) v[u] = v[u] / c2;
+                if (r[u] >= 0 && a.row_cal[r[u]]) v[u] = div_rn(v[u], c2, rc2);   // = v[u] / c2
         double s = 0.0;
 #pragma unroll
         for (int u = 0; u < 8; u++) s += v[u];
