@@ -30,6 +30,7 @@
 #include <set>
 #include <sstream>
 
+#include "divrn.h"
 #include "quadform.h"
 #include "smallgauss.h"
 
@@ -1020,9 +1021,9 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
         double n2 = 0.0;
 #pragma unroll
         for (int k = 0; k < M; k++) n2 = fma(G[k], G[k], n2);
-        const double sg = sqrt(n2);
+        const double sg = sqrt(n2), rsg = 1.0 / sg;
 #pragma unroll
-        for (int k = 0; k < M; k++) V[k] = n2 > 0.0 ? G[k] / sg : (k == r ? 1.0 : 0.0);
+        for (int k = 0; k < M; k++) V[k] = n2 > 0.0 ? div_rn(G[k], sg, rsg) : (k == r ? 1.0 : 0.0);   // G[k] / sg
         // |g_r| is |lambda_r| and g_r / |g_r| is sign(lambda_r) u_r, so the norm alone
         // loses the sign of an eigenvalue of a matrix that is not positive definite
         // (a trial theory C can be): lambda_r = (A v)_i / v_i at the largest |v_i|,

@@ -6,6 +6,8 @@
 // of the ranges used here: raw window sums over cal^2).
 #pragma once
 
+#include <hip/hip_runtime.h>
+
 namespace cmamd {
 
 __device__ __forceinline__ double div_rn(double x, double d, double r)

@@ -252,8 +252,8 @@ __device__ void rot_matrix(Walker &k, int off, int n)
                 for (int q = 0; q < n; q++) norm += k.vec[q] * k.vec[q];
                 if (norm > 1e-3) break;
             }
-            const double sn = sqrt(norm);
-            for (int q = 0; q < n; q++) k.R[off + j * n + q] = k.vec[q] / sn;
+            const double sn = sqrt(norm), rsn = 1.0 / sn;
+            for (int q = 0; q < n; q++) k.R[off + j * n + q] = div_rn(k.vec[q], sn, rsn);   // = vec(q) / sn
         }
     } else {
         for (int i = 0; i < n * n; i++) k.R[off + i] = 0.0;
