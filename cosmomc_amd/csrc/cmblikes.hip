@@ -958,7 +958,9 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
                     // sweep; below it this sweep's rotation leaves them near cos^2 squared
                     big = big || alh * alh > HL_SWEEP_COS2 * (all * ahh);
                     const double d = ahh - all, e = 2.0 * alh;
-                    const double den = fabs(d) + sqrt(d * d + e * e);
+                    // the hardware square root (not correctly rounded): den only sets the
+                    // angle, and c, s stay orthonormal to rounding whatever t is
+                    const double den = fabs(d) + __builtin_amdgcn_sqrt(d * d + e * e);
                     double q = __builtin_amdgcn_rcp(den);           // reciprocal + two Newton steps
                     q = fma(q, fma(-den, q, 1.0), q);
                     q = fma(q, fma(-den, q, 1.0), q);
