@@ -961,9 +961,7 @@ __device__ bool hl_ojacobi(double (&G)[M], double (&V)[M], HLRowsLds<M> &S, int 
                     // the hardware square root (not correctly rounded): den only sets the
                     // angle, and c, s stay orthonormal to rounding whatever t is
                     const double den = fabs(d) + __builtin_amdgcn_sqrt(d * d + e * e);
-                    double q = __builtin_amdgcn_rcp(den);           // reciprocal + two Newton steps
-                    q = fma(q, fma(-den, q, 1.0), q);
-                    q = fma(q, fma(-den, q, 1.0), q);
+                    const double q = __builtin_amdgcn_rcp(den);     // the hardware reciprocal: likewise
                     const double t = ((d >= 0) == (e >= 0) ? fabs(e) : -fabs(e)) * q;
                     const double c = rsqrt(t * t + 1.0), s = t * c;
 #ifdef CMAMD_STAMPS
