@@ -97,6 +97,9 @@ struct CLDev {
     const BKMap *bkmaps;
     const double *bp_nu, *bp_R, *bp_dnu;
     const double *bp_lnu;           // log(nu) of every bandpass sample
+    int nsamp;                      // bandpass samples, all maps
+    double *td_den;                 // [nsamp] exp(G nu / Td0) - 1 for the launch's first walker's Td0 (cmbl_bk_tdtab)
+    double *td0;                    // [1] that Td0
     const double *log_l80;          // log(l / 80), l = 0 .. LP-1
     double fpivot_dust, fpivot_sync, decorr_dust[2], decorr_sync[2];
     int lform_dust, lform_sync;     // 0 flat, 1 lin, 2 quad
@@ -134,6 +137,20 @@ __device__ inline double bk_decorr(double Delta, double nu0, double nu1, const d
     return exp(log(Delta) * scl_nu * scl_ell);
 }
 
+// The dust greybody's denominators exp(G nu / T_dust) - 1 of every bandpass
+// sample at the first walker's T_dust (a fixed parameter in the BK15 runs, so
+// every walker's): cmbl_bk_prologue takes them from here when its walker's
+// T_dust is the same value -- the same operations, so the same bits -- and
+// forms them itself otherwise.  One of its three exponentials per sample.
+__global__ __launch_bounds__(256) void cmbl_bk_tdtab(CLDev c, const double *__restrict__ nuis)
+{
+    const double Tdust = nuis[4];   // DataParams(5) of walker 0 (row 0 exists whenever a prologue runs)
+    const double G = ghz_kelvin();
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k < c.nsamp) c.td_den[k] = exp(G * c.bp_nu[k] / Tdust) - 1;
+    if (k == 0) c.td0[0] = Tdust;
+}
+
 // BK per-walker foreground set-up (TBK_planck_AddForegrounds :250-285): the
 // SED factors of every map (one wave per map, bandpass integrals as wave
 // reductions) and the dust / sync / dust-sync l profiles.
@@ -153,13 +170,15 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
     const double nu0d = c.fpivot_dust, nu0s = c.fpivot_sync;
     const double gb0 = pow(nu0d, 3 + betadust) / (exp(G * nu0d / Tdust) - 1);
     const double pl0 = pow(nu0s, 2 + betasync);
+    const bool tab = Tdust == c.td0[0];              // cmbl_bk_tdtab's denominators apply
     for (int i = wave; i < c.nreq; i += 4) {
         const BKMap m = c.bkmaps[i];
         double gb = 0.0, pl = 0.0;
         for (int k = lane; k < m.n; k += 64) {
             const double nu = c.bp_nu[m.off + k], R = c.bp_R[m.off + k], dn = c.bp_dnu[m.off + k];
             const double lnu = c.bp_lnu[m.off + k];          // nu^e as exp(e log nu): one exp instead of a pow
-            gb += dn * R * exp((3 + betadust) * lnu) / (exp(G * nu / Tdust) - 1);
+            const double den = tab ? c.td_den[m.off + k] : exp(G * nu / Tdust) - 1;
+            gb += dn * R * exp((3 + betadust) * lnu) / den;
             pl += dn * R * exp((2 + betasync) * lnu);
         }
         gb = wave_sum(gb);
@@ -1468,7 +1487,7 @@ struct CMBLikes final : Like {
     bool has_map_names = false, bk = false;
     std::vector<std::string> map_names, used_map_order;
     std::vector<int> map_fields, use_map, require_map, map_used_index, map_required_index, required_order;
-    int approx = 0, nmaps = 0, nreq = 0, ncl = 0, ncl_used = 0;   // approx: 1 HL, 2 gaussian, 3 exact
+    int approx = 0, nmaps = 0, nreq = 0, ncl = 0, ncl_used = 0, nsamp = 0;   // approx: 1 HL, 2 gaussian, 3 exact
     bool binned = true;
     double fksy = 1.0;                                              // fullsky_exact_fksy
     int lmin = 0, lmax = 0, nbins = 0, bin_min = 1, bin_max = 0, nb = 0;
@@ -1488,7 +1507,7 @@ struct CMBLikes final : Like {
     bool items_even = true, small_gauss = false;
     bool use_group = false;      // BK foregrounds: grouped-pair window kernel
     int n_gitem = 0;
-    DevBuf d_gitems, d_gw, d_bplnu, d_logl80;
+    DevBuf d_gitems, d_gw, d_bplnu, d_logl80, d_tdden, d_td0;
     int small_ntask = 0;
     SmallDev sdev{};
     DevBuf d_invcov, d_stasks, d_smt, d_sct;
@@ -2294,6 +2313,9 @@ struct CMBLikes final : Like {
             for (int l = 1; l < (int)ll80.size(); l++) ll80[l] = std::log(l / 80.0);
             up(d_bplnu, blnu.data(), blnu.size() * 8);
             up(d_logl80, ll80.data(), ll80.size() * 8);
+            d_tdden.alloc(std::max<size_t>(1, bnu.size()) * 8);
+            d_td0.alloc(8);
+            nsamp = (int)bnu.size();
         }
         qf.init(invcov, nX);
         up(d_invcov, invcov.data(), invcov.size() * 8);
@@ -2319,6 +2341,9 @@ struct CMBLikes final : Like {
         dev.bkmaps = bk ? d_bkmaps.as<BKMap>() : nullptr;
         dev.bp_nu = bk ? d_bpnu.as<double>() : nullptr;
         dev.bp_lnu = bk ? d_bplnu.as<double>() : nullptr;
+        dev.nsamp = bk ? nsamp : 0;
+        dev.td_den = bk ? d_tdden.as<double>() : nullptr;
+        dev.td0 = bk ? d_td0.as<double>() : nullptr;
         dev.log_l80 = bk ? d_logl80.as<double>() : nullptr;
         dev.bp_R = bk ? d_bpR.as<double>() : nullptr;
         dev.bp_dnu = bk ? d_bpdnu.as<double>() : nullptr;
@@ -2476,6 +2501,8 @@ struct CMBLikes final : Like {
         const double *nu = nuis ? nuis : dl;   // never read when n_nuis == 0
         const int tiles = (W + 63) / 64;
         if (bk) {
+            hipLaunchKernelGGL(cmbl_bk_tdtab, dim3((dev.nsamp + 255) / 256), dim3(256), 0, stream, dev, nu);
+            HIP_CHECK(hipGetLastError());
             timed_launch("cmbl_bk_prologue", stream, [&](hipEvent_t e0, hipEvent_t e1) {
                 hipExtLaunchKernelGGL(cmbl_bk_prologue, dim3(W), dim3(256), 0, stream, e0, e1, 0, dev, nu, ld_nuis,
                                       coef, prof, W);
