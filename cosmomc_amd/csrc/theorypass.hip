@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <map>
 
+#include "divrn.h"
 #include "theorypass.h"
 
 namespace cmamd {
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_kernel(TPD
     for (int q = tid; q < nstep * (TP_MAXCOL / 4); q += 256)
         reinterpret_cast<unsigned int *>(msh)[q] =
             reinterpret_cast<const unsigned int *>(c.cmap + (long long)it.soff * TP_MAXCOL)[q];
-    double c2[TP_MAXOUT];
+    double c2[TP_MAXOUT], rc2[TP_MAXOUT];   // cal^2 and its reciprocal (div_rn)
 #pragma unroll
     for (int o = 0; o < TP_MAXOUT; o++) {
         const int ci = o ? c.out[1].cal_index : c.out[0].cal_index;
@@ -177,6 +178,7 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_kernel(TPD
         double cl = 1.0;
         if (ci >= 0 && nu) cl = nu[(long long)wl * ldn + ci];
         c2[o] = cl * cl;
+        rc2[o] = 1.0 / c2[o];
     }
     store_w(0, 0);
     __syncthreads();
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_kernel(TPD
             const bool o1 = d.out != 0;   // selects, not a dynamically indexed kernel argument
             const int kind = o1 ? c.out[1].kind : c.out[0].kind;
             double *out = o1 ? c.out[1].out : c.out[0].out;
-            if (d.cal) v = v / (o1 ? c2[1] : c2[0]);
+            if (d.cal) v = div_rn(v, o1 ? c2[1] : c2[0], o1 ? rc2[1] : rc2[0]);   // = v / cal^2
             if (kind == 0) {
                 out[(long long)d.row * W + w] = v;
             } else {

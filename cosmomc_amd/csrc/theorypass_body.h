@@ -4,6 +4,7 @@
 // mh_step_kernel).  The LDS comes from the caller (tp_vec_lds_bytes).
 #pragma once
 
+#include "divrn.h"
 #include "theorypass.h"
 
 namespace cmamd {
@@ -118,7 +119,7 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
     for (int q = tid; q < nstep * (TP_MAXCOL / 4); q += 256)
         reinterpret_cast<unsigned int *>(msh)[q] =
             reinterpret_cast<const unsigned int *>(c.cmap + (long long)it.soff * TP_MAXCOL)[q];
-    double c2[TP_MAXOUT] = {1.0, 1.0};
+    double c2[TP_MAXOUT] = {1.0, 1.0}, rc2[TP_MAXOUT] = {1.0, 1.0};   // cal^2 and its reciprocal (div_rn)
     if (!RAW) {
 #pragma unroll
         for (int o = 0; o < TP_MAXOUT; o++) {
@@ -128,6 +129,7 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
             double cl = 1.0;
             if (ci >= 0 && nu) cl = nu[(long long)wl * ldn + ci];
             c2[o] = cl * cl;
+            rc2[o] = 1.0 / c2[o];
         }
     }
     store_w(0);
@@ -155,7 +157,7 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
             a0[r] = on[r] ? 0.0 : a0[r];
             b0[r] = on[r] ? 0.0 : b0[r];
             const bool o1 = d[r].out != 0;
-            const double q = (!RAW && d[r].cal) ? v / (o1 ? c2[1] : c2[0]) : v;
+            const double q = (!RAW && d[r].cal) ? div_rn(v, o1 ? c2[1] : c2[0], o1 ? rc2[1] : rc2[0]) : v;   // v / cal^2
             if (on[r] && w < W) {
                 double *out = o1 ? c.out[1].out : c.out[0].out;
                 if ((o1 ? c.out[1].kind : c.out[0].kind) == 0)

@@ -20,8 +20,11 @@ d = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])
 print(f"[{sys.argv[1]}] rep {sys.argv[2]}: {d['value'] / 1e6:.3f} M evals/s {d['ms_per_step'] * 1e3:.2f} us/step",
       {k: round(v, 2) for k, v in d["roofline"]["avg_kernel_us"].items() if v}, flush=True)
 for leg in ("config1_tt", "config4_fast21", "config5_bk15_plik", "config2_drag"):
-    if isinstance(d.get(leg), dict) and "ms_per_step" in d[leg]:
-        print(f"    {leg}: {d[leg]['ms_per_step'] * 1e3:.2f} us/step", d[leg].get("kernel_us_per_step", ""), flush=True)
+    c = d.get(leg)
+    if isinstance(c, dict) and ("ms_per_step" in c or "ms_per_drag_step" in c):
+        t = c.get("ms_per_step", c.get("ms_per_drag_step"))
+        print(f"    {leg}: {t * 1e3:.2f} us/step", c.get("kernel_us_per_step", c.get("kernel_us_per_drag_step", "")),
+              flush=True)
 PY
   done
 done
