@@ -1175,9 +1175,12 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fa
         qfs_body<true>(lds, item_ix, tile, t.q);
         tail_arrive(tw, tile);
     } else if (rr.x == TAIL_GAUSS) {
-        if (lb >= t.ng) return;
-        small_gauss_body<UNI_WT, true, true>(t.g, lds, lb);
-        tail_arrive(tw, lb * UNI_WT / 64);
+        // contiguous walker groups per XCD (lb % 8 is the XCD): each partial row's
+        // 128-byte lines are read by one XCD's L2 instead of four (35.1 -> 34.5 us)
+        const int grows = (t.ng + 7) >> 3, q = (lb & 7) * grows + (lb >> 3);
+        if (q >= t.ng) return;
+        small_gauss_body<UNI_WT, true, true>(t.g, lds, q);
+        tail_arrive(tw, q * UNI_WT / 64);
     } else if (rr.x == TAIL_PASS) {
         if (lb >= t.np) return;
         tp_vec_body<2, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
