@@ -809,10 +809,11 @@ struct SmallDev {
 };
 
 template <int WT>
-__global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(SmallGaussLaunch a)
+__global__ __launch_bounds__(256) void cmbl_gauss_small_kernel(SmallGaussLaunch a, int ng)
 {
     __shared__ double lds[small_gauss_lds_doubles<WT>()];
-    small_gauss_body<WT>(a, lds, blockIdx.x);
+    const int q = small_gauss_group(blockIdx.x, ng);
+    if (q < ng) small_gauss_body<WT>(a, lds, q);
 }
 
 // ---------------------------------------------------------------- HL
@@ -2576,8 +2577,9 @@ struct CMBLikes final : Like {
         if (small_gauss) {
             const SmallGaussLaunch a = small_args(W, nu, ld_nuis, out, ws);
             timed_launch("cmbl_gauss_small_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                hipExtLaunchKernelGGL(cmbl_gauss_small_kernel<SMALL_WT>, dim3((W + SMALL_WT - 1) / SMALL_WT), dim3(256),
-                                      0, stream, e0, e1, 0, a);
+                const int ng = (W + SMALL_WT - 1) / SMALL_WT;
+                hipExtLaunchKernelGGL(cmbl_gauss_small_kernel<SMALL_WT>, dim3(small_gauss_blocks(ng)), dim3(256), 0,
+                                      stream, e0, e1, 0, a, ng);
             });
             HIP_CHECK(hipGetLastError());
             return QFDeferred{};

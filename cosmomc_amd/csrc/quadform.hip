@@ -218,10 +218,11 @@ __global__ __launch_bounds__(256, 2) void quadform_corun(
 {
     static_assert(small_gauss_lds_doubles<WT>() <= QF_LDS_DOUBLES, "co-run LDS");
     __shared__ __attribute__((aligned(16))) double smem[QF_LDS_DOUBLES];
-    const int nq = gridDim.x - ns;
+    const int nq = gridDim.x - small_gauss_blocks(ns);
     const int b = blockIdx.x;
     if (b >= nq) {
-        small_gauss_body<WT>(co, smem, b - nq);
+        const int q = small_gauss_group(b - nq, ns);
+        if (q < ns) small_gauss_body<WT>(co, smem, q);
         return;
     }
     int item_ix, tile;
@@ -337,7 +338,8 @@ QFDeferred QuadForm::launch_deferred(int W, void *ws, const double *addend, hipS
     if (co) {
         const int ns = (co->W + SMALL_WT - 1) / SMALL_WT;
         timed_launch(co_prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(quadform_corun<SMALL_WT>, dim3(n_items * tiles + ns), dim3(256), 0, stream, e0, e1, 0,
+            hipExtLaunchKernelGGL(quadform_corun<SMALL_WT>, dim3(n_items * tiles + small_gauss_blocks(ns)), dim3(256), 0,
+                                  stream, e0, e1, 0,
                                   d_ct.as<double>(), Np, (const double *)x, W, d_items[kb].as<QFItem>(), n_items,
                                   (int)(tiles % 8 == 0), partial, *co, ns);
         });
@@ -396,8 +398,9 @@ __global__ __launch_bounds__(256, 2) void quadform_pair_ticket(QFSource qa, doub
         return;
     }
     b -= nq + nq_b;
-    if (b < ng) small_gauss_body<WT>(ga, smem, b);
-    else if (b < 2 * ng) small_gauss_body<WT>(gb, smem, b - ng);
+    const int gp = small_gauss_blocks(ng);
+    const int q = small_gauss_group(b < gp ? b : b - gp, ng);
+    if (q < ng) small_gauss_body<WT>(b < gp ? ga : gb, smem, q);
 }
 
 void launch_qf_pair(const QFSource &qa, double *out_a, const QFSource *qb, double *out_b, int W,
@@ -408,7 +411,7 @@ void launch_qf_pair(const QFSource &qa, double *out_a, const QFSource *qb, doubl
     const SmallGaussLaunch none{};
     // one set: [quadratic form a][chi^2 a]
     const int nq_b = qb ? nq : 0, ng_b = gb ? ng : 0;
-    const dim3 grid(nq + nq_b + ng + ng_b);
+    const dim3 grid(nq + nq_b + small_gauss_blocks(ng) + small_gauss_blocks(ng_b));
     timed_launch(prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
         hipExtLaunchKernelGGL(quadform_pair_ticket<SMALL_WT>, grid, dim3(256), 0, stream, e0, e1, 0, qa, out_a,
                               qb ? *qb : qa, out_b, W, nq, ga ? *ga : none, gb ? *gb : none, ng, nq_b);

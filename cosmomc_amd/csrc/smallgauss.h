@@ -33,6 +33,17 @@ template <int WT> constexpr int small_gauss_lds_doubles(int nX) {
     return SMALL_MAXTASK * WT + SMALL_NX * WT + 256 + nX * nX;
 }
 
+// Walker group of workgroup lb among ng (a launch gives the role 8 ceil(ng / 8)
+// workgroups, from a multiple of 8): workgroup b runs on XCD b % 8, so with
+// lb % 8 the XCD each XCD takes a contiguous range of groups and a partial
+// row's 128-byte lines (16 walkers) are read by one L2 instead of four.
+// Groups >= ng: none.
+__device__ __forceinline__ int small_gauss_group(int lb, int ng)
+{
+    return (lb & 7) * ((ng + 7) >> 3) + (lb >> 3);
+}
+__host__ __device__ inline int small_gauss_blocks(int ng) { return (ng + 7) & ~7; }
+
 // RAWCAL: partial rows are raw window sums; rows flagged in a.row_cal are
 // divided by the walker's cal^2 as they are loaded (SmallGaussLaunch)
 // SIGNAL: -lnL is stored agent-scope (write-through) for a consumer in the
