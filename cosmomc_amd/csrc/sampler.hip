@@ -1185,6 +1185,9 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fa
         if (lb >= t.np) return;
         tp_vec_body<2, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
     } else if (lb < nmh) {
+        // the chain is latency on one lane: its waves, dispatched last (the youngest,
+        // so the last in issue arbitration), take the SIMD first (34.6 -> 34.0 us)
+        __builtin_amdgcn_s_setprio(3);
         mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, 0, lds, lb, ACCEPT ? &tw : nullptr);
     }
 }
