@@ -1172,7 +1172,7 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fa
         if (lb >= t.nq) return;
         int item_ix, tile;
         qf_place(lb, t.q.src.n_items, t.q.src.xcd_map, item_ix, tile);
-        qfs_body<true>(lds, item_ix, tile, t.q);
+        qfs_body<true, !PROPOSE>(lds, item_ix, tile, t.q);
         tail_arrive(tw, tile);
     } else if (rr.x == TAIL_GAUSS) {
         // contiguous walker groups per XCD (lb % 8 is the XCD): each partial row's
