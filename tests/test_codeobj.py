@@ -40,3 +40,27 @@ def test_no_argument_copy_in_scratch(kernels):
     assert not big, big
     mh = {n: k["scratch"] for n, k in hot.items() if "mh_" in n and k["scratch"] > 64}
     assert not mh, mh
+
+
+def test_asm_loads_waited_before_use(tmp_path):
+    """The unified launch's quadratic form loads the raw sums with inline asm
+    and waits for them with a hand-counted vmcnt (qfs_body.h): rebuild
+    sampler.hip's gfx950 assembly and check that no instruction reads, copies
+    or reuses a load's registers before a wait covers it
+    (tools/check_asm_loads.py; a dead prefetch's registers once became MFMA
+    accumulators while the load was in flight)."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = os.path.join(ROOT, "cosmomc_amd", "csrc")
+    out = str(tmp_path / "sampler.s")
+    subprocess.run([hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-x", "hip",
+                    "-S", "sampler.hip", "-o", out, "--offload-device-only"], cwd=src, check=True,
+                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_asm_loads.py"), out],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:]
+    last = r.stdout.strip().splitlines()[-1]
+    assert last.endswith("0 bad, 0 to review") and int(last.split()[0]) > 0, r.stdout[-2000:]
