@@ -128,7 +128,7 @@ __device__ __forceinline__ void qfs_body_nj(double *smem, int item_ix, int tile,
     const int Np = q.Np, W = a.W;
     const int w0 = tile * QF_TILE;
     const QFItem it = q.items[item_ix];
-    // unrolled: an asm load's registers are in flight across the next step, and a
+    // unrolled: an asm load's registers are in flight into the next step, and a
     // loop's back edge may copy them (reading them before they land)
     constexpr int nsteps = NJ * (QF_TILE / BK);   // even, >= 2
     const int kbase0 = it.J0 * QF_TILE;
@@ -137,11 +137,12 @@ __device__ __forceinline__ void qfs_body_nj(double *smem, int item_ix, int tile,
     double *xI = xs + QFS_XS_D;                 // [64] X over the I panel
     const double *Sw0 = a.S + (size_t)w0 * Np;
     const int n = 16 * wave + li;               // this lane's walker in the tile
-    // The VGPR loads (the calibration, the raw sums) are inline asm counted by
-    // hand: beside LDS-DMA the compiler waits vmcnt(0) for any load of its own
-    // (cdna_hip_programming.md, the LDS-DMA GEMM traps).  Every vector memory
-    // operation counts in issue order, so one counted vmcnt per step covers
-    // both queues.  tools/check_asm_loads.py checks the built code.
+    // The VGPR loads (the calibration, the raw sums) are inline asm waited for
+    // by hand: beside LDS-DMA the compiler waits vmcnt(0) for any load of its
+    // own (cdna_hip_programming.md, the LDS-DMA GEMM traps), which at the last
+    // step would wait for the Delta_I rows too.  Every vector memory operation
+    // counts in issue order; each step's own wait covers both queues.
+    // tools/check_asm_loads.py (tests/test_codeobj.py) checks the built code.
     double cv;
     const bool has_cal = a.cal_index >= 0;
     {                                           // the emit's c2 = cal * cal (walkers past W: never stored)
