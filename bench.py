@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="per-round CPU baseline sample (5 rounds)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-lensing", action="store_true", help="plik_lite only (configs[2] minus lensing)")
+    p.add_argument("--cache-steps", type=int, default=200,
+                   help="steps of the separately labelled binned-theory-cache leg (SURVEY 8(d)); -1 skips it")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse ranks")
     p.add_argument("--converge-seconds", type=float, default=20.0,
                    help="R-1 vs wall-clock run after the throughput timing (0 = skip)")
@@ -314,6 +316,54 @@ N_B_TT = 215                                    # plik_lite TT bins
 N_L_TT = 2479                                   # l = 30..2508
 FLOPS_EVAL_TT = 2 * N_L_TT + 2 * N_B_TT * N_B_TT + 4 * N_B_TT   # 98,268 (SURVEY 8d with TT's sizes)
 BYTES_BIN_TT = 8 * N_L_TT + 8
+
+
+def binned_cache_run(smp, W, world, steps, warmup=20):
+    """SURVEY 8(d)'s labelled variant, never the headline: the same sampler
+    and workload with cmbs_set_binned_cache -- each walker's theory binned once
+    per call (the theory is fixed within a fast-step call and the raw window
+    sums are calibration-independent), so a step is plik's quadratic form, the
+    lensing chi^2 and the Metropolis chain.  Roofline with the 2 N_l term
+    dropped from F and the 8 N_l term from B, as 8(d) prescribes; the lensing
+    likelihood's work is not counted."""
+    import torch
+    from cosmomc_amd import _native as N
+    smp.set_binned_cache(True)
+    smp.step(warmup, fast_only=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    smp.step(steps, fast_only=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    N.profile_reset()
+    N.profile_enable(True)
+    smp.step(steps, fast_only=True)
+    torch.cuda.synchronize()
+    N.profile_enable(False)
+    tot, cnt = N.profile_read("mh_step_kernel")
+    smp.set_binned_cache(False)
+    f_eval = 2 * N_B * N_B + 4 * N_B                                   # F without 2 N_l
+    b_eval = 16 + (8 * N_B * N_B + 8 * 2479 + 8 * N_B) / W             # B without 8 N_l
+    per_gpu = W * steps / dt
+    ceil = min(PEAK_FP64_TFLOPS * 1e12, f_eval / b_eval * PEAK_HBM_GBS * 1e9)
+    avg_us = tot / cnt * 1e3 if cnt else None
+    qf = W * FLOPS_QUADFORM
+    return {"label": "binned-theory cache (SURVEY 8(d) variant; NOT the headline): theory binned once per "
+                     "cmbs_step call, every step runs plik's quadratic form + the lensing chi^2 + the chain",
+            "walkers_total": W * world, "evals_per_s": W * world * steps / dt, "ms_per_step": dt / steps * 1e3,
+            "step_roofline": {"achieved_tflops": per_gpu * f_eval / 1e12, "ceiling_tflops": ceil / 1e12,
+                              "frac": per_gpu * f_eval / ceil,
+                              "note": "per GPU: F = 2 N_b^2 + 4 N_b = 753,990 flop/eval, B = 16 + 3,030,888 / W "
+                                      "bytes/eval (8(d) with the N_l terms dropped)"},
+            "mh_step_kernel": {"avg_launch_us": avg_us,
+                               "mfma_frac": (qf / (avg_us * 1e-6) / 1e12 / PEAK_FP64_TFLOPS) if avg_us else None,
+                               "note": "the quadratic form's 2 N_b^2 + 2 N_b flops per walker over the launch "
+                                       "(chi^2 and chain in the same launch)"}}
 
 
 def config1_run(W, rank, world, tmpdir, seconds, steps=300):
@@ -812,6 +862,9 @@ def main():
         kern = {k: v for k, v in kern.items() if v[1]}
         _, _, _, nacc = smp.state()
         acc_rate = float(nacc.sum()) / (W * (args.warmup + 2 * args.steps))
+        cache = None
+        if args.cache_steps > 0 and not args.no_lensing:
+            cache = binned_cache_run(smp, W, world, args.cache_steps)
         conv = None
         if args.converge_seconds > 0:
             conv = convergence_run(W, rank, world, td, args.converge_seconds, lensing=not args.no_lensing)
@@ -863,6 +916,8 @@ def main():
         }
         if conv is not None:
             out["convergence"] = conv
+        if cache is not None:
+            out["binned_cache"] = cache
         if c1 is not None:
             out["config1_tt"] = c1
         if c4 is not None:

@@ -80,6 +80,8 @@ def lib():
         L.cmbl_last_error.restype = C.c_char_p
         L.cmbl_info.argtypes = [vp, C.POINTER(i), C.POINTER(i), C.POINTER(i), C.POINTER(C.c_char_p),
                                 C.POINTER(C.c_char_p)]
+        L.cmbl_derived_info.argtypes = [vp, C.POINTER(i), C.POINTER(C.c_char_p)]
+        L.cmbl_derived_batch.argtypes = [vp, i, vp, ll, vp, ll, vp]
         L.cmbl_workspace_size.argtypes = [vp, i]
         L.cmbl_workspace_size.restype = sz
         L.cmbl_loglike_batch.argtypes = [vp, i, vp, ll, ll, vp, ll, vp, vp, vp]
@@ -99,6 +101,7 @@ def lib():
         L.cmbs_set_start.argtypes = [vp, vp, vp]
         L.cmbs_step.argtypes = [vp, i, i, vp]
         L.cmbs_set_groups.argtypes = [vp, i]
+        L.cmbs_set_binned_cache.argtypes = [vp, i]
         L.cmbs_history_host.argtypes = [vp, i, i, vp]
         L.cmbs_set_trial_theory.argtypes = [vp, i, vp, ll, ll]
         L.cmbs_step_drag.argtypes = [vp, i, d, THEORY_FN, vp, vp]

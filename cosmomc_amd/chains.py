@@ -31,6 +31,10 @@ source/GeneralTypes.f90:671-776): ``chi2_<tag>`` = 2 x each likelihood's -lnL
 at the point (``cmbs_history_terms_host``), ``chi2_prior`` = 2 x (like -
 sum of terms), and ``chi2_<type>`` sums for every likelihood type used more
 than once; ``root.likelihoods`` lists them (OutputDescription, :792-812).
+With ``derived`` given, the likelihoods' own derived parameters (the '*'
+names of their nuisance .paramnames, e.g. SMICA's D_l(2000)) come first among
+the derived columns, as in addLikelihoodDerivedParams (:772-777):
+``LikelihoodDerived`` evaluates them on the device for every history row.
 """
 from __future__ import annotations
 
@@ -67,10 +71,12 @@ class ChainWriter:
     ranges: list of (min, max) or None."""
 
     def __init__(self, root: str, names, labels=None, ranges=None, walkers=None, first_chain: int = 1,
-                 likelihoods=None, burn_in: int = 2, thin: int = 1):
+                 likelihoods=None, burn_in: int = 2, thin: int = 1, derived=None):
         """likelihoods: one (tag, type, name, version) per sampler likelihood,
         in add_likelihood order, to add the chi2_* columns.  burn_in / thin as
-        TChainSampler%burn_in and MoveDone's thin_fac (module docstring)."""
+        TChainSampler%burn_in and MoveDone's thin_fac (module docstring).
+        derived: a LikelihoodDerived (its names, and the columns it computes
+        from the history's points)."""
         self.root = root
         self.names = list(names)
         self.labels = list(labels) if labels is not None else list(names)
@@ -78,6 +84,7 @@ class ChainWriter:
         self.walkers = walkers
         self.first_chain = first_chain
         self.likelihoods = [tuple(x) for x in likelihoods] if likelihoods else []
+        self.like_derived = derived
         self.pending = {}                          # walker -> [point values (like, P..., chi2...), count]
         self.next_step = None
         self.burn_in, self.thin = int(burn_in), max(1, int(thin))
@@ -91,6 +98,8 @@ class ChainWriter:
         with open(root + ".paramnames", "w") as f:
             for n, lab in zip(self.names, self.labels):
                 f.write(f"{n}\t{lab}\n")
+            for n, lab in (self.like_derived.names if self.like_derived else []):
+                f.write(f"{n}*\t{lab}\n")
             for n, lab in derived:
                 f.write(f"{n}*\t{lab}\n")
         if ranges is not None:
@@ -160,8 +169,11 @@ class ChainWriter:
         if self.likelihoods and (terms is None or np.shape(terms)[1] != len(self.likelihoods)):
             raise ValueError("chi2 columns need the per-likelihood history terms of every likelihood")
         walkers = range(W) if self.walkers is None else self.walkers
+        dcols = self.like_derived.columns(rows[:, :n1 - 1, :]) if self.like_derived else None   # [steps, nd, W]
         for w in walkers:
             pts = np.concatenate([rows[:, n1 - 1:n1, w], rows[:, :n1 - 1, w]], axis=1)   # like, P...
+            if dcols is not None:
+                pts = np.concatenate([pts, dcols[:, :, w]], axis=1)
             if self.likelihoods:
                 pts = np.concatenate([pts, self._derived(rows[:, n1 - 1, w], np.asarray(terms)[:, :, w])], axis=1)
             with open(self._file(w), "a") as fh:
@@ -229,3 +241,45 @@ class ChainWriter:
         """End of the run: the points the chains sit at are not written
         (MoveDone writes a point only when the chain leaves it)."""
         self.pending = {}
+
+
+class LikelihoodDerived:
+    """The likelihoods' derived parameters for chain rows
+    (addLikelihoodDerivedParams, GeneralTypes.f90:772-777:
+    Derived(derived_indices) = derivedParameters(Theory, P(nuisance_indices))).
+
+    likes: the LikelihoodList after add_nuisance_parameters; params_used: the
+    1-based parameter indices of the history rows; P_fixed: the full parameter
+    vector supplying the values of parameters that are not used (fixed)."""
+
+    def __init__(self, likes, params_used, P_fixed, labels=None):
+        self.likes = [l for l in likes if getattr(l, "derived_names", None)]
+        self.params_used = [int(i) for i in params_used]
+        self.P_fixed = np.asarray(P_fixed, dtype=np.float64)
+        order = []
+        for l in self.likes:
+            for nm, ix in zip(l.derived_names, l.derived_indices):
+                order.append((ix, nm))
+        self.n = max([ix for ix, _ in order], default=0)
+        names = [""] * self.n
+        for ix, nm in order:
+            names[ix - 1] = nm
+        labels = labels or {}
+        self.names = [(nm, labels.get(nm, nm)) for nm in names]
+
+    def columns(self, P_used):
+        """P_used [steps, n_used, W] -> derived [steps, n_derived, W] (device
+        evaluation through cmbl_derived_batch)."""
+        import torch
+        steps, nu, W = P_used.shape
+        full = np.broadcast_to(self.P_fixed, (steps, W, self.P_fixed.size)).copy()
+        for k, i in enumerate(self.params_used):
+            full[:, :, i - 1] = P_used[:, k, :]
+        full = full.reshape(steps * W, -1)
+        out = np.zeros((steps * W, self.n))
+        for l in self.likes:
+            nuis = torch.tensor(full[:, [i - 1 for i in l.nuisance_indices]], device="cuda")
+            d = l.derived_batch(nuis).cpu().numpy()
+            for k, ix in enumerate(l.derived_indices):
+                out[:, ix - 1] = d[:, k]
+        return out.reshape(steps, W, self.n).transpose(0, 2, 1)

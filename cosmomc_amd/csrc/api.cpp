@@ -2,6 +2,7 @@
 // catches internal errors and turns them into codes + messages.
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 
 #include "sampler.h"
@@ -99,9 +100,9 @@ int cmbl_open(const char *tag, const char *dataset_path, const char *override_in
         // tag -> likelihood class as CMBLikelihood_Add (source/CMB.f90:80-97)
         if (t == "PLIK_LITE") h->like = cmamd::make_plik_lite(ini);
         else if (t == "SPTPOL_TEEE" || t == "SPTPOL_BB") h->like = cmamd::make_sptpol(ini, t);   // CMB.f90:86-91
-        else if (t == "WMAP" || t == "SMICA")
-            cmamd::fail(CMBL_ERR_UNSUPPORTED, "cmbl_open: dataset tag '%s' not supported yet", tag);
-        else h->like = cmamd::make_cmblikes(ini, t);      // TCMBLikes, or TBK_planck for BKPLANCK
+        else if (t == "WMAP")   // CMB.f90:75-84: needs the external WMAP likelihood library
+            cmamd::fail(CMBL_ERR_UNSUPPORTED, "cmbl_open: dataset tag '%s' not supported", tag);
+        else h->like = cmamd::make_cmblikes(ini, t);      // TCMBLikes, TBK_planck (BKPLANCK), TSmica_planck (SMICA)
         *out = h.release();
     });
     if (rc) put_err(errbuf, errlen, err.c_str());
@@ -122,6 +123,22 @@ int cmbl_info(const cmbl_t *h, int *n_nuis, int *cl_lmax, int *speed, const char
     if (name) *name = L.name.c_str();
     if (nuisance_names) *nuisance_names = L.nuisance_names.c_str();
     return CMBL_OK;
+}
+
+int cmbl_derived_info(const cmbl_t *h, int *n_derived, const char **derived_names) {
+    if (!h || !h->like) return CMBL_ERR_ARG;
+    if (n_derived) *n_derived = h->like->n_derived;
+    if (derived_names) *derived_names = h->like->derived_names.c_str();
+    return CMBL_OK;
+}
+
+int cmbl_derived_batch(cmbl_t *h, int W, const double *nuis, long long ld_nuis, double *derived, long long ld_derived,
+                       void *stream) {
+    if (!h || !h->like) return CMBL_ERR_ARG;
+    return guarded(&h->like->last_error, [&] {
+        if (W < 0) cmamd::fail(CMBL_ERR_ARG, "cmbl_derived_batch: bad arguments");
+        h->like->derived_batch(W, nuis, ld_nuis, derived, ld_derived, (hipStream_t)stream);
+    });
 }
 
 size_t cmbl_workspace_size(const cmbl_t *h, int W) { return h && h->like ? h->like->workspace_size(W) : 0; }
@@ -274,7 +291,10 @@ int cmbs_create(const cmbs_config_t *cfg, cmbs_t **out, char *errbuf, size_t err
     if (const char *e = std::getenv("CMAMD_PIPE")) {   // fast-step schedule for A/B runs (cmamd_debug_pipeline)
         const int m = std::atoi(e);
         if (m == 0 || m == 3) s->pipe_mode = m;
+        else   // modes 1, 2 and 4 were deleted in round 5: say so rather than run the default unannounced
+            std::fprintf(stderr, "cosmomc_amd: CMAMD_PIPE=%s ignored (accepted: 0 unpipelined, 3 unified)\n", e);
     }
+    if (const char *e = std::getenv("CMAMD_FOLD_G")) s->fold_g = std::atoi(e) != 0;   // A/B runs
     int rc = guarded(&err, [&] { cmamd::sampler_create(s.get(), cfg); });
     if (rc) {
         put_err(errbuf, errlen, err.c_str());
@@ -392,6 +412,12 @@ int cmbs_collector_limits(cmbs_t *s, const int *params, int n_check, double limf
 int cmbs_set_groups(cmbs_t *s, int n_groups) {
     if (!s) return CMBL_ERR_ARG;
     return guarded(&s->last_error, [&] { cmamd::sampler_set_groups(s, n_groups); });
+}
+
+int cmbs_set_binned_cache(cmbs_t *s, int on) {
+    if (!s) return CMBL_ERR_ARG;
+    s->binned_cache = on != 0;
+    return CMBL_OK;
 }
 
 int cmbs_enable_history(cmbs_t *s, int capacity) {

@@ -52,7 +52,7 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 struct CLPair {      // one required map pair (i >= j)
     int field;       // theory field index 0..9 (TT TE EE BT BE BB PT PE PB PP)
     int cmb;         // both theory indices <= B: aberration and calibration apply
-    int fg;          // foregrounds: 0 none, 1 EE, 2 BB
+    int fg;          // foregrounds: 0 none, 1 BK EE, 2 BK BB, 3 SMICA TT
     int mi, mj;      // required-map indices (0-based)
 };
 
@@ -94,12 +94,15 @@ struct CLDev {
     // BK foregrounds
     int bk, nreq;
     int LP;                         // profile row length: prof[w][3][LP], indexed by l (zero outside lmin..lmax)
+                                    // (SMICA: prof[w][0] = A1 exp(..), prof[w][1] = A2 (l/pivot)^n2)
+    double smica_pivot;             // TSmica_planck%pivot (CMBlikes.f90:1270)
     const BKMap *bkmaps;
     const double *bp_nu, *bp_R, *bp_dnu;
     const double *bp_lnu;           // log(nu) of every bandpass sample
     int nsamp;                      // bandpass samples, all maps
-    double *td_den;                 // [nsamp] exp(G nu / Td0) - 1 for the launch's first walker's Td0 (cmbl_bk_tdtab)
-    double *td0;                    // [1] that Td0
+    double *td_den;                 // [nsamp] exp(G nu / Td0) - 1 for the launch's first walker's Td0 (cmbl_bk_tdtab);
+    double *td0;                    // [1] that Td0.  Both live in the call's workspace, so launches on other
+                                    // streams with their own workspaces never share the table
     const double *log_l80;          // log(l / 80), l = 0 .. LP-1
     double fpivot_dust, fpivot_sync, decorr_dust[2], decorr_sync[2];
     int lform_dust, lform_sync;     // 0 flat, 1 lin, 2 quad
@@ -214,6 +217,58 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
     }
 }
 
+// SMICA's TT foreground (TSmica_planck_AddForegrounds, CMBlikes.f90:1295-1322)
+// per walker and l as two profile rows, added to every TT map pair in window
+// staging in the reference's order: (D_l + A1 exp(n1 lnr + n1run/2 lnr^2)) +
+// A2 (l/pivot)^n2, lnr = ln(l/pivot).  prof[w][3][LP]; row 2 unused.
+__global__ __launch_bounds__(256) void cmbl_smica_prologue(CLDev c, const double *__restrict__ nuis, long long ld_nuis,
+                                                          double *__restrict__ prof, int W)
+{
+    const int w = blockIdx.y;
+    if (w >= live_walkers(c.wcount, W)) return;
+    const int l = blockIdx.x * 256 + threadIdx.x;
+    const int LP = c.LP;
+    if (l >= LP) return;
+    const double *P = nuis + (long long)w * ld_nuis;
+    double *pw = prof + (long long)w * 3 * LP;
+    if (l < c.lmin || l > c.lmax) {
+        pw[l] = pw[LP + l] = 0.0;
+        return;
+    }
+    const double A1 = P[0], n1 = P[1], n1run = P[2], A2 = P[3], n2 = P[4];
+    const double x = (double)l / c.smica_pivot;
+    const double lnrat = log(x);
+    pw[l] = A1 * exp(n1 * lnrat + n1run / 2 * (lnrat * lnrat));
+    pw[LP + l] = A2 * pow(x, n2);
+}
+
+// TSmica_planck_derivedParameters (CMBlikes.f90:1324-1337): derived(1) =
+// Cls(1,1)%CL(2000) of map cross-spectra initialised to zero plus the
+// foregrounds, i.e. the TT foreground at l = 2000 when the first required map
+// pair is TT (0 otherwise); any further derived columns 0 (the base
+// TDataLikelihood_derivedParameters, GeneralTypes.f90:504-512).  NaN when
+// l = 2000 is outside pcl_lmin..pcl_lmax (the reference reads out of bounds).
+__global__ __launch_bounds__(64) void cmbl_smica_derived(CLDev c, int tt11, const double *__restrict__ nuis,
+                                                        long long ld_nuis, double *__restrict__ out, long long ld_out,
+                                                        int nd, int W)
+{
+    const int w = blockIdx.x * 64 + threadIdx.x;
+    if (w >= W) return;
+    const double *P = nuis + (long long)w * ld_nuis;
+    double *o = out + (long long)w * ld_out;
+    const int l = 2000;
+    double v = 0.0;
+    if (l < c.lmin || l > c.lmax) v = __builtin_nan("");
+    else if (tt11) {
+        const double A1 = P[0], n1 = P[1], n1run = P[2], A2 = P[3], n2 = P[4];
+        const double x = (double)l / c.smica_pivot;
+        const double lnrat = log(x);
+        v = (v + A1 * exp(n1 * lnrat + n1run / 2 * (lnrat * lnrat))) + A2 * pow(x, n2);
+    }
+    o[0] = v;
+    for (int k = 1; k < nd; k++) o[k] = 0.0;
+}
+
 // Window contractions on the f64 MFMA.  One workgroup = 64 walkers x one work
 // item (map pair, up to WK_NCH chunks of WK_CHUNK l, <= WK_COLS window columns):
 //   partial[col][w] = sum_l Wt[l][col] MapCl_w(l)
@@ -258,7 +313,7 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
         if constexpr (FG) {
             dust[u] = sync[u] = dsync[u] = nui[u] = nuj[u] = 0.0;
             ddf[u] = dsf[u] = Ddust[u] = Dsync[u] = 1.0;
-            if (fg) {                                         // :296-328
+            if (fg && pr.fg != 3) {                           // :296-328
                 const double *cw = coef + (long long)w * 3 * c.nreq;
                 const int a = pr.mi, b = pr.mj;
                 double d = cw[a] * cw[b], sy = cw[c.nreq + a] * cw[c.nreq + b];
@@ -342,7 +397,11 @@ __global__ __launch_bounds__(256) void cmbl_window_kernel(CLDev c, const double 
                         v = v + c.aberration * (el * el * (el + 1) * deriv);
                     }
                     if constexpr (FG) {
-                        if (fg) {                             // :329-334
+                        if (fg && pr.fg == 3) {               // SMICA TT (CMBlikes.f90:1314-1317)
+                            const double *pw = prof + (long long)w * 3 * c.LP + l;
+                            v = v + pw[0];
+                            v = v + pw[c.LP];
+                        } else if (fg) {                      // :329-334
                             const double *pw = prof + (long long)w * 3 * c.LP + l;
                             const double Dd = (dd_l && Ddust[u] != 1.0)
                                                   ? bk_decorr(Ddust[u], nui[u], nuj[u], c.decorr_dust, l, c.lform_dust)
@@ -1485,7 +1544,7 @@ struct Windows {                   // TBinWindows (:27-34) for bins bin_min..bin
 
 struct CMBLikes final : Like {
     // ReadIni state
-    bool has_map_names = false, bk = false;
+    bool has_map_names = false, bk = false, smica = false;
     std::vector<std::string> map_names, used_map_order;
     std::vector<int> map_fields, use_map, require_map, map_used_index, map_required_index, required_order;
     int approx = 0, nmaps = 0, nreq = 0, ncl = 0, ncl_used = 0, nsamp = 0;   // approx: 1 HL, 2 gaussian, 3 exact
@@ -1508,7 +1567,7 @@ struct CMBLikes final : Like {
     bool items_even = true, small_gauss = false;
     bool use_group = false;      // BK foregrounds: grouped-pair window kernel
     int n_gitem = 0;
-    DevBuf d_gitems, d_gw, d_bplnu, d_logl80, d_tdden, d_td0;
+    DevBuf d_gitems, d_gw, d_bplnu, d_logl80;
     int small_ntask = 0;
     SmallDev sdev{};
     DevBuf d_invcov, d_stasks, d_smt, d_sct;
@@ -1679,6 +1738,7 @@ struct CMBLikes final : Like {
     CMBLikes(const Ini &ini, const std::string &tag_) {
         tag = tag_;
         bk = (tag == "BKPLANCK");
+        smica = (tag == "SMICA");       // TSmica_planck (CMB.f90:94-95)
         name = ini.str("name");
         if (name.empty()) {
             std::string fn = ini.filename();
@@ -1751,6 +1811,7 @@ struct CMBLikes final : Like {
         if (approx == 3 && nmaps > EXACT_MAXMAPS)
             fail(CMBL_ERR_UNSUPPORTED, "CMBlikes exact: at most %d maps", EXACT_MAXMAPS);
         if (approx == 3 && bk) fail(CMBL_ERR_UNSUPPORTED, "BKPLANCK with like_approx = exact is not supported");
+        if (approx == 3 && smica) fail(CMBL_ERR_UNSUPPORTED, "SMICA with like_approx = exact is not supported");
         if (nreq > CL_MAXREQ) fail(CMBL_ERR_UNSUPPORTED, "CMBlikes: at most %d required maps", CL_MAXREQ);
         map_required_index.assign(nm, 0);
         map_used_index.assign(nm, 0);
@@ -1848,9 +1909,30 @@ struct CMBLikes final : Like {
         std::string cp = ini.relative_filename("calibration_param", false);
         if (bk && !cp.empty()) fail(CMBL_ERR_UNSUPPORTED, "BKPLANCK with calibration_param is not supported");
         if (!cp.empty()) {
-            nuisance_names = load_paramnames(cp, &n_nuis);
+            nuisance_names = load_paramnames(cp, &n_nuis, &derived_names, &n_derived);
             cal_index = n_nuis - 1;
             log_cal_prior = ini_double(ini, "log_calibration_prior", -1.0);
+        }
+        // ---- Tsmica_planck_ReadIni (CMBlikes.f90:1281-1293): after the base ReadIni
+        // (which may have set a calibration index from calibration_param), the
+        // nuisance names are replaced by nuisance_params (loadParamNames ->
+        // nuisance_params%init), and calibration_paramname, when given, sets the
+        // calibration index to that name's position in them (ParamNames%Index:
+        // -1, i.e. no calibration, for an unknown name)
+        if (smica) {
+            nuisance_names = load_paramnames(ini.relative_filename("nuisance_params", true), &n_nuis, &derived_names,
+                                             &n_derived);
+            if (n_nuis < 5) fail(CMBL_ERR_FORMAT, "SMICA: nuisance_params needs the foreground parameters A1 n1 n1run A2 n2");
+            if (ini.has("calibration_paramname")) {
+                const std::string cn = ini.str("calibration_paramname");
+                const auto nm = split_ws(nuisance_names), dn = split_ws(derived_names);
+                int ix = -1;
+                for (size_t k = 0; k < nm.size() && ix < 0; k++)
+                    if (nm[k] == cn) ix = (int)k;
+                for (size_t k = 0; k < dn.size() && ix < 0; k++)
+                    if (dn[k] == cn) fail(CMBL_ERR_FORMAT, "SMICA: calibration_paramname %s is a derived parameter", cn.c_str());
+                cal_index = ix;   // -1: none
+            }
         }
         // ---- TBK_planck_ReadIni (CMB_BK_Planck.f90:36-70)
         std::vector<BKMap> bkm;
@@ -2218,7 +2300,8 @@ struct CMBLikes final : Like {
                 CLPair p{};
                 p.field = f1 * (f1 - 1) / 2 + (f2 - 1);
                 p.cmb = (f1 <= 3 && f2 <= 3);
-                p.fg = bk ? ((f1 == 2 && f2 == 2) ? 1 : (f1 == 3 && f2 == 3) ? 2 : 0) : 0;
+                p.fg = bk ? ((f1 == 2 && f2 == 2) ? 1 : (f1 == 3 && f2 == 3) ? 2 : 0)
+                          : (smica && f1 == 1 && f2 == 1) ? 3 : 0;   // SMICA: CL%theory_i == 1 .and. CL%theory_j == 1
                 p.mi = i - 1;
                 p.mj = j - 1;
                 pairs.push_back(p);
@@ -2314,8 +2397,6 @@ struct CMBLikes final : Like {
             for (int l = 1; l < (int)ll80.size(); l++) ll80[l] = std::log(l / 80.0);
             up(d_bplnu, blnu.data(), blnu.size() * 8);
             up(d_logl80, ll80.data(), ll80.size() * 8);
-            d_tdden.alloc(std::max<size_t>(1, bnu.size()) * 8);
-            d_td0.alloc(8);
             nsamp = (int)bnu.size();
         }
         qf.init(invcov, nX);
@@ -2339,12 +2420,13 @@ struct CMBLikes final : Like {
         dev.bk = bk ? 1 : 0;
         dev.nreq = nreq;
         dev.LP = (lmax + 2) & ~1;
+        dev.smica_pivot = 2000.0;
         dev.bkmaps = bk ? d_bkmaps.as<BKMap>() : nullptr;
         dev.bp_nu = bk ? d_bpnu.as<double>() : nullptr;
         dev.bp_lnu = bk ? d_bplnu.as<double>() : nullptr;
         dev.nsamp = bk ? nsamp : 0;
-        dev.td_den = bk ? d_tdden.as<double>() : nullptr;
-        dev.td0 = bk ? d_td0.as<double>() : nullptr;
+        dev.td_den = nullptr;   // per call, in the workspace (layout().td)
+        dev.td0 = nullptr;
         dev.log_l80 = bk ? d_logl80.as<double>() : nullptr;
         dev.bp_R = bk ? d_bpR.as<double>() : nullptr;
         dev.bp_dnu = bk ? d_bpdnu.as<double>() : nullptr;
@@ -2365,7 +2447,7 @@ struct CMBLikes final : Like {
 
     // workspace: quadratic form | partial dots [rows][W] | C matrices [W][nE] (HL) |
     //            BK coef [W][3 nreq] + profiles [3][L][W] | addend [W]
-    struct WsLayout { size_t part, cmat, coef, prof, add, total; };
+    struct WsLayout { size_t part, cmat, coef, prof, add, td, total; };
     WsLayout layout(int W) const {
         auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
         WsLayout o{};
@@ -2373,8 +2455,9 @@ struct CMBLikes final : Like {
         o.cmat = o.part + al((size_t)n_part_rows * W * 8);
         o.coef = o.cmat + al(approx == 1 ? (size_t)W * nb * ncl * 8 : 0);
         o.prof = o.coef + al(bk ? (size_t)W * 3 * nreq * 8 : 0);
-        o.add = o.prof + al(bk ? (size_t)3 * dev.LP * W * 8 : 0);   // prof [W][3][LP]
-        o.total = o.add + al((size_t)W * 8);
+        o.add = o.prof + al((bk || smica) ? (size_t)3 * dev.LP * W * 8 : 0);   // prof [W][3][LP]
+        o.td = o.add + al((size_t)W * 8);
+        o.total = o.td + al(bk ? (size_t)(nsamp + 1) * 8 : 0);   // T_dust table: td0, then nsamp denominators
         return o;
     }
     size_t workspace_size(int W) const override { return approx == 3 ? 256 : layout(W).total; }
@@ -2393,7 +2476,7 @@ struct CMBLikes final : Like {
     // window stage: the direct path's work items (no BK foregrounds, no
     // aberration), one column per (item, window column) writing its partial row
     bool window_stage(WinStage &st) const override {
-        if (approx == 3 || bk || aberration != 0.0 || use_group || !binned) return false;
+        if (approx == 3 || bk || smica || aberration != 0.0 || use_group || !binned) return false;
         st.kind = 0;
         st.cal_index = cal_index;
         st.cols.clear();
@@ -2434,7 +2517,7 @@ struct CMBLikes final : Like {
         return true;
     }
     bool window_resegment(const std::map<int, std::vector<int>> &starts) override {
-        if (approx == 3 || bk || aberration != 0.0 || use_group || !binned) return false;
+        if (approx == 3 || bk || smica || aberration != 0.0 || use_group || !binned) return false;
         const int L = lmax - lmin + 1;
         seg_starts.clear();
         for (auto &kv : starts) {
@@ -2502,11 +2585,22 @@ struct CMBLikes final : Like {
         const double *nu = nuis ? nuis : dl;   // never read when n_nuis == 0
         const int tiles = (W + 63) / 64;
         if (bk) {
+            // the T_dust table is per call (this workspace), so concurrent calls on
+            // other streams -- the sampler's walker groups -- cannot overwrite it
+            dev.td0 = reinterpret_cast<double *>(base + o.td);
+            dev.td_den = dev.td0 + 1;
             hipLaunchKernelGGL(cmbl_bk_tdtab, dim3((dev.nsamp + 255) / 256), dim3(256), 0, stream, dev, nu);
             HIP_CHECK(hipGetLastError());
             timed_launch("cmbl_bk_prologue", stream, [&](hipEvent_t e0, hipEvent_t e1) {
                 hipExtLaunchKernelGGL(cmbl_bk_prologue, dim3(W), dim3(256), 0, stream, e0, e1, 0, dev, nu, ld_nuis,
                                       coef, prof, W);
+            });
+            HIP_CHECK(hipGetLastError());
+        }
+        if (smica) {
+            timed_launch("cmbl_smica_prologue", stream, [&](hipEvent_t e0, hipEvent_t e1) {
+                hipExtLaunchKernelGGL(cmbl_smica_prologue, dim3((dev.LP + 255) / 256, W), dim3(256), 0, stream, e0, e1,
+                                      0, dev, nu, ld_nuis, prof, W);
             });
             HIP_CHECK(hipGetLastError());
         }
@@ -2522,7 +2616,7 @@ struct CMBLikes final : Like {
                                       ld_nuis, (const double *)coef, (const double *)prof, dev.LP, partial, W, tiles,
                                       (int)gvec);
             });
-        } else if (!bk && aberration == 0.0) {
+        } else if (!bk && !smica && aberration == 0.0) {
             const int nblk = 8 * tiles * ((dev.nitem + 7) / 8);
             timed_launch("cmbl_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
                 hipExtLaunchKernelGGL(cmbl_window_direct, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, dev, dl,
@@ -2535,7 +2629,7 @@ struct CMBLikes final : Like {
                           ld_field, ld_walker, nu, ld_nuis, (const double *)coef, (const double *)prof, partial, W,    \
                           (int)vec_ok)
             const bool ab = aberration != 0.0;
-            if (bk) {
+            if (bk || smica) {
                 if (ab) CMBL_WINDOW(true, true);
                 else CMBL_WINDOW(false, true);
             } else {
@@ -2546,6 +2640,17 @@ struct CMBLikes final : Like {
         });
         HIP_CHECK(hipGetLastError());
         return post_window(W, nu, ld_nuis, out, ws, stream, wcount, defer);
+    }
+
+    void derived_batch(int W, const double *nuis, long long ld_nuis, double *out, long long ld_out,
+                       hipStream_t stream) override {
+        if (W <= 0 || n_derived <= 0) return;
+        if (!out || ld_out < n_derived) fail(CMBL_ERR_ARG, "derived output needs %d columns", n_derived);
+        if (!smica) return Like::derived_batch(W, nuis, ld_nuis, out, ld_out, stream);
+        if (!nuis) fail(CMBL_ERR_ARG, "%s needs its %d nuisance parameters", name.c_str(), n_nuis);
+        hipLaunchKernelGGL(cmbl_smica_derived, dim3((W + 63) / 64), dim3(64), 0, stream, dev,
+                           pairs.empty() ? 0 : (int)(pairs[0].fg == 3), nuis, ld_nuis, out, ld_out, n_derived, W);
+        HIP_CHECK(hipGetLastError());
     }
 
     SmallGaussLaunch small_args(int W, const double *nu, long long ld_nuis, double *out, void *ws) const {

@@ -155,7 +155,8 @@ bool file_exists(const std::string &path);
 std::vector<std::vector<double>> load_txt(const std::string &path);
 std::vector<std::string> split_ws(const std::string &s);
 // .paramnames file -> space-separated names (derived '*' stripped), count
-std::string load_paramnames(const std::string &path, int *count);
+std::string load_paramnames(const std::string &path, int *count, std::string *derived = nullptr,
+                            int *n_derived = nullptr);
 
 struct PlikBinArgs;   // plikbin.h
 
@@ -170,7 +171,7 @@ struct QFDeferred {
 };
 
 // A deferred quadratic form whose operand rows a later launch forms itself from
-// a window pass's raw sums (the sampler's split pipelined steps, steptail.hip):
+// a window pass's raw sums (the sampler's unified step launch, mh_step_kernel):
 // Delta[w][k] = X[k] - S[w][k] / cal_w^2, every row calibrated.
 struct QFItem;
 struct QFSource {
@@ -207,7 +208,7 @@ struct SmallGaussLaunch {
     const double *M;         // [nX][nX] inverse covariance
     double *out;             // [W] -lnL
     int W;
-    // the sampler's split pipelined steps (steptail.hip): partial holds the window
+    // the sampler's unified step launch (mh_step_kernel): partial holds the window
     // pass's raw sums, and a row r with row_cal[r] != 0 is divided by cal^2 (cal =
     // nuis[w * ld_nuis + stage_cal]) as it is loaded -- the operation the pass's
     // emit would have applied before storing it
@@ -239,6 +240,18 @@ struct Like {
     virtual ~Like() = default;
     std::string name, tag, nuisance_names;
     int n_nuis = 0;
+    // derived parameters (the '*' names of the nuisance paramnames,
+    // DataLike%derivedParameters, GeneralTypes.f90:504-512, 658-664)
+    std::string derived_names;
+    int n_derived = 0;
+    // (the base returns zeros, as TDataLikelihood_derivedParameters does)
+    virtual void derived_batch(int W, const double *nuis, long long ld_nuis, double *out, long long ld_out,
+                               hipStream_t stream) {
+        (void)nuis, (void)ld_nuis;
+        if (W <= 0 || n_derived <= 0) return;
+        if (!out || ld_out < n_derived) fail(CMBL_ERR_ARG, "derived output needs %d columns", n_derived);
+        HIP_CHECK(hipMemset2DAsync(out, (size_t)ld_out * 8, 0, (size_t)n_derived * 8, W, stream));
+    }
     int speed = -1;
     int cl_lmax[16] = {0};
     std::string last_error;

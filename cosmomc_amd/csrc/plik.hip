@@ -99,20 +99,31 @@ static std::vector<double> read_fortran_binary_matrix(const std::string &path, i
     return rm;
 }
 
-std::string load_paramnames(const std::string &path, int *count) {
+// ParamNames_Init (ObjectParamNames.f90:119-151): one name per non-empty line;
+// a trailing '*' marks a derived parameter.  Returns the non-derived (MCMC)
+// names -- the likelihood's DataParams, num_MCMC of them in *count -- and the
+// derived ones (their DataLike%derivedParameters outputs) in *derived.
+std::string load_paramnames(const std::string &path, int *count, std::string *derived, int *n_derived) {
     std::ifstream f(path);
     if (!f) fail(CMBL_ERR_IO, "cannot read paramnames %s", path.c_str());
-    std::string line, names;
-    int n = 0;
+    std::string line, names, dnames;
+    int n = 0, nd = 0;
     while (std::getline(f, line)) {
         auto t = split_ws(line);
         if (t.empty() || t[0][0] == '#') continue;
         std::string nm = t[0];
-        if (!nm.empty() && nm.back() == '*') nm.pop_back();   // derived marker
+        if (!nm.empty() && nm.back() == '*') {   // derived marker
+            nm.pop_back();
+            dnames += (nd ? " " : "") + nm;
+            nd++;
+            continue;
+        }
         names += (n ? " " : "") + nm;
         n++;
     }
     *count = n;
+    if (derived) *derived = dnames;
+    if (n_derived) *n_derived = nd;
     return names;
 }
 

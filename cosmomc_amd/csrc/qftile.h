@@ -1,5 +1,5 @@
 // Device pieces of the f64-MFMA quadratic form shared by its kernels
-// (quadform.hip) and by the sampler's step-tail launch (steptail.hip): the
+// (quadform.hip) and by the sampler's unified step launch (mh_step_kernel): the
 // swizzled LDS operand tiles, their LDS-DMA fill and the XCD-aware
 // workgroup -> (item, walker tile) placement.
 #pragma once

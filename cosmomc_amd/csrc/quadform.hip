@@ -214,17 +214,20 @@ template <int WT>
 __global__ __launch_bounds__(256, 2) void quadform_corun(
     const double *__restrict__ Ct, int Np, const double *__restrict__ delta, int W,
     const QFItem *__restrict__ items, int n_items, int xcd_map, double *__restrict__ partial,
-    SmallGaussLaunch co, int ns)
+    SmallGaussLaunch co, int ns, int nq)
 {
     static_assert(small_gauss_lds_doubles<WT>() <= QF_LDS_DOUBLES, "co-run LDS");
     __shared__ __attribute__((aligned(16))) double smem[QF_LDS_DOUBLES];
-    const int nq = gridDim.x - small_gauss_blocks(ns);
+    // the chi^2 workgroups start at a multiple of 8, so small_gauss_group's
+    // lb % 8 is the XCD (blockIdx.x % 8); workgroups nq .. nqp - 1 are padding
+    const int nqp = (nq + 7) & ~7;
     const int b = blockIdx.x;
-    if (b >= nq) {
-        const int q = small_gauss_group(b - nq, ns);
+    if (b >= nqp) {
+        const int q = small_gauss_group(b - nqp, ns);
         if (q < ns) small_gauss_body<WT>(co, smem, q);
         return;
     }
+    if (b >= nq) return;
     int item_ix, tile;
     qf_place(b, n_items, xcd_map, item_ix, tile);
     quadform_body<false>(smem, item_ix, tile, Ct, Np, delta, W, items, n_items, partial, nullptr, nullptr, nullptr,
@@ -338,10 +341,11 @@ QFDeferred QuadForm::launch_deferred(int W, void *ws, const double *addend, hipS
     if (co) {
         const int ns = (co->W + SMALL_WT - 1) / SMALL_WT;
         timed_launch(co_prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(quadform_corun<SMALL_WT>, dim3(n_items * tiles + small_gauss_blocks(ns)), dim3(256), 0,
-                                  stream, e0, e1, 0,
+            const int nq = n_items * tiles;
+            hipExtLaunchKernelGGL(quadform_corun<SMALL_WT>, dim3(((nq + 7) & ~7) + small_gauss_blocks(ns)), dim3(256),
+                                  0, stream, e0, e1, 0,
                                   d_ct.as<double>(), Np, (const double *)x, W, d_items[kb].as<QFItem>(), n_items,
-                                  (int)(tiles % 8 == 0), partial, *co, ns);
+                                  (int)(tiles % 8 == 0), partial, *co, ns, nq);
         });
     } else
     timed_launch(prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
@@ -397,7 +401,8 @@ __global__ __launch_bounds__(256, 2) void quadform_pair_ticket(QFSource qa, doub
                             nullptr, second ? out_b : out_a, nullptr);
         return;
     }
-    b -= nq + nq_b;
+    b -= (nq + nq_b + 7) & ~7;   // the chi^2 workgroups start at a multiple of 8 (small_gauss_group's XCD)
+    if (b < 0) return;
     const int gp = small_gauss_blocks(ng);
     const int q = small_gauss_group(b < gp ? b : b - gp, ng);
     if (q < ng) small_gauss_body<WT>(b < gp ? ga : gb, smem, q);
@@ -411,7 +416,7 @@ void launch_qf_pair(const QFSource &qa, double *out_a, const QFSource *qb, doubl
     const SmallGaussLaunch none{};
     // one set: [quadratic form a][chi^2 a]
     const int nq_b = qb ? nq : 0, ng_b = gb ? ng : 0;
-    const dim3 grid(nq + nq_b + small_gauss_blocks(ng) + small_gauss_blocks(ng_b));
+    const dim3 grid(((nq + nq_b + 7) & ~7) + small_gauss_blocks(ng) + small_gauss_blocks(ng_b));
     timed_launch(prof_name, stream, [&](hipEvent_t e0, hipEvent_t e1) {
         hipExtLaunchKernelGGL(quadform_pair_ticket<SMALL_WT>, grid, dim3(256), 0, stream, e0, e1, 0, qa, out_a,
                               qb ? *qb : qa, out_b, W, nq, ga ? *ga : none, gb ? *gb : none, ng, nq_b);

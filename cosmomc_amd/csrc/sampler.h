@@ -244,6 +244,9 @@ struct cmbs {
     cmamd::StepTailPlan uni_plan[3];         // rows: propose + pass, tails + pass + accept/propose, tails + accept
     size_t uni_lds = 0;
     int tail_nosignal = 0;                   // debug (cmamd_debug_tail_nosignal)
+    bool binned_cache = false;               // cmbs_set_binned_cache: bin once per fast-step call
+    int fold_g = 1;                          // unified launch: the small chi^2 in the Metropolis workgroups
+                                             // (CMAMD_FOLD_G=0: as rows of its own, for A/B runs)
     // a pipelined hand-off that gave up (unified launch, bin co-run): the device word, its
     // pinned copy taken at the end of each step call, checked at the next
     int *pipe_status_host = nullptr;         // pinned, mapped (pipe_status_init)

@@ -1138,9 +1138,8 @@ __device__ __forceinline__ void tail_arrive(const TailWait &tw, int tile)
 }
 
 template <bool ACCEPT, bool PROPOSE>
-__global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fast_only, double *hist_row,
-                                                                double *hist_terms, StepTail t,
-                                                                const int2 *__restrict__ rows, TailWait tw, int nmh)
+__device__ __forceinline__ void mh_step_body(DevCfg &c, int fast_only, double *hist_row, double *hist_terms,
+                                             StepTail &t, const int2 *__restrict__ rows, TailWait &tw, int nmh)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int2 rr = rows[blockIdx.x >> 3];
@@ -1188,8 +1187,36 @@ __global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fa
         // the chain is latency on one lane: its waves, dispatched last (the youngest,
         // so the last in issue arbitration), take the SIMD first (34.6 -> 34.0 us)
         __builtin_amdgcn_s_setprio(3);
+        if (ACCEPT && t.fold_g) {
+            // the small chi^2 of this workgroup's 16 walkers (step k's raw partial
+            // rows, whole 128-byte lines) while the quadratic form runs elsewhere:
+            // nX <= 16, so its sums are those of the 4-walker rows (same bits); the
+            // chain's loads of the term follow tail_wait's acquire
+            small_gauss_body<MB, true, false>(t.g, lds, lb);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
         mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, 0, lds, lb, ACCEPT ? &tw : nullptr);
     }
+}
+
+template <bool ACCEPT, bool PROPOSE>
+__global__ __launch_bounds__(MH_THREADS, 3) void mh_step_kernel(DevCfg c, int fast_only, double *hist_row,
+                                                                double *hist_terms, StepTail t,
+                                                                const int2 *__restrict__ rows, TailWait tw, int nmh)
+{
+    mh_step_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, t, rows, tw, nmh);
+}
+
+// The same launch without the pass, for the binned-theory cache
+// (cmbs_set_binned_cache): its own symbol, so profiles of a run with both
+// legs keep the headline launch's statistics apart
+template <bool ACCEPT, bool PROPOSE>
+__global__ __launch_bounds__(MH_THREADS, 3) void mh_tail_kernel(DevCfg c, int fast_only, double *hist_row,
+                                                                double *hist_terms, StepTail t,
+                                                                const int2 *__restrict__ rows, TailWait tw, int nmh)
+{
+    mh_step_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, t, rows, tw, nmh);
 }
 
 // ------------------------------------------------------- deferred rotations
@@ -2976,7 +3003,11 @@ static void pipe_status_init(cmbs *s) {
         HIP_CHECK(hipHostGetDevicePointer((void **)&s->pipe_status_dev, s->pipe_status_host, 0));
         HIP_CHECK(hipEventCreateWithFlags(&s->pipe_ev, hipEventDisableTiming));
     }
-    HIP_CHECK(hipDeviceSynchronize());   // no kernel of an earlier call still writes it
+    // no kernel of an earlier call still writes it: every call that launched a
+    // hand-off kernel recorded pipe_ev after it (pipe_status_post, also on the
+    // error paths), so waiting on this sampler's event suffices -- other
+    // samplers' and the caller's work on the device are not waited for
+    if (s->pipe_ev_pending) HIP_CHECK(hipEventSynchronize(s->pipe_ev));
     *reinterpret_cast<volatile int *>(s->pipe_status_host) = 0;
     s->pipe_ev_pending = false;
 }
@@ -2984,6 +3015,11 @@ static void pipe_status_init(cmbs *s) {
 static void pipe_status_post(cmbs *s, hipStream_t stream) {
     HIP_CHECK(hipEventRecord(s->pipe_ev, stream));
     s->pipe_ev_pending = true;
+}
+
+// on an error path: the event covers whatever this call launched before it
+static void pipe_status_post_nothrow(cmbs *s, hipStream_t stream) {
+    if (s->pipe_ev && hipEventRecord(s->pipe_ev, stream) == hipSuccess) s->pipe_ev_pending = true;
 }
 
 void sampler_check_pipe(cmbs *s, bool wait) {
@@ -3136,6 +3172,7 @@ static void launch_mh(cmbs *s, bool accept, bool propose, int fast_only, const H
             HIP_CHECK(hipGetLastError());
         } catch (...) {
             s->pipe_ready = 0;   // both halves re-uploaded as unset next time
+            pipe_status_post_nothrow(s, stream);
             throw;
         }
         s->pipe_epoch = e;
@@ -3180,14 +3217,15 @@ static void check_theory_fresh(const cmbs *s) {
                            "theory at the restored points with cmbs_refresh_theory before stepping");
 }
 
-// The split pipelined fast steps (steptail.h): whether this run of fast steps
+// The unified pipelined fast steps (mh_step_kernel, steptail.h): whether this run of fast steps
 // can take them -- the fused pass's vectorised form over one walker group, no
 // change mask, no rotations left to rot_kernel, and its two stages a deferred
 // quadratic form (plik_lite: every row calibrated) and a small chi^2 another
 // launch can carry (Planck lensing).  Sets up the raw-sum buffers once per W.
 static bool tail_setup(cmbs *s, int fast_only) {
-    // (the step tails carry the fused pair alone: a third likelihood falls back to mode 1,
-    // whose eval_likes runs every likelihood)
+    // (the unified launch carries the fused pair alone: with a third likelihood the
+    // run takes the unpipelined steps, whose eval_likes runs every likelihood; BASELINE
+    // configs[2] with a lowl term would be such a run -- clik is absent, so none exists here)
     if (s->pipe_mode == 0 || !fast_only || !s->tpass || s->n_groups != 1 || s->mask_on ||
         (s->dc.rot_defer && s->rot_fast_any) || s->likes.size() != 2)
         return false;
@@ -3242,9 +3280,11 @@ static bool tail_setup(cmbs *s, int fast_only) {
         G.corun_small(g, s->W, s->dc.like_nuis[gi], G.n_nuis, s->like_terms.as<double>() + (size_t)gi * s->dc.ld,
                       s->like_ws[gi].p);
         s->uni_lds = std::max({s->mh_lds, (size_t)QFS_LDS_DOUBLES * 8, (size_t)tp_vec_lds_bytes<2>(),
-                               (size_t)small_gauss_lds_doubles<UNI_WT>(g.d.nX) * 8});
+                               (size_t)small_gauss_lds_doubles<UNI_WT>(g.d.nX) * 8,
+                               (size_t)small_gauss_lds_doubles<MB>(g.d.nX) * 8});
         for (const void *k : {(const void *)mh_step_kernel<false, true>, (const void *)mh_step_kernel<true, true>,
-                              (const void *)mh_step_kernel<true, false>})
+                              (const void *)mh_step_kernel<true, false>, (const void *)mh_tail_kernel<true, true>,
+                              (const void *)mh_tail_kernel<true, false>})
             HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->uni_lds));
     }
     for (auto &pl : s->uni_plan) pl.key[0] = -1;
@@ -3277,6 +3317,10 @@ static StepTail make_tail(cmbs *s, int rd, int wr) {
         t.g.row_cal = s->tail_rowcal.as<unsigned char>();
         t.g.stage_cal = s->tp_stage[s->tail_g].cal_index;
         t.ng = (W + UNI_WT - 1) / UNI_WT;
+        // the chi^2 folded into the Metropolis workgroups: bit-identical while its
+        // 16-walker body's thread groups (256 / 16) cover the bandpowers
+        t.fold_g = (s->fold_g && t.g.d.nX <= MH_THREADS / MB) ? 1 : 0;
+        if (t.fold_g) t.ng = 0;
     }
     if (wr >= 0) {
         TPOut o[2];
@@ -3344,9 +3388,17 @@ static void launch_unified(cmbs *s, hipStream_t stream, bool propose, int rd, in
     const dim3 grid((unsigned)pl.nrows * 8), b(MH_THREADS);
     const int2 *rows = pl.d_rows.as<int2>();
     static const char *names[3] = {"mh_step_first", "mh_step_kernel", "mh_step_last"};
+    static const char *cnames[3] = {"mh_step_first", "mh_tail_kernel", "mh_tail_last"};
+    const bool cached = s->binned_cache && accept && wr < 0 && rd == 0;   // the binned-cache steps (no pass)
     try {
-        timed_launch(names[v], stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            if (v == 0)
+        timed_launch(cached ? cnames[v] : names[v], stream, [&](hipEvent_t e0, hipEvent_t e1) {
+            if (cached && v == 1)
+                hipExtLaunchKernelGGL(mh_tail_kernel<true, true>, grid, b, s->uni_lds, stream, e0, e1, 0, dc,
+                                      fast_only, row.p, row.t, t, rows, tw, nmh);
+            else if (cached && v == 2)
+                hipExtLaunchKernelGGL(mh_tail_kernel<true, false>, grid, b, s->uni_lds, stream, e0, e1, 0, dc,
+                                      fast_only, row.p, row.t, t, rows, tw, nmh);
+            else if (v == 0)
                 hipExtLaunchKernelGGL(mh_step_kernel<false, true>, grid, b, s->uni_lds, stream, e0, e1, 0, dc,
                                       fast_only, row.p, row.t, t, rows, tw, nmh);
             else if (v == 1)
@@ -3359,6 +3411,7 @@ static void launch_unified(cmbs *s, hipStream_t stream, bool propose, int rd, in
         HIP_CHECK(hipGetLastError());
     } catch (...) {
         s->tail_ready = 0;   // the counters and the epoch are set up afresh next time
+        pipe_status_post_nothrow(s, stream);
         throw;
     }
     if (accept) s->tail_epoch++;
@@ -3380,6 +3433,12 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
         // in every call (the first launch zeroes them; the epochs are counted within it)
         s->tail_epoch = 0;
         launch_unified(s, stream, true, -1, 0, HistRow{}, fast_only);
+        if (s->binned_cache) {
+            // the theory is fixed within the call: every step's tails read the raw
+            // sums the first launch's pass wrote (half 0), and no launch re-bins
+            for (int k = 0; k < n_steps; k++)
+                launch_unified(s, stream, k + 1 < n_steps, 0, -1, next_hist(s), fast_only);
+        } else
         for (int k = 0; k < n_steps; k++)
             launch_unified(s, stream, k + 1 < n_steps, k % 2, k + 1 < n_steps ? (k + 1) % 2 : -1, next_hist(s),
                            fast_only);

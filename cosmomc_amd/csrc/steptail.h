@@ -35,6 +35,7 @@ struct StepTail {
     int nq = 0;              // quadratic-form workgroups (n_items x tiles), 0: none
     SmallGaussLaunch g{};
     int ng = 0;              // chi^2 workgroups, 0: none
+    int fold_g = 0;          // the chi^2 runs inside the Metropolis workgroups (16 walkers each), not as rows
     TPDev tp{};              // the raw pass (tp.out[*].out: the raw-sum buffers it writes)
     const double *dl = nullptr;
     long long ld_field = 0, ld_walker = 0;

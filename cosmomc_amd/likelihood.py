@@ -38,6 +38,7 @@ class DataLikelihood:
         self.tag = ""
         self.speed = -1                 # TCMBLikelihood_ReadParams (Likelihood_Cosmology.f90:250-251)
         self.nuisance_names: list[str] = []
+        self.derived_names: list[str] = []      # the '*' names of the nuisance .paramnames
         self.nuisance_indices: list[int] = []   # 1-based into P, filled by LikelihoodList
         self.dependent_params: set[int] = set()
         self.cl_lmax = [[0] * 4 for _ in range(4)]
@@ -80,6 +81,9 @@ class NativeCMBLikelihood(DataLikelihood):
         self.speed = speed.value
         self.nuisance_names = names.value.decode().split()
         self.cl_lmax = [[lm[i * 4 + j] for j in range(4)] for i in range(4)]
+        nd, dnames = C.c_int(), C.c_char_p()
+        N.check(N.lib().cmbl_derived_info(h, C.byref(nd), C.byref(dnames)))
+        self.derived_names = dnames.value.decode().split()
 
     @property
     def handle(self):
@@ -112,6 +116,23 @@ class NativeCMBLikelihood(DataLikelihood):
         nptr, nld = (nuis.data_ptr(), nuis.stride(0)) if nuis.numel() > 0 else (None, 0)
         rc = N.lib().cmbl_loglike_batch(self._h, W, dl.data_ptr(), dl.stride(1), dl.stride(0), nptr, nld,
                                         out.data_ptr(), ws, N.current_stream_ptr(dl.device))
+        N.check(rc, self._h)
+        return out
+
+    def derived_batch(self, nuis, out=None):
+        """derivedParameters(Theory, DataParams) for every walker
+        (cmbl_derived_batch; GeneralTypes.f90:504-512, SMICA CMBlikes.f90:1324-1337):
+        nuis cuda float64 [W, n_nuis] -> [W, n_derived] on the current stream."""
+        import torch
+        W, nd = nuis.shape[0], len(self.derived_names)
+        if out is None:
+            out = torch.empty((W, nd), dtype=torch.float64, device=nuis.device)
+        if nd == 0 or W == 0:
+            return out
+        if nuis.dtype != torch.float64 or not nuis.is_cuda or nuis.stride(1) != 1 or out.stride(1) != 1:
+            raise TypeError("nuis must be a float64 cuda tensor with contiguous rows")
+        rc = N.lib().cmbl_derived_batch(self._h, W, nuis.data_ptr(), nuis.stride(0), out.data_ptr(), out.stride(0),
+                                        N.current_stream_ptr(nuis.device))
         N.check(rc, self._h)
         return out
 
@@ -251,6 +272,7 @@ class LikelihoodList:
         contiguous 1-based nuisance indices; returns the extended name list."""
         self.items.sort(key=lambda l: l.speed)
         names = list(param_names)
+        self.derived_list = []
         self.first_fast_param = 0
         for like in self.items:
             like.new_param_block_start = len(names) + 1          # :638
@@ -263,6 +285,13 @@ class LikelihoodList:
                     idx.append(len(names))
             like.new_params = len(names) - like.new_param_block_start + 1   # :641
             like.nuisance_indices = idx
+            # derived names follow every MCMC name (ParamNames_Add orders non-derived
+            # first); derived_indices (:658-664) are 1-based into the derived list
+            like.derived_indices = []
+            for nm in like.derived_names:
+                if nm not in self.derived_list:
+                    self.derived_list.append(nm)
+                like.derived_indices.append(self.derived_list.index(nm) + 1)
             like.dependent_params = set(idx)
             if self.first_fast_param == 0 and like.speed >= 0 and like.new_params > 0 and idx:   # :650-651
                 self.first_fast_param = like.new_param_block_start

@@ -99,6 +99,12 @@ class BatchedMCMC:
         p = np.ascontiguousarray(P0, dtype=np.float64).reshape(self.W, self.np)
         self._check(N.lib().cmbs_set_start(self._h, p.ctypes.data, stream))
 
+    def set_binned_cache(self, on: bool = True):
+        """Bin each walker's theory once per fast-step call and reuse the raw
+        sums at every step (cmbs_set_binned_cache; SURVEY 8(d)'s labelled
+        variant: same results, less work per step -- never the headline)."""
+        self._check(N.lib().cmbs_set_binned_cache(self._h, int(bool(on))))
+
     def set_groups(self, n_groups: int):
         """Step the walkers as ``n_groups`` slices on concurrent internal
         streams (cmbs_set_groups; execution tuning, results unchanged)."""

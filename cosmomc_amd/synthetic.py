@@ -563,6 +563,88 @@ def make_exact(lmin: int = 2, lmax: int = 400, fksy: float = 1.0, seed: int = 19
     return ExactData(lmin, lmax, clhat, noise)
 
 
+# SMICA (TSmica_planck, source/CMBlikes.f90:1262-1339): no SMICA dataset ships
+# with the reference, so a synthetic binned TT CMBLike2 dataset in its format
+# (CMBLikes_ReadIni :466-749) with the SMICA nuisance_params file: the five
+# foreground parameters, a calibration, and the derived D_l(2000).
+SMICA_PARAMS = (("A1_smica", "A_1"), ("n1_smica", "n_1"), ("n1run_smica", "n_{1,\\rm run}"),
+                ("A2_smica", "A_2"), ("n2_smica", "n_2"), ("cal_smica", "y_{\\rm cal}"))
+SMICA_FG = (30.0, 1.2, 0.0, 20.0, 0.5)     # fiducial A1 n1 n1run A2 n2 (D_l muK^2 at l = 2000)
+
+
+def smica_edges() -> list[tuple[int, int]]:
+    return [(30 + 45 * i, 74 + 45 * i) for i in range(54)]      # 54 bins, l 30..2459
+
+
+@dataclass
+class SmicaData:
+    lmin: int
+    lmax: int
+    windows: np.ndarray     # [lmax-lmin+1, nbin]
+    clhat: np.ndarray       # [nbin] binned TT (signal)
+    clfid: np.ndarray       # [nbin] fiducial (HL)
+    noise: np.ndarray       # [nbin] noise (HL)
+    cov: np.ndarray         # [nbin, nbin]
+
+    def write(self, directory: str, like_approx: str = "gaussian", extra: dict | None = None) -> str:
+        d = os.path.abspath(directory)
+        os.makedirs(os.path.join(d, "smica_windows"), exist_ok=True)
+        nb = self.clhat.size
+        ell = np.arange(self.lmin, self.lmax + 1)
+        for b in range(nb):
+            np.savetxt(os.path.join(d, "smica_windows", f"window{b + 1}.dat"),
+                       np.column_stack([ell, self.windows[:, b]]), fmt=["%d", "%.17e"])
+        for fn, v in (("smica_clhat.dat", self.clhat), ("smica_clfid.dat", self.clfid),
+                      ("smica_noise.dat", self.noise)):
+            with open(os.path.join(d, fn), "w") as f:
+                f.write("#    L    TT\n")
+                for b in range(nb):
+                    f.write(f"{b + 1:6d} {v[b]:24.17e}\n")
+        np.savetxt(os.path.join(d, "smica_cov.dat"), self.cov, fmt="%.17e")
+        with open(os.path.join(d, "smica.paramnames"), "w") as f:
+            for n, lab in SMICA_PARAMS:
+                f.write(f"{n}    {lab}\n")
+            f.write("Dl2000_smica*    D_{2000}\n")
+        with open(os.path.join(d, "smica_cal.paramnames"), "w") as f:
+            f.write("calPlanck    y_{\\rm cal}\n")
+        lines = ["dataset_format = CMBLike2", f"like_approx = {like_approx}", "fields_use = T", "binned = T",
+                 f"nbins = {nb}", f"cl_lmin = {self.lmin}", f"cl_lmax = {self.lmax}",
+                 "bin_window_files = smica_windows/window%u.dat", "bin_window_in_order = TT",
+                 "cl_hat_file = smica_clhat.dat", "covmat_cl = TT", "covmat_fiducial = smica_cov.dat",
+                 "nuisance_params = smica.paramnames"]
+        if like_approx == "HL":
+            lines += ["cl_fiducial_file = smica_clfid.dat", "cl_noise_file = smica_noise.dat"]
+        for k, v in (extra or {}).items():
+            lines.append(f"{k} = {v}")
+        path = os.path.join(d, "smica.dataset")
+        with open(path, "w") as f:
+            f.write("\n".join(lines) + "\n")
+        return path
+
+
+def smica_foreground(ells: np.ndarray, P) -> np.ndarray:
+    """The SMICA TT foreground (CMBlikes.f90:1314-1317) in numpy, for data making."""
+    A1, n1, n1run, A2, n2 = P[:5]
+    r = np.log(ells / 2000.0)
+    return A1 * np.exp(n1 * r + n1run / 2 * r ** 2) + A2 * (ells / 2000.0) ** n2
+
+
+def make_smica(seed: int = 2015) -> SmicaData:
+    lmin, lmax = 2, 2508
+    edges = smica_edges()
+    nb = len(edges)
+    win = _smooth_windows(lmin, lmax, edges)
+    base = base_theory(lmax)
+    ells = np.arange(lmin, lmax + 1, dtype=np.float64)
+    tt = base[FIELD_TT, lmin:lmax + 1] + smica_foreground(ells, SMICA_FG)
+    g = gaussians(seed, nb + nb * nb + nb)
+    binned = win.T @ tt
+    clhat = binned * (1.0 + 0.01 * g[:nb])
+    noise = 0.02 * binned * (1.0 + 0.1 * np.abs(g[nb + nb * nb:]))
+    cov = _spd_cov(binned, g[nb:nb + nb * nb], 0.015)
+    return SmicaData(lmin, lmax, win, clhat, binned, noise, cov)
+
+
 def _py_gaussians(seed: int, n: int) -> list[float]:
     """gaussians() restated on Python floats and libm (math): the splitmix64
     uniforms are exact, and every later operation is one correctly ordered

@@ -12,6 +12,10 @@
  *                         source/CMB.f90:208-303 for PLIK_LITE)
  *   cmbl_info            TDataLikelihood metadata (source/GeneralTypes.f90:105-126):
  *                        nuisance params, cl_lmax(4,4), speed, name
+ *   cmbl_derived_info / cmbl_derived_batch
+ *                        DataLike%derivedParameters(Theory, DataParams) and its
+ *                        '*' names (source/GeneralTypes.f90:504-512, 658-664, 774-776;
+ *                        TSmica_planck_derivedParameters source/CMBlikes.f90:1324-1337)
  *   cmbl_loglike_batch   like%LogLike(CMB, Theory, DataParams) for W walkers at once
  *                        (source/CMB.f90:305-329; called from calclike.f90:380)
  *   cmbl_clik_compute_batch  clik_lnlike packing (source/cliklike.f90:129-170) routed
@@ -53,8 +57,10 @@ typedef struct cmbl cmbl_t;
  * "PLIK_LITE" native plik_lite (CMB.f90:30-329), "BKPLANCK" CMBlikes with the
  * BICEP/Keck/Planck foregrounds (CMB_BK_Planck.f90), "SPTPOL_TEEE" / "SPTPOL_BB"
  * the SPTpol TE/EE 2017 and BB 2019 likelihoods (CMB_SPTpol_TEEE_2017.f90,
- * CMB_SPTpol_BB_2019.f90; sptpol_blind_r is CMBL_ERR_UNSUPPORTED),
- * "WMAP" / "SMICA" CMBL_ERR_UNSUPPORTED, any other tag a CMBlikes
+ * CMB_SPTpol_BB_2019.f90; sptpol_blind_r is CMBL_ERR_UNSUPPORTED), "SMICA"
+ * CMBlikes with the SMICA TT foreground, nuisance_params and
+ * calibration_paramname (TSmica_planck, CMBlikes.f90:1262-1339; binned HL or
+ * gaussian), "WMAP" CMBL_ERR_UNSUPPORTED (external library), any other tag a CMBlikes
  * dataset (CMBlikes.f90; like_approx HL or gaussian, binned, or exact,
  * unbinned: ExactChiSq CMBlikes.f90:967-979, up to 4 maps).
  * override_ini: "key = value" lines applied over the dataset file, as
@@ -70,6 +76,20 @@ const char *cmbl_last_error(const cmbl_t *h);
  * .paramnames (pointer owned by the handle). */
 int  cmbl_info(const cmbl_t *h, int *n_nuis, int *cl_lmax, int *speed,
                const char **name, const char **nuisance_names);
+
+/* Derived parameters a likelihood outputs per sample (the '*' names of its
+ * nuisance .paramnames): their count and space-separated names (pointer owned
+ * by the handle).  0 for most datasets. */
+int  cmbl_derived_info(const cmbl_t *h, int *n_derived, const char **derived_names);
+
+/* The derived parameters at W points (device pointers, asynchronous on
+ * `stream`): nuis [W] x n_nuis (stride ld_nuis) as for cmbl_loglike_batch,
+ * derived [W] x n_derived (stride ld_derived >= n_derived).  SMICA: the TT
+ * foreground D_l at l = 2000 (TSmica_planck_derivedParameters); other
+ * datasets: zeros (TDataLikelihood_derivedParameters).  The reference's
+ * functions read no theory, so none is passed. */
+int  cmbl_derived_batch(cmbl_t *h, int W, const double *nuis, long long ld_nuis,
+                        double *derived, long long ld_derived, void *stream);
 
 /* Bytes of device workspace cmbl_loglike_batch needs for W walkers. */
 size_t cmbl_workspace_size(const cmbl_t *h, int W);
@@ -249,6 +269,18 @@ int  cmbs_refresh_theory(cmbs_t *s, cmbs_theory_fn theory_fn, void *user, void *
  * forked from / joined to the caller's, so the Metropolis kernel of one slice
  * overlaps the likelihood kernels of the others.  Default 1. */
 int  cmbs_set_groups(cmbs_t *s, int n_groups);
+
+/* Binned-theory cache (SURVEY 8(d)'s labelled variant, no reference
+ * counterpart): inside one cmbs_step call of fast-only steps the theory is
+ * fixed, and the window/bin sums of the theory are calibration-independent,
+ * so with on != 0 the unified fast step bins each walker's theory once per
+ * call and every step reuses those raw sums (the quadratic form, the small
+ * chi^2 and the Metropolis chain still run every step, and the calibration is
+ * applied to the sums as before, so the results are the same bits).  Only the
+ * unified schedule (plik_lite + a small gaussian CMBlikes likelihood) uses it;
+ * other runs ignore it.  Default 0: every step re-bins the theory, as the
+ * reference's LogLike does. */
+int  cmbs_set_binned_cache(cmbs_t *s, int on);
 
 /* Optional history capture for convergence statistics: every step appends
  * each walker's current used-parameter vector and CurLike to a device ring of

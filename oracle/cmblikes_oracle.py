@@ -1,8 +1,9 @@
 """ORACLE TEST INFRASTRUCTURE -- never shipped, never on the product path.
 
 numpy restatement of the reference's CMBlikes bandpower likelihood
-(source/CMBlikes.f90) and the BICEP/Keck/Planck foreground model
-(source/CMB_BK_Planck.f90), one walker at a time, written from the reference
+(source/CMBlikes.f90), the BICEP/Keck/Planck foreground model
+(source/CMB_BK_Planck.f90) and the SMICA TT foreground (smica_planck,
+source/CMBlikes.f90:1262-1339), one walker at a time, written from the reference
 routines cited on each method.  Pinned against the compiled reference by
 tests/golden/cmblikes_ref.json (oracle/gen_golden.py).  Only tests/ use it.
 
@@ -12,6 +13,7 @@ order where the order is visible in the source.
 """
 from __future__ import annotations
 
+import math
 import os
 import re
 
@@ -102,14 +104,16 @@ def _last_top_comment(path):
     return res
 
 
-def _paramnames(path):
-    names = []
+def _paramnames(path, derived=False):
+    """ParamNames_Init (ObjectParamNames.f90:119-151): the non-derived names
+    (DataParams); with derived=True also the '*' (derived) names."""
+    names, dnames = [], []
     with open(path) as f:
         for line in f:
             t = line.split()
             if t and not t[0].startswith("#"):
-                names.append(t[0].rstrip("*"))
-    return names
+                (dnames if t[0].endswith("*") else names).append(t[0].rstrip("*"))
+    return (names, dnames) if derived else names
 
 
 def _eigh(M):
@@ -122,11 +126,15 @@ def _mat_root(M, pw):               # Matrix_Root (Matrix_utils_new.f90:421-440)
 
 
 class CMBLikesOracle:
-    """TCMBLikes / TBK_planck for one dataset; loglike(dl[10][lmax+1], nuis)."""
+    """TCMBLikes / TBK_planck / TSmica_planck for one dataset;
+    loglike(dl[10][lmax+1], nuis), derived(nuis)."""
+
+    SMICA_PIVOT = 2000.0                                   # TSmica_planck%pivot (CMBlikes.f90:1270)
 
     def __init__(self, dataset, overrides=None, tag=""):
         ini = Ini(dataset, overrides)
         self.bk = tag == "BKPLANCK"
+        self.smica = tag == "SMICA"
         # CMBLikes_ReadIni (CMBlikes.f90:466-749)
         s = ini.get("map_names")
         self.has_map_names = s is not None
@@ -220,6 +228,12 @@ class CMBLikesOracle:
             self.nuisance = _paramnames(cp)
             self.cal_index = len(self.nuisance) - 1
             self.log_cal_prior = float(ini.get("log_calibration_prior", -1.0))
+        self.derived_names = []
+        if self.smica:                                     # Tsmica_planck_ReadIni :1281-1293
+            self.nuisance, self.derived_names = _paramnames(ini.fname("nuisance_params"), derived=True)
+            cn = ini.get("calibration_paramname")
+            if cn is not None:
+                self.cal_index = self.nuisance.index(cn) if cn in self.nuisance else None
         if self.bk:
             self.nuisance = _paramnames(ini.fname("nuisance_params"))
             self.fpivot_dust = float(ini.get("fpivot_dust", 353.0))
@@ -370,12 +384,41 @@ class CMBLikesOracle:
                     C[k] = (f1, f2, cl + self.aberration * dd)
         if self.bk:
             self._add_foregrounds(C, nuis)
+        if self.smica:
+            self._add_smica_foregrounds(C, nuis, ells)
         if self.cal_index is not None:
             cal = nuis[self.cal_index]
             for k, (f1, f2, cl) in C.items():
                 if f1 <= 3 and f2 <= 3:
                     C[k] = (f1, f2, cl / cal ** 2)
         return {k: v[2] for k, v in C.items()}
+
+    def _smica_fg(self, P, ells):                          # TSmica_planck_AddForegrounds :1303-1317
+        A1, n1, n1run, A2, n2 = P[:5]
+        out1 = np.empty(ells.size)
+        out2 = np.empty(ells.size)
+        for k, l in enumerate(ells):                       # scalar libm, one l at a time
+            lnrat = math.log(l / self.SMICA_PIVOT)
+            out1[k] = A1 * math.exp(n1 * lnrat + n1run / 2 * lnrat ** 2)
+            out2[k] = A2 * (l / self.SMICA_PIVOT) ** n2
+        return out1, out2
+
+    def _add_smica_foregrounds(self, C, P, ells):
+        t1, t2 = self._smica_fg(P, ells)
+        for k, (f1, f2, cl) in C.items():
+            if f1 == 1 and f2 == 1:                        # CL%theory_i == 1 .and. CL%theory_j == 1
+                C[k] = (f1, f2, (cl + t1) + t2)
+
+    def derived(self, nuis):
+        """derivedParameters (TSmica_planck_derivedParameters :1324-1337; the base
+        TDataLikelihood_derivedParameters is zeros, GeneralTypes.f90:504-512)."""
+        out = np.zeros(len(self.derived_names))
+        if self.smica and out.size:
+            f1, f2, _ = self._theory_field(np.zeros((10, self.lmax + 1)), 1, 1)
+            if f1 == 1 and f2 == 1:
+                t1, t2 = self._smica_fg(nuis, np.array([2000.0]))
+                out[0] = (0.0 + t1[0]) + t2[0]
+        return out
 
     def _add_foregrounds(self, C, P):                      # TBK_planck_AddForegrounds :229-340
         Adust, Async, alphadust, betadust, Tdust, alphasync, betasync, corr = P[:8]

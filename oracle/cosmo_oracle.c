@@ -575,6 +575,11 @@ double orc_target_loglike(const orc_target_t *t, const double *P)
     } else if (t->plik) {
         main += orc_plik_loglike(t->plik, t->plik_dl, t->plik_ld_field, P[t->plik_nuis_index - 1]);
     }
+    if (t->extra_like) {                               /* :380-387, the next likelihood of the list */
+        const double e = t->extra_like(t->extra_user, P);
+        if (e == ORC_LOGZERO) return ORC_LOGZERO;      /* :382 */
+        main += e;
+    }
     add_like_temp(&like, main, t->temperature);
     if (like == ORC_LOGZERO) return like;
     double pri = 0.0;                                  /* GetLogPriors :111-134 */

@@ -96,6 +96,12 @@ typedef struct {
     int n_lincomb;
     const double *lincomb_weights;      /* n_lincomb x num_params */
     const double *lincomb_mean, *lincomb_std;
+    /* further data likelihoods after plik_lite, in DataLikelihoods order
+     * (LogLikeWithTheorySet :374-387 sums Params%Likelihoods in list order):
+     * -lnL of one more likelihood at P, logZero rejects (NULL: none).  The
+     * tests pass a CMBlikes restatement (oracle/cmblikes_oracle.py) here. */
+    double (*extra_like)(void *user, const double *P);
+    void *extra_user;
 } orc_target_t;
 
 double orc_target_loglike(const orc_target_t *t, const double *P); /* GetLogLike :136-151 */

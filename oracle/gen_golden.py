@@ -30,8 +30,10 @@ REF_DIR = os.path.join(HERE, "_ref")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
-def run_cmb_harness(ini_text: str, theory: np.ndarray, nuis: np.ndarray, workdir: str) -> np.ndarray:
-    """theory [W, nfield, lmax+1]; nuis [W, n_nuis] -> reference -lnL [W]."""
+def run_cmb_harness(ini_text: str, theory: np.ndarray, nuis: np.ndarray, workdir: str,
+                    derived: bool = False) -> np.ndarray:
+    """theory [W, nfield, lmax+1]; nuis [W, n_nuis] -> reference -lnL [W]
+    (derived: the harness also writes derivedParameters to workdir/derived.txt)."""
     W, nfield, nl = theory.shape
     ini = os.path.join(workdir, "likes.ini")
     with open(ini, "w") as f:
@@ -42,7 +44,7 @@ def run_cmb_harness(ini_text: str, theory: np.ndarray, nuis: np.ndarray, workdir
     np.ascontiguousarray(theory, dtype="<f8").tofile(th)
     np.ascontiguousarray(nuis, dtype="<f8").tofile(nu)
     cmd = [os.path.join(REF_DIR, "plik_harness"), ini, th, nu, str(W), str(nl - 1), str(nfield),
-           str(nuis.shape[1]), out]
+           str(nuis.shape[1]), out] + ([os.path.join(workdir, "derived.txt")] if derived else [])
     env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
     if os.path.exists(out):
         os.remove(out)                # a Fortran STOP exits 0: never read a stale result
@@ -360,6 +362,54 @@ def gen_cmblikes():
         json.dump(out, f, indent=1)
 
 
+# SMICA (TSmica_planck, CMBlikes.f90:1262-1339) on the synthetic dataset
+# (cosmomc_amd.synthetic.make_smica): (name, like_approx, dataset overrides, walkers, n1run free)
+SMICA_CASES = [
+    ("smica_gauss", "gaussian", {}, 4, False),
+    ("smica_gauss_run", "gaussian", {}, 4, True),
+    ("smica_gauss_calname", "gaussian", {"calibration_paramname": "cal_smica"}, 4, True),
+    ("smica_hl_aber_calname", "HL", {"calibration_paramname": "cal_smica", "aberration_coeff": "0.0012"}, 3, True),
+    # calibration_param loaded by the base ReadIni, then replaced by nuisance_params: its
+    # calibration index (1) stays and points at A1_smica (the reference's own behaviour)
+    ("smica_calparam_override", "gaussian", {"calibration_param": "smica_cal.paramnames",
+                                             "log_calibration_prior": "0.0025"}, 3, True),
+    ("smica_calname_unknown", "gaussian", {"calibration_paramname": "no_such_param"}, 3, False),
+]
+
+
+def smica_nuisance(W, seed, run):
+    g = syn.gaussians(seed, W * 6).reshape(W, 6)
+    c = np.array(list(syn.SMICA_FG) + [1.0])
+    sd = np.array([5.0, 0.1, 0.3 if run else 0.0, 3.0, 0.1, 0.0025])
+    return c[None, :] + g * sd[None, :]
+
+
+def run_cmb_harness_derived(ini_text, theory, nuis, workdir):
+    """run_cmb_harness, also returning derivedParameters per walker."""
+    W, nfield, nl = theory.shape
+    lnl = run_cmb_harness(ini_text, theory, nuis, workdir, derived=True)
+    with open(os.path.join(workdir, "derived.txt")) as f:
+        der = [[float(x) for x in line.split()] for line in f][:W]
+    return lnl, der
+
+
+def gen_smica():
+    out = {"theory_seed": 0xC05A0C, "generator": "cosmomc_amd.synthetic.make_smica", "cases": {}}
+    with tempfile.TemporaryDirectory() as td:
+        for ci, (name, approx, over, W, run) in enumerate(SMICA_CASES):
+            path = syn.make_smica().write(os.path.join(td, name), like_approx=approx)
+            th = syn.walker_theory(W, seed=out["theory_seed"] + 10 * ci, lmax=2508, n_fields=6)
+            nu = smica_nuisance(W, 6060 + ci, run)
+            ini = f"cmb_dataset[SMICA] = {path}\n" + "".join(f"cmb_dataset[SMICA,{k}] = {v}\n" for k, v in over.items())
+            lnl, der = run_cmb_harness_derived(ini, th, nu, td)
+            out["cases"][name] = {"like_approx": approx, "overrides": over, "walkers": W, "lmax": 2508,
+                                  "theory_seed": out["theory_seed"] + 10 * ci, "nuis": nu.tolist(),
+                                  "minus_lnL": lnl.tolist(), "derived": der}
+            print(f"{name:28s} -lnL = {lnl}  derived[0] = {der[0]}")
+    with open(os.path.join(GOLDEN, "smica_ref.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 # SPTpol cases on the synthetic datasets (cosmomc_amd.synthetic.make_sptpol_*):
 # (name, tag, dataset overrides, walkers)
 SPTPOL_CASES = [
@@ -521,6 +571,8 @@ if __name__ == "__main__":
         gen_confid()
     if not only or "cmblikes" in only:
         gen_cmblikes()
+    if not only or "smica" in only:
+        gen_smica()
     if not only or "sptpol" in only:
         gen_sptpol()
     if not only or "exact" in only:

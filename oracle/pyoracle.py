@@ -37,7 +37,12 @@ class Target(C.Structure):
                 ("plik_nuis_index", C.c_int), ("plik_dl", C.c_void_p), ("plik_ld_field", C.c_long),
                 ("plik_scale_index", C.c_int), ("include_fixed_parameter_priors", C.c_int),
                 ("varying", C.c_void_p), ("n_lincomb", C.c_int), ("lincomb_weights", C.c_void_p),
-                ("lincomb_mean", C.c_void_p), ("lincomb_std", C.c_void_p)]
+                ("lincomb_mean", C.c_void_p), ("lincomb_std", C.c_void_p),
+                ("extra_like", C.c_void_p), ("extra_user", C.c_void_p)]
+
+
+# Target.extra_like: double (*)(void *user, const double *P)
+EXTRA_LIKE_FN = C.CFUNCTYPE(C.c_double, C.c_void_p, C.POINTER(C.c_double))
 
 
 def lib():

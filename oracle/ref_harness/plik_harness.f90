@@ -11,11 +11,13 @@
 ! source/CMB_BK_Planck.f90 for BKPLANCK) on theory C_l read from a binary
 ! stream file.
 !
-! usage: plik_harness <likelihoods.ini> <theory.bin> <nuis.bin> <W> <lmax> <nfield> <n_nuis> <out.txt>
+! usage: plik_harness <likelihoods.ini> <theory.bin> <nuis.bin> <W> <lmax> <nfield> <n_nuis> <out.txt> [derived.txt]
 !   theory.bin : W x nfield x (lmax+1) float64, field order TT TE EE BT BE BB PT PE PB PP
 !                (Theory%Cls(i,j), i>=j, T=1 E=2 B=3 P=4), l = 0..lmax
 !   nuis.bin   : W x n_nuis float64 (DataParams of the first likelihood)
 !   out.txt    : one -lnL per walker ("%24.17e")
+!   derived.txt: (optional) the likelihood's derivedParameters(Theory, DataParams)
+!                per walker (GeneralTypes.f90:504-512, CMBlikes.f90:1324-1337 for SMICA)
 program plik_harness
     use settings
     use IniObjects
@@ -30,9 +32,9 @@ program plik_harness
     class(TDataLikelihood), pointer :: DL
     Type(TCosmoTheoryPredictions) :: Theory
     Type(CMBParams) :: CMB
-    character(LEN=1024) :: ini_name, th_name, nu_name, out_name, arg
-    integer :: W, lmax, nfield, n_nuis, w_i, f, i, j, ix, u_th, u_nu, u_out
-    real(mcp), allocatable :: cl(:,:), nuis(:)
+    character(LEN=1024) :: ini_name, th_name, nu_name, out_name, der_name, arg
+    integer :: W, lmax, nfield, n_nuis, w_i, f, i, j, ix, u_th, u_nu, u_out, u_der, nder
+    real(mcp), allocatable :: cl(:,:), nuis(:), der(:)
     real(mcp) :: lnl
     logical :: bad
     integer, parameter :: fi(10) = [1,2,2,3,3,3,4,4,4,4], fj(10) = [1,1,2,1,2,3,1,2,3,4]
@@ -45,6 +47,8 @@ program plik_harness
     call get_command_argument(6, arg); read(arg, *) nfield
     call get_command_argument(7, arg); read(arg, *) n_nuis
     call get_command_argument(8, out_name)
+    der_name = ''
+    if (command_argument_count() >= 9) call get_command_argument(9, der_name)
 
     Feedback = 0
     call Ini%Open(trim(ini_name), bad, .false.)
@@ -62,6 +66,8 @@ program plik_harness
     open(newunit=u_nu, file=trim(nu_name), access='stream', form='unformatted', status='old')
     open(newunit=u_out, file=trim(out_name), status='replace')
     DL => Likes%Item(1)
+    nder = DL%nuisance_params%num_derived
+    if (der_name /= '') open(newunit=u_der, file=trim(der_name), status='replace')
     do w_i = 1, W
         read(u_th) cl
         if (n_nuis > 0) read(u_nu) nuis
@@ -75,7 +81,16 @@ program plik_harness
             stop 'not a CMB likelihood'
         end select
         write(u_out, '(ES25.17)') lnl
+        if (der_name /= '') then
+            if (nder > 0) then
+                der = DL%derivedParameters(Theory, nuis)
+                write(u_der, '(*(ES25.17))') der
+            else
+                write(u_der, '(a)') ''
+            end if
+        end if
     end do
     close(u_th); close(u_nu); close(u_out)
+    if (der_name /= '') close(u_der)
     ix = 0; i = 0; j = 0
 end program plik_harness

@@ -117,3 +117,18 @@ def exact_data(tmp_path_factory):
     import gen_golden as gg
     d = str(tmp_path_factory.mktemp("exact"))
     return {c[0]: gg.exact_dataset(c, d) for c in gg.EXACT_CASES}
+
+
+@pytest.fixture(scope="session")
+def smica_golden():
+    return load_golden("smica_ref.json")
+
+
+@pytest.fixture(scope="session")
+def smica_data(tmp_path_factory):
+    """The synthetic SMICA datasets (cosmomc_amd.synthetic.make_smica), gaussian
+    and HL, written once per session: {like_approx: dataset path}."""
+    from cosmomc_amd import synthetic as syn
+    d = str(tmp_path_factory.mktemp("smica"))
+    data = syn.make_smica()
+    return {a: data.write(os.path.join(d, a), like_approx=a) for a in ("gaussian", "HL")}

@@ -31,7 +31,8 @@ def test_open_missing_file_returns_error_code():
 
 def test_open_tag_dispatch(tmp_path):
     """CMBLikelihood_Add (CMB.f90:80-97): unknown tags are CMBlikes datasets;
-    SPTpol datasets need their sptpol_* keys; SMICA / WMAP are not built."""
+    SPTpol datasets need their sptpol_* keys; SMICA is a CMBlikes dataset
+    (TSmica_planck, CMBlikes.f90:1262-1339); WMAP (an external library) is not built."""
     p = tmp_path / "a.dataset"
     p.write_text("name = x\n")
     h = C.c_void_p()
@@ -40,7 +41,9 @@ def test_open_tag_dispatch(tmp_path):
     assert b"fields_use" in err.value
     assert N.lib().cmbl_open(b"SPTPOL_TEEE", str(p).encode(), None, C.byref(h), err, 256) == -3
     assert b"sptpol_TEEE_params_file" in err.value
-    assert N.lib().cmbl_open(b"SMICA", str(p).encode(), None, C.byref(h), err, 256) == -6
+    assert N.lib().cmbl_open(b"SMICA", str(p).encode(), None, C.byref(h), err, 256) == -3   # CMBlikes ReadIni
+    assert b"fields_use" in err.value
+    assert N.lib().cmbl_open(b"WMAP", str(p).encode(), None, C.byref(h), err, 256) == -6
 
 
 def test_sptpol_blind_r_rejected(tmp_path):

@@ -1122,7 +1122,7 @@ def test_bin_corun_bitwise(tmp_path, W, shared):
         assert terms[-1, 0, w] == pytest.approx(ref, rel=1e-9)
 
 
-def _config5_sampler(refdata, tmp_path, W, groups):
+def _config5_sampler(refdata, tmp_path, W, groups, tdust_free=False):
     """BASELINE configs[4] as bench.py's config5_bk15_plik builds it: BK15 (12
     B maps x 9 bins, HL, batch3/BK15.ini foreground parameters) + plik_lite
     TTTEEE on one shared slow point, 8 fast parameters in the blocks the
@@ -1149,12 +1149,17 @@ def _config5_sampler(refdata, tmp_path, W, groups):
     pm[4], ps[4] = 1.59, 0.11
     pm[7], ps[7] = -3.1, 0.3
     used = [1, 2, 3, 4, 5, 7, 8, 9]
+    width = [0.0025, 0.5, 1.0, 0.1, 0.1, 0.1, 0.3, 0.2]
+    if tdust_free:          # T_dust (DataParams(5) of BK15) a fast parameter, different in every walker
+        pmin[5], pmax[5] = 15.0, 25.0
+        used = [1, 2, 3, 4, 5, 6, 7, 8, 9]
+        width.insert(5, 0.5)
+    width = np.array(width)
     ll = LikelihoodList()
     ll.add(plik)
     ll.add(bk)
     ll.add_nuisance_parameters([])
     blk = set_fast_slow_params(17, [i + 1 in used for i in range(17)], list(ll), num_theory_params=0)
-    width = np.array([0.0025, 0.5, 1.0, 0.1, 0.1, 0.1, 0.3, 0.2])
     s = BatchedMCMC(W, 17, used, blk.param_blocks, blk.slow_block_max, pmin, pmax, pm, ps, propose_scale=2.4,
                     seed_ij=3003, seed_kl=9373)
     s.set_covariance(np.diag(width ** 2))
@@ -1164,7 +1169,7 @@ def _config5_sampler(refdata, tmp_path, W, groups):
     s.add_likelihood(plik, dl)
     s.add_likelihood(bk, dl)
     start = np.tile(P0, (W, 1))
-    g = syn.gaussians(91, W * 8).reshape(W, 8)
+    g = syn.gaussians(91, W * len(used)).reshape(W, len(used))
     for c, i in enumerate([u - 1 for u in used]):
         start[:, i] = np.clip(P0[i] + 2 * width[c] * g[:, c], pmin[i] + 1e-9, pmax[i] - 1e-9)
     s.set_start(start)
@@ -1205,3 +1210,131 @@ def test_config5_joint_path_vs_oracles(refdata, tmp_path):
     for w in (0, 511, 1023):
         assert a[4][-1, 0, w] == pytest.approx(op.loglike(th[:3], a[0][w, 0]), rel=1e-9)
         assert a[4][-1, 1, w] == pytest.approx(ob.loglike(th, a[0][w, 1:17]), rel=1e-9)
+
+
+def test_bk_tdust_per_walker_groups_bitwise(refdata, tmp_path):
+    """BK15's dust greybody denominators are tabulated per call for the first
+    walker's T_dust (cmbl_bk_tdtab) in the call's own workspace.  With T_dust a
+    fast parameter that differs between walkers, two and four walker groups
+    (each group's BK evaluation on its own stream, concurrently) give the same
+    bits as one group, and the final terms are the oracle's (the
+    table used to live in the likelihood object, shared across streams)."""
+    import os
+
+    import cmblikes_oracle as co
+    W, steps = 256, 4
+    runs = []
+    for groups in (1, 2, 4):
+        s, data, th, maps = _config5_sampler(refdata, tmp_path, W, groups, tdust_free=True)
+        s.enable_history(steps)
+        s.step(steps, fast_only=True)
+        P, lk, mult, nacc = s.state()
+        runs.append((P.copy(), lk.copy(), mult.copy(), nacc.copy(), s.history_terms(0, steps)))
+        s.close()
+    a = runs[0]
+    assert np.unique(a[0][:, 5]).size > W // 2        # T_dust differs between walkers
+    assert a[3].sum() > 0
+    for b in runs[1:]:
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    ob = co.CMBLikesOracle(os.path.join(refdata, "BK15/BK15_dust.dataset"), {"maps_use": maps}, "BKPLANCK")
+    for w in (0, 127, 128, 255):
+        assert a[4][-1, 1, w] == pytest.approx(ob.loglike(th, a[0][w, 1:17]), rel=1e-9)
+
+
+def test_headline_chain_follows_oracle_step_by_step(tmp_path):
+    """BASELINE configs[2]'s headline fast step exactly as bench.py builds it
+    (plik_lite TTTEEE + Planck 2018 lensing on per-walker theory, calPlanck
+    fast with its prior, W = 1024) on the default schedule -- the unified
+    launch (mh_step_kernel) with the lean chain -- for 24 steps.  Walkers
+    {0, W/2 - 1, W - 1} follow an oracle chain step by step: the C oracle's
+    FastParameterSample (orc_mh_step: BlockedProposer, RANMAR, GetLogLike,
+    MetropolisAccept) on a target of pyoracle.PlikLite + the CMBlikes numpy
+    restatement of the lensing likelihood (LogLikeWithTheorySet,
+    calclike.f90:357-389, in list order) + the calPlanck prior.  Every accept
+    decision matches, and the point and CurLike after every step match at
+    rtol 1e-11 / 1e-9 (MCMC.f90:309-335, calclike.f90:136-151)."""
+    import os
+
+    import bench
+    import cmblikes_oracle as co
+    from cosmomc_amd import _native as N
+    from cosmomc_amd.sampler import walker_seed
+    W, steps = 1024, 24
+    smp, likes, theory, _ = bench.build_problem(W, 0, str(tmp_path))
+    smp.enable_history(steps)
+    N.profile_enable(True)
+    N.profile_reset()
+    smp.step(steps, fast_only=True)
+    torch.cuda.synchronize()
+    assert N.profile_read("mh_step_kernel")[1] == steps - 1     # the unified launch ran every middle step
+    N.profile_enable(False)
+    rows = smp.history_host(0, steps)                              # [steps, 8, W]: P(1..7), CurLike
+    th = theory.cpu().numpy()
+    data = syn.make_plik_lite(12345)
+    plik = po.PlikLite(data)
+    lens = co.CMBLikesOracle(os.path.join(str(tmp_path), "refdata", bench.LENS_DATASET))
+    P0 = np.array([0.02237, 0.1200, 1.04092, 0.0544, 3.044, 0.9649, 1.0])
+    sig = np.array([0.00015, 0.0012, 0.00031, 0.0073, 0.014, 0.0042, 0.0025])
+    pmin, pmax = P0 - 50 * sig, P0 + 50 * sig
+    pmin[6], pmax[6] = 0.9, 1.1
+    pm, ps = np.zeros(7), np.zeros(7)
+    pm[6], ps[6] = 1.0, 0.0025
+    keep = [np.ascontiguousarray(a) for a in (pmin, pmax, pm, ps)]
+    n_acc_total = 0
+    for w in (0, W // 2 - 1, W - 1):
+        dlw = np.ascontiguousarray(th[w])
+        calls = []
+
+        def lensing_term(user, Pp, dlw=dlw, calls=calls):
+            calls.append(1)
+            return float(lens.loglike(dlw, np.array([Pp[6]])))
+        cb = po.EXTRA_LIKE_FN(lensing_term)
+        t = po.Target()
+        t.num_params = 7
+        t.pmin, t.pmax, t.prior_mean, t.prior_std = [a.ctypes.data for a in keep]
+        t.temperature = 1.0
+        t.plik, t.plik_nuis_index, t.plik_dl, t.plik_ld_field = plik.h, 7, dlw.ctypes.data, dlw.shape[1]
+        t.extra_like = C.cast(cb, C.c_void_p)
+        blocks = np.array([1, 2, 3, 4, 5, 6, 7], dtype=np.int32)
+        h = po.lib().orc_proposer_create(2, np.array([6, 1], dtype=np.int32), blocks, 1, 1, 2.4, 7,
+                                         np.arange(1, 8, dtype=np.int32))
+        po.lib().orc_proposer_set_covariance(h, np.ascontiguousarray(np.diag(sig ** 2)))
+        r = po.Ranmar(*walker_seed(1802, 9373, w))
+        Q = P0.copy()
+        cur = C.c_double(po.lib().orc_target_loglike(C.byref(t), Q))
+        for k in range(steps):
+            prev = rows[k - 1, :7, w] if k else P0
+            acc = po.lib().orc_mh_step(h, C.byref(r.s), C.byref(t), Q, C.byref(cur), 1, None)
+            moved = not np.array_equal(rows[k, :7, w], prev)
+            assert bool(acc) == moved, (w, k)
+            n_acc_total += acc
+            np.testing.assert_allclose(rows[k, :7, w], Q, rtol=1e-11, atol=0, err_msg=f"walker {w} step {k}")
+            assert rows[k, 7, w] == pytest.approx(cur.value, rel=1e-9), (w, k)
+        po.lib().orc_proposer_free(h)
+        assert steps // 2 < len(calls) <= steps + 1     # trials out of bounds never reach the likelihoods
+    assert n_acc_total > 10
+    smp.close()
+
+
+def test_binned_cache_same_bits(tmp_path):
+    """cmbs_set_binned_cache: the unified fast step binning each walker's
+    theory once per call and reusing the raw sums gives the same chains,
+    history rows and terms bit for bit as re-binning at every step (the
+    theory is fixed inside a call; the sums are calibration-independent)."""
+    import bench
+    W = 256
+    out = []
+    for cache in (False, True):
+        smp, likes, theory, _ = bench.build_problem(W, 0, str(tmp_path / f"c{int(cache)}"))
+        smp.set_binned_cache(cache)
+        smp.enable_history(40)
+        smp.step(15, fast_only=True)
+        smp.step(9, fast_only=True)
+        k = smp.history_count()
+        out.append((smp.history_host(0, k), smp.history_terms(0, k), *smp.state()))
+        smp.close()
+    a, b = out
+    assert np.any(a[5] > 0)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)

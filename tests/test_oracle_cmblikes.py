@@ -39,3 +39,23 @@ def test_exact_oracle_vs_reference(exact_golden, exact_data, case):
     nu = np.array(c["nuis"]).reshape(c["walkers"], -1)
     got = np.array([o.loglike(th[w], nu[w]) for w in range(c["walkers"])])
     np.testing.assert_allclose(got, c["minus_lnL"], rtol=1e-11, atol=1e-9)
+
+
+SMICA = ["smica_gauss", "smica_gauss_run", "smica_gauss_calname", "smica_hl_aber_calname", "smica_calparam_override",
+         "smica_calname_unknown"]
+
+
+@pytest.mark.parametrize("case", SMICA)
+def test_smica_oracle_vs_reference(smica_golden, smica_data, case):
+    """TSmica_planck (CMBlikes.f90:1262-1339): the TT foreground, nuisance_params,
+    calibration_paramname (and the base calibration_param it overrides) and the
+    derived D_l(2000), against the compiled reference (tests/golden/smica_ref.json)."""
+    c = smica_golden["cases"][case]
+    o = co.CMBLikesOracle(smica_data[c["like_approx"]], c["overrides"], "SMICA")
+    th = syn.walker_theory(c["walkers"], seed=c["theory_seed"], lmax=c["lmax"], n_fields=6)
+    nu = np.array(c["nuis"])
+    got = np.array([o.loglike(th[w], nu[w]) for w in range(c["walkers"])])
+    np.testing.assert_allclose(got, c["minus_lnL"], rtol=1e-11, atol=1e-9)
+    der = np.array([o.derived(nu[w]) for w in range(c["walkers"])])
+    np.testing.assert_allclose(der, np.array(c["derived"]), rtol=1e-14, atol=0)
+    assert o.derived_names == ["Dl2000_smica"]

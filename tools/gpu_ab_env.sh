@@ -1,13 +1,13 @@
 #!/bin/bash
 # Interleaved A/B of the headline bench under environment switches.
-#   tools/gpu_ab_env.sh "base" "CMAMD_PIPE=3" "HIP_FORCE_DEV_KERNARG=0 CMAMD_PIPE=1" ...
+#   tools/gpu_ab_env.sh "base" "CMAMD_PIPE=0" "CMAMD_UNI_WT=8" ...
 # Each argument is one variant ("base": no extra environment); REPS (default 2)
 # rounds run every variant in turn; BENCH_ARGS replaces the default bench
 # arguments (headline only, 300 steps).
 set -u
 mkdir -p gpurun_out/ab
 REPS=${REPS:-2}
-ARGS=${BENCH_ARGS:---steps 300 --warmup 20 --no-cpu-baseline --converge-seconds 0 --config1-seconds -1 --config4-seconds -1 --config5-seconds -1 --drag-seconds -1}
+ARGS=${BENCH_ARGS:---steps 300 --warmup 20 --no-cpu-baseline --cache-steps -1 --converge-seconds 0 --config1-seconds -1 --config4-seconds -1 --config5-seconds -1 --drag-seconds -1}
 for rep in $(seq 1 $REPS); do
   i=0
   for v in "$@"; do

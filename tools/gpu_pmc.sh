@@ -1,13 +1,14 @@
 #!/bin/bash
 # PMC counter passes over a short headline bench run (one rocprofv3 run per
 # pass, no tracing domain combined with --pmc), plus the kernel-trace --stats
-# pass whose durations tools/pmc_summary.py divides by.  Extra args go to bench.py.
+# pass whose durations tools/pmc_summary.py divides by.  PMC_BENCH_ARGS replaces
+# the bench arguments (e.g. the configs[1] leg alone).
 set -u
 OUTD=${PMC_OUT:-pmc}
 mkdir -p gpurun_out/$OUTD
 cd /tmp && export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"
-B="--no-cpu-baseline --steps 60 --warmup 5 --converge-seconds 0 --config1-seconds -1 --config4-seconds -1 --config5-seconds -1 --drag-seconds -1"
+B=${PMC_BENCH_ARGS:-"--no-cpu-baseline --steps 60 --warmup 5 --cache-steps -1 --converge-seconds 0 --config1-seconds -1 --config4-seconds -1 --config5-seconds -1 --drag-seconds -1"}
 pass() {
   name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$R/gpurun_out/$OUTD/$name" -o run \

@@ -12,12 +12,12 @@ rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/$TAG/gpu_tests.log; [ $rc -eq 0 
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" 2>&1 | grep -v amdgpu.ids; rc=${PIPESTATUS[0]}; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/$TAG/bench_driver.json 2> gpurun_out/$TAG/bench_driver.err; rc=$?; echo "driver-cmd bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python3 -c "import json;d=json.load(open('gpurun_out/$TAG/bench_driver.json'));print(round(d['value']/1e6,3),'M',round(d['ms_per_step']*1e3,2),'us/step',d['roofline']['kernel'],round(d['roofline']['frac'],3),d['roofline']['avg_kernel_us'])"
-timeout -k 10 300 python3 bench.py --steps 500 --no-cpu-baseline --converge-seconds 0 --config1-seconds -1 --config4-seconds -1 --config5-seconds -1 --drag-seconds -1 > gpurun_out/$TAG/bench_500.json 2>/dev/null; rc=$?; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 bench.py --steps 500 --no-cpu-baseline --cache-steps -1 --converge-seconds 0 --config1-seconds -1 --config4-seconds -1 --config5-seconds -1 --drag-seconds -1 > gpurun_out/$TAG/bench_500.json 2>/dev/null; rc=$?; [ $rc -eq 0 ] || exit $rc
 python3 -c "import json;d=json.load(open('gpurun_out/$TAG/bench_500.json'));print('500 steps:',round(d['value']/1e6,3),'M',round(d['ms_per_step']*1e3,2),'us/step',round(d['roofline']['frac'],3))"
 cd /tmp && export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/$TAG/prof" -o run \
-  -- python3 "$R/bench.py" --no-cpu-baseline --converge-seconds 0 --config1-seconds -1 --config4-seconds -1 --config5-seconds -1 --drag-seconds -1 \
+  -- python3 "$R/bench.py" --no-cpu-baseline --cache-steps -1 --converge-seconds 0 --config1-seconds -1 --config4-seconds -1 --config5-seconds -1 --drag-seconds -1 \
   > "$R/gpurun_out/$TAG/prof.log" 2>&1
 rc=$?; echo "prof rc=$rc"; rm -f "$R"/gpurun_out/$TAG/prof/*kernel_trace.csv; [ $rc -eq 0 ] || exit $rc
 cd "$R"
