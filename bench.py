@@ -345,7 +345,7 @@ def binned_cache_run(smp, W, world, steps, warmup=20):
     smp.step(steps, fast_only=True)
     torch.cuda.synchronize()
     N.profile_enable(False)
-    tot, cnt = N.profile_read("mh_step_kernel")
+    tot, cnt = N.profile_read("mh_tail_kernel")
     smp.set_binned_cache(False)
     f_eval = 2 * N_B * N_B + 4 * N_B                                   # F without 2 N_l
     b_eval = 16 + (8 * N_B * N_B + 8 * 2479 + 8 * N_B) / W             # B without 8 N_l
@@ -360,7 +360,7 @@ def binned_cache_run(smp, W, world, steps, warmup=20):
                               "frac": per_gpu * f_eval / ceil,
                               "note": "per GPU: F = 2 N_b^2 + 4 N_b = 753,990 flop/eval, B = 16 + 3,030,888 / W "
                                       "bytes/eval (8(d) with the N_l terms dropped)"},
-            "mh_step_kernel": {"avg_launch_us": avg_us,
+            "mh_tail_kernel": {"avg_launch_us": avg_us,
                                "mfma_frac": (qf / (avg_us * 1e-6) / 1e12 / PEAK_FP64_TFLOPS) if avg_us else None,
                                "note": "the quadratic form's 2 N_b^2 + 2 N_b flops per walker over the launch "
                                        "(chi^2 and chain in the same launch)"}}

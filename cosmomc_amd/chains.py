@@ -278,7 +278,7 @@ class LikelihoodDerived:
         full = full.reshape(steps * W, -1)
         out = np.zeros((steps * W, self.n))
         for l in self.likes:
-            nuis = torch.tensor(full[:, [i - 1 for i in l.nuisance_indices]], device="cuda")
+            nuis = torch.tensor(np.ascontiguousarray(full[:, [i - 1 for i in l.nuisance_indices]]), device="cuda")
             d = l.derived_batch(nuis).cpu().numpy()
             for k, ix in enumerate(l.derived_indices):
                 out[:, ix - 1] = d[:, k]

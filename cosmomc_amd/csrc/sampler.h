@@ -137,8 +137,9 @@ struct DevCfg {
 struct TailWait {
     unsigned int *cnt;       // [tiles] arrivals
     unsigned int epoch;      // launches with producers so far, this one included
+    unsigned int epoch_g;    // of them, those whose chi^2 ran as workgroups of its own (not folded)
     int nq_items;            // quadratic-form workgroups per tile
-    int ng, gwt;             // chi^2 workgroups and walkers per chi^2 workgroup
+    int ng, gwt;             // chi^2 workgroups (of an unfolded launch) and walkers per chi^2 workgroup
     int *status;             // CMBL_STATUS_PIPE_WAIT when a wait gives up
     int nosignal;            // debug: the producers never arrive (the give-up test)
     int stamp_slot;          // instrumented builds: the stamp buffer (0 middle launches, 1 the last)
@@ -241,10 +242,13 @@ struct cmbs {
     cmamd::DevBuf tail_cnt;                  // [tiles] TailWait::cnt
     size_t tail_cnt_bytes = 0;
     unsigned tail_epoch = 0;
+    unsigned tail_epoch_g = 0;               // accepting unified launches with the chi^2 as rows (not folded)
     cmamd::StepTailPlan uni_plan[3];         // rows: propose + pass, tails + pass + accept/propose, tails + accept
     size_t uni_lds = 0;
     int tail_nosignal = 0;                   // debug (cmamd_debug_tail_nosignal)
     bool binned_cache = false;               // cmbs_set_binned_cache: bin once per fast-step call
+    int qf_ahead = 0;                        // unified launch: CMAMD_QF_AHEAD (A/B of qfs_body_nj in the middle launches)
+    int fold_late_prio = 0;                  // unified launch: CMAMD_FOLD_LATE_PRIO (A/B)
     int fold_g = 1;                          // unified launch: the small chi^2 in the Metropolis workgroups
                                              // (CMAMD_FOLD_G=0: as rows of its own, for A/B runs)
     // a pipelined hand-off that gave up (unified launch, bin co-run): the device word, its

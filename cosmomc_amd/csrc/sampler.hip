@@ -612,7 +612,9 @@ __device__ __forceinline__ void tail_wait(const TailWait &tw, int tile)
     if (threadIdx.x == 0) {
         const int gpt = 64 / tw.gwt, g0 = tile * gpt;
         const int gq = max(0, min(gpt, tw.ng - g0));
-        const unsigned target = tw.epoch * (unsigned)(tw.nq_items + gq);
+        // every accepting launch adds its quadratic-form workgroups, and those whose
+        // chi^2 ran as workgroups of its own (not folded) add the tile's chi^2 ones
+        const unsigned target = tw.epoch * (unsigned)tw.nq_items + tw.epoch_g * (unsigned)gq;
         for (long it = 0;; it++) {
             const unsigned v = __hip_atomic_load(tw.cnt + tile * TW_PAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (v >= target) break;
@@ -1171,7 +1173,10 @@ __device__ __forceinline__ void mh_step_body(DevCfg &c, int fast_only, double *h
         if (lb >= t.nq) return;
         int item_ix, tile;
         qf_place(lb, t.q.src.n_items, t.q.src.xcd_map, item_ix, tile);
-        qfs_body<true, !PROPOSE>(lds, item_ix, tile, t.q);
+        if (PROPOSE && t.qf_ahead)   // A/B (CMAMD_QF_AHEAD): the two-step-ahead form in the middle launches too
+            qfs_body<true, true>(lds, item_ix, tile, t.q);
+        else
+            qfs_body<true, !PROPOSE>(lds, item_ix, tile, t.q);
         tail_arrive(tw, tile);
     } else if (rr.x == TAIL_GAUSS) {
         // contiguous walker groups per XCD (lb % 8 is the XCD): each partial row's
@@ -1186,7 +1191,7 @@ __device__ __forceinline__ void mh_step_body(DevCfg &c, int fast_only, double *h
     } else if (lb < nmh) {
         // the chain is latency on one lane: its waves, dispatched last (the youngest,
         // so the last in issue arbitration), take the SIMD first (34.6 -> 34.0 us)
-        __builtin_amdgcn_s_setprio(3);
+        if (!t.fold_late_prio) __builtin_amdgcn_s_setprio(3);
         if (ACCEPT && t.fold_g) {
             // the small chi^2 of this workgroup's 16 walkers (step k's raw partial
             // rows, whole 128-byte lines) while the quadratic form runs elsewhere:
@@ -1196,6 +1201,7 @@ __device__ __forceinline__ void mh_step_body(DevCfg &c, int fast_only, double *h
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
+        if (t.fold_late_prio) __builtin_amdgcn_s_setprio(3);   // A/B: the folded chi^2 at the default priority
         mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, 0, lds, lb, ACCEPT ? &tw : nullptr);
     }
 }
@@ -3272,6 +3278,7 @@ static bool tail_setup(cmbs *s, int fast_only) {
     s->tail_cnt.alloc(s->tail_cnt_bytes);
     HIP_CHECK(hipMemset(s->tail_cnt.p, 0, s->tail_cnt_bytes));
     s->tail_epoch = 0;
+    s->tail_epoch_g = 0;
     pipe_status_init(s);
     {
         const int gi = s->tp_like[s->tail_g];
@@ -3319,7 +3326,11 @@ static StepTail make_tail(cmbs *s, int rd, int wr) {
         t.ng = (W + UNI_WT - 1) / UNI_WT;
         // the chi^2 folded into the Metropolis workgroups: bit-identical while its
         // 16-walker body's thread groups (256 / 16) cover the bandpowers
-        t.fold_g = (s->fold_g && t.g.d.nX <= MH_THREADS / MB) ? 1 : 0;
+        // (middle launches only: in the accept-only launch that ends a call the
+        // chi^2 would sit on the chain's critical path, 21.5 against 23.3 us)
+        t.fold_g = (s->fold_g && wr >= 0 && t.g.d.nX <= MH_THREADS / MB) ? 1 : 0;
+        t.qf_ahead = s->qf_ahead;
+        t.fold_late_prio = s->fold_late_prio;
         if (t.fold_g) t.ng = 0;
     }
     if (wr >= 0) {
@@ -3366,9 +3377,10 @@ static void launch_unified(cmbs *s, hipStream_t stream, bool propose, int rd, in
     TailWait tw{};
     tw.cnt = s->tail_cnt.as<unsigned int>();
     tw.epoch = s->tail_epoch + (accept ? 1u : 0u);
+    tw.epoch_g = s->tail_epoch_g + ((accept && !t.fold_g) ? 1u : 0u);
     tw.nq_items = t.q.src.n_items;
-    tw.ng = ng_rows;
-    tw.gwt = UNI_WT;
+    tw.ng = accept ? (s->W + UNI_WT - 1) / UNI_WT : 0;   // an unfolded launch's chi^2 workgroups (the target's
+    tw.gwt = UNI_WT;                                      // per-tile count for the epoch_g launches)
     tw.status = s->pipe_status_dev;
     tw.nosignal = s->tail_nosignal;
     tw.stamp_slot = propose ? 0 : 1;
@@ -3415,6 +3427,7 @@ static void launch_unified(cmbs *s, hipStream_t stream, bool propose, int rd, in
         throw;
     }
     if (accept) s->tail_epoch++;
+    if (accept && !t.fold_g) s->tail_epoch_g++;
 }
 
 void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
@@ -3432,6 +3445,7 @@ void sampler_step(cmbs *s, int n_steps, int fast_only, hipStream_t stream) {
         // tails(n) + accept(n): one launch per step.  The arrival counters start from 0
         // in every call (the first launch zeroes them; the epochs are counted within it)
         s->tail_epoch = 0;
+        s->tail_epoch_g = 0;
         launch_unified(s, stream, true, -1, 0, HistRow{}, fast_only);
         if (s->binned_cache) {
             // the theory is fixed within the call: every step's tails read the raw

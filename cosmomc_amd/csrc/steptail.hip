@@ -9,12 +9,15 @@ namespace cmamd {
 
 // The rows' order: CMAMD_TAIL_ORDER lists the roles (q: quadratic form, g:
 // chi^2, p: pass) in dispatch order; "q*p" deals the q and p rows in
-// proportion to their counts, interleaved.  Default "gqp" ("qpg" measured 58.4
+// proportion to their counts, interleaved.  Default "gqp", "mqp" with the chi^2 folded ("qpg" measured 58.4
 // against 40.9 us/step, round 4; with the Metropolis rows placed earlier, 61-94
 // against 38.5, round 5: profiles/r05_schedules.txt).
 std::vector<int2> tail_rows(int nq, int ng, int np, int nm) {
     static const char *env = std::getenv("CMAMD_TAIL_ORDER");
-    const std::string order = env && *env ? env : "gqp";
+    // with the chi^2 folded into the Metropolis workgroups (ng = 0) they come first and
+    // compute it while the quadratic form runs: "mqp" 32.6-32.7 against "gqp" 41.0 and
+    // the chi^2 as rows of its own 33.6-33.8 us a middle launch (round 6, r6a)
+    const std::string order = env && *env ? env : (ng > 0 ? "gqp" : "mqp");
     const int cnt[3] = {(nq + 7) / 8, (ng + 7) / 8, (np + 7) / 8};
     auto role = [](char c) { return c == 'q' ? TAIL_QF : c == 'g' ? TAIL_GAUSS : c == 'p' ? TAIL_PASS : -1; };
     std::vector<int2> rows;

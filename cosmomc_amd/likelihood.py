@@ -129,7 +129,8 @@ class NativeCMBLikelihood(DataLikelihood):
             out = torch.empty((W, nd), dtype=torch.float64, device=nuis.device)
         if nd == 0 or W == 0:
             return out
-        if nuis.dtype != torch.float64 or not nuis.is_cuda or nuis.stride(1) != 1 or out.stride(1) != 1:
+        if nuis.dtype != torch.float64 or not nuis.is_cuda or (nuis.shape[1] > 1 and nuis.stride(1) != 1) or \
+                (nd > 1 and out.stride(1) != 1):
             raise TypeError("nuis must be a float64 cuda tensor with contiguous rows")
         rc = N.lib().cmbl_derived_batch(self._h, W, nuis.data_ptr(), nuis.stride(0), out.data_ptr(), out.stride(0),
                                         N.current_stream_ptr(nuis.device))
