@@ -24,6 +24,7 @@
 //   quadform_ksplit         bigX^T C^-1 bigX / 2 on the f64 MFMA (quadform.hip).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <fstream>
@@ -613,7 +614,7 @@ __global__ __launch_bounds__(256, 2) void cmbl_window_group(CLDev c, const GItem
                                                         const double *__restrict__ nuis, long long ld_nuis,
                                                         const double *__restrict__ coef, const double *__restrict__ prof,
                                                         int LP, double *__restrict__ partial, int W, int tiles,
-                                                        int vec_ok)
+                                                        int vec_ok, int tile_xcd)
 {
     constexpr int LPL = 4, STEP = 4 * LPL;
     // per-(pair, walker) SED coefficients: [GP][8][64] = dust, sync, dsync, ddf, dsf, nui, nuj, flags
@@ -621,10 +622,20 @@ __global__ __launch_bounds__(256, 2) void cmbl_window_group(CLDev c, const GItem
     // the item's window weights of one step, double-buffered: [GP * 16 columns][STEP (+2 pad)]
     constexpr int WR = STEP + 2;
     __shared__ __attribute__((aligned(16))) double wsh[2][GP * 16 * WR];
-    // blocks are dealt to the XCDs round-robin: all walker tiles of an item on one XCD
-    // (its weights in one L2); measured faster than an XCD-balanced split of the units
+    // blocks are dealt to the XCDs round-robin.  tile_xcd (tiles % 8 == 0): each XCD
+    // owns tiles / 8 walker tiles and runs every item for them, so a walker's four
+    // rows are fetched into one L2 (the items of one l segment re-read them once per
+    // pair group); else all walker tiles of an item on one XCD (its weights in one L2)
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
-    const int item = xcd + 8 * (j / tiles), tile = j % tiles;
+    int item, tile;
+    if (tile_xcd) {
+        const int tpx = tiles >> 3;
+        tile = xcd + 8 * (j % tpx);
+        item = j / tpx;
+    } else {
+        item = xcd + 8 * (j / tiles);
+        tile = j % tiles;
+    }
     if (item >= ngitem) return;
     const int Wc = live_walkers(c.wcount, W);
     if (tile * 64 >= Wc) return;
@@ -802,39 +813,43 @@ __global__ __launch_bounds__(256) void cmbl_reduce_kernel(CLDev c, const double 
                                                          double *__restrict__ addend, unsigned int *__restrict__ counters,
                                                          int n_counters, int W)
 {
-    __shared__ double red[2][4][64];
-    const int e = blockIdx.y;
+    // a workgroup is 64 walkers x four elements, one per wave (BK15's 702 elements
+    // have 3 partial rows each: 702 x 16 four-wave workgroups, three waves of each
+    // mostly idle, took 11.8 us)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int e = blockIdx.y * 4 + wave;
     const int w = blockIdx.x * 64 + lane;
-    if (blockIdx.x == 0 && e == 0)
+    if (blockIdx.x == 0 && blockIdx.y == 0)
         for (int i = threadIdx.x; i < n_counters; i += 256) counters[i] = 0u;
     const int Wc = live_walkers(c.wcount, W);
-    if (blockIdx.x * 64 >= Wc) return;
+    if (blockIdx.x * 64 >= Wc || e >= c.nE) return;
     // window columns in window order, each the l-chunk partials in order (flattened on
-    // the host); wave v sums rows v, v+4, ... eight loads at a time, the four wave sums
-    // are combined in fixed order: deterministic
+    // the host); four interleaved sums k over rows k, k+4, ... eight loads at a time,
+    // combined in fixed order: deterministic (and the order the earlier four-wave
+    // form had, wave k taking sum k)
     auto rows_sum = [&](const int *off, const int *rows) {
-        double v = 0.0;
+        double v[4] = {0.0, 0.0, 0.0, 0.0};
         if (w < Wc) {
             const int q0 = off[e], q1 = off[e + 1];
-            for (int q = q0 + wave; q < q1; q += 32) {
-                double t[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++)
-                    t[u] = (q + 4 * u < q1) ? partial[(long long)rows[q + 4 * u] * W + w] : 0.0;
+            for (int k = 0; k < 4; k++)
+                for (int q = q0 + k; q < q1; q += 32) {
+                    double t[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) v += t[u];
-            }
+                    for (int u = 0; u < 8; u++)
+                        t[u] = (q + 4 * u < q1) ? partial[(long long)rows[q + 4 * u] * W + w] : 0.0;
+#pragma unroll
+                    for (int u = 0; u < 8; u++) v[k] += t[u];
+                }
         }
-        return v;
+        return ((v[0] + v[1]) + v[2]) + v[3];
     };
-    red[0][wave][lane] = rows_sum(c.e_main_off, c.e_main_rows);
-    red[1][wave][lane] = c.has_corr ? rows_sum(c.e_corr_off, c.e_corr_rows) : 0.0;
-    __syncthreads();
-    if (wave != 0 || w >= Wc) return;
-    double s = c.e_main_const[e] + (((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane]);
+    const double main = rows_sum(c.e_main_off, c.e_main_rows);
+    const double corr = c.has_corr ? rows_sum(c.e_corr_off, c.e_corr_rows) : 0.0;
+    if (w >= Wc) return;
+    double s = c.e_main_const[e] + main;
     if (c.has_corr) {
-        const double cs = c.e_corr_const[e] + (((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane]);
+        const double cs = c.e_corr_const[e] + corr;
         s = s + (cs - c.fidcorr[e]);
     }
     double *x = xrows + (long long)w * c.Np;
@@ -2609,12 +2624,17 @@ struct CMBLikes final : Like {
                       items_even && (lmax + 1 < ld_field || (lmax % 2 == 1 && lmax + 1 <= ld_field));
         if (use_group) {
             const bool gvec = ((reinterpret_cast<uintptr_t>(dl) & 15) == 0) && ld_field % 2 == 0 && ld_walker % 2 == 0;
-            const int nblk = 8 * tiles * ((n_gitem + 7) / 8);
+            static const int map_env = [] {   // A/B: CMAMD_WG_MAP=0 forces the item-per-XCD placement
+                const char *e = std::getenv("CMAMD_WG_MAP");
+                return e ? std::atoi(e) : 1;
+            }();
+            const int txcd = (map_env && tiles % 8 == 0) ? 1 : 0;
+            const int nblk = txcd ? tiles * n_gitem : 8 * tiles * ((n_gitem + 7) / 8);
             timed_launch("cmbl_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
                 hipExtLaunchKernelGGL(cmbl_window_group, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, dev,
                                       d_gitems.as<GItem>(), n_gitem, d_gw.as<double>(), dl, ld_field, ld_walker, nu,
                                       ld_nuis, (const double *)coef, (const double *)prof, dev.LP, partial, W, tiles,
-                                      (int)gvec);
+                                      (int)gvec, txcd);
             });
         } else if (!bk && !smica && aberration == 0.0) {
             const int nblk = 8 * tiles * ((dev.nitem + 7) / 8);
@@ -2690,7 +2710,7 @@ struct CMBLikes final : Like {
             return QFDeferred{};
         }
         timed_launch("cmbl_reduce_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-            hipExtLaunchKernelGGL(cmbl_reduce_kernel, dim3(tiles, dev.nE), dim3(256), 0, stream, e0, e1, 0, dev,
+            hipExtLaunchKernelGGL(cmbl_reduce_kernel, dim3(tiles, (dev.nE + 3) / 4), dim3(256), 0, stream, e0, e1, 0, dev,
                                   (const double *)partial, nu, ld_nuis, qf.x_rows(qws), cmat, use_add ? addend : nullptr,
                                   qf.counters(qws, W), qf.n_counters(W), W);
         });

@@ -247,7 +247,7 @@ struct cmbs {
     size_t uni_lds = 0;
     int tail_nosignal = 0;                   // debug (cmamd_debug_tail_nosignal)
     bool binned_cache = false;               // cmbs_set_binned_cache: bin once per fast-step call
-    int qf_ahead = 0;                        // unified launch: CMAMD_QF_AHEAD (A/B of qfs_body_nj in the middle launches)
+    int qf_ahead = 1;                        // unified launch: qfs_body_nj in the middle launches too (CMAMD_QF_AHEAD=0: the loop form)
     int fold_late_prio = 0;                  // unified launch: CMAMD_FOLD_LATE_PRIO (A/B)
     int fold_g = 1;                          // unified launch: the small chi^2 in the Metropolis workgroups
                                              // (CMAMD_FOLD_G=0: as rows of its own, for A/B runs)
