@@ -297,6 +297,8 @@ int cmbs_create(const cmbs_config_t *cfg, cmbs_t **out, char *errbuf, size_t err
     if (const char *e = std::getenv("CMAMD_FOLD_G")) s->fold_g = std::atoi(e) != 0;   // A/B runs
     if (const char *e = std::getenv("CMAMD_QF_AHEAD")) s->qf_ahead = std::atoi(e) != 0;
     if (const char *e = std::getenv("CMAMD_FOLD_LATE_PRIO")) s->fold_late_prio = std::atoi(e) != 0;
+    if (const char *e = std::getenv("CMAMD_QF_PRIO")) s->qf_prio = std::atoi(e) != 0;
+    if (const char *e = std::getenv("CMAMD_FOLD_TPF")) s->fold_tpf = std::atoi(e) == 2 ? 2 : 1;
     int rc = guarded(&err, [&] { cmamd::sampler_create(s.get(), cfg); });
     if (rc) {
         put_err(errbuf, errlen, err.c_str());

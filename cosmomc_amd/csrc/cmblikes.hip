@@ -608,6 +608,10 @@ struct GItem {
     long long woff;     // weights [GP][16][nstep * 32] (zero padded)
 };
 
+// LDEC: l-dependent decorrelation possible (lform_dust or lform_sync lin / quad);
+// without it no pair's flags can be set, and the inner loop carries no
+// decorrelation code (same arithmetic on the flags = 0 path)
+template <bool LDEC>
 __global__ __launch_bounds__(256, 2) void cmbl_window_group(CLDev c, const GItem *__restrict__ gitems, int ngitem,
                                                         const double *__restrict__ wts, const double *__restrict__ dl,
                                                         long long ld_field, long long ld_walker,
@@ -764,7 +768,7 @@ __global__ __launch_bounds__(256, 2) void cmbl_window_group(CLDev c, const GItem
 #pragma unroll
             for (int s = 0; s < LPL; s++) {
                 double Dd = cf[g][3][wr_], Ds = cf[g][4][wr_];
-                if (flags) {
+                if (LDEC && flags) {
                     const int l = it.l0 + lr + s;
                     if (flags & 1) Dd = bk_decorr(Delta_dust, cf[g][5][wr_], cf[g][6][wr_], c.decorr_dust, l, c.lform_dust);
                     if (flags & 2) Ds = bk_decorr(Delta_sync, cf[g][5][wr_], cf[g][6][wr_], c.decorr_sync, l, c.lform_sync);
@@ -2631,10 +2635,16 @@ struct CMBLikes final : Like {
             const int txcd = (map_env && tiles % 8 == 0) ? 1 : 0;
             const int nblk = txcd ? tiles * n_gitem : 8 * tiles * ((n_gitem + 7) / 8);
             timed_launch("cmbl_window_kernel", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                hipExtLaunchKernelGGL(cmbl_window_group, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, dev,
-                                      d_gitems.as<GItem>(), n_gitem, d_gw.as<double>(), dl, ld_field, ld_walker, nu,
-                                      ld_nuis, (const double *)coef, (const double *)prof, dev.LP, partial, W, tiles,
-                                      (int)gvec, txcd);
+                if (dev.lform_dust != 0 || dev.lform_sync != 0)
+                    hipExtLaunchKernelGGL(cmbl_window_group<true>, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, dev,
+                                          d_gitems.as<GItem>(), n_gitem, d_gw.as<double>(), dl, ld_field, ld_walker,
+                                          nu, ld_nuis, (const double *)coef, (const double *)prof, dev.LP, partial, W,
+                                          tiles, (int)gvec, txcd);
+                else
+                    hipExtLaunchKernelGGL(cmbl_window_group<false>, dim3(nblk), dim3(256), 0, stream, e0, e1, 0, dev,
+                                          d_gitems.as<GItem>(), n_gitem, d_gw.as<double>(), dl, ld_field, ld_walker,
+                                          nu, ld_nuis, (const double *)coef, (const double *)prof, dev.LP, partial, W,
+                                          tiles, (int)gvec, txcd);
             });
         } else if (!bk && !smica && aberration == 0.0) {
             const int nblk = 8 * tiles * ((dev.nitem + 7) / 8);

@@ -31,7 +31,7 @@
 namespace cmamd {
 // mh_step_kernel (tools/uni_stamps.py), [0] the middle launches, [1] the last
 // (accept-only) launch: start, the Metropolis wait's end, XCC id, end, role + 1
-__device__ unsigned long long g_uni_stamps[2][2048][5];
+__device__ unsigned long long g_uni_stamps[2][2048][6];   // start, wait done, xcc, end, role + 1, folded chi^2 done
 }
 #endif
 #include "theorypass_body.h"
@@ -1157,6 +1157,7 @@ __device__ __forceinline__ void mh_step_body(DevCfg &c, int fast_only, double *h
         g_uni_stamps[slot][blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
         g_uni_stamps[slot][blockIdx.x][2] = xcc & 15;
         g_uni_stamps[slot][blockIdx.x][4] = 0;
+        g_uni_stamps[slot][blockIdx.x][5] = 0;
     }
     struct End {
         bool on;
@@ -1173,6 +1174,7 @@ __device__ __forceinline__ void mh_step_body(DevCfg &c, int fast_only, double *h
         if (lb >= t.nq) return;
         int item_ix, tile;
         qf_place(lb, t.q.src.n_items, t.q.src.xcd_map, item_ix, tile);
+        if (t.qf_prio) __builtin_amdgcn_s_setprio(2);   // A/B (CMAMD_QF_PRIO)
         if (PROPOSE && t.qf_ahead)   // A/B (CMAMD_QF_AHEAD): the two-step-ahead form in the middle launches too
             qfs_body<true, true>(lds, item_ix, tile, t.q);
         else
@@ -1197,9 +1199,14 @@ __device__ __forceinline__ void mh_step_body(DevCfg &c, int fast_only, double *h
             // rows, whole 128-byte lines) while the quadratic form runs elsewhere:
             // nX <= 16, so its sums are those of the 4-walker rows (same bits); the
             // chain's loads of the term follow tail_wait's acquire
-            small_gauss_body<MB, true, false>(t.g, lds, lb);
+            if (t.fold_tpf == 2) small_gauss_body<MB, true, false, 2>(t.g, lds, lb);
+            else small_gauss_body<MB, true, false, 1>(t.g, lds, lb);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+#ifdef CMAMD_STAMPS
+            if (threadIdx.x == 0 && blockIdx.x < 2048)
+                g_uni_stamps[PROPOSE ? 0 : 1][blockIdx.x][5] = __builtin_amdgcn_s_memrealtime();
+#endif
         }
         if (t.fold_late_prio) __builtin_amdgcn_s_setprio(3);   // A/B: the folded chi^2 at the default priority
         mh_body<ACCEPT, PROPOSE>(c, fast_only, hist_row, hist_terms, 0, lds, lb, ACCEPT ? &tw : nullptr);
@@ -3330,6 +3337,8 @@ static StepTail make_tail(cmbs *s, int rd, int wr) {
         // chi^2 would sit on the chain's critical path, 21.5 against 23.3 us)
         t.fold_g = (s->fold_g && wr >= 0 && t.g.d.nX <= MH_THREADS / MB) ? 1 : 0;
         t.qf_ahead = s->qf_ahead;
+        t.qf_prio = s->qf_prio;
+        t.fold_tpf = s->fold_tpf;
         t.fold_late_prio = s->fold_late_prio;
         if (t.fold_g) t.ng = 0;
     }

@@ -48,7 +48,10 @@ __host__ __device__ inline int small_gauss_blocks(int ng) { return (ng + 7) & ~7
 // divided by the walker's cal^2 as they are loaded (SmallGaussLaunch)
 // SIGNAL: -lnL is stored agent-scope (write-through) for a consumer in the
 // same launch (the sampler's unified step launch)
-template <int WT, bool RAWCAL = false, bool SIGNAL = false>
+// TPF: tasks whose loads a thread group has in flight at once (the same sums,
+// task by task; the folded chi^2 of the unified launch, which is latency on the
+// Metropolis workgroups' path, takes 2)
+template <int WT, bool RAWCAL = false, bool SIGNAL = false, int TPF = 1>
 __device__ __forceinline__ void small_gauss_body(const SmallGaussLaunch &a, double *lds, int blk)
 {
     constexpr int NG = 256 / WT;             // thread groups of WT walkers
@@ -85,21 +88,35 @@ __device__ __forceinline__ void small_gauss_body(const SmallGaussLaunch &a, doub
     };
     Elem e0{-1, 0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0};
     if (g < c.nE) e0 = elem(g);   // this group's first element, in flight with the partials
-    for (int t = g; t < c.ntask; t += NG) {
-        const int4 ra = *reinterpret_cast<const int4 *>(c.trow + 8 * t);
-        const int4 rb = *reinterpret_cast<const int4 *>(c.trow + 8 * t + 4);
-        const int r[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
-        double v[8];
+    for (int t0 = g; t0 < c.ntask; t0 += NG * TPF) {
+        int r[TPF][8];
+        double v[TPF][8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = (act && r[u] >= 0) ? a.partial[(long long)r[u] * W + w] : 0.0;
-        if (RAWCAL)
+        for (int p = 0; p < TPF; p++) {
+            const int t = t0 + p * NG;
+            const bool ok = t < c.ntask;
+            const int4 ra = ok ? *reinterpret_cast<const int4 *>(c.trow + 8 * t) : make_int4(-1, -1, -1, -1);
+            const int4 rb = ok ? *reinterpret_cast<const int4 *>(c.trow + 8 * t + 4) : make_int4(-1, -1, -1, -1);
+            r[p][0] = ra.x; r[p][1] = ra.y; r[p][2] = ra.z; r[p][3] = ra.w;
+            r[p][4] = rb.x; r[p][5] = rb.y; r[p][6] = rb.z; r[p][7] = rb.w;
+        }
 #pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (r[u] >= 0 && a.row_cal[r[u]]) v[u] = div_rn(v[u], c2, rc2);   // = v[u] / c2
-        double s = 0.0;
+        for (int p = 0; p < TPF; p++)
 #pragma unroll
-        for (int u = 0; u < 8; u++) s += v[u];
-        tp[t * WT + wl] = s;
+            for (int u = 0; u < 8; u++) v[p][u] = (act && r[p][u] >= 0) ? a.partial[(long long)r[p][u] * W + w] : 0.0;
+#pragma unroll
+        for (int p = 0; p < TPF; p++) {
+            const int t = t0 + p * NG;
+            if (t >= c.ntask) break;
+            if (RAWCAL)
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (r[p][u] >= 0 && a.row_cal[r[p][u]]) v[p][u] = div_rn(v[p][u], c2, rc2);   // = v / c2
+            double s = 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; u++) s += v[p][u];
+            tp[t * WT + wl] = s;
+        }
     }
     __syncthreads();
     for (int e = g; e < c.nE; e += NG) {

@@ -38,6 +38,8 @@ struct StepTail {
     int fold_g = 0;          // the chi^2 runs inside the Metropolis workgroups (16 walkers each), not as rows
     int qf_ahead = 0;        // middle launches: the quadratic form's two-step-ahead form (qfs_body_nj)
     int fold_late_prio = 0;  // the Metropolis workgroups take issue priority only after the folded chi^2
+    int qf_prio = 0;         // the quadratic-form waves at issue priority 2
+    int fold_tpf = 1;        // the folded chi^2's tasks in flight per thread group
     TPDev tp{};              // the raw pass (tp.out[*].out: the raw-sum buffers it writes)
     const double *dl = nullptr;
     long long ld_field = 0, ld_walker = 0;

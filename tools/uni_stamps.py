@@ -33,13 +33,13 @@ if __name__ == "__main__":
         smp, *_ = bench.build_problem(1024, 0, td)
         smp.step(20, fast_only=True)
         torch.cuda.synchronize()
-        st2 = np.zeros((2, 2048, 5), dtype=np.uint64)
+        st2 = np.zeros((2, 2048, 6), dtype=np.uint64)
         assert N.lib().cmamd_debug_uni_stamps(st2.ctypes.data_as(C.c_void_p)) == 0
     for which, st in (("a middle launch", st2[0]), ("the last (accept-only) launch", st2[1])):
         s = st[st[:, 4] > 0].astype(np.int64)
         t0 = s[:, 0].min()
         us = lambda x: (x - t0) / 100.0
-        print(f"{which} ({os.environ.get('CMAMD_TAIL_ORDER', 'gqp')}): quantiles 0/10/50/90/100, "
+        print(f"{which} ({os.environ.get('CMAMD_TAIL_ORDER', 'default order')}): quantiles 0/10/50/90/100, "
               f"us from the first block's start; launch {us(s[:, 3].max()):.2f} us")
         for r, name in ROLES.items():
             b = s[s[:, 4] == r]
@@ -48,4 +48,6 @@ if __name__ == "__main__":
             print(f"  {name:10s} {len(b):4d}  start {q(us(b[:, 0]))}   end {q(us(b[:, 3]))}   "
                   f"dur {q((b[:, 3] - b[:, 0]) / 100.0)}")
             if r == 4:
+                if (b[:, 5] > 0).all():
+                    print(f"  {'':10s}       folded chi^2 done {q(us(b[:, 5]))}")
                 print(f"  {'':10s}       wait done {q(us(b[:, 1]))}")
