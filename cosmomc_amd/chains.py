@@ -252,10 +252,11 @@ class LikelihoodDerived:
     1-based parameter indices of the history rows; P_fixed: the full parameter
     vector supplying the values of parameters that are not used (fixed)."""
 
-    def __init__(self, likes, params_used, P_fixed, labels=None):
+    def __init__(self, likes, params_used, P_fixed, labels=None, device="cuda"):
         self.likes = [l for l in likes if getattr(l, "derived_names", None)]
         self.params_used = [int(i) for i in params_used]
         self.P_fixed = np.asarray(P_fixed, dtype=np.float64)
+        self.device = device
         order = []
         for l in self.likes:
             for nm, ix in zip(l.derived_names, l.derived_indices):
@@ -278,7 +279,7 @@ class LikelihoodDerived:
         full = full.reshape(steps * W, -1)
         out = np.zeros((steps * W, self.n))
         for l in self.likes:
-            nuis = torch.tensor(np.ascontiguousarray(full[:, [i - 1 for i in l.nuisance_indices]]), device="cuda")
+            nuis = torch.tensor(np.ascontiguousarray(full[:, [i - 1 for i in l.nuisance_indices]]), device=self.device)
             d = l.derived_batch(nuis).cpu().numpy()
             for k, ix in enumerate(l.derived_indices):
                 out[:, ix - 1] = d[:, k]

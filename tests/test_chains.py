@@ -142,3 +142,56 @@ def test_weights_thin_and_burn(tmp_path):
     cw.close()
     c = np.loadtxt(str(tmp_path / "h_1.txt"), ndmin=2)
     np.testing.assert_allclose(c, [[2.0, 13.0, 3.0], [1.0, 14.0, 4.0]])
+
+
+def test_likelihood_derived_columns_and_paramnames(tmp_path):
+    """Likelihood-derived parameters (addLikelihoodDerivedParams,
+    GeneralTypes.f90:772-777): derived_indices from the likelihood list (derived
+    names after every MCMC name, ParamNames_Add), the columns evaluated from each
+    likelihood's DataParams (fixed parameters from P_fixed), written before the
+    chi2 columns with '*' names."""
+    import torch
+
+    from cosmomc_amd.chains import ChainWriter, LikelihoodDerived
+    from cosmomc_amd.likelihood import DataLikelihood, LikelihoodList
+
+    class Fake(DataLikelihood):
+        def __init__(self, names, dnames, fn):
+            super().__init__()
+            self.nuisance_names, self.derived_names, self.fn = names, dnames, fn
+            self.speed = 0
+
+        def derived_batch(self, nuis):
+            return self.fn(nuis)
+
+    a = Fake(["A1", "A2", "cal"], ["D2000"], lambda n: (n[:, 0] + n[:, 1]).reshape(-1, 1))
+    b = Fake(["cal", "B"], ["Bsq", "Bcube"], lambda n: torch.stack([n[:, 1] ** 2, n[:, 1] ** 3], 1))
+    a.tag, b.tag = "smica", "other"
+    ll = LikelihoodList()
+    ll.add(a)
+    ll.add(b)
+    names = ll.add_nuisance_parameters(["omegabh2"])
+    assert names == ["omegabh2", "A1", "A2", "cal", "B"]
+    assert a.derived_indices == [1] and b.derived_indices == [2, 3]
+    P_fixed = np.array([0.0222, 30.0, 20.0, 1.0, 2.0])
+    used = [2, 5]                                   # A1 and B vary; A2, cal fixed
+    der = LikelihoodDerived(ll, used, P_fixed, device="cpu")
+    assert [n for n, _ in der.names] == ["D2000", "Bsq", "Bcube"]
+    steps, W = 3, 2
+    rows = np.zeros((steps, 3, W))
+    rows[:, 0, :] = 30.0 + np.arange(steps)[:, None] + np.arange(W)[None, :]
+    rows[:, 1, :] = 2.0 + 0.5 * np.arange(W)[None, :]
+    rows[:, 2, :] = 5.0 + np.arange(steps)[:, None]  # CurLike
+    cols = der.columns(rows[:, :2, :])
+    assert cols.shape == (steps, 3, W)
+    np.testing.assert_array_equal(cols[:, 0, :], rows[:, 0, :] + 20.0)
+    np.testing.assert_array_equal(cols[:, 1, :], rows[:, 1, :] ** 2)
+    np.testing.assert_array_equal(cols[:, 2, :], rows[:, 1, :] ** 3)
+    root = str(tmp_path / "c")
+    cw = ChainWriter(root, ["A1", "B"], likelihoods=[a.description(), b.description()], derived=der, burn_in=0)
+    cw.add_rows(rows, terms=np.ones((steps, 2, W)))
+    cw.close()
+    pn = [l.split("\t")[0] for l in open(root + ".paramnames").read().splitlines()]
+    assert pn == ["A1", "B", "D2000*", "Bsq*", "Bcube*", "chi2_smica*", "chi2_other*", "chi2_prior*", "chi2_CMB*"]
+    data = np.loadtxt(root + "_1.txt", ndmin=2)
+    assert data.shape[1] == 1 + 1 + 2 + 3 + 4
