@@ -1926,7 +1926,6 @@ struct CMBLikes final : Like {
             read_bin_windows(ini, "linear_correction_bin_window", cw);
         }
         std::string cp = ini.relative_filename("calibration_param", false);
-        if (bk && !cp.empty()) fail(CMBL_ERR_UNSUPPORTED, "BKPLANCK with calibration_param is not supported");
         if (!cp.empty()) {
             nuisance_names = load_paramnames(cp, &n_nuis, &derived_names, &n_derived);
             cal_index = n_nuis - 1;
@@ -1953,7 +1952,10 @@ struct CMBLikes final : Like {
                 cal_index = ix;   // -1: none
             }
         }
-        // ---- TBK_planck_ReadIni (CMB_BK_Planck.f90:36-70)
+        // ---- TBK_planck_ReadIni (CMB_BK_Planck.f90:36-70).  As for SMICA, a
+        // calibration_param read by the base ReadIni (:43) sets the calibration index
+        // to its name count and loadParamNames (:46, nuisance_params%init) then replaces
+        // the names: the index stays and points into the BK parameters
         std::vector<BKMap> bkm;
         std::vector<double> bnu, bR, bdnu;
         if (bk) {

@@ -457,6 +457,17 @@ def _bk15_order(dataset_path: str) -> list[str]:
     raise ValueError("covmat_cl missing in " + dataset_path)
 
 
+def write_refdata_extras(d: str) -> None:
+    """Files the tests add beside the reference's extracted data (``d``): the
+    synthetic BK15 covariance (configs[4]) and a one-name calibration parameter
+    file for BKPLANCK + calibration_param."""
+    if os.path.isdir(os.path.join(d, "BK15")):
+        write_bk15_covmat(os.path.join(d, "BK15"))
+    if os.path.isdir(os.path.join(d, "BKPlanck")):
+        with open(os.path.join(d, "BKPlanck", "bk_cal.paramnames"), "w") as f:
+            f.write("calBK   c_{BK}\n")
+
+
 def write_bk15_covmat(bk15_dir: str, seed: int = 1515, rank: int = 24) -> str:
     """Write BK15_covmat_dust.dat into ``bk15_dir`` (the extracted data/BK15)."""
     order = _bk15_order(os.path.join(bk15_dir, "BK15_dust.dataset"))

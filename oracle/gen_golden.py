@@ -297,6 +297,12 @@ CMBL_CASES = [
     # BASELINE configs[4]: BK15 B-only, 12 maps x 9 bins (batch3/BK15.ini), synthetic covariance
     ("bk15_B_12maps", "BKPLANCK", BK15, {"maps_use": BK15_MAPS, "use_min": "1", "use_max": "9"}, 3, 600, "bk_sync"),
     ("bk15_B_decorr_bandcentre", "BKPLANCK", BK15, {"maps_use": BK15_MAPS}, 3, 600, "bk15_bc"),
+    # calibration_param read by the base ReadIni, then the names replaced by BK's
+    # nuisance_params (CMB_BK_Planck.f90:43-46): the calibration index (1) stays and
+    # points at BBdust (the reference's own behaviour), with its log prior
+    ("bkplanck_calparam_prior", "BKPLANCK", BKP, {"maps_use": "B2K_B P217_B P353_B", "use_max": "5",
+                                                  "calibration_param": "bk_cal.paramnames",
+                                                  "log_calibration_prior": "0.5"}, 3, 600, "bk_fid"),
 ]
 BK_FID = [3.0, 0.0, -0.42, 1.59, 19.6, -0.6, -3.3, 0.0, 2.0, 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0]
 
@@ -339,8 +345,7 @@ def refdata_dir(td):
             tar.extractall(d, filter="data")
         except TypeError:
             tar.extractall(d)
-    if os.path.isdir(os.path.join(d, "BK15")):
-        syn.write_bk15_covmat(os.path.join(d, "BK15"))
+    syn.write_refdata_extras(d)
     return d
 
 

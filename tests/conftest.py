@@ -78,9 +78,8 @@ def refdata(tmp_path_factory):
             tar.extractall(d, filter="data")
         except TypeError:
             tar.extractall(d)
-    if os.path.isdir(os.path.join(d, "BK15")):        # configs[4]: synthetic BK15 covariance
-        from cosmomc_amd import synthetic as syn
-        syn.write_bk15_covmat(os.path.join(d, "BK15"))
+    from cosmomc_amd import synthetic as syn
+    syn.write_refdata_extras(d)                       # configs[4]'s BK15 covariance, bk_cal.paramnames
     return d
 
 

@@ -18,9 +18,10 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 CASES = ["lensing_consext8", "bkplanck_3map_bins1to5", "bkplanck_all_maps", "bkplanck_decorr_lin_quad",
-         "bkplanck_EB_4map", "sptsz_aberration_calprior", "bk15_B_12maps", "bk15_B_decorr_bandcentre"]
+         "bkplanck_EB_4map", "sptsz_aberration_calprior", "bk15_B_12maps", "bk15_B_decorr_bandcentre",
+         "bkplanck_calparam_prior"]
 HL = {"bkplanck_3map_bins1to5", "bkplanck_all_maps", "bkplanck_decorr_lin_quad", "bkplanck_EB_4map",
-      "bk15_B_12maps", "bk15_B_decorr_bandcentre"}
+      "bk15_B_12maps", "bk15_B_decorr_bandcentre", "bkplanck_calparam_prior"}
 
 
 def _open(refdata, c):
@@ -45,7 +46,7 @@ def test_cmblikes_vs_reference_golden(cmbl_golden, refdata, case):
 
 
 @pytest.mark.parametrize("case", ["lensing_consext8", "bkplanck_3map_bins1to5", "sptsz_aberration_calprior",
-                                  "bk15_B_12maps"])
+                                  "bk15_B_12maps", "bkplanck_calparam_prior"])
 @pytest.mark.parametrize("W", [1, 63, 64, 65, 130])
 def test_cmblikes_walker_counts_vs_oracle(cmbl_golden, refdata, case, W):
     c = cmbl_golden["cases"][case]

@@ -13,7 +13,8 @@ import cmblikes_oracle as co
 from cosmomc_amd import synthetic as syn
 
 CASES = ["lensing_consext8", "bkplanck_3map_bins1to5", "bkplanck_all_maps", "bkplanck_decorr_lin_quad",
-         "bkplanck_EB_4map", "sptsz_aberration_calprior", "bk15_B_12maps", "bk15_B_decorr_bandcentre"]
+         "bkplanck_EB_4map", "sptsz_aberration_calprior", "bk15_B_12maps", "bk15_B_decorr_bandcentre",
+         "bkplanck_calparam_prior"]
 
 
 @pytest.mark.parametrize("case", CASES)
