@@ -1973,6 +1973,9 @@ struct CMBLikes final : Like {
             };
             dev.lform_dust = lform("lform_dust_decorr");
             dev.lform_sync = lform("lform_sync_decorr");
+            // the reference reads nmaps_required bandpasses named by used_map_order (:64-66),
+            // which holds only the nmaps used maps: a required map beyond them has no defined
+            // bandpass there, so the case is refused rather than given a meaning
             if (nreq != nmaps) fail(CMBL_ERR_UNSUPPORTED, "BKPLANCK: maps_required beyond maps_use not supported");
             const double G = ghz_kelvin();
             for (int i = 0; i < nreq; i++) {
