@@ -249,7 +249,7 @@ struct cmbs {
     bool binned_cache = false;               // cmbs_set_binned_cache: bin once per fast-step call
     int qf_ahead = 1;                        // unified launch: qfs_body_nj in the middle launches too (CMAMD_QF_AHEAD=0: the loop form)
     int fold_late_prio = 0;                  // unified launch: CMAMD_FOLD_LATE_PRIO (A/B)
-    int qf_prio = 0;                         // unified launch: CMAMD_QF_PRIO (A/B)
+    int qf_prio = 1;                         // unified launch: the QF waves at priority 2 (CMAMD_QF_PRIO=0 off)
     int fold_tpf = 1;                        // unified launch: CMAMD_FOLD_TPF (A/B, 1 or 2)
     int fold_g = 1;                          // unified launch: the small chi^2 in the Metropolis workgroups
                                              // (CMAMD_FOLD_G=0: as rows of its own, for A/B runs)

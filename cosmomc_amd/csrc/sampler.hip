@@ -1174,7 +1174,10 @@ __device__ __forceinline__ void mh_step_body(DevCfg &c, int fast_only, double *h
         if (lb >= t.nq) return;
         int item_ix, tile;
         qf_place(lb, t.q.src.n_items, t.q.src.xcd_map, item_ix, tile);
-        if (t.qf_prio) __builtin_amdgcn_s_setprio(2);   // A/B (CMAMD_QF_PRIO)
+        // the quadratic form's waves above the pass's at issue (the Metropolis
+        // waves' 3 stays highest): 35.98 / 36.26 -> 35.90 / 35.80 us per step in two
+        // interleaved repetitions (round 6, tools/gpu_r6f.sh); CMAMD_QF_PRIO=0 turns it off
+        if (t.qf_prio) __builtin_amdgcn_s_setprio(2);
         if (PROPOSE && t.qf_ahead)   // A/B (CMAMD_QF_AHEAD): the two-step-ahead form in the middle launches too
             qfs_body<true, true>(lds, item_ix, tile, t.q);
         else
