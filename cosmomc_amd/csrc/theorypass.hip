@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256, NB <= 2 ? 3 : 2) void theory_window_vec(TPDev 
                                                                          long long ld_field, long long ld_walker, int W)
 {
     __shared__ __attribute__((aligned(16))) char lds[tp_vec_lds_bytes<NB>()];
-    tp_vec_body<NB, false>(c, dl, ld_field, ld_walker, W, lds, blockIdx.x);
+    tp_vec_body<NB, false, true>(c, dl, ld_field, ld_walker, W, lds, blockIdx.x);
 }
 
 // The pass over two theory sets in one launch (the dragging steps' end and
@@ -281,9 +281,9 @@ __global__ __launch_bounds__(256, 3) void theory_window_pair(TPDev ca, const dou
     const int b = (int)blockIdx.x - (second ? n : 0);
     if (b == 0 && (int)threadIdx.x < nz) (second ? zb : za)[threadIdx.x] = 0u;
     if (second)
-        tp_vec_body<2, false>(cb, dlb, lfb, lwb, W, lds, b);
+        tp_vec_body<2, false, true>(cb, dlb, lfb, lwb, W, lds, b);
     else
-        tp_vec_body<2, false>(ca, dla, lfa, lwa, W, lds, b);
+        tp_vec_body<2, false, true>(ca, dla, lfa, lwa, W, lds, b);
 }
 
 // ------------------------------------------------------------------ host side

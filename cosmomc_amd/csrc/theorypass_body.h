@@ -14,6 +14,7 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 #ifndef TP_STAMP
 #define TP_STAMP(i) ((void)0)
 #endif
+
 template <int NB> constexpr int tp_vec_lds_bytes() {
     return 2 * NB * 16 * (32 + 2) * 8 + TP_MAXCOL * (int)sizeof(TPCol) + TP_MAXCOL * 8 + TP_MAXSTEP * 8 +
            TP_MAXSTEP * TP_MAXCOL;
@@ -35,7 +36,12 @@ template <int NB> constexpr int tp_vec_lds_bytes() {
 // the consumers apply the calibrations of the step that reads them with the
 // emit's own operations (X - v / cal^2 in the quadratic form's operand, v /
 // cal^2 in the small chi^2's partial rows), so the results are the same bits.
-template <int NB, bool RAW = false>
+//
+// W2: the weight tiles two steps ahead in two register sets (the standalone
+// kernels: theory_window_pair 41.1 -> 40.0 us a launch, the drag step 416.5-417.5
+// -> 412.4-415.6 us; in the unified launch, whose registers the other roles
+// share, it measured 0.3 us slower: there the one-step form runs)
+template <int NB, bool RAW = false, bool W2 = false>
 __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__restrict__ dl, long long ld_field,
                                             long long ld_walker, int W, char *lds, int b)
 {
@@ -73,23 +79,30 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
     };
     const int wc = tid >> 4, wp = 2 * (tid & 15);
     double2 wr0{}, wr1{}, wr2{}, wr3{};      // named registers: an array here lands in scratch
-    auto fetch_w = [&](int st) {
+#define TP_WR wr0, wr1, wr2, wr3
+    // W2: two named register sets: step st fetches the weights of st + 2 into
+    // one while the other holds those of st + 1 (fetched a whole step earlier)
+    // for the LDS store at the step's end
+    double2 wa0{}, wa1{}, wa2{}, wa3{}, wb0{}, wb1{}, wb2{}, wb3{};
+#define TP_WA wa0, wa1, wa2, wa3
+#define TP_WB wb0, wb1, wb2, wb3
+    auto fetch_w = [&](int st, double2 &r0, double2 &r1, double2 &r2, double2 &r3) {
         const int ch = st / NSUB, sub = st % NSUB;
         const double *base = c.w + it.woff + (long long)ch * ncb * 16 * TP_CHUNK + sub * STEP + wc * TP_CHUNK + wp;
-        wr0 = *reinterpret_cast<const double2 *>(base);
-        wr1 = *reinterpret_cast<const double2 *>(base + 16 * TP_CHUNK);
+        r0 = *reinterpret_cast<const double2 *>(base);
+        r1 = *reinterpret_cast<const double2 *>(base + 16 * TP_CHUNK);
         if constexpr (NB > 2) {
-            wr2 = *reinterpret_cast<const double2 *>(base + 2 * 16 * TP_CHUNK);
-            wr3 = *reinterpret_cast<const double2 *>(base + 3 * 16 * TP_CHUNK);
+            r2 = *reinterpret_cast<const double2 *>(base + 2 * 16 * TP_CHUNK);
+            r3 = *reinterpret_cast<const double2 *>(base + 3 * 16 * TP_CHUNK);
         }
     };
-    auto store_w = [&](int buf) {
+    auto store_w = [&](int buf, const double2 &r0, const double2 &r1, const double2 &r2, const double2 &r3) {
         double *d = wsh + (buf * NB * 16 + wc) * WROW + wp;
-        *reinterpret_cast<double2 *>(d) = wr0;
-        *reinterpret_cast<double2 *>(d + 16 * WROW) = wr1;
+        *reinterpret_cast<double2 *>(d) = r0;
+        *reinterpret_cast<double2 *>(d + 16 * WROW) = r1;
         if constexpr (NB > 2) {
-            *reinterpret_cast<double2 *>(d + 2 * 16 * WROW) = wr2;
-            *reinterpret_cast<double2 *>(d + 3 * 16 * WROW) = wr3;
+            *reinterpret_cast<double2 *>(d + 2 * 16 * WROW) = r2;
+            *reinterpret_cast<double2 *>(d + 3 * 16 * WROW) = r3;
         }
     };
     auto read_w = [&](int buf, int cb) {
@@ -107,7 +120,12 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
     // prologue: theory steps 0, 1; weights of step 0 into LDS, of step 1 in registers
     load_t(0, tA);
     load_t(1, tB);                       // nstep >= 2: an item is whole 64-l chunks
-    fetch_w(0);
+    if constexpr (W2) {
+        fetch_w(0, TP_WA);
+        fetch_w(1, TP_WB);
+    } else {
+        fetch_w(0, TP_WR);
+    }
     if (tid < it.ncol) {
         const TPCol d = c.cols[it.cdesc + tid];
         csh[tid] = d;
@@ -132,7 +150,10 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
             rc2[o] = 1.0 / c2[o];
         }
     }
-    store_w(0);
+    if constexpr (W2)
+        store_w(0, TP_WA);
+    else
+        store_w(0, TP_WR);
     __syncthreads();
     TP_STAMP(1);
     auto emit = [&](int st, unsigned long long e, int cb, f64x4 &a0, f64x4 &b0) {
@@ -193,40 +214,90 @@ __device__ __forceinline__ void tp_vec_body(const TPDev &c, const double *__rest
                 }
             }
     };
-    // main steps: weights of st + 1 and theory of st + 2 in flight; step s
-    // lives in buffer s mod 3 (A, B, C)
-    auto step = [&](int st, const double *tc, double *tl) {
-        fetch_w(st + 1);
-        load_t(st + 2, tl);
-        compute(st, tc, false);
-        closes(st);
-        store_w((st & 1) ^ 1);
-        __syncthreads();
-    };
     int st = 0;
-    while (st + 2 < nstep) {
-        step(st, tA, tC);
-        if (++st + 2 >= nstep) break;
-        step(st, tB, tA);
-        if (++st + 2 >= nstep) break;
-        step(st, tC, tB);
-        ++st;
+    if constexpr (W2) {
+        // main steps: weights of st + 2 and theory of st + 2 in flight; step s's
+        // theory lives in buffer s mod 3 (A, B, C), its weights' registers in set
+        // s mod 2 (A, B) until stored at step s - 1
+        auto step = [&](int st, const double *tc, double *tl, double2 &f0, double2 &f1, double2 &f2, double2 &f3,
+                        const double2 &s0, const double2 &s1, const double2 &s2, const double2 &s3) {
+            fetch_w(st + 2, f0, f1, f2, f3);
+            load_t(st + 2, tl);
+            compute(st, tc, false);
+            closes(st);
+            store_w((st & 1) ^ 1, s0, s1, s2, s3);
+            __syncthreads();
+        };
+        while (st + 2 < nstep) {
+            step(st, tA, tC, TP_WA, TP_WB);
+            if (++st + 2 >= nstep) break;
+            step(st, tB, tA, TP_WB, TP_WA);
+            if (++st + 2 >= nstep) break;
+            step(st, tC, tB, TP_WA, TP_WB);
+            if (++st + 2 >= nstep) break;
+            step(st, tA, tC, TP_WB, TP_WA);
+            if (++st + 2 >= nstep) break;
+            step(st, tB, tA, TP_WA, TP_WB);
+            if (++st + 2 >= nstep) break;
+            step(st, tC, tB, TP_WB, TP_WA);
+            ++st;
+        }
+        // the last two steps: nothing more to load; step st + 1's weights (set
+        // (st + 1) mod 2) go to the buffer step st - 1 read, behind its barrier
+        if (st & 1)
+            store_w((st & 1) ^ 1, TP_WA);
+        else
+            store_w((st & 1) ^ 1, TP_WB);
+        auto tail = [&](const double *t0, const double *t1) {
+            compute(st, t0, true);
+            __syncthreads();
+            closes(st);
+            compute(st + 1, t1, true);
+            closes(st + 1);
+        };
+        switch (st % 3) {
+            case 0: tail(tA, tB); break;
+            case 1: tail(tB, tC); break;
+            default: tail(tC, tA); break;
+        }
+    } else {
+        // main steps: weights of st + 1 and theory of st + 2 in flight; step s
+        // lives in buffer s mod 3 (A, B, C)
+        auto step = [&](int st, const double *tc, double *tl) {
+            fetch_w(st + 1, TP_WR);
+            load_t(st + 2, tl);
+            compute(st, tc, false);
+            closes(st);
+            store_w((st & 1) ^ 1, TP_WR);
+            __syncthreads();
+        };
+        while (st + 2 < nstep) {
+            step(st, tA, tC);
+            if (++st + 2 >= nstep) break;
+            step(st, tB, tA);
+            if (++st + 2 >= nstep) break;
+            step(st, tC, tB);
+            ++st;
+        }
+        // the last two steps: nothing more to load
+        auto tail = [&](const double *t0, const double *t1) {
+            fetch_w(st + 1, TP_WR);
+            compute(st, t0, true);
+            store_w((st & 1) ^ 1, TP_WR);
+            __syncthreads();
+            closes(st);
+            compute(st + 1, t1, true);
+            closes(st + 1);
+        };
+        switch (st % 3) {
+            case 0: tail(tA, tB); break;
+            case 1: tail(tB, tC); break;
+            default: tail(tC, tA); break;
+        }
     }
-    // the last two steps: nothing more to load
-    auto tail = [&](const double *t0, const double *t1) {
-        fetch_w(st + 1);
-        compute(st, t0, true);
-        store_w((st & 1) ^ 1);
-        __syncthreads();
-        closes(st);
-        compute(st + 1, t1, true);
-        closes(st + 1);
-    };
-    switch (st % 3) {
-        case 0: tail(tA, tB); break;
-        case 1: tail(tB, tC); break;
-        default: tail(tC, tA); break;
-    }
+#undef TP_WR
+#undef TP_WA
+#undef TP_WB
     TP_STAMP(2);
 #ifdef CMAMD_TP_STAMPS
     if (threadIdx.x == 0 && b < 4096) {
