@@ -15,12 +15,17 @@ static constexpr int TP_MAXOUT = 2;    // likelihoods per pass
 static constexpr int TP_CHUNK = 64;    // l per weight chunk
 static constexpr int TP_MAXCOL = 64;   // columns per work item (four 16-column MFMA blocks)
 #ifndef CMAMD_TP_MAXL
-#define CMAMD_TP_MAXL 288
+#define CMAMD_TP_MAXL 352
 #endif
 // l per work item, unless overlapping columns force more (at most
-// TP_MAXSTEP * 32 - 1 in any case).  288 (9 steps): with slot reuse the
-// headline's 1024 walkers make about 2 blocks per CU; measured 22.7 us
-// against 24.0 (256), 23.2 (272), 23.3 (300), 23.6 (320), 24.9 (384)
+// TP_MAXSTEP * 32 - 1 in any case).  Round 2 (the standalone pass alone):
+// 288 (9 steps), 22.7 us against 24.0 (256), 23.2 (272), 23.3 (300), 23.6 (320),
+// 24.9 (384).  Round 6, with the pass inside the unified step launch (fewer,
+// longer units beside the quadratic form) and the two-step weight prefetch:
+// 352 (11 steps), middle launch 33.2-33.7 -> 32.0-32.5 us and the drag step
+// 407-413 -> 399-405 us, against 192 / 224 / 256 / 384 / 416 / 448 (34.2 /
+// 34.6 / 33.2 / 32.6-32.7 / 33.3 / 34.0 us a launch; tools/gpu_r6j.sh); at 480
+// some l range needs more than TP_MAXCOL columns and the fused pass is not built
 static constexpr int TP_MAXL = CMAMD_TP_MAXL;
 
 struct TPOut {            // a stage's output for one launch
