@@ -311,6 +311,10 @@ int QuadForm::choose_kb(int /*tiles*/) {
             best_kb = kb;
         }
     }
+    if (const char *e = std::getenv("CMAMD_QF_KB")) {   // A/B: a fixed chunk (1 .. QF_MAXKB)
+        const int k = std::atoi(e);
+        if (k >= 1 && k <= MAXKB) best_kb = k;
+    }
     kb_for_tiles[tiles] = best_kb;
     return best_kb;
 }
