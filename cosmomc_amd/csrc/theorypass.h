@@ -23,8 +23,10 @@ static constexpr int TP_MAXCOL = 64;   // columns per work item (four 16-column 
 // 24.9 (384).  Round 6, with the pass inside the unified step launch (fewer,
 // longer units beside the quadratic form) and the two-step weight prefetch:
 // 352 (11 steps), middle launch 33.2-33.7 -> 32.0-32.5 us and the drag step
-// 407-413 -> 399-405 us, against 192 / 224 / 256 / 384 / 416 / 448 (34.2 /
-// 34.6 / 33.2 / 32.6-32.7 / 33.3 / 34.0 us a launch; tools/gpu_r6j.sh); at 480
+// 407-413 -> 399-405 us, against 192 / 224 / 256 / 320 / 336 / 368 / 384 / 416 /
+// 448 (34.2 / 34.6 / 33.2 / 33.2 / 32.6-32.9 / 32.9-33.0 / 32.6-32.7 / 33.3 / 34.0 us
+// a launch; tools/gpu_r6j.sh; the drag's pair pass 165-180 us a drag step at
+// 320-368 against 152-153 at 352); at 480
 // some l range needs more than TP_MAXCOL columns and the fused pass is not built
 static constexpr int TP_MAXL = CMAMD_TP_MAXL;
 
