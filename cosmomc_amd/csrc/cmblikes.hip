@@ -597,8 +597,20 @@ __global__ __launch_bounds__(256) void cmbl_window_direct(CLDev c, const double 
 // element is read once per item instead of once per pair (78 B x B pairs for
 // BK15).  l-dependent decorrelation (lform lin / quad with Delta /= 1) is
 // evaluated per value, as in the staged kernel.
-static constexpr int GP = 8;        // pairs per grouped item
-static constexpr int GSEG = 256;    // l per grouped item
+#ifndef CMAMD_GP
+#define CMAMD_GP 8
+#endif
+#ifndef CMAMD_GSEG
+#define CMAMD_GSEG 224
+#endif
+// l per grouped item: 224 (BK15's l range in three items a pair group),
+// cmbl_window_group 85.8 -> 78.1 us and configs[4] 396.4-397.8 -> 388.2-390.3
+// us/step, against 160 / 192 / 256 / 320 / 608 (406 / 417-418 / 397 / 412-414 /
+// 441 us/step; tools/gpu_r6m.sh); 6 pairs per item 400-401
+static constexpr int GP = CMAMD_GP;       // pairs per grouped item
+static constexpr int GSEG = CMAMD_GSEG;   // l per grouped item (a multiple of 32)
+static_assert(GSEG % 32 == 0, "grouped items are whole 32-l steps");
+static_assert((GP * 16 * 16 / 2) % 256 == 0, "the weight staging moves GP * 16 rows of 16 l in whole passes");
 
 struct GItem {
     int field, npair, l0, nstep;
