@@ -596,6 +596,12 @@ static constexpr int TW_PAD = CMAMD_TW_PAD;
 #define CMAMD_UNI_WT 4
 #endif
 static constexpr int UNI_WT = CMAMD_UNI_WT;
+// the pass role's weight prefetch: one step ahead (0), or two as the standalone
+// kernels (1: measured 0.3 us slower a launch with 288-l items, and the same
+// within noise with 352-l items: 32.6 / 32.0 / 31.8 against 32.1 / 32.4 / 31.9 us, round 6)
+#ifndef CMAMD_UNI_W2
+#define CMAMD_UNI_W2 0
+#endif
 static constexpr long TAIL_WAIT_SPINS = (1l << 25) / CMAMD_TW_SLEEP;   // polls: ~1 s
 
 // A give-up: the sampler's status word lives in pinned host memory (mapped),
@@ -1192,7 +1198,7 @@ __device__ __forceinline__ void mh_step_body(DevCfg &c, int fast_only, double *h
         tail_arrive(tw, q * UNI_WT / 64);
     } else if (rr.x == TAIL_PASS) {
         if (lb >= t.np) return;
-        tp_vec_body<2, true>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
+        tp_vec_body<2, true, CMAMD_UNI_W2 != 0>(t.tp, t.dl, t.ld_field, t.ld_walker, t.W, reinterpret_cast<char *>(lds), lb);
     } else if (lb < nmh) {
         // the chain is latency on one lane: its waves, dispatched last (the youngest,
         // so the last in issue arbitration), take the SIMD first (34.6 -> 34.0 us)
