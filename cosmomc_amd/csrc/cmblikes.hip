@@ -159,7 +159,11 @@ __global__ __launch_bounds__(256) void cmbl_bk_tdtab(CLDev c, const double *__re
 // SED factors of every map (one wave per map, bandpass integrals as wave
 // reductions) and the dust / sync / dust-sync l profiles.
 //   coef[w][3][nreq] = fdust, fsync, band-centre error;  prof[w][3][L]
-__global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *__restrict__ nuis, long long ld_nuis,
+#ifndef CMAMD_BKP_THREADS
+#define CMAMD_BKP_THREADS 256
+#endif
+static constexpr int BKP_THREADS = CMAMD_BKP_THREADS;   // a wave per map at a time
+__global__ __launch_bounds__(BKP_THREADS) void cmbl_bk_prologue(CLDev c, const double *__restrict__ nuis, long long ld_nuis,
                                                        double *__restrict__ coef, double *__restrict__ prof, int W)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -175,7 +179,7 @@ __global__ __launch_bounds__(256) void cmbl_bk_prologue(CLDev c, const double *_
     const double gb0 = pow(nu0d, 3 + betadust) / (exp(G * nu0d / Tdust) - 1);
     const double pl0 = pow(nu0s, 2 + betasync);
     const bool tab = Tdust == c.td0[0];              // cmbl_bk_tdtab's denominators apply
-    for (int i = wave; i < c.nreq; i += 4) {
+    for (int i = wave; i < c.nreq; i += BKP_THREADS / 64) {
         const BKMap m = c.bkmaps[i];
         double gb = 0.0, pl = 0.0;
         for (int k = lane; k < m.n; k += 64) {
@@ -2628,7 +2632,7 @@ struct CMBLikes final : Like {
             hipLaunchKernelGGL(cmbl_bk_tdtab, dim3((dev.nsamp + 255) / 256), dim3(256), 0, stream, dev, nu);
             HIP_CHECK(hipGetLastError());
             timed_launch("cmbl_bk_prologue", stream, [&](hipEvent_t e0, hipEvent_t e1) {
-                hipExtLaunchKernelGGL(cmbl_bk_prologue, dim3(W), dim3(256), 0, stream, e0, e1, 0, dev, nu, ld_nuis,
+                hipExtLaunchKernelGGL(cmbl_bk_prologue, dim3(W), dim3(BKP_THREADS), 0, stream, e0, e1, 0, dev, nu, ld_nuis,
                                       coef, prof, W);
             });
             HIP_CHECK(hipGetLastError());
