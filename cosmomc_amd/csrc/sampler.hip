@@ -2007,7 +2007,10 @@ __global__ __launch_bounds__(MH_THREADS) void drag_staged_kernel(DevCfg c, DragC
         v.ss = dd + (size_t)(3 * np + 2) * MB + lane;
         v.se = dd + (size_t)(3 * np + 3) * MB + lane;
         v.dst = dst_l + lane;
+        const int i97_0 = k.r.i97;
         drag_logic<STAGE>(c, g, t, k, v, w, hist_row, hist_terms);
+        dst_l[MB + lane] = k.r.nd < 97 ? k.r.nd : 97;   // rows 1, 2: the ring entries the draws overwrote
+        dst_l[2 * MB + lane] = i97_0;
         sd[(size_t)R.C * MB + lane] = k.r.c;
         sd[(size_t)R.G * MB + lane] = k.r.gset;
         si[(size_t)R.I97 * MB + lane] = k.r.i97;
@@ -2016,11 +2019,22 @@ __global__ __launch_bounds__(MH_THREADS) void drag_staged_kernel(DevCfg c, DragC
         si[(size_t)R.FASTIX * MB + lane] = k.fast_ix;
     }
     __syncthreads();
+    // of the RANMAR ring only the entries this stage's draws overwrote
+    // (positions i97 - 1, i97 - 2, ... mod 97 of the first index), as mh_body:
+    // the stages 63.4-63.8 against 63.8-67.4 us a drag step (round 6, tools/gpu_r6u.sh)
+    if (w < c.W) {
+        const int nd = dst_l[MB + lane], i0 = dst_l[2 * MB + lane];
+        for (int q = threadIdx.x / MB; q < nd; q += NV) {
+            int p = i0 - 1 - q;
+            if (p < 0) p += 97;
+            c.sd[(size_t)(R.U + p) * W + w] = sd[(size_t)(R.U + p) * MB + lane];
+        }
+    }
     if (skipR) {
-        stage_out(c.sd, sd, 0, 0, R.R, W, wb);
+        stage_out(c.sd, sd, R.C, R.C, R.R, W, wb);
         stage_out(c.sd, sd, R.R, rEnd, R.ND, W, wb);
     } else {
-        stage_out(c.sd, sd, 0, 0, R.ND, W, wb);
+        stage_out(c.sd, sd, R.C, R.C, R.ND, W, wb);
     }
     stage_out(g.dd, dd, 0, 0, nr, W, wb);
     stage_out(c.si, si, 0, 0, ni_st, W, wb);
